@@ -1,0 +1,10 @@
+"""stgcn_amd — MI355X-native ST-GCN block training path.
+
+Drop-in for the reference's ``src/network`` module API
+(``SpatialTemporalConv`` / ``SpatialConv``, st_graphconv.py:4-152) whose
+forward/backward run on hand-written gfx950 HIP kernels behind a C-ABI
+library (``include/stgcn_hip.h``). Import via ``stgcn_loader.load()``.
+"""
+from . import graph  # noqa: F401
+
+__all__ = ["graph"]

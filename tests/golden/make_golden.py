@@ -1,0 +1,221 @@
+"""Generate golden fixtures by running the REFERENCE itself (this container only).
+
+Usage: python3 -B tests/golden/make_golden.py [/root/reference]
+
+The reference (nagyrajmund/st-gcn, pure Python over PyTorch) is imported from
+its read-only checkout; nothing of it is copied. Two third-party modules it
+imports but that are absent here and off the arithmetic path are replaced by
+in-process stubs: ``pytorch_lightning`` (``lightning_model.py:5-7,21``) and
+``seaborn`` (pulled in by ``lightning_model.py:19``). Bytecode writing is
+disabled so the read-only tree is untouched.
+
+Outputs (small .npz files next to this script):
+  adjacency.npz   normalized A for V=25 (strategies 0-3), V=18 / V=50 (0-2)
+                  computed by src/data/adjacency.py with adj_list/nr_of_joints
+                  patched for V != 25.
+  block_*.npz     one SpatialTemporalConv (src/network/st_graphconv.py) in
+                  training mode: params, x, upstream grad g, y, every grad,
+                  running stats after the step.
+  stack_cfg1.npz  full L_STGCN (src/lightning_model.py) cfg1 plumbing case:
+                  logits, loss, param checksums and sampled grads.
+"""
+import argparse
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_stubs():
+    pl = types.ModuleType("pytorch_lightning")
+    core = types.ModuleType("pytorch_lightning.core")
+    lightning = types.ModuleType("pytorch_lightning.core.lightning")
+    callbacks = types.ModuleType("pytorch_lightning.callbacks")
+
+    class LightningModule(nn.Module):
+        pass
+
+    class Trainer:
+        @staticmethod
+        def add_argparse_args(parser):
+            return parser
+
+    class EarlyStopping:
+        def __init__(self, *a, **k):
+            pass
+
+    lightning.LightningModule = LightningModule
+    core.lightning = lightning
+    pl.core = core
+    pl.Trainer = Trainer
+    callbacks.EarlyStopping = EarlyStopping
+    pl.callbacks = callbacks
+    sys.modules.update({
+        "pytorch_lightning": pl,
+        "pytorch_lightning.core": core,
+        "pytorch_lightning.core.lightning": lightning,
+        "pytorch_lightning.callbacks": callbacks,
+    })
+    sns = types.ModuleType("seaborn")
+    sns.set = lambda *a, **k: None
+    sys.modules.setdefault("seaborn", sns)
+
+
+COCO18_ADJ = None  # filled from the build's graph module (same edges)
+
+
+def _graph_lists(V):
+    """adj_list / opposite_joints dicts for V in {18, 50} from the build's
+    graph definitions (the reference has V=25 only)."""
+    sys.path.insert(0, os.path.join(HERE, "..", ".."))
+    from stgcn_loader import load
+    g = load().graph.graph_for(V)
+    return g.adj_list, g.opposite_joints
+
+
+def _patched_adjacency(adjacency, V):
+    import contextlib
+
+    @contextlib.contextmanager
+    def ctx():
+        saved = (adjacency.adj_list, adjacency.nr_of_joints, adjacency.opposite_joints)
+        if V != 25:
+            adj, opp = _graph_lists(V)
+            adjacency.adj_list, adjacency.nr_of_joints, adjacency.opposite_joints = adj, V, opp
+        try:
+            yield
+        finally:
+            adjacency.adj_list, adjacency.nr_of_joints, adjacency.opposite_joints = saved
+    return ctx()
+
+
+def _distance_file(V, tmpdir):
+    path = os.path.join(tmpdir, f"dist{V}.npy")
+    np.save(path, np.linspace(1.0, 2.0, V))
+    return path
+
+
+def make_adjacency(adjacency, tmpdir):
+    out = {}
+    for V, strats in ((25, (0, 1, 2, 3)), (18, (0, 1, 2)), (50, (0, 1, 2))):
+        for s in strats:
+            for d in ((1, 2) if s in (0, 1) else (1,)):
+                with _patched_adjacency(adjacency, V):
+                    A = adjacency.get_normalized_adjacency_matrices(
+                        s, d, distance_file=_distance_file(V, tmpdir))
+                out[f"V{V}_s{s}_d{d}"] = A.numpy().astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "adjacency.npz"), **out)
+    return out
+
+
+BLOCK_CASES = [
+    # name, C_in, C_out, stride, V, strategy, N, T, residual
+    ("b3x64_v18", 3, 64, 1, 18, 0, 2, 32, False),
+    ("b64x64_v18", 64, 64, 1, 18, 0, 2, 24, False),
+    ("b64x128s2_v18", 64, 128, 2, 18, 0, 2, 24, False),
+    ("b128x256s2_v18", 128, 256, 2, 18, 0, 2, 8, False),
+    ("b64x64_v25k3", 64, 64, 1, 25, 2, 2, 20, False),
+    ("b64x128s2_v25k3", 64, 128, 2, 25, 2, 2, 16, False),
+    ("b3x64_v50k3", 3, 64, 1, 50, 2, 2, 12, False),
+    ("res64x64_v18", 64, 64, 1, 18, 0, 2, 20, True),
+    ("res64x128s2_v18", 64, 128, 2, 18, 0, 2, 20, True),
+]
+
+
+def make_block(st_graphconv, adj_mats, name, C_in, C_out, stride, V, strat, N, T, residual):
+    A = torch.from_numpy(adj_mats[f"V{V}_s{strat}_d1"])
+    torch.manual_seed(0)
+    blk = st_graphconv.SpatialTemporalConv(C_in, C_out, A, 9, stride, 4,
+                                           dropout_rate=0, residual=residual)
+    # BN affine params at init are 1/0; perturb them (seeded) so the affine
+    # paths are exercised by the fixture.
+    g0 = torch.Generator().manual_seed(3)
+    with torch.no_grad():
+        for bn in (blk.batch_n, blk.batch_n_2):
+            bn.weight.copy_(1.0 + 0.1 * torch.randn(bn.weight.shape, generator=g0))
+            bn.bias.copy_(0.1 * torch.randn(bn.bias.shape, generator=g0))
+    blk.train()
+    params0 = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    x = torch.randn(N, C_in, T, V, generator=torch.Generator().manual_seed(1))
+    x.requires_grad_(True)
+    y = blk(x)
+    g = torch.randn(y.shape, generator=torch.Generator().manual_seed(2))
+    (y * g).sum().backward()
+    rec = {"x": x.detach().numpy(), "g": g.numpy(), "y": y.detach().numpy(),
+           "grad.x": x.grad.numpy()}
+    for k, v in params0.items():
+        rec["param." + k] = v.numpy()
+    for k, p in blk.named_parameters():
+        rec["grad." + k] = p.grad.numpy()
+    for k, v in blk.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            rec["after." + k] = v.numpy()
+    meta = np.array([C_in, C_out, stride, V, strat, N, T, int(residual)], dtype=np.int64)
+    rec["meta"] = meta
+    np.savez_compressed(os.path.join(HERE, f"block_{name}.npz"), **rec)
+
+
+def make_stack_cfg1(lightning_model, adjacency):
+    parser = lightning_model.build_argument_parser()
+    hp = parser.parse_args(["--C_in", "3", "--nr_classes", "2"])
+    with _patched_adjacency(adjacency, 18):
+        torch.manual_seed(0)
+        model = lightning_model.L_STGCN(hp)
+    model.train()
+    N, T, V, C = 4, 50, 18, 3
+    x = torch.randn(N, T, V, C, generator=torch.Generator().manual_seed(1))
+    y = torch.randint(0, 2, (N,), generator=torch.Generator().manual_seed(2))
+    logits = model(x)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    rec = {"x": x.numpy(), "labels": y.numpy(), "logits": logits.detach().numpy(),
+           "loss": np.array(loss.item())}
+    gen = torch.Generator().manual_seed(4)
+    for k, p in model.named_parameters():
+        flat_p = p.detach().reshape(-1)
+        flat_g = p.grad.reshape(-1)
+        idx = torch.randint(0, flat_p.numel(), (min(256, flat_p.numel()),), generator=gen)
+        rec["pidx." + k] = idx.numpy()
+        rec["pval." + k] = flat_p[idx].numpy()
+        rec["psum." + k] = np.array(flat_p.double().sum().item())
+        rec["gval." + k] = flat_g[idx].numpy()
+        rec["gsum." + k] = np.array(flat_g.double().sum().item())
+        rec["gnorm." + k] = np.array(flat_g.double().norm().item())
+    for k, v in model.state_dict().items():
+        if "running" in k:
+            rec["after." + k] = v.numpy()
+    np.savez_compressed(os.path.join(HERE, "stack_cfg1.npz"), **rec)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("reference", nargs="?", default="/root/reference")
+    args = ap.parse_args()
+    _install_stubs()
+    sys.path.insert(0, os.path.join(args.reference, "src"))
+    import io
+    import contextlib
+    with contextlib.redirect_stdout(io.StringIO()):
+        from data import adjacency  # noqa: E402
+        from network import st_graphconv  # noqa: E402
+        import lightning_model  # noqa: E402
+    torch.set_num_threads(8)
+    with tempfile.TemporaryDirectory() as tmp:
+        mats = make_adjacency(adjacency, tmp)
+    with contextlib.redirect_stdout(io.StringIO()):
+        for case in BLOCK_CASES:
+            make_block(st_graphconv, mats, *case)
+        make_stack_cfg1(lightning_model, adjacency)
+    print("wrote fixtures to", HERE)
+
+
+if __name__ == "__main__":
+    main()
