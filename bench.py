@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Skeleton clips/s of the ST-GCN training step on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): Kinetics-skeleton
+shape, synthetic input (N, 3, 300, 18) NCTV per GPU with N=128, V=18, uni
+labelling (K=1), 400 classes, fp32. One step = forward of the 10-block stack
+(fused HIP blocks) + avg-pool/FC head + cross-entropy + backward + (N>1) RCCL
+gradient all-reduce + Adam update. Inputs are resident in HBM before timing.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+     (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from stgcn_loader import load  # noqa: E402
+
+CFG = dict(N=128, C=3, T=300, V=18, K=1, classes=400)
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0
+
+
+def build_model(pkg, cfg, device):
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(cfg["V"]))
+    torch.manual_seed(0)
+    import io
+    import contextlib
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = pkg.STGCNStack(cfg["C"], cfg["classes"], A)
+    return model.to(device)
+
+
+def cpu_baseline(cfg, seconds=12.0):
+    """The oracle (CPU restatement of the reference, fp32 torch ops) timed on
+    this host's cores on a bounded sample of the same workload."""
+    from oracle import ref_cpu
+    pkg = load()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(cfg["V"]))
+    p, b = ref_cpu.init_stack_params(cfg["C"], cfg["classes"], A, seed=0)
+    p = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    st = ref_cpu.Stack(p, b)
+    n = 8
+    x = torch.randn(n, cfg["T"], cfg["V"], cfg["C"], generator=torch.Generator().manual_seed(1))
+    y = torch.randint(0, cfg["classes"], (n,), generator=torch.Generator().manual_seed(2))
+
+    def step():
+        loss = torch.nn.functional.cross_entropy(st.forward(x), y)
+        loss.backward()
+
+    step()  # warm-up
+    iters, t0 = 0, time.perf_counter()
+    while iters < 2 or time.perf_counter() - t0 < seconds:
+        step()
+        iters += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * iters / dt, 3), "unit": "clips/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/ref_cpu.py fp32 stack fwd+bwd+loss, N={n} clips x {iters} iters "
+                      f"(T=300, V=18, K=1, 400 classes), {threads} threads, {dt:.1f}s"}
+
+
+def kernel_roofline(pkg, device, iters=20):
+    """Average launch time of the dominant kernel (temporal (9,1) conv forward
+    of layer 1, 64->64, N=128, T=300, V=18) timed with HIP events on the stream
+    it runs on, through the library's timing entry point."""
+    import ctypes
+    hl = pkg.hip_lib
+    lib = hl.lib()
+    if not hasattr(lib, "stgcn_time_kernel"):
+        return None
+    d = pkg.fused.make_desc((CFG["N"], 64, CFG["T"], CFG["V"]), 64, 1, 1, 4, 1e-5, 0.1, True)
+    res = {}
+    for which, name in ((0, "tconv_fwd"), (1, "tconv_dgrad"), (2, "tconv_wgrad"),
+                        (3, "spatial_gemm")):
+        nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
+        scratch = torch.randn(nbytes // 4 + 1, device=device)
+        ms = ctypes.c_float(0)
+        flops = ctypes.c_double(0)
+        hl.check(lib.stgcn_time_kernel(ctypes.byref(d), which, hl.ptr(scratch), nbytes, iters,
+                                       hl.stream_handle(device), ctypes.byref(ms),
+                                       ctypes.byref(flops)))
+        res[name] = (ms.value, flops.value)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=CFG["N"], help="clips per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    pkg = load()
+    cfg = dict(CFG, N=args.batch)
+
+    model = build_model(pkg, cfg, device)
+    params = [p for p in model.parameters()]
+    opt = torch.optim.Adam(params, lr=1e-3)
+    dp = pkg.dp.GradAllReduce(model, world) if world > 1 else None
+    gen = torch.Generator(device="cpu").manual_seed(1 + rank)
+    x = torch.randn(cfg["N"], cfg["C"], cfg["T"], cfg["V"], generator=gen).to(device)
+    labels = torch.randint(0, cfg["classes"], (cfg["N"],), generator=gen).to(device)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        logits = model.forward_nctv(x)
+        loss = torch.nn.functional.cross_entropy(logits, labels)
+        loss.backward()
+        if dp is not None:
+            dp.synchronize()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    ms = dt / args.steps * 1e3
+    clips = cfg["N"] * world * args.steps / dt
+    gf_clip = pkg.flops_per_clip(cfg["C"], cfg["T"], cfg["V"], cfg["K"], cfg["classes"]) / 1e9
+
+    if rank == 0:
+        out = {
+            "metric": "skeleton clips/sec (fwd+bwd), synthetic (N,3,300,18); 1/2/4/8-GPU scaling",
+            "value": round(clips, 2), "unit": "clips/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic (random N(0,1) skeletons, random labels)",
+            "config": {"workload": "cfg2 Kinetics-skeleton shape: 10-block ST-GCN stack "
+                                   "fwd+bwd+CE+Adam, V=18, T=300, K=1 (uni), 400 classes",
+                       "per_gpu_batch": cfg["N"], "global_batch": cfg["N"] * world,
+                       "seq_len": cfg["T"], "parallelism": f"dp{world}"},
+            "model_tflops": round(clips * gf_clip / 1e3, 2),
+            "loss": round(float(loss.item()), 5),
+        }
+        rl = kernel_roofline(pkg, device)
+        if rl:
+            name = max(rl, key=lambda k: rl[k][0])
+            ms_k, fl = rl[name]
+            ach = fl / (ms_k * 1e-3) / 1e12
+            out["roofline"] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2),
+                               "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                               "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                               "avg_launch_ms": round(ms_k, 4),
+                               "all_kernels_ms": {k: round(v[0], 4) for k, v in rl.items()}}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,116 @@
+/*
+ * stgcn_hip.h — C-ABI of libstgcn_hip.so, the MI355X (gfx950) ST-GCN block.
+ *
+ * This is the drop-in boundary for ONE hot path of nagyrajmund/st-gcn: the
+ * non-residual ST-GCN block in training (and eval) mode,
+ *
+ *   y = ReLU(BN2(Conv9x1(SpatialConv(BN1(x)))))      (dropout_rate == 0)
+ *
+ * i.e. SpatialTemporalConv.forward (src/network/st_graphconv.py:97-109) with
+ * SpatialConv.forward (st_graphconv.py:139-152) and its autograd backward.
+ * The reference has no FFI of its own (pure Python over PyTorch); the entry
+ * points below are what its module boundary binds to (the ctypes binding in
+ * st-gcn_amd/hip_lib.py, shown in INTEGRATION.md):
+ *
+ *   stgcn_block_fwd  replaces SpatialTemporalConv.forward, st_graphconv.py:85-109
+ *                    (BatchNorm2d :34/:98, SpatialConv :139-152, temporalConv
+ *                    :41-43/:99, BatchNorm2d :46/:100, ReLU :49/:105)
+ *   stgcn_block_bwd  replaces the autograd backward of the same ops
+ *                    (driven by lightning_model.py:199-205 -> loss.backward())
+ *
+ * Conventions
+ *   - All tensors are caller-owned, contiguous, fp32, device memory, layout
+ *     NCTV (N clips, C channels, T frames, V joints) as in the reference.
+ *   - A is (K,V,V), W is (K*C_out, C_in) (the reference's 1x1 Conv2d weight),
+ *     Wt is (C_out, C_out, 9) (the (9,1) Conv2d weight).
+ *   - The workspace is caller-allocated (query *_workspace_bytes first); the
+ *     library allocates nothing on the hot path and keeps no mutable global
+ *     state besides the thread-local error string.
+ *   - Every launch goes on the caller's stream (a hipStream_t passed as void*).
+ *   - Return 0 on success, a negative STGCN_E* code otherwise; the message is
+ *     in stgcn_last_error() (thread-local).
+ */
+#ifndef STGCN_HIP_H
+#define STGCN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STGCN_ABI_VERSION 1
+
+enum {
+  STGCN_OK = 0,
+  STGCN_E_INVALID = -1,     /* bad pointer / shape / parameter            */
+  STGCN_E_UNSUPPORTED = -2, /* residual, dropout, V > 256, gamma != 9 ... */
+  STGCN_E_HIP = -3          /* a HIP launch / runtime error               */
+};
+
+/* Block descriptor (one SpatialTemporalConv, st_graphconv.py:9). */
+typedef struct stgcn_desc {
+  int32_t N, C_in, C_out, T, T_out, V, K;
+  int32_t gamma;       /* temporal kernel size: 9 (lightning_model.py:263)   */
+  int32_t stride;      /* temporal stride 1 or 2                             */
+  int32_t pad;         /* temporal padding (gamma-1)/2 = 4                   */
+  float eps;           /* BatchNorm eps 1e-5                                 */
+  float momentum;      /* BatchNorm momentum 0.1                             */
+  int32_t training;    /* 1: batch statistics + running-stat update          */
+  int32_t need_dx;     /* backward: write dx (0 for the network's first block)*/
+  int32_t flags;       /* must be 0 (residual / dropout: STGCN_E_UNSUPPORTED) */
+} stgcn_desc_t;
+
+/* Forward arguments. Saved tensors (Z, U, stats) are kept by the caller for
+ * stgcn_block_bwd. stats holds mean1[C_in], invstd1[C_in], mean2[C_out],
+ * invstd2[C_out] (fp32) as used by the forward. */
+typedef struct stgcn_fwd_args {
+  const float *x;                       /* N,C_in,T,V                         */
+  const float *A, *W, *bW, *Wt, *bWt;   /* SpatialConv.A / W ; temporalConv   */
+  const float *g1, *b1, *g2, *b2;       /* batch_n / batch_n_2 affine         */
+  float *rm1, *rv1, *rm2, *rv2;         /* running stats (updated if training)*/
+  float *y;                             /* out: N,C_out,T_out,V               */
+  float *Z;                             /* saved: spatial output N,C_out,T,V  */
+  float *U;                             /* saved: temporal output N,C_out,T_out,V */
+  float *stats;                         /* saved: 2*C_in + 2*C_out floats     */
+} stgcn_fwd_args_t;
+
+/* Backward arguments: the gradients of every input of the forward. */
+typedef struct stgcn_bwd_args {
+  const float *dy;                      /* N,C_out,T_out,V                    */
+  const float *x, *Z, *U, *stats;       /* saved by the forward               */
+  const float *A, *W, *bW, *Wt, *g1, *b1, *g2, *b2;
+  float *dx;                            /* N,C_in,T,V (ignored if !need_dx)   */
+  float *dA, *dW, *dbW, *dWt, *dbWt;
+  float *dg1, *db1, *dg2, *db2;
+} stgcn_bwd_args_t;
+
+int stgcn_abi_version(void);
+const char *stgcn_last_error(void);
+
+/* Validate a descriptor without touching the GPU (0 = supported). */
+int stgcn_check_desc(const stgcn_desc_t *d);
+
+size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d);
+size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d);
+
+int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
+                    void *workspace, size_t workspace_bytes, void *stream);
+int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a,
+                    void *workspace, size_t workspace_bytes, void *stream);
+
+/* Measurement (bench.py roofline): time one of the block's GEMM kernels,
+ * launched `iters` times with the exact parameters the block uses for this
+ * descriptor, between two hipEvents on `stream`. which: 0 temporal conv fwd,
+ * 1 temporal conv data-grad, 2 temporal conv weight-grad, 3 spatial channel
+ * GEMM. scratch (>= stgcn_time_kernel_bytes) supplies operand memory.
+ * *flops receives the algorithmic FLOPs of one launch. */
+size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which);
+int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t scratch_bytes,
+                      int iters, void *stream, float *avg_ms, double *flops);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STGCN_HIP_H */

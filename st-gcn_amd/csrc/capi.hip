@@ -1,0 +1,575 @@
+// C-ABI entry points of libstgcn_hip.so (declared in include/stgcn_hip.h).
+//
+// stgcn_block_fwd / stgcn_block_bwd enqueue the kernel sequence of one
+// non-residual ST-GCN block on the caller's stream. The reference op order
+// (st_graphconv.py:97-109, :148-150) is
+//     BN1 -> Y = W x + b -> Z = sum_k Y_k A_k^T -> Conv9x1 -> BN2 -> ReLU;
+// here the joint contraction is applied on the narrower (input-channel) side,
+//     Z = sum_k W_k (BN1(x) A_k^T) + (sum_k b_k rowsum(A_k))          (1)
+// which is the same linear map (exact in real arithmetic) and never
+// materialises the K*C_out-channel Y.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/stgcn_hip.h"
+#include "internal.h"
+
+using namespace stgcn;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(STGCN_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Frames per conv tile: as many whole frames as fit 256 columns.
+int conv_ft(int V) { return std::max(1, kTileCols / V); }
+// Frames per wgrad work item: as many whole frames as fit 128 columns.
+int wgrad_ft(int V) { return std::max(1, 128 / V); }
+
+int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }
+int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
+
+struct Carve {
+  char *base;
+  size_t off = 0;
+  explicit Carve(void *b) : base((char *)b) {}
+  template <class T>
+  T *take(size_t count) {
+    T *p = base ? (T *)(base + off) : nullptr;
+    off += align_up(count * sizeof(T));
+    return p;
+  }
+};
+
+int wgrad_splits(int tiles, int items) {
+  int S = (2048 + tiles - 1) / tiles;
+  return std::max(1, std::min(S, items));
+}
+
+WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R, int Mframes,
+                       const float *Q, int64_t qb, int C, int T_src, int NQ, int s_in, int off,
+                       float *slab) {
+  WgradParams w{};
+  w.P = P;
+  w.Q = Q;
+  w.slab = slab;
+  w.p_bstride = pb;
+  w.q_bstride = qb;
+  w.R = R;
+  w.C = C;
+  w.NQ = NQ;
+  w.s_in = s_in;
+  w.off = off;
+  w.M = Mframes;
+  w.T_src = T_src;
+  w.V = d->V;
+  w.FT = wgrad_ft(d->V);
+  w.n_mtiles = (Mframes + w.FT - 1) / w.FT;
+  w.n_rtiles = (R + 63) / 64;
+  w.n_jtiles = (C * NQ + 63) / 64;
+  w.N = d->N;
+  w.S = wgrad_splits(w.n_rtiles * w.n_jtiles, d->N * w.n_mtiles);
+  return w;
+}
+
+struct BwdLayout {
+  double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
+  float *dU, *dZ, *G, *H, *slab;
+  size_t dbl_bytes, total;
+};
+
+BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
+  Carve c(ws);
+  BwdLayout L{};
+  const int R = d->C_out, C = d->C_in, K = d->K;
+  L.sg = c.take<double>(R);
+  L.sgu = c.take<double>(R);
+  L.sdu = c.take<double>(R);
+  L.sd = c.take<double>(C);
+  L.sdn = c.take<double>(C);
+  L.SdZ = c.take<double>((size_t)R * d->V);
+  L.dbl_bytes = c.off;
+  L.dU = c.take<float>((size_t)d->N * R * nTo(d));
+  L.dZ = c.take<float>((size_t)d->N * R * nT(d));
+  L.G = c.take<float>((size_t)d->N * K * C * nT(d));
+  L.H = c.take<float>((size_t)d->N * K * C * nT(d));
+  WgradParams w1 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, R, d->T, 9, d->stride,
+                              -d->pad, nullptr);
+  WgradParams w2 =
+      make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
+  const size_t s1 = (size_t)w1.S * R * R * 9, s2 = (size_t)w2.S * R * K * C;
+  L.slab = c.take<float>(std::max(s1, s2));
+  L.total = c.off;
+  return L;
+}
+
+struct FwdLayout {
+  double *s1, *q1, *s2, *q2;
+  float *G, *Wpk, *biasZ;
+  size_t dbl_bytes, total;
+};
+
+FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
+  Carve c(ws);
+  FwdLayout L{};
+  const int R = d->C_out, C = d->C_in, K = d->K;
+  L.s1 = c.take<double>(C);
+  L.q1 = c.take<double>(C);
+  L.s2 = c.take<double>(R);
+  L.q2 = c.take<double>(R);
+  L.dbl_bytes = c.off;
+  L.G = c.take<float>((size_t)d->N * K * C * nT(d));
+  L.Wpk = c.take<float>((size_t)R * K * C);
+  L.biasZ = c.take<float>((size_t)R * d->V);
+  L.total = c.off;
+  return L;
+}
+
+ConvGemmParams conv_base(const stgcn_desc_t *d) {
+  ConvGemmParams p{};
+  p.V = d->V;
+  p.FT = conv_ft(d->V);
+  p.N = d->N;
+  return p;
+}
+
+void conv_tiles(ConvGemmParams &p) {
+  p.n_mtiles = (p.M + p.FT - 1) / p.FT;
+  p.n_rtiles = (p.R + kTileRows - 1) / kTileRows;
+}
+
+}  // namespace
+
+extern "C" {
+
+int stgcn_abi_version(void) { return STGCN_ABI_VERSION; }
+
+const char *stgcn_last_error(void) { return g_err.c_str(); }
+
+int stgcn_check_desc(const stgcn_desc_t *d) {
+  if (!d) return fail(STGCN_E_INVALID, "null descriptor");
+  if (d->N <= 0 || d->C_in <= 0 || d->C_out <= 0 || d->T <= 0 || d->V <= 0 || d->K <= 0)
+    return fail(STGCN_E_INVALID, "non-positive dimension");
+  if (d->flags != 0)
+    return fail(STGCN_E_UNSUPPORTED, "residual / dropout variants are not implemented");
+  if (d->gamma != 9 || d->pad != 4)
+    return fail(STGCN_E_UNSUPPORTED, "only gamma=9, pad=4 (the reference default)");
+  if (d->stride != 1 && d->stride != 2) return fail(STGCN_E_UNSUPPORTED, "stride must be 1 or 2");
+  if (d->T_out != (d->T + 2 * d->pad - d->gamma) / d->stride + 1)
+    return fail(STGCN_E_INVALID, "T_out inconsistent with T, stride, pad");
+  if (d->V > kTileCols) return fail(STGCN_E_UNSUPPORTED, "V > 256");
+  if (d->K * d->V * d->V > 8192) return fail(STGCN_E_UNSUPPORTED, "K*V*V > 8192");
+  if ((int64_t)d->N * d->K * d->C_in * d->T * d->V > INT32_MAX ||
+      (int64_t)d->N * d->C_out * d->T * d->V > INT32_MAX)
+    return fail(STGCN_E_UNSUPPORTED, "tensor too large for 32-bit element indexing");
+  return STGCN_OK;
+}
+
+size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d) {
+  if (stgcn_check_desc(d) != STGCN_OK) return 0;
+  return fwd_layout(d, nullptr).total;
+}
+
+size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d) {
+  if (stgcn_check_desc(d) != STGCN_OK) return 0;
+  return bwd_layout(d, nullptr).total;
+}
+
+int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *workspace,
+                    size_t workspace_bytes, void *stream) {
+  int rc = stgcn_check_desc(d);
+  if (rc) return rc;
+  if (!a || !a->x || !a->A || !a->W || !a->bW || !a->Wt || !a->bWt || !a->g1 || !a->b1 ||
+      !a->g2 || !a->b2 || !a->y || !a->Z || !a->U || !a->stats)
+    return fail(STGCN_E_INVALID, "null tensor argument");
+  if (!a->rm1 || !a->rv1 || !a->rm2 || !a->rv2)
+    return fail(STGCN_E_INVALID, "null running-stat buffer");
+  const FwdLayout L = fwd_layout(d, workspace);
+  if (!workspace || workspace_bytes < L.total)
+    return fail(STGCN_E_INVALID, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V, K = d->K;
+  float *mean1 = a->stats, *invstd1 = a->stats + C;
+  float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
+
+  HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
+  // BN1 statistics of the block input (st_graphconv.py:98)
+  if (d->training) HIP_TRY(launch_bn_stats(a->x, N, C, T * V, L.s1, L.q1, s));
+  HIP_TRY(launch_bn_finalize(L.s1, L.q1, C, (int64_t)N * T * V, d->eps, d->momentum,
+                             d->training, a->rm1, a->rv1, mean1, invstd1, s));
+  // Spatial graph conv (st_graphconv.py:139-152) in the form (1).
+  HIP_TRY(launch_bias_rv(a->A, a->bW, L.biasZ, K, R, V, s));
+  const float *Wz = a->W;
+  if (K > 1) {
+    HIP_TRY(launch_pack_w(a->W, L.Wpk, K, R, C, s));
+    Wz = L.Wpk;
+  }
+  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, s));
+  {
+    ConvGemmParams p = conv_base(d);
+    p.in = L.G;
+    p.w = Wz;
+    p.out = a->Z;
+    p.bias_rv = L.biasZ;
+    p.in_bstride = (int64_t)K * C * T * V;
+    p.out_bstride = (int64_t)R * T * V;
+    p.w_sr = (int64_t)K * C;
+    p.w_sc = 1;
+    p.w_sq = 0;
+    p.C = K * C;
+    p.R = R;
+    p.NQ = 1;
+    p.s_in = 1;
+    p.off = 0;
+    p.s_out = 1;
+    p.p_out = 0;
+    p.M = T;
+    p.T_src = T;
+    p.T_dst = T;
+    conv_tiles(p);
+    HIP_TRY(launch_conv_gemm(p, s));
+  }
+  // Temporal (9,1) conv, stride (s,1), pad (4,0), bias (st_graphconv.py:41-43,99),
+  // with the BN2 batch statistics accumulated in the epilogue.
+  {
+    ConvGemmParams p = conv_base(d);
+    p.in = a->Z;
+    p.w = a->Wt;
+    p.out = a->U;
+    p.bias_r = a->bWt;
+    if (d->training) {
+      p.stat_sum = L.s2;
+      p.stat_sq = L.q2;
+    }
+    p.in_bstride = (int64_t)R * T * V;
+    p.out_bstride = (int64_t)R * To * V;
+    p.w_sr = (int64_t)R * 9;
+    p.w_sc = 9;
+    p.w_sq = 1;
+    p.C = R;
+    p.R = R;
+    p.NQ = 9;
+    p.s_in = d->stride;
+    p.off = -d->pad;
+    p.s_out = 1;
+    p.p_out = 0;
+    p.M = To;
+    p.T_src = T;
+    p.T_dst = To;
+    conv_tiles(p);
+    HIP_TRY(launch_conv_gemm(p, s));
+  }
+  // BN2 (st_graphconv.py:100) + ReLU (:105)
+  HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * To * V, d->eps, d->momentum,
+                             d->training, a->rm2, a->rv2, mean2, invstd2, s));
+  HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, s));
+  return STGCN_OK;
+}
+
+int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *workspace,
+                    size_t workspace_bytes, void *stream) {
+  int rc = stgcn_check_desc(d);
+  if (rc) return rc;
+  if (!a || !a->dy || !a->x || !a->Z || !a->U || !a->stats || !a->A || !a->W || !a->bW ||
+      !a->Wt || !a->g1 || !a->b1 || !a->g2 || !a->b2 || !a->dA || !a->dW || !a->dbW || !a->dWt ||
+      !a->dbWt || !a->dg1 || !a->db1 || !a->dg2 || !a->db2 || (d->need_dx && !a->dx))
+    return fail(STGCN_E_INVALID, "null tensor argument");
+  const BwdLayout L = bwd_layout(d, workspace);
+  if (!workspace || workspace_bytes < L.total)
+    return fail(STGCN_E_INVALID, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V, K = d->K;
+  const float *mean1 = a->stats, *invstd1 = a->stats + C;
+  const float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
+
+  HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
+  // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias)
+  HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
+                                    L.sg, L.sgu, s));
+  if (d->training) {
+    HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, L.sg, L.sgu,
+                                     L.dU, L.sdu, N, R, To * V, s));
+  } else {
+    return fail(STGCN_E_UNSUPPORTED, "backward in eval mode is not implemented");
+  }
+  HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
+
+  // Temporal conv data-gradient: dZ = conv^T(dU)
+  {
+    ConvGemmParams p = conv_base(d);
+    p.in = L.dU;
+    p.out = L.dZ;
+    p.in_bstride = (int64_t)R * To * V;
+    p.out_bstride = (int64_t)R * T * V;
+    p.w_sr = 9;
+    p.w_sc = (int64_t)R * 9;
+    p.C = R;
+    p.R = R;
+    p.T_src = To;
+    p.T_dst = T;
+    p.s_in = 1;
+    if (d->stride == 1) {
+      p.w = a->Wt + 8;
+      p.w_sq = -1;
+      p.NQ = 9;
+      p.off = -4;
+      p.s_out = 1;
+      p.p_out = 0;
+      p.M = T;
+      conv_tiles(p);
+      HIP_TRY(launch_conv_gemm(p, s));
+    } else {
+      for (int ph = 0; ph < 2; ++ph) {
+        p.w = a->Wt + (ph == 0 ? 8 : 7);
+        p.w_sq = -2;
+        p.NQ = ph == 0 ? 5 : 4;
+        p.off = ph == 0 ? -2 : -1;
+        p.s_out = 2;
+        p.p_out = ph;
+        p.M = ph == 0 ? (T + 1) / 2 : T / 2;
+        if (p.M <= 0) continue;
+        conv_tiles(p);
+        HIP_TRY(launch_conv_gemm(p, s));
+      }
+    }
+  }
+  // Temporal conv weight-gradient: dWt[co][ci][q] = sum dU[co] * Z[ci](shifted)
+  {
+    WgradParams w = make_wgrad(d, L.dU, (int64_t)R * To * V, R, To, a->Z, (int64_t)R * T * V, R,
+                               T, 9, d->stride, -d->pad, L.slab);
+    HIP_TRY(launch_wgrad(w, s));
+    HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * R * 9, a->dWt, 0, R, 1, R, s));
+  }
+  // Spatial conv backward. Recompute G = BN1(x) A^T, then
+  //   dW' = dZ G^T (split-K), H_k = W_k^T dZ, dxhat = sum_k H_k A_k,
+  //   dA = sum H_k^T BN1(x) + bias part, dbW = sum dZ rowsum(A_k).
+  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, s));
+  {
+    WgradParams w = make_wgrad(d, L.dZ, (int64_t)R * T * V, R, T, L.G, (int64_t)K * C * T * V,
+                               K * C, T, 1, 1, 0, L.slab);
+    HIP_TRY(launch_wgrad(w, s));
+    HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));
+  }
+  HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s));
+  HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
+  for (int k = 0; k < K; ++k) {
+    ConvGemmParams p = conv_base(d);
+    p.in = L.dZ;
+    p.w = a->W + (int64_t)k * R * C;
+    p.out = L.H + (int64_t)k * C * T * V;
+    p.in_bstride = (int64_t)R * T * V;
+    p.out_bstride = (int64_t)K * C * T * V;
+    p.w_sr = 1;
+    p.w_sc = C;
+    p.w_sq = 0;
+    p.C = R;
+    p.R = C;
+    p.NQ = 1;
+    p.s_in = 1;
+    p.off = 0;
+    p.s_out = 1;
+    p.p_out = 0;
+    p.M = T;
+    p.T_src = T;
+    p.T_dst = T;
+    conv_tiles(p);
+    HIP_TRY(launch_conv_gemm(p, s));
+  }
+  HIP_TRY(launch_spatial_dx(L.H, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
+                            L.sdn, N, C, T, V, K, d->need_dx, s));
+  HIP_TRY(launch_bn_grads_out(L.sd, L.sdn, nullptr, C, a->dg1, a->db1, nullptr, s));
+  if (d->need_dx)
+    HIP_TRY(launch_bn1_bwd_apply(a->dx, a->x, mean1, invstd1, a->g1, L.sd, L.sdn, N, C, T * V,
+                                 (int64_t)N * T * V, s));
+  return STGCN_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Measurement entry points (bench.py roofline): run ONE of the block's GEMM
+// kernels `iters` times on the caller's stream between two hipEvents, with the
+// exact launch parameters stgcn_block_fwd / _bwd use for this descriptor.
+//   which 0: temporal (9,1) conv forward      (k_conv_gemm<9>)
+//         1: temporal conv data-gradient      (k_conv_gemm<9> or <5>+<4>)
+//         2: temporal conv weight-gradient    (k_wgrad<9>, slab reduce excluded)
+//         3: spatial channel GEMM Z = W' G    (k_conv_gemm<1>)
+// flops = the algorithmic FLOPs of one launch (SURVEY.md §8d terms).
+// ---------------------------------------------------------------------------
+namespace {
+struct TimedPlan {
+  ConvGemmParams cp[2];
+  int ncp = 0;
+  WgradParams wp{};
+  bool wgrad = false;
+  size_t bytes = 0;
+  double flops = 0;
+};
+
+TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
+  TimedPlan P;
+  Carve c(scratch);
+  const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V, K = d->K;
+  const double tflops = 2.0 * 9 * R * (double)R * To * V * N;
+  if (which == 0) {
+    ConvGemmParams p = conv_base(d);
+    p.in = c.take<float>((size_t)N * R * T * V);
+    p.w = c.take<float>((size_t)R * R * 9);
+    p.out = c.take<float>((size_t)N * R * To * V);
+    p.bias_r = c.take<float>(R);
+    p.stat_sum = c.take<double>(R);
+    p.stat_sq = c.take<double>(R);
+    p.in_bstride = (int64_t)R * T * V;
+    p.out_bstride = (int64_t)R * To * V;
+    p.w_sr = (int64_t)R * 9;
+    p.w_sc = 9;
+    p.w_sq = 1;
+    p.C = R;
+    p.R = R;
+    p.NQ = 9;
+    p.s_in = d->stride;
+    p.off = -d->pad;
+    p.s_out = 1;
+    p.p_out = 0;
+    p.M = To;
+    p.T_src = T;
+    p.T_dst = To;
+    conv_tiles(p);
+    P.cp[P.ncp++] = p;
+    P.flops = tflops;
+  } else if (which == 1) {
+    ConvGemmParams p = conv_base(d);
+    p.in = c.take<float>((size_t)N * R * To * V);
+    const float *w = c.take<float>((size_t)R * R * 9);
+    p.out = c.take<float>((size_t)N * R * T * V);
+    p.in_bstride = (int64_t)R * To * V;
+    p.out_bstride = (int64_t)R * T * V;
+    p.w_sr = 9;
+    p.w_sc = (int64_t)R * 9;
+    p.C = R;
+    p.R = R;
+    p.T_src = To;
+    p.T_dst = T;
+    p.s_in = 1;
+    if (d->stride == 1) {
+      p.w = w ? w + 8 : nullptr;
+      p.w_sq = -1;
+      p.NQ = 9;
+      p.off = -4;
+      p.s_out = 1;
+      p.p_out = 0;
+      p.M = T;
+      conv_tiles(p);
+      P.cp[P.ncp++] = p;
+    } else {
+      for (int ph = 0; ph < 2; ++ph) {
+        p.w = w ? w + (ph == 0 ? 8 : 7) : nullptr;
+        p.w_sq = -2;
+        p.NQ = ph == 0 ? 5 : 4;
+        p.off = ph == 0 ? -2 : -1;
+        p.s_out = 2;
+        p.p_out = ph;
+        p.M = ph == 0 ? (T + 1) / 2 : T / 2;
+        conv_tiles(p);
+        if (p.M > 0) P.cp[P.ncp++] = p;
+      }
+    }
+    P.flops = tflops;
+  } else if (which == 2) {
+    const float *dU = c.take<float>((size_t)N * R * To * V);
+    const float *Z = c.take<float>((size_t)N * R * T * V);
+    WgradParams w = make_wgrad(d, dU, (int64_t)R * To * V, R, To, Z, (int64_t)R * T * V, R, T, 9,
+                               d->stride, -d->pad, nullptr);
+    w.slab = c.take<float>((size_t)w.S * R * R * 9);
+    P.wp = w;
+    P.wgrad = true;
+    P.flops = tflops;
+  } else {
+    ConvGemmParams p = conv_base(d);
+    p.in = c.take<float>((size_t)N * K * C * T * V);
+    p.w = c.take<float>((size_t)R * K * C);
+    p.out = c.take<float>((size_t)N * R * T * V);
+    p.bias_rv = c.take<float>((size_t)R * V);
+    p.in_bstride = (int64_t)K * C * T * V;
+    p.out_bstride = (int64_t)R * T * V;
+    p.w_sr = (int64_t)K * C;
+    p.w_sc = 1;
+    p.w_sq = 0;
+    p.C = K * C;
+    p.R = R;
+    p.NQ = 1;
+    p.s_in = 1;
+    p.off = 0;
+    p.s_out = 1;
+    p.p_out = 0;
+    p.M = T;
+    p.T_src = T;
+    p.T_dst = T;
+    conv_tiles(p);
+    P.cp[P.ncp++] = p;
+    P.flops = 2.0 * K * C * (double)R * T * V * N;
+  }
+  P.bytes = c.off;
+  return P;
+}
+}  // namespace
+
+extern "C" {
+
+size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which) {
+  if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 3) return 0;
+  return plan_timed(d, which, nullptr).bytes;
+}
+
+int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t scratch_bytes,
+                      int iters, void *stream, float *avg_ms, double *flops) {
+  int rc = stgcn_check_desc(d);
+  if (rc) return rc;
+  if (which < 0 || which > 3 || iters <= 0 || !avg_ms || !flops)
+    return fail(STGCN_E_INVALID, "bad timing request");
+  TimedPlan P = plan_timed(d, which, scratch);
+  if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
+  hipStream_t s = (hipStream_t)stream;
+  auto launch = [&]() -> hipError_t {
+    if (P.wgrad) return launch_wgrad(P.wp, s);
+    for (int i = 0; i < P.ncp; ++i) {
+      hipError_t e = launch_conv_gemm(P.cp[i], s);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
+  HIP_TRY(launch());  // warm-up
+  hipEvent_t e0, e1;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) HIP_TRY(launch());
+  HIP_TRY(hipEventRecord(e1, s));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *avg_ms = ms / iters;
+  *flops = P.flops;
+  return STGCN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,98 @@
+// Internal kernel-launch interface of libstgcn_hip.so (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace stgcn {
+
+constexpr int kTileRows = 64;   // output rows per workgroup (2 MFMA 32-row tiles)
+constexpr int kTileCols = 256;  // max (frames x V) columns per workgroup (8 MFMA 32-col tiles)
+
+// Generic temporal-conv-shaped GEMM on MFMA (v_mfma_f32_32x32x2_f32):
+//   out[n, r, s_out*m + p_out, v] = bias_r[r] + bias_rv[r, v]
+//        + sum_{c<C} sum_{q<NQ} w[r*w_sr + c*w_sc + q*w_sq] * in[n, c, s_in*m + q + off, v]
+// with in[] zero outside [0, T_src). Covers: the spatial W GEMM (NQ=1), the
+// (9,1) temporal conv forward (NQ=9), its data-gradient (flipped taps; stride-2
+// split into two phases, NQ=5/4) and the spatial H = W^T dZ GEMM (NQ=1).
+struct ConvGemmParams {
+  const float *in, *w;
+  float *out;
+  const float *bias_r;   // [R] or null
+  const float *bias_rv;  // [R][V] or null
+  double *stat_sum, *stat_sq;  // [R] per-row sum / sum of squares, or null
+  int64_t in_bstride, out_bstride;  // elements per clip
+  int64_t w_sr, w_sc, w_sq;
+  int C, R, NQ;
+  int s_in, off, s_out, p_out;
+  int M;      // logical output frames
+  int T_src;  // input frames
+  int T_dst;  // output physical frames
+  int V, FT;  // joints; frames per tile (FT*V <= kTileCols)
+  int n_mtiles, n_rtiles, N;
+};
+
+// Weight-gradient GEMM with split-K partial slabs:
+//   slab[split, r, c*NQ + q] = sum_{(n, m-tile) in split} sum_{m, v}
+//        P[n, r, m, v] * Q[n, c, s_in*m + q + off, v]
+struct WgradParams {
+  const float *P, *Q;
+  float *slab;
+  int64_t p_bstride, q_bstride;
+  int R, C, NQ, s_in, off;
+  int M;      // frames of P
+  int T_src;  // frames of Q
+  int V, FT;
+  int n_mtiles, n_rtiles, n_jtiles, S, N;
+};
+
+hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
+hipError_t launch_wgrad(const WgradParams &p, hipStream_t s);
+size_t conv_gemm_lds_bytes(const ConvGemmParams &p);
+size_t wgrad_lds_bytes(const WgradParams &p);
+
+// Reduction of split-K slabs: dst = sum_s slab[s]. mode 0: identity layout;
+// mode 1: slab is [R][K*C] (packed W'), dst is the (K*R, C) Conv2d weight.
+hipError_t launch_slab_reduce(const float *slab, int S, int64_t n, float *dst, int mode,
+                              int R, int K, int C, hipStream_t s);
+
+// BatchNorm helpers (fp64 accumulation of per-channel sums).
+hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, double *sq,
+                           hipStream_t s);
+hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M,
+                              float eps, float momentum, int training, float *rm, float *rv,
+                              float *mean_out, float *invstd_out, hipStream_t s);
+hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
+                              const float *g, const float *b, float *y, int N, int C, int L,
+                              hipStream_t s);
+hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
+                                     const float *invstd, const float *g, const float *b,
+                                     int N, int C, int L, double *sg, double *sgu,
+                                     hipStream_t s);
+hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
+                                    const float *invstd, const float *g, const float *b,
+                                    const double *sg, const double *sgu, float *dU,
+                                    double *sdu, int N, int C, int L, hipStream_t s);
+hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
+                               float *dgamma, float *dbeta, float *dbias, hipStream_t s);
+hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean,
+                                const float *invstd, const float *g, const double *sd,
+                                const double *sdn, int N, int C, int L, int64_t M,
+                                hipStream_t s);
+
+// Spatial (graph) helpers.
+hipError_t launch_pack_w(const float *W, float *Wpk, int K, int R, int C, hipStream_t s);
+hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K, int R, int V,
+                          hipStream_t s);
+hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
+                             const float *g, const float *b, const float *A, float *G, int N,
+                             int C, int T, int V, int K, hipStream_t s);
+hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out,
+                         hipStream_t s);
+hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K,
+                                int R, int V, float *dbW, float *dA, hipStream_t s);
+hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
+                             const float *invstd, const float *g, const float *b,
+                             const float *A, float *dx, float *dA, double *sd, double *sdn,
+                             int N, int C, int T, int V, int K, int write_dx, hipStream_t s);
+
+}  // namespace stgcn

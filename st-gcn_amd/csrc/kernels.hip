@@ -1,0 +1,819 @@
+// Device code of libstgcn_hip.so — gfx950 (MI355X / CDNA4) only.
+//
+// GEMM-shaped work (the spatial 1x1 channel contraction, the (9,1) temporal
+// convolution forward / data-grad / weight-grad) runs on the exact-fp32 matrix
+// cores (v_mfma_f32_32x32x2_f32: one fmaf chain per output, no reduced
+// precision). The joint-axis (V) contractions with the dense adjacency A run
+// on the VALU from LDS (A pinned in LDS per workgroup). BatchNorm statistics
+// accumulate in fp64.
+//
+// Wave size is 64; every block is a multiple of 64 threads.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+
+namespace stgcn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sumf(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block (NT threads) reduction of two doubles, then one fp64 atomic each.
+// `red` must hold 2*NT/64 doubles of LDS.
+template <int NT>
+__device__ __forceinline__ void block_sum2_atomic(double a, double b, double *dst_a,
+                                                  double *dst_b, double *red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[w] = a;
+    red[NT / 64 + w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sa = 0.0, sb = 0.0;
+    for (int i = 0; i < NT / 64; ++i) {
+      sa += red[i];
+      sb += red[NT / 64 + i];
+    }
+    atomicAdd(dst_a, sa);
+    if (dst_b) atomicAdd(dst_b, sb);
+  }
+  __syncthreads();
+}
+
+// XCD-aware bijective remap: hardware deals consecutive block ids round-robin
+// over the 8 XCDs; give each XCD a contiguous chunk of the logical grid so
+// workgroups that share input tiles share an L2 (speed only, never correctness).
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8;
+  const int xcd = bid % 8, loc = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// ---------------------------------------------------------------------------
+// conv_gemm: see ConvGemmParams. Workgroup = 256 threads (4 waves), tile =
+// 64 rows x (FT frames * V) columns (<= 256, padded to 8 MFMA column tiles).
+// Wave w owns rows (w&1)*32..+31 and column tiles (w>>1)*4..+3: 4 accumulators
+// of 32x32 fp32 (64 VGPRs). The reduction runs over input-channel chunks of CK
+// staged in LDS together with their (frames+halo) window; each staged channel
+// window is reused by all NQ taps (the halo shift is a per-lane LDS offset).
+// ---------------------------------------------------------------------------
+template <int NQ, int CK>
+__global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hi = lane >> 5, lo = lane & 31;
+  const int nblk = gridDim.x;
+  int bid = xcd_remap(blockIdx.x, nblk);
+  const int rt = bid % p.n_rtiles;
+  bid /= p.n_rtiles;
+  const int mt = bid % p.n_mtiles;
+  const int n = bid / p.n_mtiles;
+  const int r0 = rt * kTileRows, m0 = mt * p.FT;
+  const int V = p.V;
+  const int span = (p.s_in * (p.FT - 1) + NQ) * V;
+  const int SP = span | 1;  // odd pitch
+  float *Ws = smem;                 // [CK][NQ][64]
+  float *Is = smem + CK * NQ * 64;  // [CK][SP]
+  const int f0 = p.s_in * m0 + p.off;
+  const int64_t cstride = (int64_t)p.T_src * V;
+  const float *inN = p.in + (int64_t)n * p.in_bstride;
+  const int ncols = p.FT * V;
+
+  const int mi = wave & 1;
+  const int nj0 = (wave >> 1) * 4;
+  int bbase[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    if (col < ncols) {
+      const int mf = col / V;
+      bbase[j] = p.s_in * mf * V + (col - mf * V);
+    } else {
+      bbase[j] = 0;  // padding column: read any staged value, result discarded
+    }
+  }
+  floatx16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+
+  for (int c0 = 0; c0 < p.C; c0 += CK) {
+    __syncthreads();
+    for (int e = tid; e < CK * NQ * 64; e += 256) {
+      const int r = e & 63, cq = e >> 6;
+      const int c = cq / NQ, q = cq - c * NQ;
+      float w = 0.f;
+      if (r0 + r < p.R && c0 + c < p.C)
+        w = p.w[(int64_t)(r0 + r) * p.w_sr + (int64_t)(c0 + c) * p.w_sc + (int64_t)q * p.w_sq];
+      Ws[cq * 64 + r] = w;
+    }
+    const int64_t g0 = (int64_t)f0 * V;
+#pragma unroll
+    for (int c = 0; c < CK; ++c) {
+      const bool cval = c0 + c < p.C;
+      const float *src = inN + (int64_t)(c0 + c) * cstride;
+      for (int o = tid; o < span; o += 256) {
+        const int64_t g = g0 + o;
+        float v = 0.f;
+        if (cval && g >= 0 && g < cstride) v = src[g];
+        Is[c * SP + o] = v;
+      }
+    }
+    __syncthreads();
+    const float *wp = Ws + hi * NQ * 64 + mi * 32 + lo;
+    const float *ip = Is + hi * SP;
+#pragma unroll 2
+    for (int cp = 0; cp < CK / 2; ++cp) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const float a = wp[(2 * cp * NQ + q) * 64];
+        const float *iq = ip + 2 * cp * SP + q * V;
+        const float b0 = iq[bbase[0]], b1 = iq[bbase[1]], b2 = iq[bbase[2]], b3 = iq[bbase[3]];
+        acc[0] = mfma32(a, b0, acc[0]);
+        acc[1] = mfma32(a, b1, acc[1]);
+        acc[2] = mfma32(a, b2, acc[2]);
+        acc[3] = mfma32(a, b3, acc[3]);
+      }
+    }
+  }
+
+  // Epilogue: bias, store, optional per-row BN statistics (fp64).
+  float *outN = p.out + (int64_t)n * p.out_bstride;
+  const int64_t ostride = (int64_t)p.T_dst * V;
+  int64_t ocol[4];
+  bool cok[4];
+  int cv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    const int mf = col / V;
+    const int v = col - mf * V;
+    const int m = m0 + mf;
+    cok[j] = col < ncols && m < p.M;
+    cv[j] = v;
+    ocol[j] = (int64_t)(p.s_out * m + p.p_out) * V + v;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+    const bool rok = row < p.R;
+    const float br = (rok && p.bias_r) ? p.bias_r[row] : 0.f;
+    double s = 0.0, sq = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (rok && cok[j]) {
+        float val = acc[j][i] + br;
+        if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
+        outN[row * ostride + ocol[j]] = val;
+        s += val;
+        sq += (double)val * val;
+      }
+    }
+    if (p.stat_sum) {
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        sq += __shfl_xor(sq, o, 64);
+      }
+      if (lo == 0 && rok) {
+        atomicAdd(p.stat_sum + row, s);
+        atomicAdd(p.stat_sq + row, sq);
+      }
+    }
+  }
+}
+
+size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
+  const int CK = p.NQ == 1 ? 32 : 8;
+  const int span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
+  return sizeof(float) * ((size_t)CK * p.NQ * 64 + (size_t)CK * (span | 1));
+}
+
+hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s) {
+  const int nblk = p.N * p.n_mtiles * p.n_rtiles;
+  const size_t lds = conv_gemm_lds_bytes(p);
+  switch (p.NQ) {
+    case 1:
+      hipLaunchKernelGGL((k_conv_gemm<1, 32>), dim3(nblk), dim3(256), lds, s, p);
+      break;
+    case 4:
+      hipLaunchKernelGGL((k_conv_gemm<4, 8>), dim3(nblk), dim3(256), lds, s, p);
+      break;
+    case 5:
+      hipLaunchKernelGGL((k_conv_gemm<5, 8>), dim3(nblk), dim3(256), lds, s, p);
+      break;
+    case 9:
+      hipLaunchKernelGGL((k_conv_gemm<9, 8>), dim3(nblk), dim3(256), lds, s, p);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// wgrad: see WgradParams. Workgroup = 256 threads, output tile 64 rows (r) x
+// 64 columns (j = c*NQ + q); every wave holds the whole 64x64 tile (2x2 MFMA
+// tiles) and takes every 4th pair of reduction columns; the 4 partial tiles
+// are summed through LDS at the end and written to this split's slab.
+// ---------------------------------------------------------------------------
+template <int NQ>
+__global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hi = lane >> 5, lo = lane & 31;
+  const int nblk = gridDim.x;
+  int bid = xcd_remap(blockIdx.x, nblk);
+  const int split = bid % p.S;
+  bid /= p.S;
+  const int jt = bid % p.n_jtiles;
+  const int rt = bid / p.n_jtiles;
+  const int r0 = rt * 64, j0 = jt * 64;
+  const int J = p.C * NQ;
+  const int V = p.V;
+  const int ncols = p.FT * V;
+  const int PP = ((ncols + 1) | 1) + 0;  // odd pitch >= ncols+1
+  const int c_lo = j0 / NQ;
+  int c_hi = (j0 + 63) / NQ + 1;
+  if (c_hi > p.C) c_hi = p.C;
+  const int nc = c_hi - c_lo;
+  const int span = (p.s_in * (p.FT - 1) + NQ) * V;
+  const int QP = span | 1;
+  float *Ps = smem;            // [64][PP]
+  float *Qs = smem + 64 * PP;  // [nc+1][QP]  (row nc = zeros)
+
+  int qoff[2];
+#pragma unroll
+  for (int nj = 0; nj < 2; ++nj) {
+    const int j = j0 + nj * 32 + lo;
+    if (j < J) {
+      const int c = j / NQ, q = j - c * NQ;
+      qoff[nj] = (c - c_lo) * QP + q * V;
+    } else {
+      qoff[nj] = nc * QP;  // zero row
+    }
+  }
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+
+  const int total = p.N * p.n_mtiles;
+  const int per = (total + p.S - 1) / p.S;
+  const int it0 = split * per;
+  int it1 = it0 + per;
+  if (it1 > total) it1 = total;
+  const int nk = (ncols + 1) / 2;
+  const int64_t pcs = (int64_t)p.M * V;      // P channel stride
+  const int64_t qcs = (int64_t)p.T_src * V;  // Q channel stride
+
+  // zero row of Qs (never overwritten)
+  for (int o = tid; o < QP; o += 256) Qs[nc * QP + o] = 0.f;
+
+  for (int it = it0; it < it1; ++it) {
+    const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
+    const int m0 = mt * p.FT;
+    __syncthreads();
+    // stage P rows (zero-padded columns up to PP)
+    const float *Pn = p.P + (int64_t)n * p.p_bstride;
+    const int64_t pg0 = (int64_t)m0 * V;
+    for (int r = 0; r < 64; ++r) {
+      const bool rok = r0 + r < p.R;
+      const float *src = Pn + (int64_t)(r0 + r) * pcs;
+      for (int o = tid; o < PP; o += 256) {
+        float v = 0.f;
+        if (rok && o < ncols && pg0 + o < pcs) v = src[pg0 + o];
+        Ps[r * PP + o] = v;
+      }
+    }
+    const float *Qn = p.Q + (int64_t)n * p.q_bstride;
+    const int64_t qg0 = (int64_t)(p.s_in * m0 + p.off) * V;
+    for (int c = 0; c < nc; ++c) {
+      const float *src = Qn + (int64_t)(c_lo + c) * qcs;
+      for (int o = tid; o < span; o += 256) {
+        const int64_t g = qg0 + o;
+        float v = 0.f;
+        if (g >= 0 && g < qcs) v = src[g];
+        Qs[c * QP + o] = v;
+      }
+    }
+    __syncthreads();
+    int col = 2 * wave + hi;
+    int mf = col / V;
+    int v = col - mf * V;
+    const float *pa0 = Ps + lo * PP;
+    const float *pa1 = Ps + (32 + lo) * PP;
+    for (int kk = wave; kk < nk; kk += 4) {
+      const float a0 = pa0[col], a1 = pa1[col];
+      const int bq = (mf < p.FT) ? p.s_in * mf * V + v : 0;
+      const float b0 = Qs[qoff[0] + bq], b1 = Qs[qoff[1] + bq];
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+      col += 8;
+      v += 8;
+      while (v >= V) {
+        v -= V;
+        ++mf;
+      }
+    }
+  }
+  // cross-wave reduction: waves 1..3 park their tiles in LDS, wave 0 sums.
+  __syncthreads();
+  float *red = smem;  // [3][64*64]
+  if (wave > 0) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = a * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int colj = b * 32 + lo;
+          red[(wave - 1) * 4096 + row * 64 + colj] = acc[a][b][i];
+        }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    float *dst = p.slab + (int64_t)split * p.R * J;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = a * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int colj = b * 32 + lo;
+          float s = acc[a][b][i] + red[row * 64 + colj] + red[4096 + row * 64 + colj] +
+                    red[8192 + row * 64 + colj];
+          if (r0 + row < p.R && j0 + colj < J) dst[(int64_t)(r0 + row) * J + j0 + colj] = s;
+        }
+  }
+}
+
+size_t wgrad_lds_bytes(const WgradParams &p) {
+  const int ncols = p.FT * p.V;
+  const int PP = ((ncols + 1) | 1);
+  const int c_span = 64 / p.NQ + 2;
+  const int nc = c_span < p.C ? c_span : p.C;
+  const int span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
+  size_t b = sizeof(float) * ((size_t)64 * PP + (size_t)(nc + 1) * (span | 1));
+  const size_t red = sizeof(float) * 3 * 4096;
+  return b > red ? b : red;
+}
+
+hipError_t launch_wgrad(const WgradParams &p, hipStream_t s) {
+  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  const size_t lds = wgrad_lds_bytes(p);
+  switch (p.NQ) {
+    case 1:
+      hipLaunchKernelGGL((k_wgrad<1>), dim3(nblk), dim3(256), lds, s, p);
+      break;
+    case 9:
+      hipLaunchKernelGGL((k_wgrad<9>), dim3(nblk), dim3(256), lds, s, p);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+__global__ void k_slab_reduce(const float *slab, int S, int64_t n, float *dst, int mode, int R,
+                              int K, int C) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  double s = 0.0;
+  for (int k = 0; k < S; ++k) s += slab[(int64_t)k * n + idx];
+  int64_t d = idx;
+  if (mode == 1) {  // idx = co*(K*C) + k*C + ci  ->  (k*R + co)*C + ci
+    const int64_t KC = (int64_t)K * C;
+    const int64_t co = idx / KC, rem = idx - co * KC;
+    const int64_t k = rem / C, ci = rem - k * C;
+    d = (k * R + co) * C + ci;
+  }
+  dst[d] = (float)s;
+}
+
+hipError_t launch_slab_reduce(const float *slab, int S, int64_t n, float *dst, int mode, int R,
+                              int K, int C, hipStream_t s) {
+  const int nb = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(k_slab_reduce, dim3(nb), dim3(256), 0, s, slab, S, n, dst, mode, R, K, C);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm kernels. One 256-thread block per (n, c) slice of L = T*V floats.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_bn_stats(const float *x, int C, int L, double *sum,
+                                                  double *sq) {
+  __shared__ double red[8];
+  const int c = blockIdx.x, n = blockIdx.y;
+  const float *src = x + ((int64_t)n * C + c) * L;
+  double s = 0.0, q = 0.0;
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const double v = src[i];
+    s += v;
+    q += v * v;
+  }
+  block_sum2_atomic<256>(s, q, sum + c, sq + c, red);
+}
+
+hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, double *sq,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_stats, dim3(C, N), dim3(256), 0, s, x, C, L, sum, sq);
+  return hipGetLastError();
+}
+
+__global__ void k_bn_finalize(const double *sum, const double *sq, int C, int64_t M, float eps,
+                              float momentum, int training, float *rm, float *rv, float *mean_out,
+                              float *invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  if (training) {
+    const double mean = sum[c] / (double)M;
+    double var = sq[c] / (double)M - mean * mean;
+    if (var < 0.0) var = 0.0;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rm) {
+      const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mean);
+      rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * unb);
+    }
+  } else {
+    mean_out[c] = rm[c];
+    invstd_out[c] = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+  }
+}
+
+hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M, float eps,
+                              float momentum, int training, float *rm, float *rv,
+                              float *mean_out, float *invstd_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, sum, sq, C, M, eps,
+                     momentum, training, rm, rv, mean_out, invstd_out);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
+                                                     const float *invstd, const float *g,
+                                                     const float *b, float *y, int C, int L) {
+  const int c = blockIdx.x, n = blockIdx.y;
+  const int64_t base = ((int64_t)n * C + c) * L;
+  const float mu = mean[c], a = invstd[c] * g[c], be = b[c];
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const float v = (U[base + i] - mu) * a + be;
+    y[base + i] = v > 0.f ? v : 0.f;
+  }
+}
+
+hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
+                              const float *g, const float *b, float *y, int N, int C, int L,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_relu_fwd, dim3(C, N), dim3(256), 0, s, U, mean, invstd, g, b, y, C, L);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, const float *U,
+                                                            const float *mean,
+                                                            const float *invstd, const float *g,
+                                                            const float *b, int C, int L,
+                                                            double *sg, double *sgu) {
+  __shared__ double red[8];
+  const int c = blockIdx.x, n = blockIdx.y;
+  const int64_t base = ((int64_t)n * C + c) * L;
+  const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
+  double s = 0.0, q = 0.0;
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const float u = U[base + i];
+    const float yv = (u - mu) * a + be;
+    if (yv > 0.f) {
+      const float gg = dy[base + i];
+      s += gg;
+      q += (double)gg * (double)((u - mu) * is);
+    }
+  }
+  block_sum2_atomic<256>(s, q, sg + c, sgu + c, red);
+}
+
+hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
+                                     const float *invstd, const float *g, const float *b, int N,
+                                     int C, int L, double *sg, double *sgu, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_relu_bwd_reduce, dim3(C, N), dim3(256), 0, s, dy, U, mean, invstd, g, b,
+                     C, L, sg, sgu);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
+    const float *dy, const float *U, const float *mean, const float *invstd, const float *g,
+    const float *b, const double *sg, const double *sgu, float *dU, double *sdu, int C, int L,
+    double invM) {
+  __shared__ double red[8];
+  const int c = blockIdx.x, n = blockIdx.y;
+  const int64_t base = ((int64_t)n * C + c) * L;
+  const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
+  const float mg = (float)(sg[c] * invM), mgu = (float)(sgu[c] * invM);
+  double s = 0.0;
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const float u = U[base + i];
+    const float uh = (u - mu) * is;
+    const float yv = (u - mu) * a + be;
+    const float gg = yv > 0.f ? dy[base + i] : 0.f;
+    const float d = a * (gg - mg - uh * mgu);
+    dU[base + i] = d;
+    s += d;
+  }
+  block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
+}
+
+hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
+                                    const float *invstd, const float *g, const float *b,
+                                    const double *sg, const double *sgu, float *dU, double *sdu,
+                                    int N, int C, int L, hipStream_t s) {
+  const double invM = 1.0 / ((double)N * L);
+  hipLaunchKernelGGL(k_bn_relu_bwd_apply, dim3(C, N), dim3(256), 0, s, dy, U, mean, invstd, g, b,
+                     sg, sgu, dU, sdu, C, L, invM);
+  return hipGetLastError();
+}
+
+__global__ void k_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
+                               float *dgamma, float *dbeta, float *dbias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  dgamma[c] = (float)sgu[c];
+  dbeta[c] = (float)sg[c];
+  if (dbias) dbias[c] = (float)sdu[c];
+}
+
+hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
+                               float *dgamma, float *dbeta, float *dbias, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_grads_out, dim3((C + 255) / 256), dim3(256), 0, s, sg, sgu, sdu, C,
+                     dgamma, dbeta, dbias);
+  return hipGetLastError();
+}
+
+// dx = g*invstd * (dxhat - sum(dxhat)/M - xnorm * sum(dxhat*xnorm)/M), in place.
+__global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x,
+                                                       const float *mean, const float *invstd,
+                                                       const float *g, const double *sd,
+                                                       const double *sdn, int C, int L,
+                                                       double invM) {
+  const int c = blockIdx.x, n = blockIdx.y;
+  const int64_t base = ((int64_t)n * C + c) * L;
+  const float mu = mean[c], is = invstd[c], a = is * g[c];
+  const float md = (float)(sd[c] * invM), mdn = (float)(sdn[c] * invM);
+  for (int i = threadIdx.x; i < L; i += 256) {
+    const float xn = (x[base + i] - mu) * is;
+    dx[base + i] = a * (dx[base + i] - md - xn * mdn);
+  }
+}
+
+hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean, const float *invstd,
+                                const float *g, const double *sd, const double *sdn, int N, int C,
+                                int L, int64_t M, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn1_bwd_apply, dim3(C, N), dim3(256), 0, s, dx, x, mean, invstd, g, sd,
+                     sdn, C, L, 1.0 / (double)M);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Spatial (graph) kernels.
+// ---------------------------------------------------------------------------
+__global__ void k_pack_w(const float *W, float *Wpk, int K, int R, int C) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // co*(K*C) + k*C + ci
+  const int KC = K * C;
+  if (idx >= R * KC) return;
+  const int co = idx / KC, rem = idx - co * KC, k = rem / C, ci = rem - k * C;
+  Wpk[idx] = W[((int64_t)k * R + co) * C + ci];
+}
+
+hipError_t launch_pack_w(const float *W, float *Wpk, int K, int R, int C, hipStream_t s) {
+  const int n = R * K * C;
+  hipLaunchKernelGGL(k_pack_w, dim3((n + 255) / 256), dim3(256), 0, s, W, Wpk, K, R, C);
+  return hipGetLastError();
+}
+
+// bias_rv[co][v] = sum_k bW[k*R+co] * sum_w A[k][v][w]   (the 1x1-conv bias
+// pushed through the joint contraction: st_graphconv.py:148-150)
+__global__ void k_bias_rv(const float *A, const float *bW, float *bias_rv, int K, int R, int V) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= R * V) return;
+  const int co = idx / V, v = idx - co * V;
+  double s = 0.0;
+  for (int k = 0; k < K; ++k) {
+    double ra = 0.0;
+    for (int w = 0; w < V; ++w) ra += A[((int64_t)k * V + v) * V + w];
+    s += (double)bW[k * R + co] * ra;
+  }
+  bias_rv[idx] = (float)s;
+}
+
+hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K, int R, int V,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_bias_rv, dim3((R * V + 255) / 256), dim3(256), 0, s, A, bW, bias_rv, K, R,
+                     V);
+  return hipGetLastError();
+}
+
+constexpr int kGatherTC = 32;  // frames per gather block
+
+// G[n][k*C+ci][t][v] = sum_w A[k][v][w] * BN1(x)[n][ci][t][w]
+// One block per (n, frame chunk); A pinned in LDS; loop over channels.
+__global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float *mean,
+                                                    const float *invstd, const float *g,
+                                                    const float *b, const float *A, float *G,
+                                                    int C, int T, int V, int K) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *As = smem;                 // [K][V][V]
+  float *xs = smem + K * V * V;     // [TC][V]
+  const int n = blockIdx.y, t0 = blockIdx.x * kGatherTC;
+  int tc = T - t0;
+  if (tc > kGatherTC) tc = kGatherTC;
+  for (int i = threadIdx.x; i < K * V * V; i += 256) As[i] = A[i];
+  const int L = T * V;
+  const int nout = K * tc * V;
+  for (int ci = 0; ci < C; ++ci) {
+    __syncthreads();
+    const float *src = x + ((int64_t)n * C + ci) * L + (int64_t)t0 * V;
+    const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
+    for (int i = threadIdx.x; i < tc * V; i += 256) xs[i] = (src[i] - mu) * a + be;
+    __syncthreads();
+    for (int o = threadIdx.x; o < nout; o += 256) {
+      const int k = o / (tc * V);
+      const int rem = o - k * tc * V;
+      const int t = rem / V, v = rem - t * V;
+      const float *ar = As + (k * V + v) * V;
+      const float *xr = xs + t * V;
+      float s = 0.f;
+      for (int w = 0; w < V; ++w) s = fmaf(ar[w], xr[w], s);
+      G[(((int64_t)n * K + k) * C + ci) * L + (int64_t)(t0 + t) * V + v] = s;
+    }
+  }
+}
+
+hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
+                             const float *g, const float *b, const float *A, float *G, int N,
+                             int C, int T, int V, int K, hipStream_t s) {
+  const size_t lds = sizeof(float) * ((size_t)K * V * V + kGatherTC * V);
+  hipLaunchKernelGGL(k_gather_fwd, dim3((T + kGatherTC - 1) / kGatherTC, N), dim3(256), lds, s, x,
+                     mean, invstd, g, b, A, G, C, T, V, K);
+  return hipGetLastError();
+}
+
+// out[c][v] += sum_t X[n][c][t][v]   (fp64), one block per (c, n)
+__global__ __launch_bounds__(256) void k_sum_nt(const float *X, int C, int T, int V,
+                                                double *out) {
+  __shared__ double part[256];
+  const int c = blockIdx.x, n = blockIdx.y;
+  const float *src = X + ((int64_t)n * C + c) * T * V;
+  const int tpb = 256 / V;  // frame lanes per joint
+  const int tid = threadIdx.x;
+  double s = 0.0;
+  if (tid < tpb * V) {
+    const int v = tid % V, tt = tid / V;
+    for (int t = tt; t < T; t += tpb) s += src[t * V + v];
+  }
+  part[tid] = s;
+  __syncthreads();
+  if (tid < V) {
+    double acc = 0.0;
+    for (int tt = 0; tt < tpb; ++tt) acc += part[tt * V + tid];
+    atomicAdd(out + c * V + tid, acc);
+  }
+}
+
+hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out, hipStream_t s) {
+  hipLaunchKernelGGL(k_sum_nt, dim3(C, N), dim3(256), 0, s, X, C, T, V, out);
+  return hipGetLastError();
+}
+
+// dbW[k*R+co] = sum_v SdZ[co][v] * rowsum(A_k)[v]
+// dA[k][v][w]  = sum_co bW[k*R+co] * SdZ[co][v]      (bias part of dA; all w)
+__global__ void k_spatial_small(const double *SdZ, const float *A, const float *bW, int K, int R,
+                                int V, float *dbW, float *dA) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < K * R) {
+    const int k = idx / R, co = idx - k * R;
+    double s = 0.0;
+    for (int v = 0; v < V; ++v) {
+      double ra = 0.0;
+      for (int w = 0; w < V; ++w) ra += A[((int64_t)k * V + v) * V + w];
+      s += SdZ[co * V + v] * ra;
+    }
+    dbW[idx] = (float)s;
+  }
+  if (idx < K * V) {
+    const int k = idx / V, v = idx - k * V;
+    double s = 0.0;
+    for (int co = 0; co < R; ++co) s += (double)bW[k * R + co] * SdZ[co * V + v];
+    for (int w = 0; w < V; ++w) dA[((int64_t)k * V + v) * V + w] = (float)s;
+  }
+}
+
+hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K, int R,
+                                int V, float *dbW, float *dA, hipStream_t s) {
+  const int n = K * R > K * V ? K * R : K * V;
+  hipLaunchKernelGGL(k_spatial_small, dim3((n + 255) / 256), dim3(256), 0, s, SdZ, A, bW, K, R, V,
+                     dbW, dA);
+  return hipGetLastError();
+}
+
+constexpr int kDxTC = 16;  // frames per spatial-dx block
+
+// Per (n, frame chunk), looping over input channels ci:
+//   dxhat[t][w] = sum_k sum_v H[k*C+ci][t][v] * A[k][v][w]     (-> dx buffer)
+//   dA[k][v][w] += sum_t H[k*C+ci][t][v] * BN1(x)[ci][t][w]     (LDS accumulator)
+//   sd[ci] += sum dxhat, sdn[ci] += sum dxhat * xnorm          (BN1 backward)
+__global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float *x,
+                                                    const float *mean, const float *invstd,
+                                                    const float *g, const float *b,
+                                                    const float *A, float *dx, float *dA,
+                                                    double *sd, double *sdn, int C, int T, int V,
+                                                    int K, int write_dx) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double red[8];
+  const int KVV = K * V * V;
+  float *As = smem;             // [K][V][V]
+  float *dAs = As + KVV;        // [K][V][V] block-local dA
+  float *xb = dAs + KVV;        // [TC][V] BN1 output
+  float *Hs = xb + kDxTC * V;   // [K][TC][V]
+  const int n = blockIdx.y, t0 = blockIdx.x * kDxTC;
+  int tc = T - t0;
+  if (tc > kDxTC) tc = kDxTC;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < KVV; i += 256) {
+    As[i] = A[i];
+    dAs[i] = 0.f;
+  }
+  const int L = T * V;
+  for (int ci = 0; ci < C; ++ci) {
+    __syncthreads();
+    const int64_t xo = ((int64_t)n * C + ci) * L + (int64_t)t0 * V;
+    const float mu = mean[ci], is = invstd[ci], a = is * g[ci], be = b[ci];
+    for (int i = tid; i < tc * V; i += 256) xb[i] = (x[xo + i] - mu) * a + be;
+    for (int i = tid; i < K * tc * V; i += 256) {
+      const int k = i / (tc * V), rem = i - k * tc * V;
+      Hs[k * kDxTC * V + rem] = H[(((int64_t)n * K + k) * C + ci) * L + (int64_t)t0 * V + rem];
+    }
+    __syncthreads();
+    // dxhat and BN1 partial sums
+    double s = 0.0, sn = 0.0;
+    for (int o = tid; o < tc * V; o += 256) {
+      const int t = o / V, w = o - t * V;
+      float acc = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float *hr = Hs + (k * kDxTC + t) * V;
+        const float *ac = As + k * V * V + w;
+        for (int v = 0; v < V; ++v) acc = fmaf(hr[v], ac[v * V], acc);
+      }
+      const float xn = (x[xo + o] - mu) * is;
+      if (write_dx) dx[xo + o] = acc;
+      s += acc;
+      sn += (double)acc * xn;
+    }
+    // dA partials: each thread owns entries e = tid + 256*j
+    for (int e = tid; e < KVV; e += 256) {
+      const int k = e / (V * V), rem = e - k * V * V;
+      const int v = rem / V, w = rem - v * V;
+      float acc = dAs[e];
+      for (int t = 0; t < tc; ++t) acc = fmaf(Hs[(k * kDxTC + t) * V + v], xb[t * V + w], acc);
+      dAs[e] = acc;
+    }
+    block_sum2_atomic<256>(s, sn, sd + ci, sdn + ci, red);
+  }
+  for (int e = tid; e < KVV; e += 256) atomicAdd(dA + e, dAs[e]);
+}
+
+hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
+                             const float *invstd, const float *g, const float *b, const float *A,
+                             float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
+                             int V, int K, int write_dx, hipStream_t s) {
+  if (K * V * V > 8192) return hipErrorInvalidValue;
+  const size_t lds = sizeof(float) * (2 * (size_t)K * V * V + kDxTC * V + (size_t)K * kDxTC * V);
+  hipLaunchKernelGGL(k_spatial_dx, dim3((T + kDxTC - 1) / kDxTC, N), dim3(256), lds, s, H, x,
+                     mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, V, K, write_dx);
+  return hipGetLastError();
+}
+
+}  // namespace stgcn

@@ -1,0 +1,91 @@
+"""``StgcnBlockFn`` — the fused ST-GCN block as a torch.autograd.Function.
+
+Forward and backward are single calls into libstgcn_hip.so
+(``stgcn_block_fwd`` / ``stgcn_block_bwd``) on the current HIP stream. The
+math is that of ``SpatialTemporalConv.forward`` (non-residual, no dropout,
+src/network/st_graphconv.py:97-109 with SpatialConv :139-152) and of its
+autograd backward (driven by lightning_model.py:199-205).
+"""
+import ctypes
+
+import torch
+
+from . import hip_lib
+
+
+def _f32c(t, name):
+    if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+        raise RuntimeError(f"{name}: expected a contiguous float32 GPU tensor")
+    return t
+
+
+def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1, gamma=9):
+    N, C_in, T, V = x_shape
+    T_out = (T + 2 * pad - gamma) // stride + 1
+    return hip_lib.Desc(N, C_in, C_out, T, T_out, V, K, gamma, stride, pad, eps, momentum,
+                        int(training), int(need_dx), 0)
+
+
+class StgcnBlockFn(torch.autograd.Function):
+    """forward(x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
+               stride, pad, eps, momentum, training) -> y
+
+    Running stats (rm*, rv*) are updated in place when ``training``.
+    Backward returns dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2.
+    """
+
+    @staticmethod
+    def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
+                stride, pad, eps, momentum, training):
+        lib = hip_lib.lib()
+        x = x.contiguous()
+        names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
+                 "rm1", "rv1", "rm2", "rv2")
+        tensors = (x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2)
+        for t, n in zip(tensors, names):
+            _f32c(t, n)
+        N, C_in, T, V = x.shape
+        K = A.shape[0]
+        C_out = Wt.shape[0]
+        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training)
+        hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
+        dev = x.device
+        y = torch.empty((N, C_out, desc.T_out, V), device=dev, dtype=torch.float32)
+        Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
+        U = torch.empty_like(y)
+        stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
+        nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
+        ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
+            x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats)])
+        hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
+                                          hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
+        ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2)
+        ctx.cfg = (stride, pad, eps, momentum, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = hip_lib.lib()
+        x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2 = ctx.saved_tensors
+        stride, pad, eps, momentum, training = ctx.cfg
+        need_dx = bool(ctx.needs_input_grad[0])
+        dy = dy.contiguous()
+        C_out = Wt.shape[0]
+        desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
+                         need_dx=need_dx)
+        dx = torch.empty_like(x) if need_dx else None
+        grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
+        dbWt = torch.empty(C_out, device=x.device, dtype=torch.float32)
+        dg1, db1, dg2, db2 = (torch.empty_like(t) for t in (g1, b1, g2, b2))
+        nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
+        ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+        args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
+            dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
+            grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2)])
+        hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
+                                          hip_lib.ptr(ws), nbytes,
+                                          hip_lib.stream_handle(x.device)))
+        dA, dW, dbW, dWt = grads
+        return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
+                None, None, None, None, None, None, None, None, None)

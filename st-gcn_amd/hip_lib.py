@@ -1,0 +1,108 @@
+"""ctypes binding of libstgcn_hip.so (the C-ABI in include/stgcn_hip.h).
+
+The library is built in-tree (``st-gcn_amd/lib/libstgcn_hip.so``, see
+``build.py``). There is no fallback: if the library or a HIP device is
+missing, ``lib()`` raises.
+
+torch is imported first on purpose: torch ships its own HIP runtime
+(``libamdhip64.so``, SONAME ``libamdhip64.so.7``); loading it before the
+library makes the library bind to that same runtime, so the hipStream_t handed
+over from ``torch.cuda.current_stream()`` is valid inside the library.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libstgcn_hip.so")
+ABI_VERSION = 1
+
+_c_int = ctypes.c_int32
+_c_float = ctypes.c_float
+_vp = ctypes.c_void_p
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [("N", _c_int), ("C_in", _c_int), ("C_out", _c_int), ("T", _c_int),
+                ("T_out", _c_int), ("V", _c_int), ("K", _c_int), ("gamma", _c_int),
+                ("stride", _c_int), ("pad", _c_int), ("eps", _c_float),
+                ("momentum", _c_float), ("training", _c_int), ("need_dx", _c_int),
+                ("flags", _c_int)]
+
+
+class FwdArgs(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in (
+        "x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
+        "rm1", "rv1", "rm2", "rv2", "y", "Z", "U", "stats")]
+
+
+class BwdArgs(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in (
+        "dy", "x", "Z", "U", "stats", "A", "W", "bW", "Wt", "g1", "b1", "g2", "b2",
+        "dx", "dA", "dW", "dbW", "dWt", "dbWt", "dg1", "db1", "dg2", "db2")]
+
+
+# Every symbol include/stgcn_hip.h declares (checked by tests/test_capi.py).
+EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
+            "stgcn_fwd_workspace_bytes", "stgcn_bwd_workspace_bytes",
+            "stgcn_block_fwd", "stgcn_block_bwd", "stgcn_time_kernel_bytes",
+            "stgcn_time_kernel")
+
+_LIB = None
+
+
+def load_library(path=LIB_PATH):
+    """dlopen the library and declare prototypes (no GPU needed)."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"libstgcn_hip.so not found at {path}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    lib.stgcn_abi_version.restype = ctypes.c_int
+    lib.stgcn_last_error.restype = ctypes.c_char_p
+    lib.stgcn_check_desc.argtypes = [ctypes.POINTER(Desc)]
+    lib.stgcn_check_desc.restype = ctypes.c_int
+    for f in (lib.stgcn_fwd_workspace_bytes, lib.stgcn_bwd_workspace_bytes):
+        f.argtypes = [ctypes.POINTER(Desc)]
+        f.restype = ctypes.c_size_t
+    lib.stgcn_block_fwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(FwdArgs), _vp,
+                                    ctypes.c_size_t, _vp]
+    lib.stgcn_block_fwd.restype = ctypes.c_int
+    lib.stgcn_block_bwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(BwdArgs), _vp,
+                                    ctypes.c_size_t, _vp]
+    lib.stgcn_block_bwd.restype = ctypes.c_int
+    lib.stgcn_time_kernel_bytes.argtypes = [ctypes.POINTER(Desc), ctypes.c_int]
+    lib.stgcn_time_kernel_bytes.restype = ctypes.c_size_t
+    lib.stgcn_time_kernel.argtypes = [ctypes.POINTER(Desc), ctypes.c_int, _vp, ctypes.c_size_t,
+                                      ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_float),
+                                      ctypes.POINTER(ctypes.c_double)]
+    lib.stgcn_time_kernel.restype = ctypes.c_int
+    if lib.stgcn_abi_version() != ABI_VERSION:
+        raise RuntimeError("libstgcn_hip.so ABI version mismatch; rebuild it")
+    return lib
+
+
+def lib():
+    """The loaded library, for GPU use. Raises when it cannot run."""
+    global _LIB
+    if _LIB is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("stgcn HIP path requires a ROCm GPU (torch.cuda.is_available() "
+                               "is False); there is no CPU fallback")
+        _LIB = load_library()
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().stgcn_last_error().decode(errors="replace")
+        raise RuntimeError(f"libstgcn_hip error {rc}: {msg}")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,57 @@
+"""The ST-GCN stack as built by ``L_STGCN`` (src/lightning_model.py:35-112),
+on the drop-in blocks. Same child names and state_dict keys
+(``conv.{i}.*``, ``fc_layer.*``), same module construction order (so the same
+``torch.manual_seed`` yields the same initial parameters), same forward:
+NTVC -> permute -> 10 blocks -> avg_pool2d over (T, V) -> Linear.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .network import SpatialTemporalConv
+
+# (C_out, temporal stride) per block, lightning_model.py:65-86.
+LAYERS = [(64, 1), (64, 1), (64, 1), (64, 1), (128, 2), (128, 1), (128, 1),
+          (256, 2), (256, 1), (256, 1)]
+
+
+class STGCNStack(nn.Module):
+    def __init__(self, C_in, nr_classes, A, gamma=9, dropout_rate=0, residual=False):
+        super().__init__()
+        pad = (gamma - 1) // 2
+        self.K, self.V = A.shape[0], A.shape[1]
+        self.nr_classes = nr_classes
+        blocks, c = [], C_in
+        for co, s in LAYERS:
+            blocks.append(SpatialTemporalConv(c, co, A, gamma, s, pad,
+                                              dropout_rate=dropout_rate, residual=residual))
+            c = co
+        self.conv = nn.Sequential(*blocks).float()
+        self.fc_layer = nn.Linear(256, nr_classes).float()
+
+    def forward_nctv(self, x):
+        x = self.conv(x)
+        N = x.shape[0]
+        x = F.avg_pool2d(x, (x.shape[2], self.V))
+        x = x.view(N, x.shape[1])
+        return self.fc_layer(x)
+
+    def forward(self, x):
+        """x: (N, T, V, C_in) as in L_STGCN.forward (lightning_model.py:101)."""
+        return self.forward_nctv(x.permute(0, 3, 1, 2))
+
+
+def flops_per_clip(C_in, T, V, K, nr_classes, gamma=9):
+    """Algorithmic fwd+bwd FLOPs per clip:
+    per layer fwd = 2*C_in*K*C_out*T*V + 2*K*C_out*T*V^2 + 2*gamma*C_out^2*T_out*V;
+    bwd = dgrad (same three terms, minus the W term for layer 0) + wgrad (same
+    three terms); plus the head 3 * 2*256*classes."""
+    total, c, t = 0, C_in, T
+    for i, (co, s) in enumerate(LAYERS):
+        to = (t + 2 * ((gamma - 1) // 2) - gamma) // s + 1
+        w = 2 * c * K * co * t * V
+        a = 2 * K * co * t * V * V
+        tc = 2 * gamma * co * co * to * V
+        total += (w + a + tc) + ((0 if i == 0 else w) + a + tc) + (w + a + tc)
+        c, t = co, to
+    return total + 3 * 2 * 256 * nr_classes

@@ -1,0 +1,94 @@
+"""Drop-in module API of the reference's ``src/network/st_graphconv.py``.
+
+``SpatialTemporalConv`` and ``SpatialConv`` keep the reference's constructor
+signatures, child-module names and state_dict keys (st_graphconv.py:9-58,
+:116-136), so ``L_STGCN`` (lightning_model.py:65-86) / ``STGCN``
+(stgcn.py:40-51) build unchanged against them and checkpoints interchange.
+``forward`` runs the fused MI355X HIP block (``fused.StgcnBlockFn``).
+
+There is no CPU fallback: on a CPU tensor or without the HIP library the
+forward raises.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .fused import StgcnBlockFn
+
+
+class SpatialConv(nn.Module):
+    """Reference: st_graphconv.py:111-152. Holds the trainable adjacency A
+    (K, V, V) and the 1x1 conv W (C_in -> K*C_out). In this build the layer's
+    arithmetic runs inside the fused block (``SpatialTemporalConv``); a
+    standalone ``forward`` is not part of the accelerated path."""
+
+    def __init__(self, C_in, C_out, A):
+        super().__init__()
+        self.C_in = C_in
+        self.C_out = C_out
+        self.A = nn.Parameter(A.float())
+        self.K = self.A.shape[0]
+        self.V = self.A.shape[1]
+        self.W = nn.Conv2d(C_in, self.K * C_out, (1, 1))
+
+    def forward(self, f_in):
+        raise NotImplementedError(
+            "SpatialConv.forward on its own is not on the accelerated path; "
+            "use it through SpatialTemporalConv (the fused HIP block)")
+
+
+class SpatialTemporalConv(nn.Module):
+    """Reference: st_graphconv.py:4-109 (same arguments, children, state_dict).
+
+    Accelerated: the non-residual block, training and eval mode. Dropout
+    (p > 0, training) is applied after the fused block with torch's dropout.
+    The residual variant is not implemented on the HIP path yet and raises.
+    """
+
+    def __init__(self, C_in, C_out, A, gamma, temporal_stride, temporal_padding,
+                 dropout_rate=0.5, residual=False):
+        super().__init__()
+        if residual:
+            if C_in == C_out and temporal_stride == 1:
+                self.apply_residual = lambda x: x
+            else:
+                self.apply_residual = nn.Conv2d(C_in, C_out, kernel_size=1,
+                                                stride=(temporal_stride, 1))
+        self.residual = residual
+        self.batch_n = nn.BatchNorm2d(C_in)
+        self.spatialConv = SpatialConv(C_in, C_out, A)
+        self.temporalConv = nn.Conv2d(C_out, C_out, kernel_size=(gamma, 1),
+                                      stride=(temporal_stride, 1),
+                                      padding=(temporal_padding, 0))
+        self.batch_n_2 = nn.BatchNorm2d(C_out)
+        self.relu = nn.ReLU(inplace=True)
+        if dropout_rate != 0:
+            print('Using dropout')
+            self.dropout = nn.Dropout(dropout_rate, inplace=True)
+        else:
+            print('Not using dropout')
+            self.dropout = None
+        self.gamma = gamma
+        self.stride = temporal_stride
+        self.pad = temporal_padding
+
+    def forward(self, f_in):
+        if self.residual:
+            raise NotImplementedError("residual ST-GCN block is not implemented on the HIP path")
+        bn1, bn2 = self.batch_n, self.batch_n_2
+        if bn1.momentum is None or bn2.momentum is None:
+            raise NotImplementedError("BatchNorm momentum=None (cumulative average)")
+        training = self.training
+        if training:
+            bn1.num_batches_tracked.add_(1)
+            bn2.num_batches_tracked.add_(1)
+        sc = self.spatialConv
+        x = f_in.float()
+        y = StgcnBlockFn.apply(
+            x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
+            self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
+            bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
+            self.stride, self.pad, bn1.eps, bn1.momentum, training)
+        if self.dropout is None:
+            return y
+        return F.dropout(y, self.dropout.p, training=training)

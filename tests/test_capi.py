@@ -1,0 +1,74 @@
+"""The C-ABI library builds, loads and exports every symbol include/stgcn_hip.h
+declares; descriptor validation and workspace sizing work without a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "stgcn_hip.h")
+
+
+def _header_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\s*\*)\s*\*?\s*(stgcn_\w+)\s*\(",
+                                 text, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib(pkg):
+    return pkg.hip_lib.load_library()
+
+
+def test_header_declares_entry_points(pkg):
+    assert _header_functions() == sorted(pkg.hip_lib.EXPORTED)
+
+
+def test_library_exports_every_header_symbol(lib):
+    for name in _header_functions():
+        assert hasattr(lib, name), name
+    assert lib.stgcn_abi_version() == 1
+
+
+def _desc(pkg, **kw):
+    base = dict(N=128, C_in=64, C_out=64, T=300, T_out=300, V=18, K=1, gamma=9, stride=1,
+                pad=4, eps=1e-5, momentum=0.1, training=1, need_dx=1, flags=0)
+    base.update(kw)
+    return pkg.hip_lib.Desc(**base)
+
+
+def test_check_desc_accepts_north_star_shapes(pkg, lib):
+    for kw in (dict(), dict(C_in=3), dict(C_in=64, C_out=128, stride=2, T_out=150),
+               dict(V=25, K=3), dict(V=50, K=3, C_in=256, C_out=256, T=75, T_out=75)):
+        d = _desc(pkg, **kw)
+        assert lib.stgcn_check_desc(ctypes.byref(d)) == 0, kw
+        assert lib.stgcn_fwd_workspace_bytes(ctypes.byref(d)) > 0
+        assert lib.stgcn_bwd_workspace_bytes(ctypes.byref(d)) > 0
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(flags=1), -2), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
+    (dict(T_out=299), -1), (dict(N=0), -1), (dict(V=300), -2)])
+def test_check_desc_rejects(pkg, lib, kw, code):
+    d = _desc(pkg, **kw)
+    assert lib.stgcn_check_desc(ctypes.byref(d)) == code
+    assert lib.stgcn_last_error()
+    assert lib.stgcn_fwd_workspace_bytes(ctypes.byref(d)) == 0
+
+
+def test_null_arguments_fail_without_touching_gpu(pkg, lib):
+    d = _desc(pkg)
+    args = pkg.hip_lib.FwdArgs()
+    assert lib.stgcn_block_fwd(ctypes.byref(d), ctypes.byref(args), None, 0, None) == -1
+    assert b"null" in lib.stgcn_last_error()
+
+
+def test_cpu_tensors_fail_loudly(pkg):
+    """No CPU fallback on the product path."""
+    import torch
+    A = torch.ones(1, 18, 18)
+    blk = pkg.SpatialTemporalConv(3, 64, A, 9, 1, 4, dropout_rate=0)
+    with pytest.raises(RuntimeError):
+        blk(torch.randn(2, 3, 20, 18))
