@@ -70,10 +70,16 @@ def spatial_conv(x, A, W, bW):
 
 
 def block_forward(x, p, b, stride, pad=4, residual=False, training=True,
-                  momentum=0.1, eps=1e-5, dtype=torch.float32):
+                  momentum=0.1, eps=1e-5, dtype=torch.float32, relu_mask=None,
+                  return_pre_relu=False):
     """One SpatialTemporalConv step. ``p``: parameter tensors keyed by the
     reference's state_dict names (BLOCK_PARAM_NAMES [+ apply_residual.*]);
-    ``b``: running buffers (updated in place when ``training``)."""
+    ``b``: running buffers (updated in place when ``training``).
+
+    ``relu_mask`` (optional, 0/1 tensor shaped like the output): use this
+    mask for the final ReLU instead of ``f > 0`` — used by the parity tests to
+    differentiate through the SAME subgradient choice as the implementation
+    under test at ReLU ties (|pre-ReLU| below fp32 resolution)."""
     x = x.to(dtype)
     A = p["spatialConv.A"]
     if residual:
@@ -96,6 +102,10 @@ def block_forward(x, p, b, stride, pad=4, residual=False, training=True,
         f = F.conv2d(f, p["temporalConv.weight"], p["temporalConv.bias"],
                      stride=(stride, 1), padding=(pad, 0))
         f = _bn(f, p, b, "batch_n_2", training, momentum, eps)
+    if return_pre_relu:
+        return f
+    if relu_mask is not None:
+        return f * relu_mask.to(f.dtype)
     return F.relu(f.clone())
 
 
@@ -114,7 +124,7 @@ def block_params_from_arrays(arrays, prefix="param.", dtype=torch.float32, requi
     return p, b
 
 
-def block_step(arrays, dtype=torch.float64):
+def block_step(arrays, dtype=torch.float64, relu_mask=None):
     """Run fwd+bwd of one block fixture on the oracle; returns a dict with
     the same keys the fixture stores (y, grad.*, after.*)."""
     meta = arrays["meta"]
@@ -122,7 +132,7 @@ def block_step(arrays, dtype=torch.float64):
     p, b = block_params_from_arrays(arrays, dtype=dtype)
     x = torch.as_tensor(arrays["x"]).to(dtype).requires_grad_(True)
     g = torch.as_tensor(arrays["g"]).to(dtype)
-    y = block_forward(x, p, b, stride, residual=residual, dtype=dtype)
+    y = block_forward(x, p, b, stride, residual=residual, dtype=dtype, relu_mask=relu_mask)
     (y * g).sum().backward()
     out = {"y": y.detach(), "grad.x": x.grad}
     for k, t in p.items():
@@ -130,6 +140,15 @@ def block_step(arrays, dtype=torch.float64):
     for k, t in b.items():
         out["after." + k] = t
     return out
+
+
+def block_pre_relu(arrays, dtype=torch.float64):
+    """Pre-ReLU output (BN2 output) of a block fixture, no grad."""
+    meta = arrays["meta"]
+    p, b = block_params_from_arrays(arrays, dtype=dtype, requires_grad=False)
+    with torch.no_grad():
+        return block_forward(torch.as_tensor(arrays["x"]), p, b, int(meta[2]),
+                             residual=bool(meta[7]), dtype=dtype, return_pre_relu=True)
 
 
 class Stack:

@@ -40,8 +40,15 @@ size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Frames per conv tile: as many whole frames as fit 256 columns.
 int conv_ft(int V) { return std::max(1, kTileCols / V); }
-// Frames per wgrad work item: as many whole frames as fit 128 columns.
-int wgrad_ft(int V) { return std::max(1, 128 / V); }
+// Frames per wgrad work item: as many whole frames as fit 80 columns.
+int wgrad_ft(int V) { return std::max(1, 80 / V); }
+
+// Upper bound of the packed-weight scratch any conv_gemm launch of this block needs.
+size_t wpk_floats(const stgcn_desc_t *d) {
+  const int rows = std::max(d->C_out, d->C_in);
+  const int red = std::max(d->C_out, d->K * d->C_in);
+  return (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32) * 9;
+}
 
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }
 int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
@@ -59,7 +66,7 @@ struct Carve {
 };
 
 int wgrad_splits(int tiles, int items) {
-  int S = (2048 + tiles - 1) / tiles;
+  int S = (512 + tiles - 1) / tiles;
   return std::max(1, std::min(S, items));
 }
 
@@ -81,9 +88,10 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   w.T_src = T_src;
   w.V = d->V;
   w.FT = wgrad_ft(d->V);
+  while (w.FT > 1 && wgrad_lds_bytes(w) > 80 * 1024) --w.FT;  // 2 workgroups per CU
   w.n_mtiles = (Mframes + w.FT - 1) / w.FT;
   w.n_rtiles = (R + 63) / 64;
-  w.n_jtiles = (C * NQ + 63) / 64;
+  w.n_jtiles = wgrad_ntiles_j(C, NQ);
   w.N = d->N;
   w.S = wgrad_splits(w.n_rtiles * w.n_jtiles, d->N * w.n_mtiles);
   return w;
@@ -91,7 +99,7 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
 
 struct BwdLayout {
   double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
-  float *dU, *dZ, *G, *H, *slab;
+  float *dU, *dZ, *G, *H, *slab, *wpk;
   size_t dbl_bytes, total;
 };
 
@@ -116,13 +124,14 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
       make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
   const size_t s1 = (size_t)w1.S * R * R * 9, s2 = (size_t)w2.S * R * K * C;
   L.slab = c.take<float>(std::max(s1, s2));
+  L.wpk = c.take<float>(wpk_floats(d));
   L.total = c.off;
   return L;
 }
 
 struct FwdLayout {
   double *s1, *q1, *s2, *q2;
-  float *G, *Wpk, *biasZ;
+  float *G, *Wpk, *biasZ, *wpk;
   size_t dbl_bytes, total;
 };
 
@@ -138,12 +147,14 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
   L.G = c.take<float>((size_t)d->N * K * C * nT(d));
   L.Wpk = c.take<float>((size_t)R * K * C);
   L.biasZ = c.take<float>((size_t)R * d->V);
+  L.wpk = c.take<float>(wpk_floats(d));
   L.total = c.off;
   return L;
 }
 
-ConvGemmParams conv_base(const stgcn_desc_t *d) {
+ConvGemmParams conv_base(const stgcn_desc_t *d, float *wpk) {
   ConvGemmParams p{};
+  p.wpk = wpk;
   p.V = d->V;
   p.FT = conv_ft(d->V);
   p.N = d->N;
@@ -157,11 +168,31 @@ void conv_tiles(ConvGemmParams &p) {
 
 }  // namespace
 
+// Every GEMM launch of the block fits its LDS budget.
+static bool geometry_supported(const stgcn_desc_t *d) {
+  const int R = d->C_out, C = d->C_in, K = d->K;
+  WgradParams w1 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, R, d->T, 9, d->stride,
+                              -d->pad, nullptr);
+  WgradParams w2 = make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
+  if (!wgrad_supported(w1) || !wgrad_supported(w2)) return false;
+  ConvGemmParams p = conv_base(d, nullptr);
+  p.NQ = 9;
+  p.s_in = d->stride;
+  p.R = R;
+  p.C = R;
+  if (!conv_gemm_supported(p)) return false;
+  p.NQ = 1;
+  p.s_in = 1;
+  return conv_gemm_supported(p);
+}
+
 extern "C" {
 
 int stgcn_abi_version(void) { return STGCN_ABI_VERSION; }
 
 const char *stgcn_last_error(void) { return g_err.c_str(); }
+
+static bool geometry_supported(const stgcn_desc_t *d);
 
 int stgcn_check_desc(const stgcn_desc_t *d) {
   if (!d) return fail(STGCN_E_INVALID, "null descriptor");
@@ -179,6 +210,8 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   if ((int64_t)d->N * d->K * d->C_in * d->T * d->V > INT32_MAX ||
       (int64_t)d->N * d->C_out * d->T * d->V > INT32_MAX)
     return fail(STGCN_E_UNSUPPORTED, "tensor too large for 32-bit element indexing");
+  if (!geometry_supported(d))
+    return fail(STGCN_E_UNSUPPORTED, "tile geometry exceeds LDS for this V / channel count");
   return STGCN_OK;
 }
 
@@ -223,7 +256,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   }
   HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, s));
   {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.G;
     p.w = Wz;
     p.out = a->Z;
@@ -249,7 +282,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   // Temporal (9,1) conv, stride (s,1), pad (4,0), bias (st_graphconv.py:41-43,99),
   // with the BN2 batch statistics accumulated in the epilogue.
   {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, L.wpk);
     p.in = a->Z;
     p.w = a->Wt;
     p.out = a->U;
@@ -313,7 +346,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 
   // Temporal conv data-gradient: dZ = conv^T(dU)
   {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.dU;
     p.out = L.dZ;
     p.in_bstride = (int64_t)R * To * V;
@@ -370,7 +403,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s));
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
   for (int k = 0; k < K; ++k) {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.dZ;
     p.w = a->W + (int64_t)k * R * C;
     p.out = L.H + (int64_t)k * C * T * V;
@@ -428,8 +461,9 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
   Carve c(scratch);
   const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V, K = d->K;
   const double tflops = 2.0 * 9 * R * (double)R * To * V * N;
+  float *wpk = c.take<float>(wpk_floats(d));
   if (which == 0) {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * R * T * V);
     p.w = c.take<float>((size_t)R * R * 9);
     p.out = c.take<float>((size_t)N * R * To * V);
@@ -455,7 +489,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.cp[P.ncp++] = p;
     P.flops = tflops;
   } else if (which == 1) {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * R * To * V);
     const float *w = c.take<float>((size_t)R * R * 9);
     p.out = c.take<float>((size_t)N * R * T * V);
@@ -502,7 +536,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.wgrad = true;
     P.flops = tflops;
   } else {
-    ConvGemmParams p = conv_base(d);
+    ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * K * C * T * V);
     p.w = c.take<float>((size_t)R * K * C);
     p.out = c.take<float>((size_t)N * R * T * V);

@@ -16,6 +16,7 @@ constexpr int kTileCols = 256;  // max (frames x V) columns per workgroup (8 MFM
 // split into two phases, NQ=5/4) and the spatial H = W^T dZ GEMM (NQ=1).
 struct ConvGemmParams {
   const float *in, *w;
+  float *wpk;            // workspace for the packed weights (conv_gemm_wpk_floats)
   float *out;
   const float *bias_r;   // [R] or null
   const float *bias_rv;  // [R][V] or null
@@ -29,6 +30,7 @@ struct ConvGemmParams {
   int T_dst;  // output physical frames
   int V, FT;  // joints; frames per tile (FT*V <= kTileCols)
   int n_mtiles, n_rtiles, N;
+  int Cpad;  // set by launch_conv_gemm
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -48,7 +50,11 @@ struct WgradParams {
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s);
 size_t conv_gemm_lds_bytes(const ConvGemmParams &p);
+size_t conv_gemm_wpk_floats(const ConvGemmParams &p);
+bool conv_gemm_supported(const ConvGemmParams &p);
 size_t wgrad_lds_bytes(const WgradParams &p);
+bool wgrad_supported(const WgradParams &p);
+int wgrad_ntiles_j(int C, int NQ);
 
 // Reduction of split-K slabs: dst = sum_s slab[s]. mode 0: identity layout;
 // mode 1: slab is [R][K*C] (packed W'), dst is the (K*R, C) Conv2d weight.

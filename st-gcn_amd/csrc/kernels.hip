@@ -57,6 +57,18 @@ __device__ __forceinline__ void block_sum2_atomic(double a, double b, double *ds
   __syncthreads();
 }
 
+// Zero page: out-of-range staging elements (temporal halo, padding rows and
+// columns) are DMA'd from here. Never written; device globals start zeroed.
+__device__ float g_zero_page[64];
+
+// LDS-DMA of one float per lane: LDS[lds_wave_base + lane] = *src (lane's own
+// source address). lds_wave_base must be the same for the whole wave.
+__device__ __forceinline__ void glds_f32(const float *src, float *lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, lds_wave_base, 4, 0, 0);
+}
+
+__host__ __device__ constexpr int round64(int x) { return (x + 63) & ~63; }
+
 // XCD-aware bijective remap: hardware deals consecutive block ids round-robin
 // over the 8 XCDs; give each XCD a contiguous chunk of the logical grid so
 // workgroups that share input tiles share an L2 (speed only, never correctness).
@@ -70,13 +82,36 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // conv_gemm: see ConvGemmParams. Workgroup = 256 threads (4 waves), tile =
 // 64 rows x (FT frames * V) columns (<= 256, padded to 8 MFMA column tiles).
 // Wave w owns rows (w&1)*32..+31 and column tiles (w>>1)*4..+3: 4 accumulators
-// of 32x32 fp32 (64 VGPRs). The reduction runs over input-channel chunks of CK
-// staged in LDS together with their (frames+halo) window; each staged channel
-// window is reused by all NQ taps (the halo shift is a per-lane LDS offset).
+// of 32x32 fp32 (64 VGPRs). The reduction runs over input-channel chunks of CK:
+// each chunk's weights (pre-packed [rtile][c][q][64], a contiguous block) and
+// input windows (frames + temporal halo, zero-padded) are staged global ->
+// registers -> LDS, double-buffered: the loads of chunk i+1 are in flight while
+// chunk i runs on the matrix cores; one barrier per chunk. Each staged channel
+// window serves all NQ taps (the tap shift is a per-lane LDS offset).
 // ---------------------------------------------------------------------------
+// Packs w[r*w_sr + c*w_sc + q*w_sq] into wpk[rt][c][q][r_local] (zero padded
+// to n_rtiles*64 rows and Cpad channels).
+__global__ void k_pack_conv_w(const float *w, float *wpk, int R, int C, int Cpad, int NQ,
+                              int64_t w_sr, int64_t w_sc, int64_t w_sq, int n_rtiles) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)n_rtiles * Cpad * NQ * 64;
+  if (idx >= total) return;
+  const int rl = (int)(idx & 63);
+  int64_t t = idx >> 6;
+  const int q = (int)(t % NQ);
+  t /= NQ;
+  const int c = (int)(t % Cpad);
+  const int rt = (int)(t / Cpad);
+  const int r = rt * 64 + rl;
+  float v = 0.f;
+  if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
+  wpk[idx] = v;
+}
+
 template <int NQ, int CK>
 __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int WSZ = CK * NQ * 64;   // floats of one weight chunk (multiple of 256)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hi = lane >> 5, lo = lane & 31;
   const int nblk = gridDim.x;
@@ -89,12 +124,15 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
   const int V = p.V;
   const int span = (p.s_in * (p.FT - 1) + NQ) * V;
   const int SP = span | 1;  // odd pitch
-  float *Ws = smem;                 // [CK][NQ][64]
-  float *Is = smem + CK * NQ * 64;  // [CK][SP]
-  const int f0 = p.s_in * m0 + p.off;
-  const int64_t cstride = (int64_t)p.T_src * V;
+  const int ISZ = round64(CK * SP);
+  float *Ws0 = smem, *Ws1 = smem + WSZ;
+  float *Is0 = smem + 2 * WSZ, *Is1 = smem + 2 * WSZ + ISZ;
+  const int cstride = p.T_src * V;
+  const int g0 = (p.s_in * m0 + p.off) * V;
   const float *inN = p.in + (int64_t)n * p.in_bstride;
+  const float *wblk = p.wpk + (int64_t)rt * p.Cpad * NQ * 64;
   const int ncols = p.FT * V;
+  const int nchunks = (p.C + CK - 1) / CK;
 
   const int mi = wave & 1;
   const int nj0 = (wave >> 1) * 4;
@@ -106,38 +144,51 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
       const int mf = col / V;
       bbase[j] = p.s_in * mf * V + (col - mf * V);
     } else {
-      bbase[j] = 0;  // padding column: read any staged value, result discarded
+      bbase[j] = 0;  // padding column: reads a staged value, result discarded
     }
   }
+  // LDS-DMA staging of chunk `chunk` into (Ws, Is). Input image [CK][SP]:
+  // element e -> (c = e / SP, o = e % SP); this lane starts at e = wave*64+lane
+  // and advances by 256 per instruction.
+  const int e_init = wave * 64 + lane;
+  const int c_init = e_init / SP, o_init = e_init - c_init * SP;
+  const int dc = 256 / SP, dO = 256 - dc * SP;
+  auto stage = [&](int chunk, float *Ws, float *Is) {
+    const float *wsrc = wblk + (int64_t)chunk * WSZ;
+#pragma unroll
+    for (int i = 0; i < WSZ / 256; ++i) {
+      const int E0 = (i * 4 + wave) * 64;
+      glds_f32(wsrc + E0 + lane, Ws + E0);
+    }
+    const int c0 = chunk * CK;
+    int c = c_init, o = o_init;
+    for (int E0 = wave * 64; E0 < ISZ; E0 += 256) {
+      const int g = g0 + o;
+      const bool ok = c < CK && o < span && c0 + c < p.C && g >= 0 && g < cstride;
+      const float *src = ok ? inN + (int64_t)(c0 + c) * cstride + g : g_zero_page;
+      glds_f32(src, Is + E0);
+      o += dO;
+      c += dc;
+      if (o >= SP) {
+        o -= SP;
+        ++c;
+      }
+    }
+  };
+
   floatx16 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 
-  for (int c0 = 0; c0 < p.C; c0 += CK) {
-    __syncthreads();
-    for (int e = tid; e < CK * NQ * 64; e += 256) {
-      const int r = e & 63, cq = e >> 6;
-      const int c = cq / NQ, q = cq - c * NQ;
-      float w = 0.f;
-      if (r0 + r < p.R && c0 + c < p.C)
-        w = p.w[(int64_t)(r0 + r) * p.w_sr + (int64_t)(c0 + c) * p.w_sc + (int64_t)q * p.w_sq];
-      Ws[cq * 64 + r] = w;
-    }
-    const int64_t g0 = (int64_t)f0 * V;
-#pragma unroll
-    for (int c = 0; c < CK; ++c) {
-      const bool cval = c0 + c < p.C;
-      const float *src = inN + (int64_t)(c0 + c) * cstride;
-      for (int o = tid; o < span; o += 256) {
-        const int64_t g = g0 + o;
-        float v = 0.f;
-        if (cval && g >= 0 && g < cstride) v = src[g];
-        Is[c * SP + o] = v;
-      }
-    }
-    __syncthreads();
+  stage(0, Ws0, Is0);
+  __syncthreads();
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    const bool odd = chunk & 1;
+    const float *Ws = odd ? Ws1 : Ws0;
+    const float *Is = odd ? Is1 : Is0;
+    if (chunk + 1 < nchunks) stage(chunk + 1, odd ? Ws0 : Ws1, odd ? Is0 : Is1);
     const float *wp = Ws + hi * NQ * 64 + mi * 32 + lo;
     const float *ip = Is + hi * SP;
 #pragma unroll 2
@@ -153,6 +204,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
         acc[3] = mfma32(a, b3, acc[3]);
       }
     }
+    __syncthreads();  // retires this wave's LDS-DMA (vmcnt(0)) and publishes the next chunk
   }
 
   // Epilogue: bias, store, optional per-row BN statistics (fp64).
@@ -201,13 +253,37 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
   }
 }
 
-size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
-  const int CK = p.NQ == 1 ? 32 : 8;
-  const int span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
-  return sizeof(float) * ((size_t)CK * p.NQ * 64 + (size_t)CK * (span | 1));
+static int conv_ck(int NQ) { return NQ == 1 ? 32 : 8; }
+
+int conv_gemm_cpad(const ConvGemmParams &p) {
+  const int CK = conv_ck(p.NQ);
+  return (p.C + CK - 1) / CK * CK;
 }
 
-hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s) {
+size_t conv_gemm_wpk_floats(const ConvGemmParams &p) {
+  return (size_t)p.n_rtiles * conv_gemm_cpad(p) * p.NQ * 64;
+}
+
+int conv_gemm_span(const ConvGemmParams &p) { return (p.s_in * (p.FT - 1) + p.NQ) * p.V; }
+
+size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
+  const int CK = conv_ck(p.NQ);
+  return sizeof(float) * 2 * ((size_t)CK * p.NQ * 64 + round64(CK * (conv_gemm_span(p) | 1)));
+}
+
+bool conv_gemm_supported(const ConvGemmParams &p) {
+  return p.FT * p.V <= kTileCols && conv_gemm_lds_bytes(p) <= 160 * 1024;
+}
+
+hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
+  ConvGemmParams p = p0;
+  if (!conv_gemm_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  p.Cpad = conv_gemm_cpad(p);
+  {
+    const int64_t total = (int64_t)conv_gemm_wpk_floats(p);
+    hipLaunchKernelGGL(k_pack_conv_w, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       p.w, p.wpk, p.R, p.C, p.Cpad, p.NQ, p.w_sr, p.w_sc, p.w_sq, p.n_rtiles);
+  }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   const size_t lds = conv_gemm_lds_bytes(p);
   switch (p.NQ) {
@@ -231,13 +307,17 @@ hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // wgrad: see WgradParams. Workgroup = 256 threads, output tile 64 rows (r) x
-// 64 columns (j = c*NQ + q); every wave holds the whole 64x64 tile (2x2 MFMA
-// tiles) and takes every 4th pair of reduction columns; the 4 partial tiles
-// are summed through LDS at the end and written to this split's slab.
+// JT columns (j = c*NQ + q), JT = 192 (NQ=9) or 128 (NQ=1). Wave w owns rows
+// (w&1)*32..+31 and column tiles (w>>1)*NJW..+NJW-1 (NJW = JT/64). The
+// reduction runs over work items (clip n, FT frames): P[64 rows][FT*V cols]
+// and the Q channel windows of the tile's j range are staged global ->
+// registers -> LDS, double-buffered; one barrier per item. The split's partial
+// tile is written to its slab (reduced in fixed order by k_slab_reduce).
 // ---------------------------------------------------------------------------
-template <int NQ>
+template <int NQ, int JT>
 __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NJW = JT / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hi = lane >> 5, lo = lane & 31;
   const int nblk = gridDim.x;
@@ -246,153 +326,154 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   bid /= p.S;
   const int jt = bid % p.n_jtiles;
   const int rt = bid / p.n_jtiles;
-  const int r0 = rt * 64, j0 = jt * 64;
+  const int r0 = rt * 64, j0 = jt * JT;
   const int J = p.C * NQ;
   const int V = p.V;
   const int ncols = p.FT * V;
-  const int PP = ((ncols + 1) | 1) + 0;  // odd pitch >= ncols+1
+  const int nk = (ncols + 1) / 2;
+  const int PP = (2 * nk) | 1;  // odd pitch >= ncols (+1 zero column when ncols is odd)
   const int c_lo = j0 / NQ;
-  int c_hi = (j0 + 63) / NQ + 1;
+  int c_hi = (j0 + JT - 1) / NQ + 1;
   if (c_hi > p.C) c_hi = p.C;
   const int nc = c_hi - c_lo;
   const int span = (p.s_in * (p.FT - 1) + NQ) * V;
   const int QP = span | 1;
-  float *Ps = smem;            // [64][PP]
-  float *Qs = smem + 64 * PP;  // [nc+1][QP]  (row nc = zeros)
-
-  int qoff[2];
+  const int PSZ = round64(64 * PP), QSZ = round64((nc + 1) * QP);  // Q row nc = zeros
+  float *Ps0 = smem, *Qs0 = smem + PSZ;
+  float *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
+  const int mi = wave & 1;
+  const int nj0 = (wave >> 1) * NJW;
+  int qoff[NJW];
 #pragma unroll
-  for (int nj = 0; nj < 2; ++nj) {
-    const int j = j0 + nj * 32 + lo;
+  for (int t = 0; t < NJW; ++t) {
+    const int j = j0 + (nj0 + t) * 32 + lo;
     if (j < J) {
       const int c = j / NQ, q = j - c * NQ;
-      qoff[nj] = (c - c_lo) * QP + q * V;
+      qoff[t] = (c - c_lo) * QP + q * V;
     } else {
-      qoff[nj] = nc * QP;  // zero row
+      qoff[t] = nc * QP;  // zero row
     }
   }
-  floatx16 acc[2][2];
+  floatx16 acc[NJW];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int t = 0; t < NJW; ++t)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 
   const int total = p.N * p.n_mtiles;
   const int per = (total + p.S - 1) / p.S;
   const int it0 = split * per;
   int it1 = it0 + per;
   if (it1 > total) it1 = total;
-  const int nk = (ncols + 1) / 2;
-  const int64_t pcs = (int64_t)p.M * V;      // P channel stride
-  const int64_t qcs = (int64_t)p.T_src * V;  // Q channel stride
+  const int pcs = p.M * V;      // P channel stride
+  const int qcs = p.T_src * V;  // Q channel stride
+  const int e_init = wave * 64 + lane;
+  const int prow_i = e_init / PP, po_i = e_init - prow_i * PP;
+  const int dpr = 256 / PP, dpo = 256 - dpr * PP;
+  const int qrow_i = e_init / QP, qo_i = e_init - qrow_i * QP;
+  const int dqr = 256 / QP, dqo = 256 - dqr * QP;
+  const int prow_lim = p.R - r0;
 
-  // zero row of Qs (never overwritten)
-  for (int o = tid; o < QP; o += 256) Qs[nc * QP + o] = 0.f;
-
-  for (int it = it0; it < it1; ++it) {
+  // LDS-DMA staging of work item `it` into (Ps, Qs): images [64][PP] and
+  // [nc+1][QP], lane-linear; everything out of range comes from the zero page.
+  auto stage = [&](int it, float *Ps, float *Qs) {
     const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
     const int m0 = mt * p.FT;
-    __syncthreads();
-    // stage P rows (zero-padded columns up to PP)
-    const float *Pn = p.P + (int64_t)n * p.p_bstride;
-    const int64_t pg0 = (int64_t)m0 * V;
-    for (int r = 0; r < 64; ++r) {
-      const bool rok = r0 + r < p.R;
-      const float *src = Pn + (int64_t)(r0 + r) * pcs;
-      for (int o = tid; o < PP; o += 256) {
-        float v = 0.f;
-        if (rok && o < ncols && pg0 + o < pcs) v = src[pg0 + o];
-        Ps[r * PP + o] = v;
+    const float *Pn = p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * pcs + (int64_t)m0 * V;
+    const int plim = pcs - m0 * V;
+    int row = prow_i, o = po_i;
+    for (int E0 = wave * 64; E0 < PSZ; E0 += 256) {
+      const bool ok = row < 64 && o < ncols && o < plim && row < prow_lim;
+      glds_f32(ok ? Pn + (int64_t)row * pcs + o : g_zero_page, Ps + E0);
+      o += dpo;
+      row += dpr;
+      if (o >= PP) {
+        o -= PP;
+        ++row;
       }
     }
-    const float *Qn = p.Q + (int64_t)n * p.q_bstride;
-    const int64_t qg0 = (int64_t)(p.s_in * m0 + p.off) * V;
-    for (int c = 0; c < nc; ++c) {
-      const float *src = Qn + (int64_t)(c_lo + c) * qcs;
-      for (int o = tid; o < span; o += 256) {
-        const int64_t g = qg0 + o;
-        float v = 0.f;
-        if (g >= 0 && g < qcs) v = src[g];
-        Qs[c * QP + o] = v;
+    const int qg0 = (p.s_in * m0 + p.off) * V;
+    const float *Qn = p.Q + (int64_t)n * p.q_bstride + (int64_t)c_lo * qcs;
+    row = qrow_i;
+    o = qo_i;
+    for (int E0 = wave * 64; E0 < QSZ; E0 += 256) {
+      const int g = qg0 + o;
+      const bool ok = row < nc && o < span && g >= 0 && g < qcs;
+      glds_f32(ok ? Qn + (int64_t)row * qcs + g : g_zero_page, Qs + E0);
+      o += dqo;
+      row += dqr;
+      if (o >= QP) {
+        o -= QP;
+        ++row;
       }
     }
-    __syncthreads();
-    int col = 2 * wave + hi;
-    int mf = col / V;
-    int v = col - mf * V;
-    const float *pa0 = Ps + lo * PP;
-    const float *pa1 = Ps + (32 + lo) * PP;
-    for (int kk = wave; kk < nk; kk += 4) {
-      const float a0 = pa0[col], a1 = pa1[col];
+  };
+
+  if (it0 < it1) stage(it0, Ps0, Qs0);
+  __syncthreads();
+  for (int it = it0; it < it1; ++it) {
+    const bool odd = (it - it0) & 1;
+    const float *Ps = odd ? Ps1 : Ps0;
+    const float *Qs = odd ? Qs1 : Qs0;
+    if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
+    const float *pa = Ps + (mi * 32 + lo) * PP;
+    int col = hi, mf = 0, v = hi;
+    for (int kk = 0; kk < nk; ++kk) {
+      const float a = pa[col];
       const int bq = (mf < p.FT) ? p.s_in * mf * V + v : 0;
-      const float b0 = Qs[qoff[0] + bq], b1 = Qs[qoff[1] + bq];
-      acc[0][0] = mfma32(a0, b0, acc[0][0]);
-      acc[0][1] = mfma32(a0, b1, acc[0][1]);
-      acc[1][0] = mfma32(a1, b0, acc[1][0]);
-      acc[1][1] = mfma32(a1, b1, acc[1][1]);
-      col += 8;
-      v += 8;
-      while (v >= V) {
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) acc[t] = mfma32(a, Qs[qoff[t] + bq], acc[t]);
+      col += 2;
+      v += 2;
+      if (v >= V) {
         v -= V;
         ++mf;
       }
     }
+    __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
   }
-  // cross-wave reduction: waves 1..3 park their tiles in LDS, wave 0 sums.
-  __syncthreads();
-  float *red = smem;  // [3][64*64]
-  if (wave > 0) {
+  float *dst = p.slab + (int64_t)split * p.R * J;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+  for (int t = 0; t < NJW; ++t)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = a * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-          const int colj = b * 32 + lo;
-          red[(wave - 1) * 4096 + row * 64 + colj] = acc[a][b][i];
-        }
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float *dst = p.slab + (int64_t)split * p.R * J;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = a * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-          const int colj = b * 32 + lo;
-          float s = acc[a][b][i] + red[row * 64 + colj] + red[4096 + row * 64 + colj] +
-                    red[8192 + row * 64 + colj];
-          if (r0 + row < p.R && j0 + colj < J) dst[(int64_t)(r0 + row) * J + j0 + colj] = s;
-        }
-  }
+    for (int i = 0; i < 16; ++i) {
+      const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+      const int j = j0 + (nj0 + t) * 32 + lo;
+      if (row < p.R && j < J) dst[(int64_t)row * J + j] = acc[t][i];
+    }
 }
+
+static int wgrad_jt(int NQ) { return NQ == 1 ? 128 : 192; }
+
+static void wgrad_geom(const WgradParams &p, int &PP, int &nc, int &span) {
+  const int JT = wgrad_jt(p.NQ);
+  const int ncols = p.FT * p.V;
+  PP = (2 * ((ncols + 1) / 2)) | 1;
+  nc = JT / p.NQ + 2;
+  if (nc > p.C) nc = p.C;
+  span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
+}
+
+int wgrad_ntiles_j(int C, int NQ) { return (C * NQ + wgrad_jt(NQ) - 1) / wgrad_jt(NQ); }
 
 size_t wgrad_lds_bytes(const WgradParams &p) {
-  const int ncols = p.FT * p.V;
-  const int PP = ((ncols + 1) | 1);
-  const int c_span = 64 / p.NQ + 2;
-  const int nc = c_span < p.C ? c_span : p.C;
-  const int span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
-  size_t b = sizeof(float) * ((size_t)64 * PP + (size_t)(nc + 1) * (span | 1));
-  const size_t red = sizeof(float) * 3 * 4096;
-  return b > red ? b : red;
+  int PP, nc, span;
+  wgrad_geom(p, PP, nc, span);
+  return sizeof(float) * 2 * (round64(64 * PP) + round64((nc + 1) * (span | 1)));
 }
 
+bool wgrad_supported(const WgradParams &p) { return wgrad_lds_bytes(p) <= 160 * 1024; }
+
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s) {
+  if (!wgrad_supported(p)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const size_t lds = wgrad_lds_bytes(p);
   switch (p.NQ) {
     case 1:
-      hipLaunchKernelGGL((k_wgrad<1>), dim3(nblk), dim3(256), lds, s, p);
+      hipLaunchKernelGGL((k_wgrad<1, 128>), dim3(nblk), dim3(256), lds, s, p);
       break;
     case 9:
-      hipLaunchKernelGGL((k_wgrad<9>), dim3(nblk), dim3(256), lds, s, p);
+      hipLaunchKernelGGL((k_wgrad<9, 192>), dim3(nblk), dim3(256), lds, s, p);
       break;
     default:
       return hipErrorInvalidValue;

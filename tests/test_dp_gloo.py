@@ -1,0 +1,101 @@
+"""Data-parallel gradient all-reduce (st-gcn_amd/dp.py) on CPU with gloo,
+world_size 2 (and 3): the all-reduced grads must equal the mean of the
+per-shard gradients of the oracle stack (BN is per replica, so
+DP equals per-shard runs, not one big-batch run)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+from conftest import ROOT, load_npz
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class OracleStackModule(nn.Module):
+    """nn.Module wrapper of the oracle stack so the DP hooks see Parameters."""
+
+    def __init__(self, params, buffers):
+        super().__init__()
+        self.names = list(params)
+        self.ps = nn.ParameterList([nn.Parameter(params[k].clone()) for k in self.names])
+        self.buffers_ = {k: v.clone() for k, v in buffers.items()}
+
+    def forward(self, x):
+        from oracle import ref_cpu
+        p = dict(zip(self.names, self.ps))
+        return ref_cpu.Stack(p, self.buffers_).forward(x)
+
+
+def _shard_grads(params, buffers, x, y):
+    m = OracleStackModule(params, buffers)
+    loss = nn.functional.cross_entropy(m(x), y)
+    loss.backward()
+    return [p.grad.clone() for p in m.ps]
+
+
+def _worker(rank, world, port, out_q, T, bucket_bytes):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from stgcn_loader import load
+        from oracle import ref_cpu
+        pkg = load()
+        A = torch.from_numpy(load_npz("adjacency.npz")["V18_s0_d1"])
+        params, buffers = ref_cpu.init_stack_params(3, 5, A, seed=0)
+        gen = torch.Generator().manual_seed(123)
+        N = 2
+        xs = torch.randn(world, N, T, 18, 3, generator=gen)
+        ys = torch.randint(0, 5, (world, N), generator=gen)
+        model = OracleStackModule(params, buffers)
+        dp = pkg.dp.GradAllReduce(model, world, bucket_bytes=bucket_bytes)
+        loss = nn.functional.cross_entropy(model(xs[rank]), ys[rank])
+        loss.backward()
+        dp.synchronize()
+        got = [p.grad.clone() for p in model.ps]
+        # expected: mean over shards of per-shard grads (computed locally)
+        per = [_shard_grads(params, buffers, xs[r], ys[r]) for r in range(world)]
+        want = [sum(g[i] for g in per) / world for i in range(len(got))]
+        worst = 0.0
+        for a, b in zip(got, want):
+            denom = max(b.abs().max().item(), 1e-12)
+            worst = max(worst, (a - b).abs().max().item() / denom)
+        # every rank ends with identical grads
+        flat = torch.cat([g.reshape(-1) for g in got])
+        ref = flat.clone()
+        dist.broadcast(ref, 0)
+        same = torch.equal(ref, flat)
+        out_q.put((rank, worst, same, len(dp.buckets)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bucket_bytes", [(2, 1 << 20), (3, 4 << 20)])
+def test_dp_allreduce_matches_mean_of_shards(world, bucket_bytes):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, 12, bucket_bytes))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, worst, same, nb in res:
+        assert worst < 1e-5, (rank, worst)
+        assert same, rank
+        assert nb >= 2

@@ -1,7 +1,12 @@
 """GPU parity of the fused HIP block (through the C-ABI) against the oracle.
 
-Tolerance: fp32 HIP vs the fp64 oracle, max|diff| / max|ref|
-< 1e-5 for outputs and gradients; the temporal-conv bias gradient is
+Tolerance: fp32 HIP vs the fp64 oracle, rel-to-max error
+max|diff| / max|ref| below 1e-5 for outputs and gradients -- or, where the
+reference's own fp32 arithmetic (the oracle run in fp32, same ops as the
+reference) is further than that from exact arithmetic, below twice the
+reference's own error for that tensor ("no worse than the reference"). The
+latter happens for BN-heavy small batches (T=1) and for large-N bias-type
+gradients (sums of ~1e5 cancelling terms). The temporal-conv bias gradient is
 analytically zero (BN2 follows the conv) and is checked with an absolute
 tolerance instead.
 """
@@ -46,7 +51,8 @@ def _run_hip(pkg, arrays, x, g, need_dx=True):
     return out
 
 
-def _compare(got, want, residual=False, tol=TOL):
+def _compare(got, want, residual=False, tol=TOL, floor=None):
+    """floor: optional {key: rel error of the fp32 reference vs fp64}."""
     bad = []
     for k, w in want.items():
         if k not in got or k.endswith("num_batches_tracked"):
@@ -59,9 +65,10 @@ def _compare(got, want, residual=False, tol=TOL):
                 bad.append((k, err))
             continue
         err = rel_to_max(gv, wv)
-        if err > tol:
-            bad.append((k, err))
-    assert not bad, bad
+        lim = max(tol, 2.0 * floor.get(k, 0.0)) if floor else tol
+        if err > lim:
+            bad.append((k, err, lim))
+    assert not bad, "; ".join(f"{k}: {e:.2e} > {l:.1e}" for k, e, l in bad)
 
 
 @pytest.mark.parametrize("fixture", [f for f in block_fixtures() if not f.startswith("block_res")])
@@ -70,14 +77,40 @@ def test_block_matches_reference_fixture(pkg, fixture):
     x = torch.from_numpy(ref["x"])
     g = torch.from_numpy(ref["g"])
     got = _run_hip(pkg, ref, x, g)
-    want64 = ref_cpu.block_step(ref, dtype=torch.float64)
-    _compare(got, want64)
+    want64, floor = _oracle(ref, got)
+    _compare(got, want64, floor=floor)
     # and against the reference's own fp32 outputs (its rounding included)
     _compare(got, {k: torch.from_numpy(v) for k, v in ref.items()
                    if k == "y" or k.startswith("grad.")}, tol=5e-5)
 
 
+# ReLU ties: a pre-ReLU value within fp32 rounding of 0 can land on either
+# side in any fp32 implementation (the reference's included), and flipping one
+# element changes every gradient by that element's contribution (~1e-3 of a
+# BN2 bias grad at these sizes). The parity check therefore (1) requires the
+# HIP ReLU mask to agree with the fp64 oracle's everywhere except at such ties
+# (|pre-ReLU| < TIE), and (2) differentiates the oracle through the HIP mask.
+TIE = 1e-5
+
+
+def _oracle(arrays, got):
+    mask = (got["y"] > 0)
+    pre = ref_cpu.block_pre_relu(arrays)
+    flips = (mask != (pre > 0))
+    if flips.any():
+        assert pre[flips].abs().max().item() < TIE, "ReLU mask differs away from a tie"
+    want = ref_cpu.block_step(arrays, dtype=torch.float64, relu_mask=mask)
+    ref32 = ref_cpu.block_step(arrays, dtype=torch.float32, relu_mask=mask)
+    floor = {k: rel_to_max(ref32[k].detach().double().numpy(), v.detach().double().numpy())
+             for k, v in want.items() if k in ref32 and "num_batches" not in k}
+    return want, floor
+
+
 def _random_case(pkg, C_in, C_out, stride, V, K, N, T, seed=0):
+    return _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed)
+
+
+def _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed=0):
     gr = pkg.graph
     strat = 0 if K == 1 else 2
     A = gr.get_normalized_adjacency_matrices(strat, 1, distances=gr.synthetic_distances(V),
@@ -117,17 +150,17 @@ def test_block_matches_oracle_random(pkg, case):
     C_in, C_out, stride, V, K, N, T = case
     arrays, x, g = _random_case(pkg, C_in, C_out, stride, V, K, N, T)
     got = _run_hip(pkg, arrays, x, g)
-    want = ref_cpu.block_step(arrays, dtype=torch.float64)
-    _compare(got, want)
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, floor=floor)
 
 
 def test_first_block_without_dx(pkg):
     """need_dx = 0 path (input does not require grad): params grads unchanged."""
     arrays, x, g = _random_case(pkg, 3, 64, 1, 18, 1, 2, 30)
     got = _run_hip(pkg, arrays, x, g, need_dx=False)
-    want = ref_cpu.block_step(arrays, dtype=torch.float64)
+    want, floor = _oracle(arrays, got)
     want.pop("grad.x")
-    _compare(got, want)
+    _compare(got, want, floor=floor)
 
 
 def test_full_size_block_properties(pkg):
@@ -140,8 +173,8 @@ def test_full_size_block_properties(pkg):
     assert (got["y"] >= 0).all()
     for k, v in got.items():
         assert torch.isfinite(v).all(), k
-    want = ref_cpu.block_step(arrays, dtype=torch.float64)
-    _compare(got, want)
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, floor=floor)
 
 
 def test_eval_mode_uses_running_stats(pkg):
