@@ -57,14 +57,21 @@ __device__ __forceinline__ void block_sum2_atomic(double a, double b, double *ds
   __syncthreads();
 }
 
-// Zero page: out-of-range staging elements (temporal halo, padding rows and
-// columns) are DMA'd from here. Never written; device globals start zeroed.
-__device__ float g_zero_page[64];
+// LDS-DMA through a buffer resource: LDS[lds_wave_base + lane] = base[voff/4]
+// for this lane's byte offset; offsets >= the resource's size (kOOB) return 0,
+// which zero-fills the temporal halo and all padding without branches.
+// lds_wave_base must be the same for the whole wave.
+constexpr unsigned kOOB = 0x80000000u;
 
-// LDS-DMA of one float per lane: LDS[lds_wave_base + lane] = *src (lane's own
-// source address). lds_wave_base must be the same for the whole wave.
-__device__ __forceinline__ void glds_f32(const float *src, float *lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, lds_wave_base, 4, 0, 0);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float *base, int64_t nfloats) {
+  int64_t bytes = nfloats * 4;
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void blds_f32(__amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                         float *lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds_wave_base, 4, voff, 0, 0, 0);
 }
 
 __host__ __device__ constexpr int round64(int x) { return (x + 63) & ~63; }
@@ -153,20 +160,19 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
   const int e_init = wave * 64 + lane;
   const int c_init = e_init / SP, o_init = e_init - c_init * SP;
   const int dc = 256 / SP, dO = 256 - dc * SP;
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(wblk, (int64_t)p.Cpad * NQ * 64);
+  const __amdgpu_buffer_rsrc_t rs_in = make_rsrc(inN, (int64_t)p.C * cstride);
   auto stage = [&](int chunk, float *Ws, float *Is) {
-    const float *wsrc = wblk + (int64_t)chunk * WSZ;
+    const unsigned wbase = (unsigned)(chunk * WSZ + wave * 64 + lane) * 4u;
 #pragma unroll
-    for (int i = 0; i < WSZ / 256; ++i) {
-      const int E0 = (i * 4 + wave) * 64;
-      glds_f32(wsrc + E0 + lane, Ws + E0);
-    }
-    const int c0 = chunk * CK;
+    for (int i = 0; i < WSZ / 256; ++i) blds_f32(rs_w, wbase + i * 1024u, Ws + (i * 4 + wave) * 64);
+    const int climit = p.C - chunk * CK;
+    const int cbase = chunk * CK * cstride + g0;
     int c = c_init, o = o_init;
     for (int E0 = wave * 64; E0 < ISZ; E0 += 256) {
       const int g = g0 + o;
-      const bool ok = c < CK && o < span && c0 + c < p.C && g >= 0 && g < cstride;
-      const float *src = ok ? inN + (int64_t)(c0 + c) * cstride + g : g_zero_page;
-      glds_f32(src, Is + E0);
+      const bool ok = c < CK && c < climit && o < span && g >= 0 && g < cstride;
+      blds_f32(rs_in, ok ? (unsigned)(cbase + c * cstride + o) * 4u : kOOB, Is + E0);
       o += dO;
       c += dc;
       if (o >= SP) {
@@ -329,15 +335,15 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   const int r0 = rt * 64, j0 = jt * JT;
   const int J = p.C * NQ;
   const int V = p.V;
-  const int ncols = p.FT * V;
-  const int nk = (ncols + 1) / 2;
-  const int PP = (2 * nk) | 1;  // odd pitch >= ncols (+1 zero column when ncols is odd)
+  const int Vp = (V + 1) & ~1;          // joints padded to even: k-steps never straddle frames
+  const int ncols = p.FT * Vp;          // P image columns (frame-padded)
+  const int PP = ncols | 1;             // odd pitch
   const int c_lo = j0 / NQ;
   int c_hi = (j0 + JT - 1) / NQ + 1;
   if (c_hi > p.C) c_hi = p.C;
   const int nc = c_hi - c_lo;
   const int span = (p.s_in * (p.FT - 1) + NQ) * V;
-  const int QP = span | 1;
+  const int QP = (span + 2) | 1;        // >= span + 1: the odd-V pad column reads a finite value
   const int PSZ = round64(64 * PP), QSZ = round64((nc + 1) * QP);  // Q row nc = zeros
   float *Ps0 = smem, *Qs0 = smem + PSZ;
   float *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
@@ -367,24 +373,27 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
   if (it1 > total) it1 = total;
   const int pcs = p.M * V;      // P channel stride
   const int qcs = p.T_src * V;  // Q channel stride
+  // per-lane staging walk: element e = wave*64 + lane + 256*i of each image
   const int e_init = wave * 64 + lane;
   const int prow_i = e_init / PP, po_i = e_init - prow_i * PP;
   const int dpr = 256 / PP, dpo = 256 - dpr * PP;
   const int qrow_i = e_init / QP, qo_i = e_init - qrow_i * QP;
   const int dqr = 256 / QP, dqo = 256 - dqr * QP;
-  const int prow_lim = p.R - r0;
+  const int prow_lim = min(64, p.R - r0);
 
-  // LDS-DMA staging of work item `it` into (Ps, Qs): images [64][PP] and
-  // [nc+1][QP], lane-linear; everything out of range comes from the zero page.
+  // LDS-DMA staging of work item `it`: P image [64][PP] (frame-padded columns)
+  // and Q image [nc+1][QP]; out-of-range elements read as 0 (buffer OOB).
   auto stage = [&](int it, float *Ps, float *Qs) {
     const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
     const int m0 = mt * p.FT;
-    const float *Pn = p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * pcs + (int64_t)m0 * V;
-    const int plim = pcs - m0 * V;
+    const __amdgpu_buffer_rsrc_t rs_p =
+        make_rsrc(p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * pcs, (int64_t)prow_lim * pcs);
+    const int fl = p.M - m0;  // frames left in this clip
     int row = prow_i, o = po_i;
     for (int E0 = wave * 64; E0 < PSZ; E0 += 256) {
-      const bool ok = row < 64 && o < ncols && o < plim && row < prow_lim;
-      glds_f32(ok ? Pn + (int64_t)row * pcs + o : g_zero_page, Ps + E0);
+      const int mf = o / Vp, v = o - mf * Vp;
+      const bool ok = row < prow_lim && o < ncols && v < V && mf < fl;
+      blds_f32(rs_p, ok ? (unsigned)(row * pcs + (m0 + mf) * V + v) * 4u : kOOB, Ps + E0);
       o += dpo;
       row += dpr;
       if (o >= PP) {
@@ -393,13 +402,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
       }
     }
     const int qg0 = (p.s_in * m0 + p.off) * V;
-    const float *Qn = p.Q + (int64_t)n * p.q_bstride + (int64_t)c_lo * qcs;
+    const __amdgpu_buffer_rsrc_t rs_q =
+        make_rsrc(p.Q + (int64_t)n * p.q_bstride + (int64_t)c_lo * qcs, (int64_t)nc * qcs);
     row = qrow_i;
     o = qo_i;
     for (int E0 = wave * 64; E0 < QSZ; E0 += 256) {
       const int g = qg0 + o;
       const bool ok = row < nc && o < span && g >= 0 && g < qcs;
-      glds_f32(ok ? Qn + (int64_t)row * qcs + g : g_zero_page, Qs + E0);
+      blds_f32(rs_q, ok ? (unsigned)(row * qcs + g) * 4u : kOOB, Qs + E0);
       o += dqo;
       row += dqr;
       if (o >= QP) {
@@ -409,6 +419,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
     }
   };
 
+  const int hv = Vp / 2;  // k-steps per frame
   if (it0 < it1) stage(it0, Ps0, Qs0);
   __syncthreads();
   for (int it = it0; it < it1; ++it) {
@@ -416,18 +427,16 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
     const float *Ps = odd ? Ps1 : Ps0;
     const float *Qs = odd ? Qs1 : Qs0;
     if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
-    const float *pa = Ps + (mi * 32 + lo) * PP;
-    int col = hi, mf = 0, v = hi;
-    for (int kk = 0; kk < nk; ++kk) {
-      const float a = pa[col];
-      const int bq = (mf < p.FT) ? p.s_in * mf * V + v : 0;
+    const float *pa = Ps + (mi * 32 + lo) * PP + hi;
+    const float *qb = Qs + hi;
+    for (int mf = 0; mf < p.FT; ++mf) {
+      const float *pf = pa + mf * Vp;
+      const float *qf = qb + p.s_in * mf * V;
+#pragma unroll 3
+      for (int k = 0; k < hv; ++k) {
+        const float a = pf[2 * k];
 #pragma unroll
-      for (int t = 0; t < NJW; ++t) acc[t] = mfma32(a, Qs[qoff[t] + bq], acc[t]);
-      col += 2;
-      v += 2;
-      if (v >= V) {
-        v -= V;
-        ++mf;
+        for (int t = 0; t < NJW; ++t) acc[t] = mfma32(a, qf[qoff[t] + 2 * k], acc[t]);
       }
     }
     __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
@@ -445,21 +454,20 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
 
 static int wgrad_jt(int NQ) { return NQ == 1 ? 128 : 192; }
 
-static void wgrad_geom(const WgradParams &p, int &PP, int &nc, int &span) {
+static void wgrad_geom(const WgradParams &p, int &PP, int &nc, int &QP) {
   const int JT = wgrad_jt(p.NQ);
-  const int ncols = p.FT * p.V;
-  PP = (2 * ((ncols + 1) / 2)) | 1;
+  PP = (p.FT * ((p.V + 1) & ~1)) | 1;
   nc = JT / p.NQ + 2;
   if (nc > p.C) nc = p.C;
-  span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
+  QP = ((p.s_in * (p.FT - 1) + p.NQ) * p.V + 2) | 1;
 }
 
 int wgrad_ntiles_j(int C, int NQ) { return (C * NQ + wgrad_jt(NQ) - 1) / wgrad_jt(NQ); }
 
 size_t wgrad_lds_bytes(const WgradParams &p) {
-  int PP, nc, span;
-  wgrad_geom(p, PP, nc, span);
-  return sizeof(float) * 2 * (round64(64 * PP) + round64((nc + 1) * (span | 1)));
+  int PP, nc, QP;
+  wgrad_geom(p, PP, nc, QP);
+  return sizeof(float) * 2 * (round64(64 * PP) + round64((nc + 1) * QP));
 }
 
 bool wgrad_supported(const WgradParams &p) { return wgrad_lds_bytes(p) <= 160 * 1024; }
