@@ -97,6 +97,35 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   return w;
 }
 
+// Temporal-conv weight gradient plan (k_wgrad_taps): dWt = sum dU (x) Z(shifted).
+WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float *Z,
+                            float *slab) {
+  const int R = d->C_out;
+  WgradParams w{};
+  w.P = dU;
+  w.Q = Z;
+  w.slab = slab;
+  w.p_bstride = (int64_t)R * d->T_out * d->V;
+  w.q_bstride = (int64_t)R * d->T * d->V;
+  w.R = R;
+  w.C = R;
+  w.NQ = 9;
+  w.s_in = d->stride;
+  w.off = -d->pad;
+  w.M = d->T_out;
+  w.T_src = d->T;
+  w.V = d->V;
+  w.N = d->N;
+  w.FT = std::max(1, 80 / d->V);
+  while (w.FT > 1 && !wgrad_taps_supported(w)) --w.FT;
+  w.n_mtiles = (w.M + w.FT - 1) / w.FT;
+  w.n_rtiles = (R + 63) / 64;
+  w.n_jtiles = (R + wgrad_taps_cb(w) - 1) / wgrad_taps_cb(w);
+  const int tiles = w.n_rtiles * w.n_jtiles;
+  w.S = std::max(1, std::min((256 + tiles - 1) / tiles, d->N * w.n_mtiles));
+  return w;
+}
+
 struct BwdLayout {
   double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
   float *dU, *dZ, *G, *H, *slab, *wpk;
@@ -118,8 +147,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.dZ = c.take<float>((size_t)d->N * R * nT(d));
   L.G = c.take<float>((size_t)d->N * K * C * nT(d));
   L.H = c.take<float>((size_t)d->N * K * C * nT(d));
-  WgradParams w1 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, R, d->T, 9, d->stride,
-                              -d->pad, nullptr);
+  WgradParams w1 = make_wgrad_taps(d, nullptr, nullptr, nullptr);
   WgradParams w2 =
       make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
   const size_t s1 = (size_t)w1.S * R * R * 9, s2 = (size_t)w2.S * R * K * C;
@@ -171,10 +199,9 @@ void conv_tiles(ConvGemmParams &p) {
 // Every GEMM launch of the block fits its LDS budget.
 static bool geometry_supported(const stgcn_desc_t *d) {
   const int R = d->C_out, C = d->C_in, K = d->K;
-  WgradParams w1 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, R, d->T, 9, d->stride,
-                              -d->pad, nullptr);
+  WgradParams w1 = make_wgrad_taps(d, nullptr, nullptr, nullptr);
   WgradParams w2 = make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
-  if (!wgrad_supported(w1) || !wgrad_supported(w2)) return false;
+  if (!wgrad_taps_supported(w1) || !wgrad_supported(w2)) return false;
   ConvGemmParams p = conv_base(d, nullptr);
   p.NQ = 9;
   p.s_in = d->stride;
@@ -385,9 +412,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   // Temporal conv weight-gradient: dWt[co][ci][q] = sum dU[co] * Z[ci](shifted)
   {
-    WgradParams w = make_wgrad(d, L.dU, (int64_t)R * To * V, R, To, a->Z, (int64_t)R * T * V, R,
-                               T, 9, d->stride, -d->pad, L.slab);
-    HIP_TRY(launch_wgrad(w, s));
+    WgradParams w = make_wgrad_taps(d, L.dU, a->Z, L.slab);
+    HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * R * 9, a->dWt, 0, R, 1, R, s));
   }
   // Spatial conv backward. Recompute G = BN1(x) A^T, then
@@ -529,8 +555,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
   } else if (which == 2) {
     const float *dU = c.take<float>((size_t)N * R * To * V);
     const float *Z = c.take<float>((size_t)N * R * T * V);
-    WgradParams w = make_wgrad(d, dU, (int64_t)R * To * V, R, To, Z, (int64_t)R * T * V, R, T, 9,
-                               d->stride, -d->pad, nullptr);
+    WgradParams w = make_wgrad_taps(d, dU, Z, nullptr);
     w.slab = c.take<float>((size_t)w.S * R * R * 9);
     P.wp = w;
     P.wgrad = true;
@@ -582,7 +607,7 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
   if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
   hipStream_t s = (hipStream_t)stream;
   auto launch = [&]() -> hipError_t {
-    if (P.wgrad) return launch_wgrad(P.wp, s);
+    if (P.wgrad) return launch_wgrad_taps(P.wp, s);
     for (int i = 0; i < P.ncp; ++i) {
       hipError_t e = launch_conv_gemm(P.cp[i], s);
       if (e != hipSuccess) return e;

@@ -49,6 +49,12 @@ struct WgradParams {
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s);
+// Temporal-conv weight gradient (NQ = 9) with taps-inner tiles; n_jtiles
+// counts channel blocks of wgrad_taps_cb(p) channels. Slab = (R, C, 9).
+hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s);
+int wgrad_taps_cb(const WgradParams &p);
+size_t wgrad_taps_lds_bytes(const WgradParams &p);
+bool wgrad_taps_supported(const WgradParams &p);
 size_t conv_gemm_lds_bytes(const ConvGemmParams &p);
 size_t conv_gemm_wpk_floats(const ConvGemmParams &p);
 bool conv_gemm_supported(const ConvGemmParams &p);

@@ -229,6 +229,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
     cv[j] = v;
     ocol[j] = (int64_t)(p.s_out * m + p.p_out) * V + v;
   }
+  // per-lane partial BN statistics (fp64 over this lane's 4 columns), summed
+  // across lanes and waves through LDS (the staging buffers are free now).
+  double *red = reinterpret_cast<double *>(smem);  // [4 waves][16 regs][2][64 lanes]
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
@@ -246,15 +249,25 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
       }
     }
     if (p.stat_sum) {
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) {
-        s += __shfl_xor(s, o, 64);
-        sq += __shfl_xor(sq, o, 64);
+      red[((wave * 16 + i) * 2 + 0) * 64 + lane] = s;
+      red[((wave * 16 + i) * 2 + 1) * 64 + lane] = sq;
+    }
+  }
+  if (p.stat_sum) {
+    __syncthreads();
+    if (tid < 128) {
+      // row rl of the tile: wave halves mi = rl / 32 (waves mi and mi + 2),
+      // register i and lane half h from rl % 32 = (i&3) + 8*(i>>2) + 4*h
+      const int rl = tid >> 1, st = tid & 1;
+      const int m = rl >> 5, rr = rl & 31;
+      const int h = (rr >> 2) & 1, i = (rr & 3) + 4 * (rr >> 3);
+      double acc_s = 0.0;
+      for (int w = m; w < 4; w += 2) {
+        const double *src = red + ((w * 16 + i) * 2 + st) * 64 + h * 32;
+        for (int l = 0; l < 32; ++l) acc_s += src[l];
       }
-      if (lo == 0 && rok) {
-        atomicAdd(p.stat_sum + row, s);
-        atomicAdd(p.stat_sq + row, sq);
-      }
+      const int row = r0 + rl;
+      if (row < p.R) atomicAdd((st ? p.stat_sq : p.stat_sum) + row, acc_s);
     }
   }
 }
@@ -274,7 +287,9 @@ int conv_gemm_span(const ConvGemmParams &p) { return (p.s_in * (p.FT - 1) + p.NQ
 
 size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
   const int CK = conv_ck(p.NQ);
-  return sizeof(float) * 2 * ((size_t)CK * p.NQ * 64 + round64(CK * (conv_gemm_span(p) | 1)));
+  const size_t stage = sizeof(float) * 2 * ((size_t)CK * p.NQ * 64 + round64(CK * (conv_gemm_span(p) | 1)));
+  const size_t stats = sizeof(double) * 4 * 16 * 2 * 64;  // epilogue reduction buffer
+  return stage > stats ? stage : stats;
 }
 
 bool conv_gemm_supported(const ConvGemmParams &p) {
@@ -427,18 +442,37 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
     const float *Ps = odd ? Ps1 : Ps0;
     const float *Qs = odd ? Qs1 : Qs0;
     if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
+    // k-steps walk the frame-padded P columns contiguously (A offset += 2) and
+    // the Q window of each frame (B offset += 2, jump s*V - Vp per frame).
+    // Operands of step k+1 are read before the MFMAs of step k.
     const float *pa = Ps + (mi * 32 + lo) * PP + hi;
     const float *qb = Qs + hi;
-    for (int mf = 0; mf < p.FT; ++mf) {
-      const float *pf = pa + mf * Vp;
-      const float *qf = qb + p.s_in * mf * V;
-#pragma unroll 3
-      for (int k = 0; k < hv; ++k) {
-        const float a = pf[2 * k];
+    const int nsteps = p.FT * hv;
+    const int fjump = p.s_in * V - Vp;
+    int aoff = 0, boff = 0, kin = 0;
+    float a_cur = pa[0];
+    float b_cur[NJW];
 #pragma unroll
-        for (int t = 0; t < NJW; ++t) acc[t] = mfma32(a, qf[qoff[t] + 2 * k], acc[t]);
+    for (int t = 0; t < NJW; ++t) b_cur[t] = qb[qoff[t]];
+    for (int kk = 0; kk < nsteps - 1; ++kk) {
+      aoff += 2;
+      boff += 2;
+      if (++kin == hv) {
+        kin = 0;
+        boff += fjump;
       }
+      const float a_nxt = pa[aoff];
+      float b_nxt[NJW];
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) b_nxt[t] = qb[qoff[t] + boff];
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) acc[t] = mfma32(a_cur, b_cur[t], acc[t]);
+      a_cur = a_nxt;
+#pragma unroll
+      for (int t = 0; t < NJW; ++t) b_cur[t] = b_nxt[t];
     }
+#pragma unroll
+    for (int t = 0; t < NJW; ++t) acc[t] = mfma32(a_cur, b_cur[t], acc[t]);
     __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
   }
   float *dst = p.slab + (int64_t)split * p.R * J;
@@ -450,6 +484,192 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
       const int j = j0 + (nj0 + t) * 32 + lo;
       if (row < p.R && j < J) dst[(int64_t)row * J + j] = acc[t][i];
     }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad_taps: the (9,1) temporal conv weight gradient,
+//   dWt[r][c][q] = sum_{n,m,v} P[n,r,m,v] * Q[n,c, s*m + q + off, v],
+// tile = 64 rows x CB channels x all 9 taps. 4 waves; wave w: rows
+// (w&1)*32..+31; CB=64: channels (w>>1)*32..+31, taps 0..8 (9 MFMA tiles);
+// CB=32: all 32 channels, taps (w>>1) ? 5..8 : 0..4. MFMA column tiles are
+// tap-major/channel-minor, so a B read is 32 lanes on 32 channel rows of an
+// odd-pitch image (conflict-free) and one A read feeds up to 9 MFMAs.
+// Work items (clip n, FT frames) are staged by LDS-DMA, double-buffered.
+// ---------------------------------------------------------------------------
+template <int CB>
+__global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NT = CB == 64 ? 9 : 5;  // MFMA column tiles per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hi = lane >> 5, lo = lane & 31;
+  const int nblk = gridDim.x;
+  int bid = xcd_remap(blockIdx.x, nblk);
+  const int split = bid % p.S;
+  bid /= p.S;
+  const int ct = bid % p.n_jtiles;
+  const int rt = bid / p.n_jtiles;
+  const int r0 = rt * 64, c0 = ct * CB;
+  const int V = p.V;
+  const int Vp = (V + 1) & ~1;
+  const int ncols = p.FT * Vp;
+  const int PP = ncols | 1;
+  const int span = (p.s_in * (p.FT - 1) + 9) * V;
+  const int QP = (span + 2) | 1;
+  const int PSZ = round64(64 * PP), QSZ = round64(CB * QP);
+  float *Ps0 = smem, *Qs0 = smem + PSZ;
+  float *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
+  const int mi = wave & 1;
+  const int cb = CB == 64 ? (wave >> 1) : 0;
+  const int q0 = CB == 64 ? 0 : ((wave >> 1) ? 5 : 0);
+  const int nq = CB == 64 ? 9 : ((wave >> 1) ? 4 : 5);
+  int qoff[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) qoff[t] = (cb * 32 + lo) * QP + (q0 + t) * V;
+  floatx16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  const int total = p.N * p.n_mtiles;
+  const int per = (total + p.S - 1) / p.S;
+  const int it0 = split * per;
+  int it1 = it0 + per;
+  if (it1 > total) it1 = total;
+  const int pcs = p.M * V;
+  const int qcs = p.T_src * V;
+  const int prow_lim = min(64, p.R - r0);
+  const int crow_lim = min(CB, p.C - c0);
+  // P staging: per-lane element list is the same for every item; precompute
+  // packed (offset | frame << 26), -1 when statically out of range.
+  constexpr int MAXPE = 24;  // >= ceil(64 * PP / 256) for PP <= 95
+  int ppk[MAXPE];
+  const int npe = (PSZ - wave * 64 + 255) / 256;
+  {
+#pragma unroll
+    for (int i = 0; i < MAXPE; ++i) {
+      const int e = (i * 4 + wave) * 64 + lane;
+      const int row = e / PP, o = e - row * PP;
+      const int mf = o / Vp, v = o - mf * Vp;
+      const bool ok = i < npe && row < prow_lim && o < ncols && v < V;
+      ppk[i] = ok ? ((row * pcs + mf * V + v) | (mf << 26)) : -1;
+    }
+  }
+  const int qrow_i = (wave * 64 + lane) / QP, qo_i = (wave * 64 + lane) - qrow_i * QP;
+  const int dqr = 256 / QP, dqo = 256 - dqr * QP;
+
+  auto stage = [&](int it, float *Ps, float *Qs) {
+    const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
+    const int m0 = mt * p.FT;
+    const int fl = p.M - m0;
+    const __amdgpu_buffer_rsrc_t rs_p =
+        make_rsrc(p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * pcs, (int64_t)prow_lim * pcs);
+    const int m0V = m0 * V;
+#pragma unroll
+    for (int i = 0; i < MAXPE; ++i) {
+      if (i < npe) {
+        const int pk = ppk[i];
+        const bool ok = pk >= 0 && (pk >> 26) < fl;
+        blds_f32(rs_p, ok ? (unsigned)((pk & 0x3ffffff) + m0V) * 4u : kOOB,
+                 Ps + (i * 4 + wave) * 64);
+      }
+    }
+    const int qg0 = (p.s_in * m0 + p.off) * V;
+    const __amdgpu_buffer_rsrc_t rs_q =
+        make_rsrc(p.Q + (int64_t)n * p.q_bstride + (int64_t)c0 * qcs, (int64_t)crow_lim * qcs);
+    int row = qrow_i, o = qo_i;
+    for (int E0 = wave * 64; E0 < QSZ; E0 += 256) {
+      const int g = qg0 + o;
+      const bool ok = row < crow_lim && o < span && g >= 0 && g < qcs;
+      blds_f32(rs_q, ok ? (unsigned)(row * qcs + g) * 4u : kOOB, Qs + E0);
+      o += dqo;
+      row += dqr;
+      if (o >= QP) {
+        o -= QP;
+        ++row;
+      }
+    }
+  };
+
+  const int hv = Vp / 2;
+  const int nsteps = p.FT * hv;
+  const int fjump = p.s_in * V - Vp;
+  if (it0 < it1) stage(it0, Ps0, Qs0);
+  __syncthreads();
+  for (int it = it0; it < it1; ++it) {
+    const bool odd = (it - it0) & 1;
+    const float *Ps = odd ? Ps1 : Ps0;
+    const float *Qs = odd ? Qs1 : Qs0;
+    if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
+    const float *pa = Ps + (mi * 32 + lo) * PP + hi;
+    const float *qb = Qs + hi;
+    int aoff = 0, boff = 0, kin = 0;
+    float a_cur = pa[0];
+    float b_cur[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b_cur[t] = qb[qoff[t]];
+    for (int kk = 0; kk < nsteps; ++kk) {
+      const bool more = kk + 1 < nsteps;
+      aoff += 2;
+      boff += 2;
+      if (++kin == hv) {
+        kin = 0;
+        boff += fjump;
+      }
+      float a_nxt = 0.f, b_nxt[NT];
+      if (more) {
+        a_nxt = pa[aoff];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b_nxt[t] = qb[qoff[t] + boff];
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t < nq) acc[t] = mfma32(a_cur, b_cur[t], acc[t]);
+      a_cur = a_nxt;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b_cur[t] = b_nxt[t];
+    }
+    __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
+  }
+  // slab layout = the Conv2d weight (R, C, 9)
+  float *dst = p.slab + (int64_t)split * p.R * p.C * 9;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (t >= nq) continue;
+    const int c = c0 + cb * 32 + lo;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+      if (row < p.R && c < p.C) dst[((int64_t)row * p.C + c) * 9 + q0 + t] = acc[t][i];
+    }
+  }
+}
+
+int wgrad_taps_cb(const WgradParams &p) { return p.V > 32 ? 32 : 64; }
+
+size_t wgrad_taps_lds_bytes(const WgradParams &p) {
+  const int CB = wgrad_taps_cb(p);
+  const int Vp = (p.V + 1) & ~1;
+  const int PP = (p.FT * Vp) | 1;
+  const int QP = ((p.s_in * (p.FT - 1) + 9) * p.V + 2) | 1;
+  return sizeof(float) * 2 * (round64(64 * PP) + round64(CB * QP));
+}
+
+bool wgrad_taps_supported(const WgradParams &p) {
+  const int Vp = (p.V + 1) & ~1;
+  const int PP = (p.FT * Vp) | 1;
+  return p.NQ == 9 && (64 * PP + 255) / 256 <= 24 && wgrad_taps_lds_bytes(p) <= 160 * 1024;
+}
+
+hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s) {
+  if (!wgrad_taps_supported(p)) return hipErrorInvalidValue;
+  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  const size_t lds = wgrad_taps_lds_bytes(p);
+  if (wgrad_taps_cb(p) == 64)
+    hipLaunchKernelGGL((k_wgrad_taps<64>), dim3(nblk), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL((k_wgrad_taps<32>), dim3(nblk), dim3(256), lds, s, p);
+  return hipGetLastError();
 }
 
 static int wgrad_jt(int NQ) { return NQ == 1 ? 128 : 192; }
