@@ -73,28 +73,64 @@ def cpu_baseline(cfg, seconds=12.0):
                       f"(T=300, V=18, K=1, 400 classes), {threads} threads, {dt:.1f}s"}
 
 
-def kernel_roofline(pkg, device, iters=20):
-    """Average launch time of the dominant kernel (temporal (9,1) conv forward
-    of layer 1, 64->64, N=128, T=300, V=18) timed with HIP events on the stream
-    it runs on, through the library's timing entry point."""
+# cfg2 stack layers (lightning_model.py:65-86): (C_in, C_out, T_in, stride)
+def stack_layers(cfg):
+    out, c, t = [], cfg["C"], cfg["T"]
+    for co, s in [(64, 1), (64, 1), (64, 1), (64, 1), (128, 2), (128, 1), (128, 1),
+                  (256, 2), (256, 1), (256, 1)]:
+        out.append((c, co, t, s))
+        c, t = co, (t - 1) // s + 1
+    return out
+
+
+KERNEL_KINDS = {0: "tconv_fwd", 1: "tconv_dgrad", 2: "tconv_wgrad", 3: "spatial_gemm"}
+
+
+def kernel_roofline(pkg, device, cfg, iters=10):
+    """Per-kernel timing with HIP events on the launch stream (the library's
+    stgcn_time_kernel entry point, same launch parameters as the block), over
+    every layer of the stack. Returns {kind: (total_ms, total_flops, launches)}
+    and the same aggregated per kernel symbol (k_conv_gemm<9,8> = temporal
+    forward of all layers + data-grad of the stride-1 layers)."""
     import ctypes
     hl = pkg.hip_lib
     lib = hl.lib()
-    if not hasattr(lib, "stgcn_time_kernel"):
+    kinds, symbols = {}, {}
+
+    def add(d, key, ms, fl, n):
+        t = d.get(key, (0.0, 0.0, 0))
+        d[key] = (t[0] + ms, t[1] + fl, t[2] + n)
+
+    for ci, co, t, s in stack_layers(cfg):
+        d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True)
+        for which, kind in KERNEL_KINDS.items():
+            nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
+            scratch = torch.randn(nbytes // 4 + 1, device=device)
+            ms, fl = ctypes.c_float(0), ctypes.c_double(0)
+            hl.check(lib.stgcn_time_kernel(ctypes.byref(d), which, hl.ptr(scratch), nbytes, iters,
+                                           hl.stream_handle(device), ctypes.byref(ms),
+                                           ctypes.byref(fl)))
+            del scratch
+            add(kinds, kind, ms.value, fl.value, 1)
+            sym = {0: "k_conv_gemm<9,8>", 1: "k_conv_gemm<9,8>" if s == 1 else "k_conv_gemm<5|4,8>",
+                   2: "k_wgrad_taps", 3: "k_conv_gemm<1,32>"}[which]
+            add(symbols, sym, ms.value, fl.value, 1 if (which != 1 or s == 1) else 2)
+    return kinds, symbols
+
+
+def traffic_from_profiles(symbol):
+    """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC pass
+    (profiles/pmc_*.json: FETCH_SIZE doubled per the gfx950 correction +
+    WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    if not files:
         return None
-    d = pkg.fused.make_desc((CFG["N"], 64, CFG["T"], CFG["V"]), 64, 1, 1, 4, 1e-5, 0.1, True)
-    res = {}
-    for which, name in ((0, "tconv_fwd"), (1, "tconv_dgrad"), (2, "tconv_wgrad"),
-                        (3, "spatial_gemm")):
-        nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
-        scratch = torch.randn(nbytes // 4 + 1, device=device)
-        ms = ctypes.c_float(0)
-        flops = ctypes.c_double(0)
-        hl.check(lib.stgcn_time_kernel(ctypes.byref(d), which, hl.ptr(scratch), nbytes, iters,
-                                       hl.stream_handle(device), ctypes.byref(ms),
-                                       ctypes.byref(flops)))
-        res[name] = (ms.value, flops.value)
-    return res
+    try:
+        data = json.load(open(files[-1]))
+        return data.get("hbm_bytes_per_launch", {}).get(symbol)
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -104,6 +140,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=CFG["N"], help="clips per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,16 +207,20 @@ def main():
             "model_tflops": round(clips * gf_clip / 1e3, 2),
             "loss": round(float(loss.item()), 5),
         }
-        rl = kernel_roofline(pkg, device)
-        if rl:
-            name = max(rl, key=lambda k: rl[k][0])
-            ms_k, fl = rl[name]
-            ach = fl / (ms_k * 1e-3) / 1e12
-            out["roofline"] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2),
-                               "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
-                               "avg_launch_ms": round(ms_k, 4),
-                               "all_kernels_ms": {k: round(v[0], 4) for k, v in rl.items()}}
+        if not args.no_roofline:
+            kinds, symbols = kernel_roofline(pkg, device, cfg)
+            sym = max(symbols, key=lambda k: symbols[k][0])
+            ms_tot, fl_tot, nl = symbols[sym]
+            ach = fl_tot / (ms_tot * 1e-3) / 1e12
+            traffic = traffic_from_profiles(sym)
+            out["roofline"] = {
+                "kernel": sym, "bound": "mfma", "achieved": round(ach, 2),
+                "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "avg_launch_ms": round(ms_tot / nl, 4), "launches_per_step": nl,
+                "per_kind_tflops": {k: round(v[1] / (v[0] * 1e-3) / 1e12, 1)
+                                    for k, v in kinds.items()},
+                "per_kind_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()}}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(out), flush=True)

@@ -6,7 +6,6 @@ NTVC -> permute -> 10 blocks -> avg_pool2d over (T, V) -> Linear.
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .network import SpatialTemporalConv
 
@@ -31,9 +30,10 @@ class STGCNStack(nn.Module):
 
     def forward_nctv(self, x):
         x = self.conv(x)
-        N = x.shape[0]
-        x = F.avg_pool2d(x, (x.shape[2], self.V))
-        x = x.view(N, x.shape[1])
+        # global average pool over (T, V) (lightning_model.py:105): a mean over
+        # the contiguous T*V axis; ROCm's avg_pool2d with a (T, V) window is a
+        # slow generic kernel (1.7 ms at N=128), the reduction is ~20 us.
+        x = x.flatten(2).mean(dim=2)
         return self.fc_layer(x)
 
     def forward(self, x):
