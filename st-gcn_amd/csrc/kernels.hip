@@ -10,6 +10,8 @@
 // Wave size is 64; every block is a multiple of 64 threads.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "internal.h"
 
 namespace stgcn {
@@ -981,9 +983,488 @@ __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Joint-axis (V) contractions, one workgroup per (channel ci, clip n) slice,
+// one thread per frame row, the row's V-wide math fully unrolled (template V).
+// A is pinned in LDS with rows padded to VP (multiple of 4) and read with
+// 16-byte broadcast loads (every lane of a wave reads the same A element).
+// Slices are loaded with coalesced loads into LDS first; frames are processed
+// in chunks of TC rows.
+// ---------------------------------------------------------------------------
+template <int V>
+struct JointCfg {
+  static constexpr int VP = (V + 3) & ~3;
+};
+
+// G[n][k*C+ci][t][v] = sum_w A[k][v][w] * BN1(x)[n][ci][t][w]
+template <int V>
+__global__ __launch_bounds__(256) void k_gather2(const float *__restrict__ x,
+                                                 const float *__restrict__ mean,
+                                                 const float *__restrict__ invstd,
+                                                 const float *__restrict__ g,
+                                                 const float *__restrict__ b,
+                                                 const float *__restrict__ A, float *G, int C,
+                                                 int T, int K, int TC) {
+  constexpr int VP = JointCfg<V>::VP;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *As = smem;              // [K][V][VP]
+  float *Xs = As + K * V * VP;   // [TC][VP] BN1(x)
+  float *Os = Xs + TC * VP;      // [TC*V] output staging (coalesced stores)
+  const int ci = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < K * V * VP; i += nt) {
+    const int kv = i / VP, w = i - kv * VP;
+    As[i] = w < V ? A[kv * V + w] : 0.f;
+  }
+  const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
+  const float *xs = x + ((int64_t)n * C + ci) * T * V;
+  for (int t0 = 0; t0 < T; t0 += TC) {
+    const int tc = min(TC, T - t0);
+    __syncthreads();
+    for (int e = tid; e < tc * V; e += nt) {
+      const int r = e / V, w = e - r * V;
+      Xs[r * VP + w] = (xs[(int64_t)t0 * V + e] - mu) * a + be;
+    }
+    __syncthreads();
+    float xr[VP];
+    const int row = tid;
+    if (row < tc) {
+#pragma unroll
+      for (int w4 = 0; w4 < VP; w4 += 4) {
+        const float4 q = *reinterpret_cast<const float4 *>(Xs + row * VP + w4);
+        xr[w4] = q.x;
+        xr[w4 + 1] = q.y;
+        xr[w4 + 2] = q.z;
+        xr[w4 + 3] = q.w;
+      }
+    }
+    for (int k = 0; k < K; ++k) {
+      if (row < tc) {
+        const float *Ak = As + k * V * VP;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          float acc = 0.f;
+#pragma unroll
+          for (int w4 = 0; w4 < VP; w4 += 4) {
+            const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
+            acc = fmaf(q.x, xr[w4], acc);
+            if (w4 + 1 < V) acc = fmaf(q.y, xr[w4 + 1], acc);
+            if (w4 + 2 < V) acc = fmaf(q.z, xr[w4 + 2], acc);
+            if (w4 + 3 < V) acc = fmaf(q.w, xr[w4 + 3], acc);
+          }
+          Os[row * V + v] = acc;
+        }
+      }
+      __syncthreads();
+      float *gout = G + (((int64_t)n * K + k) * C + ci) * T * V + (int64_t)t0 * V;
+      for (int e = tid; e < tc * V; e += nt) gout[e] = Os[e];
+      __syncthreads();
+    }
+  }
+}
+
+// Per (ci, n) slice, for every frame row t:
+//   dxhat[t][w] = sum_k sum_v H[k*C+ci][t][v] * A[k][v][w]   (-> dx, if write_dx)
+//   sd[ci] += sum dxhat, sdn[ci] += sum dxhat * xnorm       (BN1 backward)
+//   dA[k][v][w] += sum_t H[k*C+ci][t][v] * BN1(x)[t][w]
+// dA is a V x V output with the slice's rows as reduction: an MFMA GEMM
+// (v_mfma_f32_32x32x2_f32, v and w padded to 32-tiles); the 4 waves split the
+// rows, their partial tiles are summed through LDS once per workgroup.
+template <int V>
+__global__ __launch_bounds__(256) void k_spatial_bwd2(
+    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
+    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
+    int K, int TC, int write_dx) {
+  constexpr int VP = JointCfg<V>::VP;
+  constexpr int NT = (V + 31) / 32;      // 32-tiles along v and along w
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double red[8];
+  float *As = smem;                 // [K][V][VP]
+  float *Hs = As + K * V * VP;      // [K][TC][V]
+  float *XRs = Hs + K * TC * V;     // [TC][VP] raw x
+  float *Os = XRs + TC * VP;        // [TC*V] dx staging (coalesced stores)
+  const int ci = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6, hi = lane >> 5, lo = lane & 31;
+  for (int i = tid; i < K * V * VP; i += nt) {
+    const int kv = i / VP, w = i - kv * VP;
+    As[i] = w < V ? A[kv * V + w] : 0.f;
+  }
+  const float mu = mean[ci], is = invstd[ci], be = b[ci], a = is * g[ci];
+  const int64_t xo = ((int64_t)n * C + ci) * T * V;
+  double s = 0.0, sn = 0.0;
+  floatx16 dacc[3][NT][NT];  // K <= 3
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+      for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dacc[k][p2][q2][i] = 0.f;
+  for (int t0 = 0; t0 < T; t0 += TC) {
+    const int tc = min(TC, T - t0);
+    __syncthreads();
+    for (int e = tid; e < tc * V; e += nt) {
+      const int r = e / V, w = e - r * V;
+      XRs[r * VP + w] = x[xo + (int64_t)t0 * V + e];
+    }
+    for (int k = 0; k < K; ++k) {
+      const float *hk = H + (((int64_t)n * K + k) * C + ci) * T * V + (int64_t)t0 * V;
+      for (int e = tid; e < tc * V; e += nt) Hs[k * TC * V + e] = hk[e];
+    }
+    __syncthreads();
+    for (int row = tid; row < tc; row += nt) {
+      float acc[VP];
+#pragma unroll
+      for (int w = 0; w < VP; ++w) acc[w] = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float *hr = Hs + (k * TC + row) * V;
+        const float *Ak = As + k * V * VP;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float h = hr[v];
+#pragma unroll
+          for (int w4 = 0; w4 < VP; w4 += 4) {
+            const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
+            acc[w4] = fmaf(h, q.x, acc[w4]);
+            acc[w4 + 1] = fmaf(h, q.y, acc[w4 + 1]);
+            acc[w4 + 2] = fmaf(h, q.z, acc[w4 + 2]);
+            acc[w4 + 3] = fmaf(h, q.w, acc[w4 + 3]);
+          }
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < V; ++w) {
+        const float xn = (XRs[row * VP + w] - mu) * is;
+        s += acc[w];
+        sn += (double)acc[w] * xn;
+        Os[row * V + w] = acc[w];
+      }
+    }
+    __syncthreads();
+    if (write_dx) {
+      float *dxo = dx + xo + (int64_t)t0 * V;
+      for (int e = tid; e < tc * V; e += nt) dxo[e] = Os[e];
+    }
+    // dA partial on MFMA: A-frag H[k][row][v], B-frag BN1(x)[row][w]; wave w
+    // takes row pairs kk = wave, wave + 4, ... (rows 2kk + hi).
+    const int nk = (tc + 1) / 2;
+    for (int k = 0; k < K; ++k) {
+      const float *hk = Hs + k * TC * V;
+      for (int kk = wave; kk < nk; kk += 4) {
+        const int r = 2 * kk + hi;
+        const bool rok = r < tc;
+#pragma unroll
+        for (int p2 = 0; p2 < NT; ++p2) {
+          const int v = p2 * 32 + lo;
+          const float av = (rok && v < V) ? hk[r * V + v] : 0.f;
+#pragma unroll
+          for (int q2 = 0; q2 < NT; ++q2) {
+            const int w = q2 * 32 + lo;
+            const float bw = (rok && w < V) ? (XRs[r * VP + w] - mu) * a + be : 0.f;
+            if (k == 0) dacc[0][p2][q2] = mfma32(av, bw, dacc[0][p2][q2]);
+            else if (k == 1) dacc[1][p2][q2] = mfma32(av, bw, dacc[1][p2][q2]);
+            else dacc[2][p2][q2] = mfma32(av, bw, dacc[2][p2][q2]);
+          }
+        }
+      }
+    }
+  }
+  // sum the 4 waves' dA tiles in LDS (reuse the staging area), one atomic each
+  __syncthreads();
+  float *dred = smem;  // [K][NT*32][NT*32]
+  const int DW = NT * 32;
+  for (int i = tid; i < K * DW * DW; i += nt) dred[i] = 0.f;
+  __syncthreads();
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+      for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int w = q2 * 32 + lo;
+          const float val = k == 0 ? dacc[0][p2][q2][i] : (k == 1 ? dacc[1][p2][q2][i]
+                                                                   : dacc[2][p2][q2][i]);
+          if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, val);  // LDS atomic
+        }
+  __syncthreads();
+  for (int i = tid; i < K * V * V; i += nt) {
+    const int k = i / (V * V), rem = i - k * V * V, v = rem / V, w = rem - v * V;
+    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
+  }
+  // BN1 partial sums (the block size is a multiple of 64)
+  s = wave_sum(s);
+  sn = wave_sum(sn);
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = s;
+    red[4 + (tid >> 6)] = sn;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int w = 0; w < nt / 64; ++w) {
+      a0 += red[w];
+      a1 += red[4 + w];
+    }
+    atomicAdd(sd + ci, a0);
+    atomicAdd(sdn + ci, a1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Flat row-parallel joint kernels: one thread per (n, ci, t) row of the whole
+// tensor (rows are contiguous in NCTV memory), RB rows per workgroup, no
+// per-slice chunk loop. A sits in LDS ([K][V][VP], 16-B broadcast reads).
+// ---------------------------------------------------------------------------
+template <int V>
+__global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
+                                                 const float *__restrict__ mean,
+                                                 const float *__restrict__ invstd,
+                                                 const float *__restrict__ g,
+                                                 const float *__restrict__ b,
+                                                 const float *__restrict__ A, float *G, int C,
+                                                 int T, int K, int64_t rows) {
+  constexpr int VP = JointCfg<V>::VP;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *As = smem;  // [K][V][VP]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < K * V * VP; i += blockDim.x) {
+    const int kv = i / VP, w = i - kv * VP;
+    As[i] = w < V ? A[kv * V + w] : 0.f;
+  }
+  __syncthreads();
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + tid;
+  if (r >= rows) return;
+  const int64_t CT = (int64_t)C * T;
+  const int64_t n = r / CT;
+  const int rem = (int)(r - n * CT);
+  const int ci = rem / T, t = rem - ci * T;
+  const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
+  const float *xr = x + r * V;
+  float xv[VP];
+#pragma unroll
+  for (int w = 0; w < VP; ++w) xv[w] = w < V ? (xr[w] - mu) * a + be : 0.f;
+  for (int k = 0; k < K; ++k) {
+    float *gout = G + ((n * K + k) * C + ci) * (int64_t)T * V + (int64_t)t * V;
+    const float *Ak = As + k * V * VP;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w4 = 0; w4 < VP; w4 += 4) {
+        const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
+        acc = fmaf(q.x, xv[w4], acc);
+        acc = fmaf(q.y, xv[w4 + 1], acc);
+        acc = fmaf(q.z, xv[w4 + 2], acc);
+        acc = fmaf(q.w, xv[w4 + 3], acc);
+      }
+      gout[v] = acc;
+    }
+  }
+}
+
+// Flat-row spatial backward (see k_spatial_bwd2 for the math). Per block:
+// dx rows, BN1 sums reduced per channel segment in LDS (rows are sorted by
+// channel), dA over the block's rows on MFMA, wave partials summed in LDS.
+template <int V>
+__global__ __launch_bounds__(256) void k_spatial_bwd3(
+    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
+    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
+    int K, int64_t rows, int write_dx) {
+  constexpr int VP = JointCfg<V>::VP;
+  constexpr int NT = (V + 31) / 32;
+  constexpr int MAXSEG = 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
+  const int RB = blockDim.x;
+  float *As = smem;                 // [K][V][VP]
+  float *Hs = As + K * V * VP;      // [K][RB][V]
+  float *XBs = Hs + K * RB * V;     // [RB][VP] BN1(x)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hi = lane >> 5, lo = lane & 31;
+  for (int i = tid; i < K * V * VP; i += RB) {
+    const int kv = i / VP, w = i - kv * VP;
+    As[i] = w < V ? A[kv * V + w] : 0.f;
+  }
+  if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
+  const int64_t r0 = (int64_t)blockIdx.x * RB;
+  const int64_t r = r0 + tid;
+  const bool live = r < rows;
+  const int64_t CT = (int64_t)C * T;
+  // channel segment of this row relative to the block's first row
+  const int64_t cfirst = (r0 / CT) * C + (int)((r0 % CT) / T);  // global (n*C + ci) of row r0
+  int64_t n = 0;
+  int ci = 0, t = 0;
+  if (live) {
+    n = r / CT;
+    const int rem = (int)(r - n * CT);
+    ci = rem / T;
+    t = rem - ci * T;
+  }
+  const int seg = live ? (int)((n * C + ci) - cfirst) : 0;
+  const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
+  __syncthreads();
+  float s = 0.f, sn = 0.f;
+  if (live) {
+    const float mu = mean[ci], is = invstd[ci], a = is * g[ci], be = b[ci];
+    const float *xr = x + r * V;
+    float xv[VP];
+#pragma unroll
+    for (int w = 0; w < VP; ++w) xv[w] = w < V ? xr[w] : 0.f;
+    float acc[VP];
+#pragma unroll
+    for (int w = 0; w < VP; ++w) acc[w] = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float *hr = H + ((n * K + k) * C + ci) * (int64_t)T * V + (int64_t)t * V;
+      const float *Ak = As + k * V * VP;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float h = hr[v];
+        Hs[(k * RB + tid) * V + v] = h;
+#pragma unroll
+        for (int w4 = 0; w4 < VP; w4 += 4) {
+          const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
+          acc[w4] = fmaf(h, q.x, acc[w4]);
+          acc[w4 + 1] = fmaf(h, q.y, acc[w4 + 1]);
+          acc[w4 + 2] = fmaf(h, q.z, acc[w4 + 2]);
+          acc[w4 + 3] = fmaf(h, q.w, acc[w4 + 3]);
+        }
+      }
+    }
+    float *dxr = dx + r * V;
+#pragma unroll
+    for (int w = 0; w < V; ++w) {
+      const float xn = (xv[w] - mu) * is;
+      s += acc[w];
+      sn = fmaf(acc[w], xn, sn);
+      if (write_dx) dxr[w] = acc[w];
+      XBs[tid * VP + w] = (xv[w] - mu) * a + be;
+    }
+  } else {
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int v = 0; v < V; ++v) Hs[(k * RB + tid) * V + v] = 0.f;
+#pragma unroll
+    for (int w = 0; w < V; ++w) XBs[tid * VP + w] = 0.f;
+  }
+  // BN1 partial sums per channel segment
+  if (seg_lds) {
+    if (live) {
+      atomicAdd(&seg_s[seg], (double)s);
+      atomicAdd(&seg_n[seg], (double)sn);
+    }
+  } else if (live) {
+    atomicAdd(sd + ci, (double)s);
+    atomicAdd(sdn + ci, (double)sn);
+  }
+  __syncthreads();
+  if (seg_lds && tid < MAXSEG) {
+    const int64_t gc = cfirst + tid;  // global (n*C + ci)
+    const int64_t rlast = min(r0 + RB, rows) - 1;
+    const int64_t glast = (rlast / CT) * C + (int)((rlast % CT) / T);
+    if (gc <= glast) {
+      const int cc = (int)(gc % C);
+      atomicAdd(sd + cc, seg_s[tid]);
+      atomicAdd(sdn + cc, seg_n[tid]);
+    }
+  }
+  // dA on MFMA over the block's rows (wave takes row pairs kk = wave, +nw, ...)
+  const int nw = RB / 64;
+  const int nk = RB / 2;
+  float *dred = XBs + RB * VP;  // [K][NT*32][NT*32] (zeroed below)
+  const int DW = NT * 32;
+  for (int i = tid; i < K * DW * DW; i += RB) dred[i] = 0.f;
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    floatx16 dacc[NT][NT];
+#pragma unroll
+    for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+      for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dacc[p2][q2][i] = 0.f;
+    const float *hk = Hs + k * RB * V;
+    for (int kk = wave; kk < nk; kk += nw) {
+      const int rr = 2 * kk + hi;
+#pragma unroll
+      for (int p2 = 0; p2 < NT; ++p2) {
+        const int v = p2 * 32 + lo;
+        const float av = v < V ? hk[rr * V + v] : 0.f;
+#pragma unroll
+        for (int q2 = 0; q2 < NT; ++q2) {
+          const int w = q2 * 32 + lo;
+          const float bw = w < V ? XBs[rr * VP + w] : 0.f;
+          dacc[p2][q2] = mfma32(av, bw, dacc[p2][q2]);
+        }
+      }
+    }
+#pragma unroll
+    for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+      for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int w = q2 * 32 + lo;
+          if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, dacc[p2][q2][i]);
+        }
+  }
+  __syncthreads();
+  for (int i = tid; i < K * V * V; i += RB) {
+    const int k = i / (V * V), rem = i - k * V * V, v = rem / V, w = rem - v * V;
+    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
+  }
+}
+
+static int bwd3_rows(int V, int K) {
+  // rows per block: 256 when the per-row LDS footprint is small, else 64
+  const int VP = (V + 3) & ~3;
+  return (K * V + VP) * 4 * 256 <= 48 * 1024 ? 256 : 64;
+}
+
+static int joint_tc(int V, int K, int bytes_per_row_extra) {
+  // rows per chunk: as many as fit ~48 KB of LDS, multiple of 64, <= 256
+  const int VP = (V + 3) & ~3;
+  const int per_row = (K * V + VP + V + bytes_per_row_extra) * 4;
+  int tc = (48 * 1024 - K * V * VP * 4) / per_row;
+  tc = tc / 64 * 64;
+  return tc < 64 ? 64 : (tc > 256 ? 256 : tc);
+}
+
+static bool joint_fast(int V) { return V == 18 || V == 25 || V == 50; }
+
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, hipStream_t s) {
+  if (joint_fast(V)) {
+    const int VP = (V + 3) & ~3;
+    const int64_t rows = (int64_t)N * C * T;
+    const size_t lds3 = sizeof(float) * (size_t)K * V * VP;
+    const dim3 grid3((unsigned)((rows + 255) / 256));
+    if (V == 18)
+      hipLaunchKernelGGL(k_gather3<18>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+    else if (V == 25)
+      hipLaunchKernelGGL(k_gather3<25>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+    else
+      hipLaunchKernelGGL(k_gather3<50>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+    return hipGetLastError();
+  }
+  if (false) {
+    const int VP = (V + 3) & ~3;
+    const int TC = joint_tc(V, 0, 0);
+    const int nt = 256;
+    const size_t lds = sizeof(float) * ((size_t)K * V * VP + (size_t)TC * VP + (size_t)TC * V);
+    const dim3 grid(C, N);
+    if (V == 18)
+      hipLaunchKernelGGL(k_gather2<18>, grid, dim3(nt), lds, s, x, mean, invstd, g, b, A, G, C, T, K, TC);
+    else if (V == 25)
+      hipLaunchKernelGGL(k_gather2<25>, grid, dim3(nt), lds, s, x, mean, invstd, g, b, A, G, C, T, K, TC);
+    else
+      hipLaunchKernelGGL(k_gather2<50>, grid, dim3(nt), lds, s, x, mean, invstd, g, b, A, G, C, T, K, TC);
+    return hipGetLastError();
+  }
   const size_t lds = sizeof(float) * ((size_t)K * V * V + kGatherTC * V);
   hipLaunchKernelGGL(k_gather_fwd, dim3((T + kGatherTC - 1) / kGatherTC, N), dim3(256), lds, s, x,
                      mean, invstd, g, b, A, G, C, T, V, K);
@@ -1118,6 +1599,45 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b, const float *A,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
                              int V, int K, int write_dx, hipStream_t s) {
+  if (joint_fast(V) && K <= 3) {
+    const int VP = (V + 3) & ~3;
+    const int RB = bwd3_rows(V, K);
+    const int64_t rows = (int64_t)N * C * T;
+    const int DW3 = (V + 31) / 32 * 32;
+    const size_t lds3 = sizeof(float) * ((size_t)K * V * VP + (size_t)K * RB * V + (size_t)RB * VP +
+                                         (size_t)K * DW3 * DW3);
+    const dim3 grid3((unsigned)((rows + RB - 1) / RB));
+    if (V == 18)
+      hipLaunchKernelGGL(k_spatial_bwd3<18>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx);
+    else if (V == 25)
+      hipLaunchKernelGGL(k_spatial_bwd3<25>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx);
+    else
+      hipLaunchKernelGGL(k_spatial_bwd3<50>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx);
+    return hipGetLastError();
+  }
+  if (false) {
+    const int VP = (V + 3) & ~3;
+    const int TC = joint_tc(V, K, 0);
+    const int nt = 256;  // dA quad ownership assumes 256 threads
+    const int DW = (V + 31) / 32 * 32;
+    const size_t lds = sizeof(float) * std::max((size_t)K * V * VP + (size_t)K * TC * V +
+                                                    (size_t)TC * VP + (size_t)TC * V,
+                                                (size_t)K * DW * DW);
+    const dim3 grid(C, N);
+    if (V == 18)
+      hipLaunchKernelGGL(k_spatial_bwd2<18>, grid, dim3(nt), lds, s, H, x, mean, invstd, g, b, A,
+                         dx, dA, sd, sdn, C, T, K, TC, write_dx);
+    else if (V == 25)
+      hipLaunchKernelGGL(k_spatial_bwd2<25>, grid, dim3(nt), lds, s, H, x, mean, invstd, g, b, A,
+                         dx, dA, sd, sdn, C, T, K, TC, write_dx);
+    else
+      hipLaunchKernelGGL(k_spatial_bwd2<50>, grid, dim3(nt), lds, s, H, x, mean, invstd, g, b, A,
+                         dx, dA, sd, sdn, C, T, K, TC, write_dx);
+    return hipGetLastError();
+  }
   if (K * V * V > 8192) return hipErrorInvalidValue;
   const size_t lds = sizeof(float) * (2 * (size_t)K * V * V + kDxTC * V + (size_t)K * kDxTC * V);
   hipLaunchKernelGGL(k_spatial_dx, dim3((T + kDxTC - 1) / kDxTC, N), dim3(256), lds, s, H, x,
