@@ -498,10 +498,13 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
 // odd-pitch image (conflict-free) and one A read feeds up to 9 MFMAs.
 // Work items (clip n, FT frames) are staged by LDS-DMA, double-buffered.
 // ---------------------------------------------------------------------------
-template <int CB>
-__global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
+template <int CB, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int NT = CB == 64 ? 9 : 5;  // MFMA column tiles per wave
+  // waves: (row half mi, channel half cb, tap group qh); CB=64/NW=8 -> 2x2x2,
+  // CB=32/NW=4 -> 2x1x2; tap groups 0..4 and 5..8
+  constexpr int NT = 5;  // MFMA column tiles per wave
+  constexpr int NTH = NW * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hi = lane >> 5, lo = lane & 31;
   const int nblk = gridDim.x;
@@ -521,9 +524,10 @@ __global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
   float *Ps0 = smem, *Qs0 = smem + PSZ;
   float *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
   const int mi = wave & 1;
-  const int cb = CB == 64 ? (wave >> 1) : 0;
-  const int q0 = CB == 64 ? 0 : ((wave >> 1) ? 5 : 0);
-  const int nq = CB == 64 ? 9 : ((wave >> 1) ? 4 : 5);
+  const int cb = CB == 64 ? ((wave >> 1) & 1) : 0;
+  const int qh = CB == 64 ? (wave >> 2) : (wave >> 1);
+  const int q0 = qh ? 5 : 0;
+  const int nq = qh ? 4 : 5;
   int qoff[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) qoff[t] = (cb * 32 + lo) * QP + (q0 + t) * V;
@@ -544,13 +548,13 @@ __global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
   const int crow_lim = min(CB, p.C - c0);
   // P staging: per-lane element list is the same for every item; precompute
   // packed (offset | frame << 26), -1 when statically out of range.
-  constexpr int MAXPE = 24;  // >= ceil(64 * PP / 256) for PP <= 95
+  constexpr int MAXPE = 24 * 4 / NW;  // >= ceil(64 * PP / NTH) for PP <= 95
   int ppk[MAXPE];
-  const int npe = (PSZ - wave * 64 + 255) / 256;
+  const int npe = (PSZ - wave * 64 + NTH - 1) / NTH;
   {
 #pragma unroll
     for (int i = 0; i < MAXPE; ++i) {
-      const int e = (i * 4 + wave) * 64 + lane;
+      const int e = (i * NW + wave) * 64 + lane;
       const int row = e / PP, o = e - row * PP;
       const int mf = o / Vp, v = o - mf * Vp;
       const bool ok = i < npe && row < prow_lim && o < ncols && v < V;
@@ -558,7 +562,7 @@ __global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
     }
   }
   const int qrow_i = (wave * 64 + lane) / QP, qo_i = (wave * 64 + lane) - qrow_i * QP;
-  const int dqr = 256 / QP, dqo = 256 - dqr * QP;
+  const int dqr = NTH / QP, dqo = NTH - dqr * QP;
 
   auto stage = [&](int it, float *Ps, float *Qs) {
     const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
@@ -573,14 +577,14 @@ __global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
         const int pk = ppk[i];
         const bool ok = pk >= 0 && (pk >> 26) < fl;
         blds_f32(rs_p, ok ? (unsigned)((pk & 0x3ffffff) + m0V) * 4u : kOOB,
-                 Ps + (i * 4 + wave) * 64);
+                 Ps + (i * NW + wave) * 64);
       }
     }
     const int qg0 = (p.s_in * m0 + p.off) * V;
     const __amdgpu_buffer_rsrc_t rs_q =
         make_rsrc(p.Q + (int64_t)n * p.q_bstride + (int64_t)c0 * qcs, (int64_t)crow_lim * qcs);
     int row = qrow_i, o = qo_i;
-    for (int E0 = wave * 64; E0 < QSZ; E0 += 256) {
+    for (int E0 = wave * 64; E0 < QSZ; E0 += NTH) {
       const int g = qg0 + o;
       const bool ok = row < crow_lim && o < span && g >= 0 && g < qcs;
       blds_f32(rs_q, ok ? (unsigned)(row * qcs + g) * 4u : kOOB, Qs + E0);
@@ -605,31 +609,45 @@ __global__ __launch_bounds__(256, 1) void k_wgrad_taps(WgradParams p) {
     if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
     const float *pa = Ps + (mi * 32 + lo) * PP + hi;
     const float *qb = Qs + hi;
+    // 2x-unrolled ping-pong operand sets: the reads of step k+1 are issued
+    // before the MFMAs of step k and land in the other register set (no
+    // rotation moves, so the wait before step k+1 covers only its own reads).
     int aoff = 0, boff = 0, kin = 0;
-    float a_cur = pa[0];
-    float b_cur[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) b_cur[t] = qb[qoff[t]];
-    for (int kk = 0; kk < nsteps; ++kk) {
-      const bool more = kk + 1 < nsteps;
+    auto advance = [&]() {
       aoff += 2;
       boff += 2;
       if (++kin == hv) {
         kin = 0;
         boff += fjump;
       }
-      float a_nxt = 0.f, b_nxt[NT];
-      if (more) {
-        a_nxt = pa[aoff];
+    };
+    float a0 = pa[0], a1 = 0.f;
+    float b0[NT], b1[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) b_nxt[t] = qb[qoff[t] + boff];
+    for (int t = 0; t < NT; ++t) b0[t] = qb[qoff[t]];
+    int kk = 0;
+    for (; kk + 1 < nsteps; kk += 2) {
+      advance();
+      a1 = pa[aoff];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b1[t] = qb[qoff[t] + boff];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        if (t < nq) acc[t] = mfma32(a0, b0[t], acc[t]);
+      if (kk + 2 < nsteps) {
+        advance();
+        a0 = pa[aoff];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b0[t] = qb[qoff[t] + boff];
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        if (t < nq) acc[t] = mfma32(a_cur, b_cur[t], acc[t]);
-      a_cur = a_nxt;
+        if (t < nq) acc[t] = mfma32(a1, b1[t], acc[t]);
+    }
+    if (kk < nsteps) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) b_cur[t] = b_nxt[t];
+      for (int t = 0; t < NT; ++t)
+        if (t < nq) acc[t] = mfma32(a0, b0[t], acc[t]);
     }
     __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
   }
@@ -668,9 +686,9 @@ hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s) {
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const size_t lds = wgrad_taps_lds_bytes(p);
   if (wgrad_taps_cb(p) == 64)
-    hipLaunchKernelGGL((k_wgrad_taps<64>), dim3(nblk), dim3(256), lds, s, p);
+    hipLaunchKernelGGL((k_wgrad_taps<64, 8>), dim3(nblk), dim3(512), lds, s, p);
   else
-    hipLaunchKernelGGL((k_wgrad_taps<32>), dim3(nblk), dim3(256), lds, s, p);
+    hipLaunchKernelGGL((k_wgrad_taps<32, 4>), dim3(nblk), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
