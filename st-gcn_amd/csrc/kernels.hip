@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "internal.h"
 
@@ -266,7 +267,187 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
       double acc_s = 0.0;
       for (int w = m; w < 4; w += 2) {
         const double *src = red + ((w * 16 + i) * 2 + st) * 64 + h * 32;
-        for (int l = 0; l < 32; ++l) acc_s += src[l];
+        // rotated start: the 32 lanes of a wave half read 32 different banks
+        for (int l = 0; l < 32; ++l) acc_s += src[(l + tid) & 31];
+      }
+      const int row = r0 + rl;
+      if (row < p.R) atomicAdd((st ? p.stat_sq : p.stat_sum) + row, acc_s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_tconv: conv_gemm specialised on the joint count V and the input stride
+// (FT = kTileCols / V frames per tile). With the image geometry known at
+// compile time every LDS operand read is (per-lane base + immediate), the
+// input DMA offsets of a lane are the same for every channel chunk (computed
+// once; the chunk and the channel bound live in the buffer resource, so the
+// last partial chunk and the temporal halo zero-fill through the hardware
+// range check), the packed-weight chunk moves in 16-byte LDS-DMA pieces, and
+// the k-loop is fully unrolled with explicitly double-buffered operands (the
+// LDS reads of step s+1 are in flight under the 4 MFMAs of step s).
+// ---------------------------------------------------------------------------
+template <int NQ, int CK, int V, int SIN>
+struct ConvGeo {
+  static constexpr int FT = kTileCols / V;
+  static constexpr int NCOLS = FT * V;
+  static constexpr int SPAN = (SIN * (FT - 1) + NQ) * V;
+  static constexpr int SP = SPAN | 1;  // odd pitch
+  static constexpr int ISZ = round64(CK * SP);
+  static constexpr int WSZ = CK * NQ * 64;
+  static constexpr int IROWS = ISZ / 64;              // 64-float DMA rows of the input image
+  static constexpr int NI = (IROWS + 3) / 4;          // rows per wave (upper bound)
+  static constexpr int WROWS = WSZ / 256;             // 256-float (16 B/lane) weight rows
+  static constexpr int NS = CK / 2 * NQ;              // MFMA k-steps per chunk
+  static_assert(WSZ % 256 == 0, "weight chunk must be whole 16-byte DMA rows");
+};
+
+template <int NQ, int CK, int V, int SIN>
+__global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
+  using G = ConvGeo<NQ, CK, V, SIN>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid % p.n_rtiles;
+  bid /= p.n_rtiles;
+  const int mt = bid % p.n_mtiles;
+  const int n = bid / p.n_mtiles;
+  const int r0 = rt * kTileRows, m0 = mt * G::FT;
+  float *Ws0 = smem, *Ws1 = smem + G::WSZ;
+  float *Is0 = smem + 2 * G::WSZ, *Is1 = smem + 2 * G::WSZ + G::ISZ;
+  const int cstride = p.T_src * V;
+  const int g0 = (SIN * m0 + p.off) * V;
+  const float *inN = p.in + (int64_t)n * p.in_bstride;
+  const float *wblk = p.wpk + (int64_t)rt * p.Cpad * NQ * 64;
+  const int nchunks = (p.C + CK - 1) / CK;
+  const int mi = wave & 1;
+  const int nj0 = (wave >> 1) * 4;
+
+  int bb[4];  // per-lane LDS offset of this lane's B column (k-row hi) in the image
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    const int mf = col / V;
+    bb[j] = hi * G::SP + (col < G::NCOLS ? SIN * mf * V + (col - mf * V) : 0);
+  }
+  unsigned voff[G::NI];  // input DMA byte offsets (relative to the chunk's first channel)
+#pragma unroll
+  for (int i = 0; i < G::NI; ++i) {
+    const int e = (i * 4 + wave) * 64 + lane;
+    const int c = e / G::SP, o = e - c * G::SP;
+    const int g = g0 + o;
+    const bool ok = c < CK && o < G::SPAN && g >= 0 && g < cstride;
+    voff[i] = ok ? (unsigned)(c * cstride + g) * 4u : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(wblk, (int64_t)p.Cpad * NQ * 64);
+  auto stage = [&](int chunk, float *Ws, float *Is) {
+#pragma unroll
+    for (int k = 0; k < (G::WROWS + 3) / 4; ++k) {
+      const int r = k * 4 + wave;
+      if (r < G::WROWS)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs_w, Ws + r * 256, 16, (unsigned)(chunk * G::WSZ + r * 256 + lane * 4) * 4u, 0, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t rs_in =
+        make_rsrc(inN + (int64_t)chunk * CK * cstride, (int64_t)(p.C - chunk * CK) * cstride);
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i)
+      if (i * 4 + wave < G::IROWS) blds_f32(rs_in, voff[i], Is + (i * 4 + wave) * 64);
+  };
+
+  floatx16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+
+  stage(0, Ws0, Is0);
+  __syncthreads();
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    const bool odd = chunk & 1;
+    const float *Ws = odd ? Ws1 : Ws0;
+    const float *Is = odd ? Is1 : Is0;
+    if (chunk + 1 < nchunks) stage(chunk + 1, odd ? Ws0 : Ws1, odd ? Is0 : Is1);
+    const float *wp = Ws + hi * NQ * 64 + mi * 32 + lo;
+    const float *ib0 = Is + bb[0], *ib1 = Is + bb[1], *ib2 = Is + bb[2], *ib3 = Is + bb[3];
+    float a[2], b[2][4];
+    auto ld = [&](int s, int set) {
+      const int cp = s / NQ, q = s - cp * NQ;
+      const int bo = 2 * cp * G::SP + q * V;
+      a[set] = wp[(2 * cp * NQ + q) * 64];
+      b[set][0] = ib0[bo];
+      b[set][1] = ib1[bo];
+      b[set][2] = ib2[bo];
+      b[set][3] = ib3[bo];
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int s = 0; s < G::NS; ++s) {
+      if (s + 1 < G::NS) ld(s + 1, (s + 1) & 1);
+      const int c = s & 1;
+      acc[0] = mfma32(a[c], b[c][0], acc[0]);
+      acc[1] = mfma32(a[c], b[c][1], acc[1]);
+      acc[2] = mfma32(a[c], b[c][2], acc[2]);
+      acc[3] = mfma32(a[c], b[c][3], acc[3]);
+      // issue order per step: step s+1's 5 LDS reads, then step s's 4 MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // retires this wave's LDS-DMA (vmcnt(0)) and publishes the next chunk
+  }
+
+  // Epilogue: bias, store, optional per-row BN statistics (fp64), as k_conv_gemm.
+  float *outN = p.out + (int64_t)n * p.out_bstride;
+  const int ostride = p.T_dst * V;
+  int ocol[4], cv[4];
+  bool cok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    const int mf = col / V;
+    const int v = col - mf * V;
+    const int m = m0 + mf;
+    cok[j] = col < G::NCOLS && m < p.M;
+    cv[j] = v;
+    ocol[j] = (p.s_out * m + p.p_out) * V + v;
+  }
+  double *red = reinterpret_cast<double *>(smem);  // [4 waves][16 regs][2][64 lanes]
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+    const bool rok = row < p.R;
+    const float br = (rok && p.bias_r) ? p.bias_r[row] : 0.f;
+    double s = 0.0, sq = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (rok && cok[j]) {
+        float val = acc[j][i] + br;
+        if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
+        outN[(int64_t)row * ostride + ocol[j]] = val;
+        s += val;
+        sq += (double)val * val;
+      }
+    }
+    if (p.stat_sum) {
+      red[((wave * 16 + i) * 2 + 0) * 64 + lane] = s;
+      red[((wave * 16 + i) * 2 + 1) * 64 + lane] = sq;
+    }
+  }
+  if (p.stat_sum) {
+    __syncthreads();
+    if (tid < 128) {
+      const int rl = tid >> 1, st = tid & 1;
+      const int m = rl >> 5, rr = rl & 31;
+      const int h = (rr >> 2) & 1, i = (rr & 3) + 4 * (rr >> 3);
+      double acc_s = 0.0;
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const double *src = red + (((m + 2 * w) * 16 + i) * 2 + st) * 64 + h * 32;
+#pragma unroll 8
+        for (int l = 0; l < 32; ++l) acc_s += src[(l + tid) & 31];
       }
       const int row = r0 + rl;
       if (row < p.R) atomicAdd((st ? p.stat_sq : p.stat_sum) + row, acc_s);
@@ -298,6 +479,29 @@ bool conv_gemm_supported(const ConvGemmParams &p) {
   return p.FT * p.V <= kTileCols && conv_gemm_lds_bytes(p) <= 160 * 1024;
 }
 
+template <int NQ, int CK, int V, int SIN>
+static bool launch_tconv_if(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
+  if (p.V != V || p.s_in != SIN || p.FT != ConvGeo<NQ, CK, V, SIN>::FT) return false;
+  hipLaunchKernelGGL((k_tconv<NQ, CK, V, SIN>), dim3(nblk), dim3(256), lds, s, p);
+  return true;
+}
+
+// Specialised instantiations: the joint counts of the reference's skeleton
+// graphs (coco18, body25, two-person body25) at input stride 1 (and 2 for the
+// strided temporal forward).
+template <int NQ, int CK>
+static bool launch_tconv_v(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
+  if (launch_tconv_if<NQ, CK, 18, 1>(p, nblk, lds, s)) return true;
+  if (launch_tconv_if<NQ, CK, 25, 1>(p, nblk, lds, s)) return true;
+  if (launch_tconv_if<NQ, CK, 50, 1>(p, nblk, lds, s)) return true;
+  if constexpr (NQ == 9) {
+    if (launch_tconv_if<NQ, CK, 18, 2>(p, nblk, lds, s)) return true;
+    if (launch_tconv_if<NQ, CK, 25, 2>(p, nblk, lds, s)) return true;
+    if (launch_tconv_if<NQ, CK, 50, 2>(p, nblk, lds, s)) return true;
+  }
+  return false;
+}
+
 hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
   ConvGemmParams p = p0;
   if (!conv_gemm_supported(p) || !p.wpk) return hipErrorInvalidValue;
@@ -309,6 +513,25 @@ hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   const size_t lds = conv_gemm_lds_bytes(p);
+  static const bool generic = getenv("STGCN_GENERIC_CONV") != nullptr;  // A/B measurement only
+  if (!generic) {
+    bool done = false;
+    switch (p.NQ) {
+      case 1:
+        done = launch_tconv_v<1, 32>(p, nblk, lds, s);
+        break;
+      case 4:
+        done = launch_tconv_v<4, 8>(p, nblk, lds, s);
+        break;
+      case 5:
+        done = launch_tconv_v<5, 8>(p, nblk, lds, s);
+        break;
+      case 9:
+        done = launch_tconv_v<9, 8>(p, nblk, lds, s);
+        break;
+    }
+    if (done) return hipGetLastError();
+  }
   switch (p.NQ) {
     case 1:
       hipLaunchKernelGGL((k_conv_gemm<1, 32>), dim3(nblk), dim3(256), lds, s, p);
