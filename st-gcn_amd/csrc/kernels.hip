@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "internal.h"
 
@@ -721,7 +722,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(WgradParams p) {
 // odd-pitch image (conflict-free) and one A read feeds up to 9 MFMAs.
 // Work items (clip n, FT frames) are staged by LDS-DMA, double-buffered.
 // ---------------------------------------------------------------------------
-template <int CB, int NW>
+// VT > 0: specialised on the joint count VT, input stride SIN and FTT frames
+// per item (compile-time image geometry, fully unrolled scheduled k-loop);
+// VT = 0: runtime geometry.
+template <int CB, int NW, int VT, int SIN, int FTT>
 __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // waves: (row half mi, channel half cb, tap group qh); CB=64/NW=8 -> 2x2x2,
@@ -737,11 +741,13 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   const int ct = bid % p.n_jtiles;
   const int rt = bid / p.n_jtiles;
   const int r0 = rt * 64, c0 = ct * CB;
-  const int V = p.V;
+  const int V = VT ? VT : p.V;
+  const int FT = VT ? FTT : p.FT;
+  const int s_in = VT ? SIN : p.s_in;
   const int Vp = (V + 1) & ~1;
-  const int ncols = p.FT * Vp;
+  const int ncols = FT * Vp;
   const int PP = ncols | 1;
-  const int span = (p.s_in * (p.FT - 1) + 9) * V;
+  const int span = (s_in * (FT - 1) + 9) * V;
   const int QP = (span + 2) | 1;
   const int PSZ = round64(64 * PP), QSZ = round64(CB * QP);
   float *Ps0 = smem, *Qs0 = smem + PSZ;
@@ -789,7 +795,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
 
   auto stage = [&](int it, float *Ps, float *Qs) {
     const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
-    const int m0 = mt * p.FT;
+    const int m0 = mt * FT;
     const int fl = p.M - m0;
     const __amdgpu_buffer_rsrc_t rs_p =
         make_rsrc(p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * pcs, (int64_t)prow_lim * pcs);
@@ -803,7 +809,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
                  Ps + (i * NW + wave) * 64);
       }
     }
-    const int qg0 = (p.s_in * m0 + p.off) * V;
+    const int qg0 = (s_in * m0 + p.off) * V;
     const __amdgpu_buffer_rsrc_t rs_q =
         make_rsrc(p.Q + (int64_t)n * p.q_bstride + (int64_t)c0 * qcs, (int64_t)crow_lim * qcs);
     int row = qrow_i, o = qo_i;
@@ -821,8 +827,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   };
 
   const int hv = Vp / 2;
-  const int nsteps = p.FT * hv;
-  const int fjump = p.s_in * V - Vp;
+  const int nsteps = FT * hv;
+  const int fjump = s_in * V - Vp;
   if (it0 < it1) stage(it0, Ps0, Qs0);
   __syncthreads();
   for (int it = it0; it < it1; ++it) {
@@ -832,6 +838,44 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
     if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
     const float *pa = Ps + (mi * 32 + lo) * PP + hi;
     const float *qb = Qs + hi;
+    if constexpr (VT > 0) {
+      // fully unrolled; issue order per step: step k+1's reads, then step k's MFMAs
+      constexpr int HV = ((VT + 1) & ~1) / 2, NS = FTT * HV;
+      constexpr int FJ = SIN * VT - 2 * HV;
+      const float *qb0 = qb + qoff[0], *qb1 = qb + qoff[1], *qb2 = qb + qoff[2];
+      const float *qb3 = qb + qoff[3], *qb4 = qb + qoff[4];
+      float a[2], b[2][NT];
+      auto ld = [&](int k, int set) {
+        const int bo = 2 * k + (k / HV) * FJ;
+        a[set] = pa[2 * k];
+        b[set][0] = qb0[bo];
+        b[set][1] = qb1[bo];
+        b[set][2] = qb2[bo];
+        b[set][3] = qb3[bo];
+        b[set][4] = qb4[bo];
+      };
+      // the tap count of the wave (5 or 4) is a template constant of the loop body
+      auto body = [&](auto nqc) {
+        constexpr int NQW = decltype(nqc)::value;
+        ld(0, 0);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          if (k + 1 < NS) ld(k + 1, (k + 1) & 1);
+          const int c = k & 1;
+#pragma unroll
+          for (int t = 0; t < NQW; ++t) acc[t] = mfma32(a[c], b[c][t], acc[t]);
+          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NQW, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      if (qh)
+        body(std::integral_constant<int, 4>{});
+      else
+        body(std::integral_constant<int, 5>{});
+      __syncthreads();
+      continue;
+    }
     // 2x-unrolled ping-pong operand sets: the reads of step k+1 are issued
     // before the MFMAs of step k and land in the other register set (no
     // rotation moves, so the wait before step k+1 covers only its own reads).
@@ -908,10 +952,31 @@ hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s) {
   if (!wgrad_taps_supported(p)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const size_t lds = wgrad_taps_lds_bytes(p);
+  static const bool generic = getenv("STGCN_GENERIC_CONV") != nullptr;  // A/B measurement only
+  if (!generic) {
+    // the plans make_wgrad_taps builds for the reference's graphs (FT = 80 / V,
+    // reduced until the double-buffered images fit in LDS)
+    if (p.V == 18 && p.FT == 4 && p.s_in == 1)
+      hipLaunchKernelGGL((k_wgrad_taps<64, 8, 18, 1, 4>), dim3(nblk), dim3(512), lds, s, p);
+    else if (p.V == 18 && p.FT == 3 && p.s_in == 2)
+      hipLaunchKernelGGL((k_wgrad_taps<64, 8, 18, 2, 3>), dim3(nblk), dim3(512), lds, s, p);
+    else if (p.V == 25 && p.FT == 3 && p.s_in == 1)
+      hipLaunchKernelGGL((k_wgrad_taps<64, 8, 25, 1, 3>), dim3(nblk), dim3(512), lds, s, p);
+    else if (p.V == 25 && p.FT == 1 && p.s_in == 2)
+      hipLaunchKernelGGL((k_wgrad_taps<64, 8, 25, 2, 1>), dim3(nblk), dim3(512), lds, s, p);
+    else if (p.V == 50 && p.FT == 1 && p.s_in == 1)
+      hipLaunchKernelGGL((k_wgrad_taps<32, 4, 50, 1, 1>), dim3(nblk), dim3(256), lds, s, p);
+    else if (p.V == 50 && p.FT == 1 && p.s_in == 2)
+      hipLaunchKernelGGL((k_wgrad_taps<32, 4, 50, 2, 1>), dim3(nblk), dim3(256), lds, s, p);
+    else
+      goto generic_path;
+    return hipGetLastError();
+  }
+generic_path:
   if (wgrad_taps_cb(p) == 64)
-    hipLaunchKernelGGL((k_wgrad_taps<64, 8>), dim3(nblk), dim3(512), lds, s, p);
+    hipLaunchKernelGGL((k_wgrad_taps<64, 8, 0, 1, 1>), dim3(nblk), dim3(512), lds, s, p);
   else
-    hipLaunchKernelGGL((k_wgrad_taps<32, 4>), dim3(nblk), dim3(256), lds, s, p);
+    hipLaunchKernelGGL((k_wgrad_taps<32, 4, 0, 1, 1>), dim3(nblk), dim3(256), lds, s, p);
   return hipGetLastError();
 }
 
