@@ -1,0 +1,66 @@
+"""HBM traffic per launch from a rocprofv3 PMC pass over bench.py
+(scripts/pmc_bench.sh) -> profiles/pmc_<tag>.json, read by bench.py's
+roofline `traffic` field.
+
+bytes/launch = 2 * FETCH_SIZE + WRITE_SIZE (both reported in KiB), the gfx950
+correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half the bytes of
+streamed reads). That correction is calibrated for 16-byte lanes; the block's
+kernels also read with 4-byte lanes, so the file carries a calibration row:
+k_bn_stats reads each layer input exactly once (known byte count) with
+4-byte loads.
+
+Usage: python scripts/pmc_traffic.py gpurun_out/pmcb_<tag> profiles/pmc_<tag>.json
+"""
+import csv
+import glob
+import json
+import re
+import sys
+from collections import defaultdict
+
+# bench.py cfg2 layer inputs (C_in, T) for N=128, V=18
+LAYER_IN = [(3, 300), (64, 300), (64, 300), (64, 300), (64, 300), (128, 150), (128, 150),
+            (128, 150), (256, 75), (256, 75)]
+
+
+def short(name):
+    m = re.search(r"stgcn::(\w+)(<[^>]*>)?", name)
+    if not m:
+        return None
+    return m.group(1) + (m.group(2) or "").replace(" ", "")
+
+
+def main(src, dst):
+    vals = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(src + "/*/run_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            k = short(r.get("Kernel_Name", r.get("Kernel-Name", "")))
+            if k:
+                vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
+                     "bench.py --steps 2 --warmup 1 --no-roofline",
+           "formula": "2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (bytes per launch)",
+           "hbm_bytes_per_launch": {}, "raw_kib": {}}
+    for k, cs in sorted(vals.items()):
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        fs = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
+        ws = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
+        out["hbm_bytes_per_launch"][k] = round(2 * fs * 1024 + ws * 1024)
+        out["raw_kib"][k] = {"FETCH_SIZE": round(fs, 1), "WRITE_SIZE": round(ws, 1),
+                             "launches": len(cs["FETCH_SIZE"])}
+    if "k_bn_stats" in out["raw_kib"]:
+        alg = sum(128 * c * t * 18 * 4 for c, t in LAYER_IN) / len(LAYER_IN)
+        fs = out["raw_kib"]["k_bn_stats"]["FETCH_SIZE"] * 1024
+        out["calibration_k_bn_stats"] = {
+            "algorithmic_read_bytes": round(alg), "fetch_size_bytes": round(fs),
+            "fetch_over_algorithmic": round(fs / alg, 3)}
+    # bench.py keys its dominant kernel as k_tconv<9,8,V,1>
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out.get("calibration_k_bn_stats"), indent=1))
+    for k, v in out["hbm_bytes_per_launch"].items():
+        print(f"{k:40s} {v / 1e6:10.1f} MB/launch")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

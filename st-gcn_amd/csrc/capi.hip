@@ -94,6 +94,7 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   w.n_jtiles = wgrad_ntiles_j(C, NQ);
   w.N = d->N;
   w.S = wgrad_splits(w.n_rtiles * w.n_jtiles, d->N * w.n_mtiles);
+  if (NQ == 1) plan_wgrad_sp(w);
   return w;
 }
 

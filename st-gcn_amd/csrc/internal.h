@@ -45,10 +45,16 @@ struct WgradParams {
   int T_src;  // frames of Q
   int V, FT;
   int n_mtiles, n_rtiles, n_jtiles, S, N;
+  int CT;  // k_wgrad_sp (NQ = 1): output columns per workgroup (64 or 128)
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s);
+// Plan of the NQ = 1 weight gradient (plain split-K GEMM over (n, t*V) chunks of
+// wgrad_sp_kc(CT) columns): sets CT, n_rtiles, n_jtiles, n_mtiles (chunks per
+// clip), S. Requires s_in = 1, off = 0, M = T_src.
+void plan_wgrad_sp(WgradParams &p);
+inline int wgrad_sp_kc(int CT) { return CT == 64 ? 64 : 32; }
 // Temporal-conv weight gradient (NQ = 9) with taps-inner tiles; n_jtiles
 // counts channel blocks of wgrad_taps_cb(p) channels. Slab = (R, C, 9).
 hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s);

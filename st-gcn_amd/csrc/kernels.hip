@@ -1000,14 +1000,189 @@ size_t wgrad_lds_bytes(const WgradParams &p) {
 
 bool wgrad_supported(const WgradParams &p) { return wgrad_lds_bytes(p) <= 160 * 1024; }
 
+// ---------------------------------------------------------------------------
+// k_wgrad_sp: weight gradient of the 1x1 spatial conv (NQ = 1) as a split-K GEMM
+//   slab[split][r][c] = sum_{(n, chunk) in split} sum_{l in chunk} P[n][r][l] Q[n][c][l]
+// over the L = T*V contiguous columns of each clip row, in chunks of KC. Both
+// operands are staged row-major [rows][PITCH = KC + 4] (PITCH/4 odd: each
+// 16-lane group of a ds_read_b128 hits 16 distinct 16-byte slots), by 16-byte
+// LDS-DMA when rows are 16-byte aligned, else 4-byte. One ds_read_b128 per
+// operand feeds 4 MFMAs: lane (i, h) holds k = kb + 4h + u for MFMA u, the same
+// k permutation on both operands. Workgroups of one split are consecutive in
+// the (XCD-remapped) grid, so the tiles sharing a chunk share an L2.
+// ---------------------------------------------------------------------------
+template <int CT, bool X4>
+__global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
+  constexpr int KC = CT == 64 ? 64 : 32, PITCH = KC + 4;
+  static_assert((PITCH / 4) % 2 == 1, "ds_read_b128 conflict-free pitch");
+  constexpr int PSZ = 64 * PITCH, QSZ = CT * PITCH;
+  constexpr int NJ = CT / 64;               // 32-column accumulators per wave
+  constexpr int G = X4 ? 4 : 1;             // floats per lane per DMA
+  constexpr int PN = (PSZ / G + 255) / 256;  // DMA rounds per wave (upper bound)
+  constexpr int QN = (QSZ / G + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *Ps0 = smem, *Qs0 = smem + PSZ, *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = p.n_rtiles * p.n_jtiles;
+  const int tile = bid % ntiles;
+  const int split = bid / ntiles;
+  const int ct = tile % p.n_jtiles, rt = tile / p.n_jtiles;
+  const int L = p.M * p.V;
+  const int r0 = rt * 64, c0 = ct * CT;
+  const int prow_lim = min(64, p.R - r0), qrow_lim = min(CT, p.C - c0);
+  const int total = p.N * p.n_mtiles;
+  const int per = (total + p.S - 1) / p.S;
+  const int it0 = split * per;
+  const int it1 = min(total, it0 + per);
+
+  // fixed per-lane staging map: DMA round i of this wave fills LDS floats
+  // [((i*4 + wave)*64 + lane) * G, +G) of the image
+  int poff[PN], pcol[PN], qoff[QN], qcol[QN];
+#pragma unroll
+  for (int i = 0; i < PN; ++i) {
+    const int pos = ((i * 4 + wave) * 64 + lane) * G;
+    const int row = pos / PITCH, col = pos - row * PITCH;
+    pcol[i] = col;
+    poff[i] = (pos < PSZ && col < KC && row < prow_lim) ? row * L + col : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < QN; ++i) {
+    const int pos = ((i * 4 + wave) * 64 + lane) * G;
+    const int row = pos / PITCH, col = pos - row * PITCH;
+    qcol[i] = col;
+    qoff[i] = (pos < QSZ && col < KC && row < qrow_lim) ? row * L + col : -1;
+  }
+  auto dma = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, float *lds) {
+    if constexpr (X4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, lds, 16, voff, 0, 0, 0);
+    else
+      blds_f32(rs, voff, lds);
+  };
+  auto stage = [&](int it, float *Ps, float *Qs) {
+    const int n = it / p.n_mtiles, kc = it - n * p.n_mtiles;
+    const int l0 = kc * KC, lrem = L - l0;
+    const __amdgpu_buffer_rsrc_t rs_p = make_rsrc(
+        p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * L + l0, (int64_t)prow_lim * L - l0);
+    const __amdgpu_buffer_rsrc_t rs_q = make_rsrc(
+        p.Q + (int64_t)n * p.q_bstride + (int64_t)c0 * L + l0, (int64_t)qrow_lim * L - l0);
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+      if ((i * 4 + wave) * 64 * G < PSZ) {
+        const bool ok = poff[i] >= 0 && pcol[i] < lrem;
+        dma(rs_p, ok ? (unsigned)poff[i] * 4u : kOOB, Ps + (i * 4 + wave) * 64 * G);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < QN; ++i) {
+      if ((i * 4 + wave) * 64 * G < QSZ) {
+        const bool ok = qoff[i] >= 0 && qcol[i] < lrem;
+        dma(rs_q, ok ? (unsigned)qoff[i] * 4u : kOOB, Qs + (i * 4 + wave) * 64 * G);
+      }
+    }
+  };
+
+  const int mi = wave & 1, nj = wave >> 1;
+  floatx16 acc[NJ];
+#pragma unroll
+  for (int t = 0; t < NJ; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  if (it0 < it1) stage(it0, Ps0, Qs0);
+  __syncthreads();
+  for (int it = it0; it < it1; ++it) {
+    const bool odd = (it - it0) & 1;
+    const float *Ps = odd ? Ps1 : Ps0;
+    const float *Qs = odd ? Qs1 : Qs0;
+    if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
+    const float *pa = Ps + (mi * 32 + lo) * PITCH + 4 * hi;
+    const float *qb = Qs + (nj * (CT / 2) + lo) * PITCH + 4 * hi;
+    // element-wise reads (merged into ds_read_b128 by the backend; a float4
+    // load here loses the alias info that keeps the next chunk's LDS-DMA from
+    // being waited on before these reads); k-block s+1 is read before the
+    // MFMAs of k-block s.
+    float a[2][4], b[2][NJ][4];
+    auto ld = [&](int kb, int set) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[set][u] = pa[kb + u];
+#pragma unroll
+      for (int t = 0; t < NJ; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[set][t][u] = qb[t * 32 * PITCH + kb + u];
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int s = 0; s < KC / 8; ++s) {
+      if (s + 1 < KC / 8) ld((s + 1) * 8, (s + 1) & 1);
+      const int c = s & 1;
+#pragma unroll
+      for (int t = 0; t < NJ; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[t] = mfma32(a[c][u], b[c][t][u], acc[t]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1 + NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * NJ, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // retires this wave's LDS-DMA and publishes the next chunk
+  }
+  float *dst = p.slab + (int64_t)split * p.R * p.C;
+#pragma unroll
+  for (int t = 0; t < NJ; ++t) {
+    const int c = c0 + nj * (CT / 2) + t * 32 + lo;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+      if (row < p.R && c < p.C) dst[(int64_t)row * p.C + c] = acc[t][i];
+    }
+  }
+}
+
+void plan_wgrad_sp(WgradParams &w) {
+  w.CT = w.C <= 64 ? 64 : 128;
+  const int KC = wgrad_sp_kc(w.CT);
+  const int L = w.M * w.V;
+  w.n_mtiles = (L + KC - 1) / KC;
+  w.n_rtiles = (w.R + 63) / 64;
+  w.n_jtiles = (w.C + w.CT - 1) / w.CT;
+  const int tiles = w.n_rtiles * w.n_jtiles;
+  w.S = std::max(1, std::min((512 + tiles - 1) / tiles, w.N * w.n_mtiles));
+}
+
+static hipError_t launch_wgrad_sp(const WgradParams &p, hipStream_t s) {
+  if ((p.CT != 64 && p.CT != 128) || p.n_mtiles != (p.M * p.V + wgrad_sp_kc(p.CT) - 1) /
+                                                       wgrad_sp_kc(p.CT))
+    return hipErrorInvalidValue;
+  const int64_t L = (int64_t)p.M * p.V;
+  const bool x4 = L % 4 == 0 && p.p_bstride % 4 == 0 && p.q_bstride % 4 == 0 &&
+                  ((uintptr_t)p.P & 15) == 0 && ((uintptr_t)p.Q & 15) == 0;
+  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  const int KC = wgrad_sp_kc(p.CT);
+  const size_t lds = sizeof(float) * 2 * (size_t)(64 + p.CT) * (KC + 4);
+  if (p.CT == 64) {
+    if (x4)
+      hipLaunchKernelGGL((k_wgrad_sp<64, true>), dim3(nblk), dim3(256), lds, s, p);
+    else
+      hipLaunchKernelGGL((k_wgrad_sp<64, false>), dim3(nblk), dim3(256), lds, s, p);
+  } else {
+    if (x4)
+      hipLaunchKernelGGL((k_wgrad_sp<128, true>), dim3(nblk), dim3(256), lds, s, p);
+    else
+      hipLaunchKernelGGL((k_wgrad_sp<128, false>), dim3(nblk), dim3(256), lds, s, p);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s) {
+  if (p.NQ == 1) {
+    if (p.s_in != 1 || p.off != 0 || p.M != p.T_src) return hipErrorInvalidValue;
+    return launch_wgrad_sp(p, s);
+  }
   if (!wgrad_supported(p)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const size_t lds = wgrad_lds_bytes(p);
   switch (p.NQ) {
-    case 1:
-      hipLaunchKernelGGL((k_wgrad<1, 128>), dim3(nblk), dim3(256), lds, s, p);
-      break;
     case 9:
       hipLaunchKernelGGL((k_wgrad<9, 192>), dim3(nblk), dim3(256), lds, s, p);
       break;
@@ -1017,12 +1192,24 @@ hipError_t launch_wgrad(const WgradParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
-__global__ void k_slab_reduce(const float *slab, int S, int64_t n, float *dst, int mode, int R,
-                              int K, int C) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n) return;
+// Block = 32 consecutive outputs x 8 split groups (group g sums splits
+// g, g+8, ... in fp64); the 8 partials are combined in a fixed order, so the
+// result is deterministic.
+__global__ __launch_bounds__(256) void k_slab_reduce(const float *slab, int S, int64_t n,
+                                                     float *dst, int mode, int R, int K, int C) {
+  __shared__ double red[8][33];
+  const int o = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t idx = (int64_t)blockIdx.x * 32 + o;
   double s = 0.0;
-  for (int k = 0; k < S; ++k) s += slab[(int64_t)k * n + idx];
+  if (idx < n) {
+#pragma unroll 8
+    for (int k = g; k < S; k += 8) s += slab[(int64_t)k * n + idx];
+  }
+  red[g][o] = s;
+  __syncthreads();
+  if (g != 0 || idx >= n) return;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) s += red[j][o];
   int64_t d = idx;
   if (mode == 1) {  // idx = co*(K*C) + k*C + ci  ->  (k*R + co)*C + ci
     const int64_t KC = (int64_t)K * C;
@@ -1035,7 +1222,7 @@ __global__ void k_slab_reduce(const float *slab, int S, int64_t n, float *dst, i
 
 hipError_t launch_slab_reduce(const float *slab, int S, int64_t n, float *dst, int mode, int R,
                               int K, int C, hipStream_t s) {
-  const int nb = (int)((n + 255) / 256);
+  const int nb = (int)((n + 31) / 32);
   hipLaunchKernelGGL(k_slab_reduce, dim3(nb), dim3(256), 0, s, slab, S, n, dst, mode, R, K, C);
   return hipGetLastError();
 }
