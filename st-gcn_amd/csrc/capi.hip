@@ -47,7 +47,8 @@ int wgrad_ft(int V) { return std::max(1, 80 / V); }
 size_t wpk_floats(const stgcn_desc_t *d) {
   const int rows = std::max(d->C_out, d->C_in);
   const int red = std::max(d->C_out, d->K * d->C_in);
-  return (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32) * 9;
+  // reduction padded to a whole number of chunks for any chunk size <= 32
+  return (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32 + 32) * 9;
 }
 
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }

@@ -298,9 +298,10 @@ struct ConvGeo {
   static constexpr int WSZ = CK * NQ * 64;
   static constexpr int IROWS = ISZ / 64;              // 64-float DMA rows of the input image
   static constexpr int NI = (IROWS + 3) / 4;          // rows per wave (upper bound)
-  static constexpr int WROWS = WSZ / 256;             // 256-float (16 B/lane) weight rows
+  static constexpr int WROWS = (WSZ + 255) / 256;     // 256-float (16 B/lane) weight rows
+  static constexpr int WLAST = (WSZ % 256) / 4;       // lanes of a partial last row (0: full)
   static constexpr int NS = CK / 2 * NQ;              // MFMA k-steps per chunk
-  static_assert(WSZ % 256 == 0, "weight chunk must be whole 16-byte DMA rows");
+  static_assert(CK % 2 == 0 && WSZ % 4 == 0, "k-steps pair channels; 16-byte weight pieces");
 };
 
 template <int NQ, int CK, int V, int SIN>
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
 #pragma unroll
     for (int k = 0; k < (G::WROWS + 3) / 4; ++k) {
       const int r = k * 4 + wave;
-      if (r < G::WROWS)
+      if (r < G::WROWS && (G::WLAST == 0 || r < G::WROWS - 1 || lane < G::WLAST))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rs_w, Ws + r * 256, 16, (unsigned)(chunk * G::WSZ + r * 256 + lane * 4) * 4u, 0, 0, 0);
     }
@@ -400,9 +401,14 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
     __syncthreads();  // retires this wave's LDS-DMA (vmcnt(0)) and publishes the next chunk
   }
 
-  // Epilogue: bias, store, optional per-row BN statistics (fp64), as k_conv_gemm.
-  float *outN = p.out + (int64_t)n * p.out_bstride;
+  // Epilogue: bias, store, optional per-row BN statistics (fp64). Buffer
+  // loads/stores with 32-bit offsets; masked elements get offset kOOB (loads
+  // return 0, stores are dropped), so there is no per-element branch.
   const int ostride = p.T_dst * V;
+  const __amdgpu_buffer_rsrc_t rs_o = make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
+  const __amdgpu_buffer_rsrc_t rs_b = make_rsrc(p.bias_r ? p.bias_r : p.out, p.bias_r ? p.R : 0);
+  const __amdgpu_buffer_rsrc_t rs_bv =
+      make_rsrc(p.bias_rv ? p.bias_rv : p.out, p.bias_rv ? (int64_t)p.R * V : 0);
   int ocol[4], cv[4];
   bool cok[4];
 #pragma unroll
@@ -415,51 +421,102 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
     cv[j] = v;
     ocol[j] = (p.s_out * m + p.p_out) * V + v;
   }
-  double *red = reinterpret_cast<double *>(smem);  // [4 waves][16 regs][2][64 lanes]
+  const int rowb = r0 + mi * 32 + 4 * hi;
+  auto epilogue = [&](auto stats_c) {
+    constexpr bool STATS = decltype(stats_c)::value;
+    double *red = reinterpret_cast<double *>(smem);  // [4 waves][2 halves][32]
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-    const bool rok = row < p.R;
-    const float br = (rok && p.bias_r) ? p.bias_r[row] : 0.f;
-    double s = 0.0, sq = 0.0;
+    for (int g = 0; g < 4; ++g) {  // groups of 4 accumulator registers
+      double gv[8];                // [stat][register]: partials over this lane's 4 columns
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (rok && cok[j]) {
-        float val = acc[j][i] + br;
-        if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
-        outN[(int64_t)row * ostride + ocol[j]] = val;
-        s += val;
-        sq += (double)val * val;
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = g * 4 + ii;
+        const int row = rowb + (i & 3) + 8 * (i >> 2);
+        const bool rok = row < p.R;
+        const float br = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rs_b, rok ? row * 4 : (int)kOOB, 0, 0));
+        double s = 0.0, sq = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = rok && cok[j];
+          float val = acc[j][i] + br;
+          val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o,
+                                                ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB, 0, 0);
+          if constexpr (STATS) {
+            const double dv = ok ? (double)val : 0.0;
+            s += dv;
+            sq += dv * dv;
+          }
+        }
+        gv[ii] = s;
+        gv[4 + ii] = sq;
+      }
+      if constexpr (STATS) {
+        // butterfly over the 32 lanes of the wave half (fp64): reduce-scatter
+        // the 8 values over lane bits 4, 3, 2, then all-reduce over bits 1, 0;
+        // lane lo ends with value (lo >> 2) = stat*4 + register-in-group
+#pragma unroll
+        for (int h = 16, n = 8; h >= 4; h >>= 1, n >>= 1) {
+          const bool up = lo & h;
+#pragma unroll
+          for (int v = 0; v < n / 2; ++v) {
+            const double send = up ? gv[v] : gv[v + n / 2];
+            const double keep = up ? gv[v + n / 2] : gv[v];
+            gv[v] = keep + __shfl_xor(send, h, 64);
+          }
+        }
+        gv[0] += __shfl_xor(gv[0], 2, 64);
+        gv[0] += __shfl_xor(gv[0], 1, 64);
+        if ((lo & 3) == 0) red[(wave * 2 + hi) * 32 + g * 8 + (lo >> 2)] = gv[0];
       }
     }
-    if (p.stat_sum) {
-      red[((wave * 16 + i) * 2 + 0) * 64 + lane] = s;
-      red[((wave * 16 + i) * 2 + 1) * 64 + lane] = sq;
-    }
-  }
-  if (p.stat_sum) {
-    __syncthreads();
-    if (tid < 128) {
-      const int rl = tid >> 1, st = tid & 1;
-      const int m = rl >> 5, rr = rl & 31;
-      const int h = (rr >> 2) & 1, i = (rr & 3) + 4 * (rr >> 3);
-      double acc_s = 0.0;
-#pragma unroll
-      for (int w = 0; w < 2; ++w) {
-        const double *src = red + (((m + 2 * w) * 16 + i) * 2 + st) * 64 + h * 32;
-#pragma unroll 8
-        for (int l = 0; l < 32; ++l) acc_s += src[(l + tid) & 31];
+    if constexpr (STATS) {
+      __syncthreads();
+      if (tid < 128) {
+        const int rl = tid >> 1, sqf = tid & 1;  // tile row, statistic
+        const int m = rl >> 5, rr = rl & 31;
+        const int h = (rr >> 2) & 1, i = (rr & 3) + 4 * (rr >> 3);
+        const int k = (i >> 2) * 8 + sqf * 4 + (i & 3);
+        const double tot = red[(m * 2 + h) * 32 + k] + red[((m + 2) * 2 + h) * 32 + k];
+        const int row = r0 + rl;
+        if (row < p.R) atomicAdd((sqf ? p.stat_sq : p.stat_sum) + row, tot);
       }
-      const int row = r0 + rl;
-      if (row < p.R) atomicAdd((st ? p.stat_sq : p.stat_sum) + row, acc_s);
     }
-  }
+  };
+  if (p.stat_sum)
+    epilogue(std::true_type{});
+  else
+    epilogue(std::false_type{});
 }
 
-static int conv_ck(int NQ) { return NQ == 1 ? 32 : 8; }
+
+
+static bool env_flag(const char *name) { return getenv(name) != nullptr; }
+
+// The (V, stride, NQ) combinations with a specialised k_tconv instantiation:
+// the joint counts of the reference's skeleton graphs (coco18, body25,
+// two-person body25), input stride 1 (and 2 for the strided temporal forward).
+static bool tconv_specialised(const ConvGemmParams &p) {
+  static const bool generic = env_flag("STGCN_GENERIC_CONV");  // A/B measurement only
+  if (generic) return false;
+  if (p.V != 18 && p.V != 25 && p.V != 50) return false;
+  if (p.FT != kTileCols / p.V) return false;
+  if (p.s_in == 2) return p.NQ == 9;
+  return p.s_in == 1 && (p.NQ == 1 || p.NQ == 4 || p.NQ == 5 || p.NQ == 9);
+}
+
+// Channels per reduction chunk. Specialised kernels: 8 for the spatial GEMM,
+// 4 for the temporal taps (small LDS images: 4-5 workgroups per CU; measured
+// against 16/32 and 6/8 with scripts/ck_sweep.sh).
+static int conv_ck(const ConvGemmParams &p) {
+  if (!tconv_specialised(p)) return p.NQ == 1 ? 32 : 8;
+  return p.NQ == 1 ? 8 : 4;
+}
 
 int conv_gemm_cpad(const ConvGemmParams &p) {
-  const int CK = conv_ck(p.NQ);
+  const int CK = conv_ck(p);
   return (p.C + CK - 1) / CK * CK;
 }
 
@@ -470,9 +527,10 @@ size_t conv_gemm_wpk_floats(const ConvGemmParams &p) {
 int conv_gemm_span(const ConvGemmParams &p) { return (p.s_in * (p.FT - 1) + p.NQ) * p.V; }
 
 size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
-  const int CK = conv_ck(p.NQ);
+  const int CK = conv_ck(p);
   const size_t stage = sizeof(float) * 2 * ((size_t)CK * p.NQ * 64 + round64(CK * (conv_gemm_span(p) | 1)));
-  const size_t stats = sizeof(double) * 4 * 16 * 2 * 64;  // epilogue reduction buffer
+  if (tconv_specialised(p)) return stage;  // stats partials (2 KiB) reuse the staging area
+  const size_t stats = sizeof(double) * 4 * 16 * 2 * 64;  // k_conv_gemm epilogue buffer
   return stage > stats ? stage : stats;
 }
 
@@ -487,9 +545,6 @@ static bool launch_tconv_if(const ConvGemmParams &p, int nblk, size_t lds, hipSt
   return true;
 }
 
-// Specialised instantiations: the joint counts of the reference's skeleton
-// graphs (coco18, body25, two-person body25) at input stride 1 (and 2 for the
-// strided temporal forward).
 template <int NQ, int CK>
 static bool launch_tconv_v(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
   if (launch_tconv_if<NQ, CK, 18, 1>(p, nblk, lds, s)) return true;
@@ -499,6 +554,17 @@ static bool launch_tconv_v(const ConvGemmParams &p, int nblk, size_t lds, hipStr
     if (launch_tconv_if<NQ, CK, 18, 2>(p, nblk, lds, s)) return true;
     if (launch_tconv_if<NQ, CK, 25, 2>(p, nblk, lds, s)) return true;
     if (launch_tconv_if<NQ, CK, 50, 2>(p, nblk, lds, s)) return true;
+  }
+  return false;
+}
+
+template <int NQ>
+static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t lds,
+                            hipStream_t s) {
+  if constexpr (NQ == 1) {
+    if (CK == 8) return launch_tconv_v<NQ, 8>(p, nblk, lds, s);
+  } else {
+    if (CK == 4) return launch_tconv_v<NQ, 4>(p, nblk, lds, s);
   }
   return false;
 }
@@ -514,24 +580,24 @@ hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   const size_t lds = conv_gemm_lds_bytes(p);
-  static const bool generic = getenv("STGCN_GENERIC_CONV") != nullptr;  // A/B measurement only
-  if (!generic) {
+  if (tconv_specialised(p)) {
+    const int CK = conv_ck(p);
     bool done = false;
     switch (p.NQ) {
       case 1:
-        done = launch_tconv_v<1, 32>(p, nblk, lds, s);
+        done = launch_tconv_ck<1>(p, CK, nblk, lds, s);
         break;
       case 4:
-        done = launch_tconv_v<4, 8>(p, nblk, lds, s);
+        done = launch_tconv_ck<4>(p, CK, nblk, lds, s);
         break;
       case 5:
-        done = launch_tconv_v<5, 8>(p, nblk, lds, s);
+        done = launch_tconv_ck<5>(p, CK, nblk, lds, s);
         break;
       case 9:
-        done = launch_tconv_v<9, 8>(p, nblk, lds, s);
+        done = launch_tconv_ck<9>(p, CK, nblk, lds, s);
         break;
     }
-    if (done) return hipGetLastError();
+    return done ? hipGetLastError() : hipErrorInvalidValue;
   }
   switch (p.NQ) {
     case 1:
