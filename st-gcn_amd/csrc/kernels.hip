@@ -798,7 +798,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   // CB=32/NW=4 -> 2x1x2; tap groups 0..4 and 5..8
   constexpr int NT = 5;  // MFMA column tiles per wave
   constexpr int NTH = NW * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 5, lo = lane & 31;
   const int nblk = gridDim.x;
   int bid = xcd_remap(blockIdx.x, nblk);
@@ -815,7 +816,9 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   const int PP = ncols | 1;
   const int span = (s_in * (FT - 1) + 9) * V;
   const int QP = (span + 2) | 1;
-  const int PSZ = round64(64 * PP), QSZ = round64(CB * QP);
+  // images padded to whole DMA rounds of the workgroup (every wave issues the
+  // same number of DMAs; the padding reads as zero)
+  const int PSZ = (64 * PP + NTH - 1) / NTH * NTH, QSZ = (CB * QP + NTH - 1) / NTH * NTH;
   float *Ps0 = smem, *Qs0 = smem + PSZ;
   float *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
   const int mi = wave & 1;
@@ -843,9 +846,10 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   const int crow_lim = min(CB, p.C - c0);
   // P staging: per-lane element list is the same for every item; precompute
   // packed (offset | frame << 26), -1 when statically out of range.
-  constexpr int MAXPE = 24 * 4 / NW;  // >= ceil(64 * PP / NTH) for PP <= 95
+  constexpr int MAXPE = VT ? (64 * ((FTT * ((VT + 1) & ~1)) | 1) + NTH - 1) / NTH
+                          : 24 * 4 / NW;  // >= ceil(64 * PP / NTH) for PP <= 95
   int ppk[MAXPE];
-  const int npe = (PSZ - wave * 64 + NTH - 1) / NTH;
+  const int npe = PSZ / NTH;
   {
 #pragma unroll
     for (int i = 0; i < MAXPE; ++i) {
@@ -858,6 +862,20 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
   }
   const int qrow_i = (wave * 64 + lane) / QP, qo_i = (wave * 64 + lane) - qrow_i * QP;
   const int dqr = NTH / QP, dqo = NTH - dqr * QP;
+  // Specialised geometry: the Q element list of a lane is also fixed per item;
+  // precompute packed (row*qcs + o) | (o << 21), -1 when statically out of range
+  // (qcs * 64 < 2^21 and o < 2^10 for the instantiated V, T <= 300).
+  constexpr int QN = VT ? (CB * ((((SIN * (FTT - 1) + 9) * VT) + 2) | 1) + NTH - 1) / NTH : 1;
+  int qpk[QN];
+  if constexpr (VT > 0) {
+#pragma unroll
+    for (int i = 0; i < QN; ++i) {
+      const int e = (i * NW + wave) * 64 + lane;
+      const int row = e / QP, o = e - row * QP;
+      const bool ok = row < crow_lim && o < span;
+      qpk[i] = ok ? ((row * qcs + o) | (o << 21)) : -1;
+    }
+  }
 
   auto stage = [&](int it, float *Ps, float *Qs) {
     const int n = it / p.n_mtiles, mt = it - n * p.n_mtiles;
@@ -868,7 +886,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
     const int m0V = m0 * V;
 #pragma unroll
     for (int i = 0; i < MAXPE; ++i) {
-      if (i < npe) {
+      if (VT > 0 || i < npe) {
         const int pk = ppk[i];
         const bool ok = pk >= 0 && (pk >> 26) < fl;
         blds_f32(rs_p, ok ? (unsigned)((pk & 0x3ffffff) + m0V) * 4u : kOOB,
@@ -878,6 +896,28 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
     const int qg0 = (s_in * m0 + p.off) * V;
     const __amdgpu_buffer_rsrc_t rs_q =
         make_rsrc(p.Q + (int64_t)n * p.q_bstride + (int64_t)c0 * qcs, (int64_t)crow_lim * qcs);
+    if constexpr (VT > 0) {
+      // interior items (no temporal halo outside the clip) skip the frame test
+      auto qdma = [&](auto interior_c) {
+        constexpr bool INTERIOR = decltype(interior_c)::value;
+#pragma unroll
+        for (int i = 0; i < QN; ++i) {
+          const int pk = qpk[i];
+          bool ok = pk >= 0;
+          if constexpr (!INTERIOR) {
+            const int g = qg0 + (pk >> 21);
+            ok = ok && g >= 0 && g < qcs;
+          }
+          blds_f32(rs_q, ok ? (unsigned)((pk & 0x1fffff) + qg0) * 4u : kOOB,
+                   Qs + (i * NW + wave) * 64);
+        }
+      };
+      if (qg0 >= 0 && qg0 + span <= qcs)
+        qdma(std::true_type{});
+      else
+        qdma(std::false_type{});
+      return;
+    }
     int row = qrow_i, o = qo_i;
     for (int E0 = wave * 64; E0 < QSZ; E0 += NTH) {
       const int g = qg0 + o;
@@ -1002,10 +1042,12 @@ int wgrad_taps_cb(const WgradParams &p) { return p.V > 32 ? 32 : 64; }
 
 size_t wgrad_taps_lds_bytes(const WgradParams &p) {
   const int CB = wgrad_taps_cb(p);
+  const int NTH = CB == 64 ? 512 : 256;
   const int Vp = (p.V + 1) & ~1;
   const int PP = (p.FT * Vp) | 1;
   const int QP = ((p.s_in * (p.FT - 1) + 9) * p.V + 2) | 1;
-  return sizeof(float) * 2 * (round64(64 * PP) + round64(CB * QP));
+  auto rnd = [&](int x) { return (x + NTH - 1) / NTH * NTH; };
+  return sizeof(float) * 2 * (rnd(64 * PP) + rnd(CB * QP));
 }
 
 bool wgrad_taps_supported(const WgradParams &p) {
@@ -1026,8 +1068,8 @@ hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s) {
       hipLaunchKernelGGL((k_wgrad_taps<64, 8, 18, 1, 4>), dim3(nblk), dim3(512), lds, s, p);
     else if (p.V == 18 && p.FT == 3 && p.s_in == 2)
       hipLaunchKernelGGL((k_wgrad_taps<64, 8, 18, 2, 3>), dim3(nblk), dim3(512), lds, s, p);
-    else if (p.V == 25 && p.FT == 3 && p.s_in == 1)
-      hipLaunchKernelGGL((k_wgrad_taps<64, 8, 25, 1, 3>), dim3(nblk), dim3(512), lds, s, p);
+    else if (p.V == 25 && p.FT == 2 && p.s_in == 1)
+      hipLaunchKernelGGL((k_wgrad_taps<64, 8, 25, 1, 2>), dim3(nblk), dim3(512), lds, s, p);
     else if (p.V == 25 && p.FT == 1 && p.s_in == 2)
       hipLaunchKernelGGL((k_wgrad_taps<64, 8, 25, 2, 1>), dim3(nblk), dim3(512), lds, s, p);
     else if (p.V == 50 && p.FT == 1 && p.s_in == 1)
