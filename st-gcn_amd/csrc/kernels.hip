@@ -1866,6 +1866,70 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
   }
 }
 
+// k_gather4: k_gather3 with the block's rows moved through LDS: the 256 rows
+// of a block are contiguous in x (256*V floats; the host checks that no block
+// crosses a clip, so each partition's 256*V outputs are contiguous in G too),
+// they arrive by 16-byte LDS-DMA, each thread contracts its row from LDS (A in
+// LDS), and the outputs leave through LDS as float4 stores. (A persistent,
+// double-buffered variant measured slower: fewer workgroups per CU.)
+template <int V>
+__global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
+                                                 const float *__restrict__ mean,
+                                                 const float *__restrict__ invstd,
+                                                 const float *__restrict__ g,
+                                                 const float *__restrict__ b,
+                                                 const float *__restrict__ A, float *G, int C,
+                                                 int T, int K, int64_t rows) {
+  constexpr int VP = JointCfg<V>::VP;
+  constexpr int BF = 256 * V;  // floats of a block (a multiple of 256: V DMA rounds)
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  float *xs = smem;     // [256][V]
+  float *os = xs + BF;  // [256][V]
+  float *As = os + BF;  // [K][V][VP]
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  {
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(x + r0 * V, BF);
+    for (int i = wave; i < V; i += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, xs + i * 256, 16, (unsigned)(i * 256 + lane * 4) * 4u,
+                                               0, 0, 0);
+  }
+  for (int i = tid; i < K * V * VP; i += 256) {
+    const int kv = i / VP, w = i - kv * VP;
+    As[i] = w < V ? A[kv * V + w] : 0.f;
+  }
+  const int64_t CT = (int64_t)C * T;
+  const int64_t n0 = r0 / CT, rem0 = r0 - n0 * CT;
+  const int ci = (int)((rem0 + tid) / T);
+  const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
+  __syncthreads();
+  float xv[VP];
+#pragma unroll
+  for (int w = 0; w < VP; ++w) xv[w] = w < V ? (xs[tid * V + w] - mu) * a + be : 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float *Ak = As + k * V * VP;
+    if (k > 0) __syncthreads();  // previous partition's stores have read os
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float acc = 0.f;
+#pragma unroll
+      for (int w4 = 0; w4 < VP; w4 += 4) {
+        const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
+        acc = fmaf(q.x, xv[w4], acc);
+        acc = fmaf(q.y, xv[w4 + 1], acc);
+        acc = fmaf(q.z, xv[w4 + 2], acc);
+        acc = fmaf(q.w, xv[w4 + 3], acc);
+      }
+      os[tid * V + v] = acc;
+    }
+    __syncthreads();
+    float *dst = G + ((n0 * K + k) * CT + rem0) * V;
+    for (int e = tid; e < BF / 4; e += 256)
+      *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(os + e * 4);
+  }
+}
+
 // Flat-row spatial backward (see k_spatial_bwd2 for the math). Per block:
 // dx rows, BN1 sums reduced per channel segment in LDS (rows are sorted by
 // channel), dA over the block's rows on MFMA, wave partials summed in LDS.
@@ -2019,6 +2083,181 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
   }
 }
 
+// k_spatial_bwd4: k_spatial_bwd3 as a persistent, double-buffered kernel with
+// coalesced block traffic. Row blocks (RB rows, contiguous in x, dx and, per
+// partition k, in H: the host checks that no block crosses a clip) are
+// striped over the grid; the H planes and x of block i+1 arrive by 16-byte
+// LDS-DMA while block i is processed, dx leaves through LDS as float4 stores.
+// Per row: dx = sum_k H_k A_k and the BN1 partial sums (per channel segment);
+// dA = sum_rows H_k^T BN1(x) on MFMA, accumulated in LDS over all blocks of
+// the workgroup and added to global memory once at the end.
+template <int V>
+__global__ __launch_bounds__(256) void k_spatial_bwd4(
+    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
+    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
+    int K, int64_t rows, int write_dx) {
+  constexpr int VP = JointCfg<V>::VP;
+  constexpr int NT = (V + 31) / 32;
+  constexpr int MAXSEG = 32;
+  constexpr int DW = NT * 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
+  const int RB = blockDim.x;
+  const int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
+  const int BUF = (K + 1) * PL;               // one buffer: K H planes + x plane
+  float *As = smem + 2 * BUF;                 // [K][V][VP]
+  float *dred = As + K * V * VP;              // [K][DW][DW]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int nw = RB / 64;
+  const int64_t CT = (int64_t)C * T;
+  const int nblocks = (int)(rows / RB);
+  const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
+
+  auto stage = [&](int blk, float *buf) {
+    const int64_t r0 = (int64_t)blk * RB;
+    const int64_t n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    const int nd = PL / 256;  // DMA rounds per plane
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + r0 * V, (int64_t)RB * V);
+    for (int i = wave; i < nd; i += nw)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + K * PL + i * 256, 16,
+                                               (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+    for (int k = 0; k < K; ++k) {
+      const __amdgpu_buffer_rsrc_t rh =
+          make_rsrc(H + ((n0 * K + k) * CT + rem0) * V, (int64_t)RB * V);
+      for (int i = wave; i < nd; i += nw)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, buf + k * PL + i * 256, 16,
+                                                 (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+    }
+  };
+
+  for (int i = tid; i < K * V * VP; i += RB) {
+    const int kv = i / VP, w = i - kv * VP;
+    As[i] = w < V ? A[kv * V + w] : 0.f;
+  }
+  for (int i = tid; i < K * DW * DW; i += RB) dred[i] = 0.f;
+  int blk = blockIdx.x;
+  if (blk < nblocks) stage(blk, smem);
+  for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
+    float *buf = smem + (it & 1) * BUF;
+    float *Hs = buf, *xs = buf + K * PL;
+    if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
+    __syncthreads();  // block blk staged (vmcnt(0)); previous block fully retired
+    if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * BUF);
+    const int64_t r0 = (int64_t)blk * RB;
+    const int64_t n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    const int rem = (int)(rem0 + tid);
+    const int ci = rem / T;
+    const int64_t cfirst = n0 * C + rem0 / T;  // global (n*C + ci) of row r0
+    const int seg = (int)(n0 * C + ci - cfirst);
+    float acc[VP];
+    float s = 0.f, sn = 0.f;
+    {
+      const float mu = mean[ci], is = invstd[ci];
+      const float a = is * g[ci], be = b[ci];
+      float xv[V];
+#pragma unroll
+      for (int w = 0; w < V; ++w) xv[w] = xs[tid * V + w];
+#pragma unroll
+      for (int w = 0; w < VP; ++w) acc[w] = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float *hr = Hs + k * PL + tid * V;
+        const float *Ak = As + k * V * VP;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float h = hr[v];
+#pragma unroll
+          for (int w4 = 0; w4 < VP; w4 += 4) {
+            const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
+            acc[w4] = fmaf(h, q.x, acc[w4]);
+            acc[w4 + 1] = fmaf(h, q.y, acc[w4 + 1]);
+            acc[w4 + 2] = fmaf(h, q.z, acc[w4 + 2]);
+            acc[w4 + 3] = fmaf(h, q.w, acc[w4 + 3]);
+          }
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < V; ++w) {
+        const float xn = (xv[w] - mu) * is;
+        s += acc[w];
+        sn = fmaf(acc[w], xn, sn);
+        xs[tid * V + w] = (xv[w] - mu) * a + be;  // BN1(x), own row only
+      }
+    }
+    // BN1 partial sums per channel segment
+    if (seg_lds) {
+      atomicAdd(&seg_s[seg], (double)s);
+      atomicAdd(&seg_n[seg], (double)sn);
+    } else {
+      atomicAdd(sd + ci, (double)s);
+      atomicAdd(sdn + ci, (double)sn);
+    }
+    __syncthreads();  // BN1(x) rows and segment sums complete
+    if (seg_lds && tid < MAXSEG) {
+      const int64_t gc = cfirst + tid;  // global (n*C + ci)
+      const int64_t rlast = r0 + RB - 1;
+      const int64_t glast = (rlast / CT) * C + (int)((rlast % CT) / T);
+      if (gc <= glast) {
+        const int cc = (int)(gc % C);
+        atomicAdd(sd + cc, seg_s[tid]);
+        atomicAdd(sdn + cc, seg_n[tid]);
+      }
+    }
+    // dA partials on MFMA (wave takes row pairs kk = wave, +nw, ...), into LDS
+    const int nk = RB / 2;
+    for (int k = 0; k < K; ++k) {
+      floatx16 dacc[NT][NT];
+#pragma unroll
+      for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+        for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dacc[p2][q2][i] = 0.f;
+      const float *hk = Hs + k * PL;
+      for (int kk = wave; kk < nk; kk += nw) {
+        const int rr = 2 * kk + hi;
+#pragma unroll
+        for (int p2 = 0; p2 < NT; ++p2) {
+          const int v = p2 * 32 + lo;
+          const float av = v < V ? hk[rr * V + v] : 0.f;
+#pragma unroll
+          for (int q2 = 0; q2 < NT; ++q2) {
+            const int w = q2 * 32 + lo;
+            const float bw = w < V ? xs[rr * V + w] : 0.f;
+            dacc[p2][q2] = mfma32(av, bw, dacc[p2][q2]);
+          }
+        }
+      }
+#pragma unroll
+      for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+        for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+            const int w = q2 * 32 + lo;
+            if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, dacc[p2][q2][i]);
+          }
+    }
+    if (write_dx) {
+      __syncthreads();  // H plane 0 no longer read
+#pragma unroll
+      for (int w = 0; w < V; ++w) Hs[tid * V + w] = acc[w];
+      __syncthreads();
+      float *dst = dx + r0 * V;
+      for (int e = tid; e < RB * V / 4; e += RB)
+        *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(Hs + e * 4);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < K * V * V; i += RB) {
+    const int k = i / (V * V), rm = i - k * V * V, v = rm / V, w = rm - v * V;
+    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
+  }
+}
+
 static int bwd3_rows(int V, int K) {
   // rows per block: 256 when the per-row LDS footprint is small, else 64
   const int VP = (V + 3) & ~3;
@@ -2039,6 +2278,20 @@ static bool joint_fast(int V) { return V == 18 || V == 25 || V == 50; }
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, hipStream_t s) {
+  static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
+  const size_t lds4 = sizeof(float) * ((size_t)2 * 256 * V + (size_t)K * V * ((V + 3) & ~3));
+  if (!joint3 && joint_fast(V) && ((int64_t)C * T) % 256 == 0 && ((uintptr_t)x & 15) == 0 &&
+      ((uintptr_t)G & 15) == 0 && lds4 <= 160 * 1024) {
+    const int64_t rows = (int64_t)N * C * T;
+    const dim3 grid4((unsigned)(rows / 256));
+    if (V == 18)
+      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+    else if (V == 25)
+      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+    else
+      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+    return hipGetLastError();
+  }
   if (joint_fast(V)) {
     const int VP = (V + 3) & ~3;
     const int64_t rows = (int64_t)N * C * T;
@@ -2200,6 +2453,35 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b, const float *A,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
                              int V, int K, int write_dx, hipStream_t s) {
+  static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
+  if (!joint3 && joint_fast(V) && K <= 3 && ((int64_t)N * C * T * V) % 4 == 0 &&
+      ((uintptr_t)x & 15) == 0 && ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+    const int VP = (V + 3) & ~3;
+    const int RB = (K + 1) * V * 256 * 4 <= 40 * 1024 ? 256 : 64;
+    const int64_t CT = (int64_t)C * T;
+    if (CT % RB == 0) {
+      const int64_t rows = (int64_t)N * CT;
+      const int PL = (RB * V + 255) / 256 * 256;
+      const int DW = (V + 31) / 32 * 32;
+      const size_t lds = sizeof(float) * ((size_t)2 * (K + 1) * PL + (size_t)K * V * VP +
+                                          (size_t)K * DW * DW);
+      // persistent grid: the workgroups that fit on the chip at once
+      const int per_cu = std::max(1, std::min(8 / (RB / 64), (int)((160 * 1024) / lds)));
+      const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
+      if (lds > 160 * 1024) {
+        // too large double-buffered (V = 50 with K = 3): k_spatial_bwd3 below
+      } else if (V == 18)
+        hipLaunchKernelGGL(k_spatial_bwd4<18>, grid, dim3(RB), lds, s, H, x, mean, invstd, g, b, A,
+                           dx, dA, sd, sdn, C, T, K, rows, write_dx);
+      else if (V == 25)
+        hipLaunchKernelGGL(k_spatial_bwd4<25>, grid, dim3(RB), lds, s, H, x, mean, invstd, g, b, A,
+                           dx, dA, sd, sdn, C, T, K, rows, write_dx);
+      else
+        hipLaunchKernelGGL(k_spatial_bwd4<50>, grid, dim3(RB), lds, s, H, x, mean, invstd, g, b, A,
+                           dx, dA, sd, sdn, C, T, K, rows, write_dx);
+      if (lds <= 160 * 1024) return hipGetLastError();
+    }
+  }
   if (joint_fast(V) && K <= 3) {
     const int VP = (V + 3) & ~3;
     const int RB = bwd3_rows(V, K);
