@@ -2258,6 +2258,255 @@ __global__ __launch_bounds__(256) void k_spatial_bwd4(
   }
 }
 
+// k_spatial_bwd5: the spatial backward with both joint contractions on MFMA.
+// Persistent and double-buffered like k_spatial_bwd4 (row blocks of RB rows,
+// contiguous in x, dx and per partition in H; H planes and x by 16-byte
+// LDS-DMA). Per block:
+//   dx[row][w] = sum_k sum_v H_k[row][v] A_k[v][w]   MFMA, A_k resident in VGPRs
+//                                                    as the B operand (k = v)
+//   BN1 sums per row from the dx tile in LDS, BN1(x) in place (one thread/row)
+//   dA_k[v][w] += sum_rows H_k[row][v] BN1(x)[row][w]  MFMA, LDS accumulator
+// dx leaves through LDS as float4 stores. Requires K * ceil(V/2) * ceil(V/32)
+// <= 48 (B-operand registers) and the k_spatial_bwd4 host conditions.
+template <int V, int RB, int KMAX>
+__global__ __launch_bounds__(256) void k_spatial_bwd5(
+    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
+    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
+    int K, int64_t rows, int write_dx) {
+  constexpr int VH = (V + 1) / 2;           // MFMA k-steps over v
+  constexpr int NT = (V + 31) / 32;         // 32-column output tiles over w
+  constexpr int DW = NT * 32;
+  constexpr int MAXSEG = 32;
+  constexpr int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
+  constexpr int NRT = RB / 32;                    // 32-row tiles per block
+  constexpr bool DREG = KMAX * NT * NT <= 4;      // dA accumulators resident in VGPRs
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
+  const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
+  float *dxs = smem + 2 * BUF;   // [RB][V]
+  float *dred = dxs + PL;        // [K][DW][DW]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int CT = C * T;  // rows per clip (rows < 2^31: host check)
+  const int nblocks = (int)(rows / RB);
+  const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
+
+  // B operand of the dx GEMM: Bm[k][s][t] = A_k[v = 2s + hi][w = 32t + lo] (0 outside)
+  float Bm[KMAX][VH][NT];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+    for (int s2 = 0; s2 < VH; ++s2)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int v = 2 * s2 + hi, w = 32 * t + lo;
+        Bm[k][s2][t] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
+      }
+
+  auto stage = [&](int blk, float *buf) {
+    const int r0 = blk * RB;
+    const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    constexpr int ND = PL / 256;  // DMA rounds per plane
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + (int64_t)r0 * V, (int64_t)RB * V);
+    for (int i = wave; i < ND; i += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + K * PL + i * 256, 16,
+                                               (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+    for (int k = 0; k < K; ++k) {
+      const __amdgpu_buffer_rsrc_t rh =
+          make_rsrc(H + ((int64_t)(n0 * K + k) * CT + rem0) * V, (int64_t)RB * V);
+      for (int i = wave; i < ND; i += 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, buf + k * PL + i * 256, 16,
+                                                 (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+    }
+  };
+
+  for (int i = tid; i < K * DW * DW; i += 256) dred[i] = 0.f;
+  floatx16 dacc[DREG ? KMAX : 1][NT][NT];
+  auto zero_dacc = [&](int kd) {
+#pragma unroll
+    for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+      for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dacc[kd][p2][q2][i] = 0.f;
+  };
+#pragma unroll
+  for (int kd = 0; kd < (DREG ? KMAX : 1); ++kd) zero_dacc(kd);
+  // dacc[kd] -> dred[k] (LDS atomics), then zero
+  auto flush_dacc = [&](int k) {
+    const int kd = DREG ? k : 0;
+#pragma unroll
+    for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+      for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int w = q2 * 32 + lo;
+          if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, dacc[kd][p2][q2][i]);
+        }
+    zero_dacc(kd);
+  };
+  int blk = blockIdx.x;
+  if (blk < nblocks) stage(blk, smem);
+  for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
+    float *buf = smem + (it & 1) * BUF;
+    float *Hs = buf, *xs = buf + K * PL;
+    if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
+    __syncthreads();  // block blk staged (vmcnt(0)); previous block fully retired
+    if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * BUF);
+    const int r0 = blk * RB;
+    const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    const int cfirst = n0 * C + rem0 / T;  // global (n*C + ci) of row r0
+    // dx tile of this wave's 32 rows on MFMA (RB = 64: waves 2, 3 idle here)
+    if (wave < NRT) {
+      floatx16 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {
+          const float *hr = Hs + k * PL + (wave * 32 + lo) * V + hi;
+#pragma unroll
+          for (int s2 = 0; s2 < VH; ++s2) {
+            const float av = (2 * s2 + hi < V) ? hr[2 * s2] : 0.f;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma32(av, Bm[k][s2][t], acc[t]);
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int w = 32 * t + lo;
+          if (w < V) dxs[row * V + w] = acc[t][i];
+        }
+    }
+    __syncthreads();  // dx tile complete
+    // per row (TPR threads each, interleaved joints): BN1 sums, BN1(x) in
+    // place; per-channel-segment sums (a wave's rows usually share one
+    // channel: then one wave reduction)
+    {
+      constexpr int TPR = 256 / RB;
+      const int rl = tid / TPR, part = tid % TPR;
+      const int rem = rem0 + rl;
+      const int ci = rem / T;
+      const int seg = n0 * C + ci - cfirst;
+      const float mu = mean[ci], is = invstd[ci];
+      const float a = is * g[ci], be = b[ci];
+      float s = 0.f, sn = 0.f;
+#pragma unroll
+      for (int j = 0; j < (V + TPR - 1) / TPR; ++j) {
+        const int w = part + j * TPR;
+        if (w < V) {
+          const float xv = xs[rl * V + w], d = dxs[rl * V + w];
+          s += d;
+          sn = fmaf(d, (xv - mu) * is, sn);
+          xs[rl * V + w] = (xv - mu) * a + be;
+        }
+      }
+      const int seg0 = __builtin_amdgcn_readfirstlane(seg);
+      if (__builtin_amdgcn_ballot_w64(seg != seg0) == 0) {
+        const double ws = wave_sum((double)s), wn = wave_sum((double)sn);
+        if (lane == 0) {
+          if (seg_lds) {
+            atomicAdd(&seg_s[seg0], ws);
+            atomicAdd(&seg_n[seg0], wn);
+          } else {
+            atomicAdd(sd + ci, ws);
+            atomicAdd(sdn + ci, wn);
+          }
+        }
+      } else if (seg_lds) {
+        atomicAdd(&seg_s[seg], (double)s);
+        atomicAdd(&seg_n[seg], (double)sn);
+      } else {
+        atomicAdd(sd + ci, (double)s);
+        atomicAdd(sdn + ci, (double)sn);
+      }
+    }
+    __syncthreads();  // BN1(x) rows and segment sums complete
+    if (seg_lds && tid < MAXSEG) {
+      const int gc = cfirst + tid;  // global (n*C + ci)
+      const int rlast = r0 + RB - 1;
+      const int glast = (rlast / CT) * C + (rlast % CT) / T;
+      if (gc <= glast) {
+        const int cc = gc % C;
+        atomicAdd(sd + cc, seg_s[tid]);
+        atomicAdd(sdn + cc, seg_n[tid]);
+      }
+    }
+    // dA partials on MFMA: wave takes row pairs kk = wave + 4j; accumulators
+    // stay in registers across blocks (DREG) or are flushed per block
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        floatx16(&dk)[NT][NT] = dacc[DREG ? k : 0];
+        const float *hk = Hs + k * PL;
+#pragma unroll
+        for (int j = 0; j < RB / 8; ++j) {
+          const int rr = 2 * (wave + 4 * j) + hi;
+          float av[NT], bw[NT];
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            const int c = t * 32 + lo;
+            av[t] = c < V ? hk[rr * V + c] : 0.f;
+            bw[t] = c < V ? xs[rr * V + c] : 0.f;
+          }
+#pragma unroll
+          for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+            for (int q2 = 0; q2 < NT; ++q2) dk[p2][q2] = mfma32(av[p2], bw[q2], dk[p2][q2]);
+        }
+        if (!DREG) flush_dacc(k);
+      }
+    }
+    if (write_dx) {
+      float *dst = dx + (int64_t)r0 * V;
+      for (int e = tid; e < RB * V / 4; e += 256)
+        *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(dxs + e * 4);
+    }
+  }
+  if constexpr (DREG) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < K) flush_dacc(k);
+  }
+  __syncthreads();
+  for (int i = tid; i < K * V * V; i += 256) {
+    const int k = i / (V * V), rm = i - k * V * V, v = rm / V, w = rm - v * V;
+    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
+  }
+}
+
+template <int V, int RB>
+static size_t bwd5_lds(int K) {
+  constexpr int PL = (RB * V + 255) / 256 * 256;
+  constexpr int DW = (V + 31) / 32 * 32;
+  return sizeof(float) * ((size_t)(2 * (K + 1) + 1) * PL + (size_t)K * DW * DW);
+}
+
+template <int V, int RB, int KT>
+static bool launch_bwd5(const float *H, const float *x, const float *mean, const float *invstd,
+                        const float *g, const float *b, const float *A, float *dx, float *dA,
+                        double *sd, double *sdn, int C, int T, int K, int64_t rows,
+                        int write_dx, hipStream_t s) {
+  const size_t lds = bwd5_lds<V, RB>(K);
+  if (lds > 160 * 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
+  const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 512))));
+  const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
+  if (K != KT) return false;
+  hipLaunchKernelGGL((k_spatial_bwd5<V, RB, KT>), grid, dim3(256), lds, s, H, x, mean, invstd, g,
+                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx);
+  return true;
+}
+
 static int bwd3_rows(int V, int K) {
   // rows per block: 256 when the per-row LDS footprint is small, else 64
   const int VP = (V + 3) & ~3;
@@ -2454,8 +2703,27 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
                              int V, int K, int write_dx, hipStream_t s) {
   static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
-  if (!joint3 && joint_fast(V) && K <= 3 && ((int64_t)N * C * T * V) % 4 == 0 &&
-      ((uintptr_t)x & 15) == 0 && ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0) {
+  static const bool joint4 = env_flag("STGCN_JOINT4");  // A/B measurement only
+  const bool aligned = ((int64_t)N * C * T * V) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                       ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0;
+  if (!joint3 && !joint4 && aligned && K <= 3 && K * ((V + 1) / 2) * ((V + 31) / 32) <= 48) {
+    const int64_t rows = (int64_t)N * C * T;
+    bool done = false;
+#define STGCN_BWD5(VV, RR, KK)                                                              \
+  launch_bwd5<VV, RR, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, s)
+    // partitions K: 1 (uniform), 2 (distance), 3 (spatial) labelling
+    if (V == 18)
+      done = STGCN_BWD5(18, 128, 1) || STGCN_BWD5(18, 64, 1) || STGCN_BWD5(18, 128, 2) ||
+             STGCN_BWD5(18, 64, 2) || STGCN_BWD5(18, 128, 3) || STGCN_BWD5(18, 64, 3);
+    else if (V == 25)
+      done = STGCN_BWD5(25, 128, 1) || STGCN_BWD5(25, 64, 1) || STGCN_BWD5(25, 128, 2) ||
+             STGCN_BWD5(25, 64, 2) || STGCN_BWD5(25, 128, 3) || STGCN_BWD5(25, 64, 3);
+    else if (V == 50)
+      done = STGCN_BWD5(50, 64, 1) || STGCN_BWD5(50, 64, 2) || STGCN_BWD5(50, 64, 3);
+#undef STGCN_BWD5
+    if (done) return hipGetLastError();
+  }
+  if (!joint3 && joint_fast(V) && K <= 3 && aligned) {
     const int VP = (V + 3) & ~3;
     const int RB = (K + 1) * V * 256 * 4 <= 40 * 1024 ? 256 : 64;
     const int64_t CT = (int64_t)C * T;
