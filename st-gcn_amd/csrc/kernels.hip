@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <initializer_list>
 #include <type_traits>
 
 #include "internal.h"
@@ -1338,23 +1339,73 @@ hipError_t launch_slab_reduce(const float *slab, int S, int64_t n, float *dst, i
 // ---------------------------------------------------------------------------
 // BatchNorm kernels. One 256-thread block per (n, c) slice of L = T*V floats.
 // ---------------------------------------------------------------------------
+// Vector width VEC (1, 2, 4 floats) for the per-(n, c) slice loops: the slice
+// base (n*C + c)*L is a multiple of VEC when L is.
+template <int N>
+struct VecF;
+template <>
+struct VecF<1> {
+  using T = float;
+};
+template <>
+struct VecF<2> {
+  using T = float2;
+};
+template <>
+struct VecF<4> {
+  using T = float4;
+};
+template <int N>
+__device__ __forceinline__ void vld(const float *p, float (&v)[N]) {
+  const typename VecF<N>::T t = *reinterpret_cast<const typename VecF<N>::T *>(p);
+  __builtin_memcpy(v, &t, sizeof(t));
+}
+template <int N>
+__device__ __forceinline__ void vst(float *p, const float (&v)[N]) {
+  typename VecF<N>::T t;
+  __builtin_memcpy(&t, v, sizeof(t));
+  *reinterpret_cast<typename VecF<N>::T *>(p) = t;
+}
+
+static int slice_vec(int L, std::initializer_list<const void *> ptrs) {
+  int vec = L % 4 == 0 ? 4 : (L % 2 == 0 ? 2 : 1);
+  for (const void *q : ptrs)
+    while (vec > 1 && ((uintptr_t)q & (4 * vec - 1)) != 0) vec >>= 1;
+  return vec;
+}
+
+#define STGCN_VEC_LAUNCH(kern, vec, grid, ...)                            \
+  do {                                                                    \
+    if ((vec) == 4)                                                       \
+      hipLaunchKernelGGL((kern<4>), grid, dim3(256), 0, s, __VA_ARGS__); \
+    else if ((vec) == 2)                                                  \
+      hipLaunchKernelGGL((kern<2>), grid, dim3(256), 0, s, __VA_ARGS__); \
+    else                                                                  \
+      hipLaunchKernelGGL((kern<1>), grid, dim3(256), 0, s, __VA_ARGS__); \
+  } while (0)
+
+template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_stats(const float *x, int C, int L, double *sum,
                                                   double *sq) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const float *src = x + ((int64_t)n * C + c) * L;
   double s = 0.0, q = 0.0;
-  for (int i = threadIdx.x; i < L; i += 256) {
-    const double v = src[i];
-    s += v;
-    q += v * v;
+  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+    float v[VEC];
+    vld<VEC>(src + i, v);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      s += (double)v[j];
+      q += (double)v[j] * (double)v[j];
+    }
   }
   block_sum2_atomic<256>(s, q, sum + c, sq + c, red);
 }
 
 hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, double *sq,
                            hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_stats, dim3(C, N), dim3(256), 0, s, x, C, L, sum, sq);
+  STGCN_VEC_LAUNCH(k_bn_stats, slice_vec(L, {x}), dim3(C, N), x, C, L, sum, sq);
   return hipGetLastError();
 }
 
@@ -1388,25 +1439,34 @@ hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_
   return hipGetLastError();
 }
 
+template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
                                                      const float *invstd, const float *g,
                                                      const float *b, float *y, int C, int L) {
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], a = invstd[c] * g[c], be = b[c];
-  for (int i = threadIdx.x; i < L; i += 256) {
-    const float v = (U[base + i] - mu) * a + be;
-    y[base + i] = v > 0.f ? v : 0.f;
+  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+    float v[VEC];
+    vld<VEC>(U + base + i, v);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float t = (v[j] - mu) * a + be;
+      v[j] = t > 0.f ? t : 0.f;
+    }
+    vst<VEC>(y + base + i, v);
   }
 }
 
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
                               hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_relu_fwd, dim3(C, N), dim3(256), 0, s, U, mean, invstd, g, b, y, C, L);
+  STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, N), U, mean, invstd, g, b, y, C,
+                   L);
   return hipGetLastError();
 }
 
+template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, const float *U,
                                                             const float *mean,
                                                             const float *invstd, const float *g,
@@ -1417,13 +1477,16 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   double s = 0.0, q = 0.0;
-  for (int i = threadIdx.x; i < L; i += 256) {
-    const float u = U[base + i];
-    const float yv = (u - mu) * a + be;
-    if (yv > 0.f) {
-      const float gg = dy[base + i];
-      s += gg;
-      q += (double)gg * (double)((u - mu) * is);
+  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+    float u[VEC], d[VEC];
+    vld<VEC>(U + base + i, u);
+    vld<VEC>(dy + base + i, d);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      if ((u[j] - mu) * a + be > 0.f) {
+        s += d[j];
+        q += (double)d[j] * (double)((u[j] - mu) * is);
+      }
     }
   }
   block_sum2_atomic<256>(s, q, sg + c, sgu + c, red);
@@ -1432,11 +1495,12 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b, int N,
                                      int C, int L, double *sg, double *sgu, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_relu_bwd_reduce, dim3(C, N), dim3(256), 0, s, dy, U, mean, invstd, g, b,
-                     C, L, sg, sgu);
+  STGCN_VEC_LAUNCH(k_bn_relu_bwd_reduce, slice_vec(L, {dy, U}), dim3(C, N), dy, U, mean, invstd,
+                   g, b, C, L, sg, sgu);
   return hipGetLastError();
 }
 
+template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
     const float *dy, const float *U, const float *mean, const float *invstd, const float *g,
     const float *b, const double *sg, const double *sgu, float *dU, double *sdu, int C, int L,
@@ -1447,14 +1511,18 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   const float mg = (float)(sg[c] * invM), mgu = (float)(sgu[c] * invM);
   double s = 0.0;
-  for (int i = threadIdx.x; i < L; i += 256) {
-    const float u = U[base + i];
-    const float uh = (u - mu) * is;
-    const float yv = (u - mu) * a + be;
-    const float gg = yv > 0.f ? dy[base + i] : 0.f;
-    const float d = a * (gg - mg - uh * mgu);
-    dU[base + i] = d;
-    s += d;
+  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+    float u[VEC], d[VEC], o[VEC];
+    vld<VEC>(U + base + i, u);
+    vld<VEC>(dy + base + i, d);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float uh = (u[j] - mu) * is;
+      const float gg = (u[j] - mu) * a + be > 0.f ? d[j] : 0.f;
+      o[j] = a * (gg - mg - uh * mgu);
+      s += o[j];
+    }
+    vst<VEC>(dU + base + i, o);
   }
   block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
 }
@@ -1464,8 +1532,8 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     const double *sg, const double *sgu, float *dU, double *sdu,
                                     int N, int C, int L, hipStream_t s) {
   const double invM = 1.0 / ((double)N * L);
-  hipLaunchKernelGGL(k_bn_relu_bwd_apply, dim3(C, N), dim3(256), 0, s, dy, U, mean, invstd, g, b,
-                     sg, sgu, dU, sdu, C, L, invM);
+  STGCN_VEC_LAUNCH(k_bn_relu_bwd_apply, slice_vec(L, {dy, U, dU}), dim3(C, N), dy, U, mean,
+                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM);
   return hipGetLastError();
 }
 
@@ -1486,6 +1554,7 @@ hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double
 }
 
 // dx = g*invstd * (dxhat - sum(dxhat)/M - xnorm * sum(dxhat*xnorm)/M), in place.
+template <int VEC>
 __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x,
                                                        const float *mean, const float *invstd,
                                                        const float *g, const double *sd,
@@ -1495,17 +1564,21 @@ __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c];
   const float md = (float)(sd[c] * invM), mdn = (float)(sdn[c] * invM);
-  for (int i = threadIdx.x; i < L; i += 256) {
-    const float xn = (x[base + i] - mu) * is;
-    dx[base + i] = a * (dx[base + i] - md - xn * mdn);
+  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+    float xv[VEC], d[VEC];
+    vld<VEC>(x + base + i, xv);
+    vld<VEC>(dx + base + i, d);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) d[j] = a * (d[j] - md - (xv[j] - mu) * is * mdn);
+    vst<VEC>(dx + base + i, d);
   }
 }
 
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean, const float *invstd,
                                 const float *g, const double *sd, const double *sdn, int N, int C,
                                 int L, int64_t M, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn1_bwd_apply, dim3(C, N), dim3(256), 0, s, dx, x, mean, invstd, g, sd,
-                     sdn, C, L, 1.0 / (double)M);
+  STGCN_VEC_LAUNCH(k_bn1_bwd_apply, slice_vec(L, {dx, x}), dim3(C, N), dx, x, mean, invstd, g,
+                   sd, sdn, C, L, 1.0 / (double)M);
   return hipGetLastError();
 }
 
