@@ -375,7 +375,8 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
     if (chunk + 1 < nchunks) stage(chunk + 1, odd ? Ws0 : Ws1, odd ? Is0 : Is1);
     const float *wp = Ws + hi * NQ * 64 + mi * 32 + lo;
     const float *ib0 = Is + bb[0], *ib1 = Is + bb[1], *ib2 = Is + bb[2], *ib3 = Is + bb[3];
-    float a[2], b[2][4];
+    constexpr int PD = 2;  // operands are read PD k-steps ahead of their MFMAs
+    float a[PD + 1], b[PD + 1][4];
     auto ld = [&](int s, int set) {
       const int cp = s / NQ, q = s - cp * NQ;
       const int bo = 2 * cp * G::SP + q * V;
@@ -385,16 +386,17 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
       b[set][2] = ib2[bo];
       b[set][3] = ib3[bo];
     };
-    ld(0, 0);
+#pragma unroll
+    for (int s = 0; s < PD && s < G::NS; ++s) ld(s, s);
 #pragma unroll
     for (int s = 0; s < G::NS; ++s) {
-      if (s + 1 < G::NS) ld(s + 1, (s + 1) & 1);
-      const int c = s & 1;
+      if (s + PD < G::NS) ld(s + PD, (s + PD) % (PD + 1));
+      const int c = s % (PD + 1);
       acc[0] = mfma32(a[c], b[c][0], acc[0]);
       acc[1] = mfma32(a[c], b[c][1], acc[1]);
       acc[2] = mfma32(a[c], b[c][2], acc[2]);
       acc[3] = mfma32(a[c], b[c][3], acc[3]);
-      // issue order per step: step s+1's 5 LDS reads, then step s's 4 MFMAs
+      // issue order per step: step s+PD's 5 LDS reads, then step s's 4 MFMAs
       __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       __builtin_amdgcn_sched_barrier(0);
@@ -946,32 +948,33 @@ __global__ __launch_bounds__(NW * 64, 1) void k_wgrad_taps(WgradParams p) {
     const float *pa = Ps + (mi * 32 + lo) * PP + hi;
     const float *qb = Qs + hi;
     if constexpr (VT > 0) {
-      // fully unrolled; issue order per step: step k+1's reads, then step k's MFMAs
+      // fully unrolled; issue order per step: step k+PD's reads, then step k's MFMAs
       constexpr int HV = ((VT + 1) & ~1) / 2, NS = FTT * HV;
       constexpr int FJ = SIN * VT - 2 * HV;
       const float *qb0 = qb + qoff[0], *qb1 = qb + qoff[1], *qb2 = qb + qoff[2];
       const float *qb3 = qb + qoff[3], *qb4 = qb + qoff[4];
-      float a[2], b[2][NT];
-      auto ld = [&](int k, int set) {
-        const int bo = 2 * k + (k / HV) * FJ;
-        a[set] = pa[2 * k];
-        b[set][0] = qb0[bo];
-        b[set][1] = qb1[bo];
-        b[set][2] = qb2[bo];
-        b[set][3] = qb3[bo];
-        b[set][4] = qb4[bo];
-      };
-      // the tap count of the wave (5 or 4) is a template constant of the loop body
+      const float *qbt[NT] = {qb0, qb1, qb2, qb3, qb4};
+      // the tap count of the wave (5 or 4) is a template constant of the loop
+      // body; operands are read PD steps ahead of their MFMAs (PD + 1 sets)
       auto body = [&](auto nqc) {
         constexpr int NQW = decltype(nqc)::value;
-        ld(0, 0);
+        constexpr int PD = 2;
+        float a[PD + 1], b[PD + 1][NQW];
+        auto ld = [&](int k, int set) {
+          const int bo = 2 * k + (k / HV) * FJ;
+          a[set] = pa[2 * k];
+#pragma unroll
+          for (int t = 0; t < NQW; ++t) b[set][t] = qbt[t][bo];
+        };
+#pragma unroll
+        for (int k = 0; k < PD; ++k) ld(k, k);
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
-          if (k + 1 < NS) ld(k + 1, (k + 1) & 1);
-          const int c = k & 1;
+          if (k + PD < NS) ld(k + PD, (k + PD) % (PD + 1));
+          const int c = k % (PD + 1);
 #pragma unroll
           for (int t = 0; t < NQW; ++t) acc[t] = mfma32(a[c], b[c][t], acc[t]);
-          __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, NQW + 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, NQW, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
