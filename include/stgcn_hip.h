@@ -2,19 +2,25 @@
  * stgcn_hip.h — C-ABI of libstgcn_hip.so, the MI355X (gfx950) ST-GCN block.
  *
  * This is the drop-in boundary for ONE hot path of nagyrajmund/st-gcn: the
- * non-residual ST-GCN block in training (and eval) mode,
+ * ST-GCN block in training (and eval) mode,
  *
- *   y = ReLU(BN2(Conv9x1(SpatialConv(BN1(x)))))      (dropout_rate == 0)
+ *   y = ReLU(BN2(Conv9x1(SpatialConv(BN1(x)))))                 (default)
+ *   y = ReLU(Conv9x1(ReLU(BN2(SpatialConv(ReLU(BN1(x)))))) + R(x))
+ *                                          (flags & STGCN_F_RESIDUAL)
  *
- * i.e. SpatialTemporalConv.forward (src/network/st_graphconv.py:97-109) with
+ * with R = identity (C_in == C_out, stride 1) or a 1x1 Conv2d with temporal
+ * stride (st_graphconv.py:24-28), i.e. SpatialTemporalConv.forward
+ * (src/network/st_graphconv.py:85-109, residual_block :60-82) with
  * SpatialConv.forward (st_graphconv.py:139-152) and its autograd backward.
+ * Dropout (p > 0) is applied by the caller on y.
  * The reference has no FFI of its own (pure Python over PyTorch); the entry
  * points below are what its module boundary binds to (the ctypes binding in
  * st-gcn_amd/hip_lib.py, shown in INTEGRATION.md):
  *
  *   stgcn_block_fwd  replaces SpatialTemporalConv.forward, st_graphconv.py:85-109
  *                    (BatchNorm2d :34/:98, SpatialConv :139-152, temporalConv
- *                    :41-43/:99, BatchNorm2d :46/:100, ReLU :49/:105)
+ *                    :41-43/:99, BatchNorm2d :46/:100, ReLU :49/:105;
+ *                    residual_block :60-82 with apply_residual :24-28)
  *   stgcn_block_bwd  replaces the autograd backward of the same ops
  *                    (driven by lightning_model.py:199-205 -> loss.backward())
  *
@@ -40,12 +46,15 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 1
+#define STGCN_ABI_VERSION 2
+
+/* stgcn_desc_t.flags */
+#define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
 
 enum {
   STGCN_OK = 0,
   STGCN_E_INVALID = -1,     /* bad pointer / shape / parameter            */
-  STGCN_E_UNSUPPORTED = -2, /* residual, dropout, V > 256, gamma != 9 ... */
+  STGCN_E_UNSUPPORTED = -2, /* V > 256, gamma != 9, unknown flags ...      */
   STGCN_E_HIP = -3          /* a HIP launch / runtime error               */
 };
 
@@ -59,12 +68,16 @@ typedef struct stgcn_desc {
   float momentum;      /* BatchNorm momentum 0.1                             */
   int32_t training;    /* 1: batch statistics + running-stat update          */
   int32_t need_dx;     /* backward: write dx (0 for the network's first block)*/
-  int32_t flags;       /* must be 0 (residual / dropout: STGCN_E_UNSUPPORTED) */
+  int32_t flags;       /* 0 or STGCN_F_RESIDUAL                              */
 } stgcn_desc_t;
 
-/* Forward arguments. Saved tensors (Z, U, stats) are kept by the caller for
- * stgcn_block_bwd. stats holds mean1[C_in], invstd1[C_in], mean2[C_out],
- * invstd2[C_out] (fp32) as used by the forward. */
+/* Forward arguments. Saved tensors (Z, U, stats; residual: Z, Za, y, stats)
+ * are kept by the caller for stgcn_block_bwd. stats holds mean1[C_in],
+ * invstd1[C_in], mean2[C_out], invstd2[C_out] (fp32) as used by the forward.
+ * Residual block: BN2 normalizes Z (the spatial output, st_graphconv.py:76),
+ * U is not used, Za = ReLU(BN2(Z)) is the temporal conv input, Wr/br is the
+ * projection (C_out, C_in) + (C_out) when C_in != C_out or stride != 1
+ * (apply_residual, st_graphconv.py:27), else null. */
 typedef struct stgcn_fwd_args {
   const float *x;                       /* N,C_in,T,V                         */
   const float *A, *W, *bW, *Wt, *bWt;   /* SpatialConv.A / W ; temporalConv   */
@@ -74,6 +87,9 @@ typedef struct stgcn_fwd_args {
   float *Z;                             /* saved: spatial output N,C_out,T,V  */
   float *U;                             /* saved: temporal output N,C_out,T_out,V */
   float *stats;                         /* saved: 2*C_in + 2*C_out floats     */
+  /* ABI 2 (residual block; null otherwise) */
+  const float *Wr, *br;                 /* apply_residual Conv2d (projection) */
+  float *Za;                            /* saved: ReLU(BN2(Z)) N,C_out,T,V    */
 } stgcn_fwd_args_t;
 
 /* Backward arguments: the gradients of every input of the forward. */
@@ -84,6 +100,10 @@ typedef struct stgcn_bwd_args {
   float *dx;                            /* N,C_in,T,V (ignored if !need_dx)   */
   float *dA, *dW, *dbW, *dWt, *dbWt;
   float *dg1, *db1, *dg2, *db2;
+  /* ABI 2 (residual block; null otherwise) */
+  const float *Wr;                      /* projection weight or null          */
+  const float *Za, *y;                  /* saved by the forward               */
+  float *dWr, *dbr;                     /* projection gradients or null       */
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);

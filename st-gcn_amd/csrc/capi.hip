@@ -1,13 +1,17 @@
 // C-ABI entry points of libstgcn_hip.so (declared in include/stgcn_hip.h).
 //
 // stgcn_block_fwd / stgcn_block_bwd enqueue the kernel sequence of one
-// non-residual ST-GCN block on the caller's stream. The reference op order
+// ST-GCN block on the caller's stream. The reference op order of the default
+// (non-residual) block
 // (st_graphconv.py:97-109, :148-150) is
 //     BN1 -> Y = W x + b -> Z = sum_k Y_k A_k^T -> Conv9x1 -> BN2 -> ReLU;
 // here the joint contraction is applied on the narrower (input-channel) side,
 //     Z = sum_k W_k (BN1(x) A_k^T) + (sum_k b_k rowsum(A_k))          (1)
 // which is the same linear map (exact in real arithmetic) and never
-// materialises the K*C_out-channel Y.
+// materialises the K*C_out-channel Y. The residual block (st_graphconv.py:60-82)
+// reuses the same kernels: ReLU folded into the joint contraction's BN1
+// input, BN2 statistics from the spatial GEMM epilogue, and the residual add +
+// final ReLU in the temporal conv's epilogue.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -53,6 +57,11 @@ size_t wpk_floats(const stgcn_desc_t *d) {
 
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }
 int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
+bool residual(const stgcn_desc_t *d) { return (d->flags & STGCN_F_RESIDUAL) != 0; }
+// residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
+bool projection(const stgcn_desc_t *d) {
+  return residual(d) && (d->C_in != d->C_out || d->stride != 1);
+}
 
 struct Carve {
   char *base;
@@ -95,7 +104,7 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   w.n_jtiles = wgrad_ntiles_j(C, NQ);
   w.N = d->N;
   w.S = wgrad_splits(w.n_rtiles * w.n_jtiles, d->N * w.n_mtiles);
-  if (NQ == 1) plan_wgrad_sp(w);
+  if (wgrad_sp_applies(w)) plan_wgrad_sp(w);
   return w;
 }
 
@@ -131,6 +140,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
 struct BwdLayout {
   double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
   float *dU, *dZ, *G, *H, *slab, *wpk;
+  float *Rg;  // residual projection data-grad (N, C_in, T, V)
   size_t dbl_bytes, total;
 };
 
@@ -152,8 +162,14 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   WgradParams w1 = make_wgrad_taps(d, nullptr, nullptr, nullptr);
   WgradParams w2 =
       make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
-  const size_t s1 = (size_t)w1.S * R * R * 9, s2 = (size_t)w2.S * R * K * C;
-  L.slab = c.take<float>(std::max(s1, s2));
+  size_t slab = std::max((size_t)w1.S * R * R * 9, (size_t)w2.S * R * K * C);
+  if (projection(d)) {
+    WgradParams w3 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, C, d->T, 1, d->stride, 0,
+                                nullptr);
+    slab = std::max(slab, (size_t)w3.S * R * C);
+    if (d->need_dx) L.Rg = c.take<float>((size_t)d->N * C * nT(d));
+  }
+  L.slab = c.take<float>(slab);
   L.wpk = c.take<float>(wpk_floats(d));
   L.total = c.off;
   return L;
@@ -162,6 +178,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
 struct FwdLayout {
   double *s1, *q1, *s2, *q2;
   float *G, *Wpk, *biasZ, *wpk;
+  float *Rp;  // residual projection output (N, C_out, T_out, V)
   size_t dbl_bytes, total;
 };
 
@@ -178,6 +195,7 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
   L.Wpk = c.take<float>((size_t)R * K * C);
   L.biasZ = c.take<float>((size_t)R * d->V);
   L.wpk = c.take<float>(wpk_floats(d));
+  if (projection(d)) L.Rp = c.take<float>((size_t)d->N * R * nTo(d));
   L.total = c.off;
   return L;
 }
@@ -212,7 +230,79 @@ static bool geometry_supported(const stgcn_desc_t *d) {
   if (!conv_gemm_supported(p)) return false;
   p.NQ = 1;
   p.s_in = 1;
-  return conv_gemm_supported(p);
+  if (!conv_gemm_supported(p)) return false;
+  if (projection(d)) {
+    p.s_in = d->stride;  // the strided 1x1 projection
+    p.R = R;
+    p.C = C;
+    WgradParams w3 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, C, d->T, 1, d->stride, 0,
+                                nullptr);
+    if (!conv_gemm_supported(p) || !(wgrad_sp_applies(w3) || wgrad_supported(w3))) return false;
+  }
+  return true;
+}
+
+// Residual block after the spatial conv (st_graphconv.py:75-80, :105):
+//   Za = ReLU(BN2(Z)); y = ReLU(Conv9x1(Za) + bt + R(x)),
+// R = x (identity) or Wr x + br with temporal stride (projection).
+static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
+                             const FwdLayout &L, hipStream_t s) {
+  const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V;
+  float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
+  HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * T * V, d->eps, d->momentum,
+                             d->training, a->rm2, a->rv2, mean2, invstd2, s));
+  HIP_TRY(launch_bn_relu_fwd(a->Z, mean2, invstd2, a->g2, a->b2, a->Za, N, R, T * V, s));
+  const float *resid = a->x;
+  if (projection(d)) {  // apply_residual: Conv2d(C_in, C_out, 1, stride (s,1)) (:27)
+    ConvGemmParams p = conv_base(d, L.wpk);
+    p.in = a->x;
+    p.w = a->Wr;
+    p.out = L.Rp;
+    p.bias_r = a->br;
+    p.in_bstride = (int64_t)C * T * V;
+    p.out_bstride = (int64_t)R * To * V;
+    p.w_sr = C;
+    p.w_sc = 1;
+    p.w_sq = 0;
+    p.C = C;
+    p.R = R;
+    p.NQ = 1;
+    p.s_in = d->stride;
+    p.off = 0;
+    p.s_out = 1;
+    p.p_out = 0;
+    p.M = To;
+    p.T_src = T;
+    p.T_dst = To;
+    conv_tiles(p);
+    HIP_TRY(launch_conv_gemm(p, s));
+    resid = L.Rp;
+  }
+  ConvGemmParams p = conv_base(d, L.wpk);
+  p.in = a->Za;
+  p.w = a->Wt;
+  p.out = a->y;
+  p.bias_r = a->bWt;
+  p.res = resid;
+  p.relu_out = 1;
+  p.in_bstride = (int64_t)R * T * V;
+  p.out_bstride = (int64_t)R * To * V;
+  p.w_sr = (int64_t)R * 9;
+  p.w_sc = 9;
+  p.w_sq = 1;
+  p.C = R;
+  p.R = R;
+  p.NQ = 9;
+  p.s_in = d->stride;
+  p.off = -d->pad;
+  p.s_out = 1;
+  p.p_out = 0;
+  p.M = To;
+  p.T_src = T;
+  p.T_dst = To;
+  conv_tiles(p);
+  HIP_TRY(launch_conv_gemm(p, s));
+  return STGCN_OK;
 }
 
 extern "C" {
@@ -227,8 +317,7 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   if (!d) return fail(STGCN_E_INVALID, "null descriptor");
   if (d->N <= 0 || d->C_in <= 0 || d->C_out <= 0 || d->T <= 0 || d->V <= 0 || d->K <= 0)
     return fail(STGCN_E_INVALID, "non-positive dimension");
-  if (d->flags != 0)
-    return fail(STGCN_E_UNSUPPORTED, "residual / dropout variants are not implemented");
+  if ((d->flags & ~STGCN_F_RESIDUAL) != 0) return fail(STGCN_E_UNSUPPORTED, "unknown flags");
   if (d->gamma != 9 || d->pad != 4)
     return fail(STGCN_E_UNSUPPORTED, "only gamma=9, pad=4 (the reference default)");
   if (d->stride != 1 && d->stride != 2) return fail(STGCN_E_UNSUPPORTED, "stride must be 1 or 2");
@@ -258,9 +347,12 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
                     size_t workspace_bytes, void *stream) {
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
+  const bool res = residual(d);
   if (!a || !a->x || !a->A || !a->W || !a->bW || !a->Wt || !a->bWt || !a->g1 || !a->b1 ||
-      !a->g2 || !a->b2 || !a->y || !a->Z || !a->U || !a->stats)
+      !a->g2 || !a->b2 || !a->y || !a->Z || (!res && !a->U) || !a->stats)
     return fail(STGCN_E_INVALID, "null tensor argument");
+  if (res && (!a->Za || (projection(d) && (!a->Wr || !a->br))))
+    return fail(STGCN_E_INVALID, "residual block: null Za / projection weights");
   if (!a->rm1 || !a->rv1 || !a->rm2 || !a->rv2)
     return fail(STGCN_E_INVALID, "null running-stat buffer");
   const FwdLayout L = fwd_layout(d, workspace);
@@ -283,13 +375,19 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     HIP_TRY(launch_pack_w(a->W, L.Wpk, K, R, C, s));
     Wz = L.Wpk;
   }
-  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, s));
+  // (residual block: SpatialConv sees ReLU(BN1(x)), st_graphconv.py:72-74)
+  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, res,
+                            s));
   {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.G;
     p.w = Wz;
     p.out = a->Z;
     p.bias_rv = L.biasZ;
+    if (res && d->training) {  // BN2 of the residual block normalizes Z (:76)
+      p.stat_sum = L.s2;
+      p.stat_sq = L.q2;
+    }
     p.in_bstride = (int64_t)K * C * T * V;
     p.out_bstride = (int64_t)R * T * V;
     p.w_sr = (int64_t)K * C;
@@ -308,6 +406,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     conv_tiles(p);
     HIP_TRY(launch_conv_gemm(p, s));
   }
+  if (res) return residual_fwd_tail(d, a, L, s);
   // Temporal (9,1) conv, stride (s,1), pad (4,0), bias (st_graphconv.py:41-43,99),
   // with the BN2 batch statistics accumulated in the epilogue.
   {
@@ -349,10 +448,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                     size_t workspace_bytes, void *stream) {
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
-  if (!a || !a->dy || !a->x || !a->Z || !a->U || !a->stats || !a->A || !a->W || !a->bW ||
-      !a->Wt || !a->g1 || !a->b1 || !a->g2 || !a->b2 || !a->dA || !a->dW || !a->dbW || !a->dWt ||
-      !a->dbWt || !a->dg1 || !a->db1 || !a->dg2 || !a->db2 || (d->need_dx && !a->dx))
+  const bool res = residual(d);
+  if (!a || !a->dy || !a->x || !a->Z || (!res && !a->U) || !a->stats || !a->A || !a->W ||
+      !a->bW || !a->Wt || !a->g1 || !a->b1 || !a->g2 || !a->b2 || !a->dA || !a->dW || !a->dbW ||
+      !a->dWt || !a->dbWt || !a->dg1 || !a->db1 || !a->dg2 || !a->db2 || (d->need_dx && !a->dx))
     return fail(STGCN_E_INVALID, "null tensor argument");
+  if (res && (!a->Za || !a->y || (projection(d) && (!a->Wr || !a->dWr || !a->dbr))))
+    return fail(STGCN_E_INVALID, "residual block: null Za / y / projection tensors");
+  if (!d->training) return fail(STGCN_E_UNSUPPORTED, "backward in eval mode is not implemented");
   const BwdLayout L = bwd_layout(d, workspace);
   if (!workspace || workspace_bytes < L.total)
     return fail(STGCN_E_INVALID, "workspace too small");
@@ -362,16 +465,20 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   const float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
 
   HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
-  // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias)
-  HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
-                                    L.sg, L.sgu, s));
-  if (d->training) {
+  if (!res) {
+    // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias)
+    HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
+                                      L.sg, L.sgu, s));
     HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, L.sg, L.sgu,
                                      L.dU, L.sdu, N, R, To * V, s));
+    HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
-    return fail(STGCN_E_UNSUPPORTED, "backward in eval mode is not implemented");
+    // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
+    // temporal and projection bias grads are its per-channel sums
+    HIP_TRY(launch_relu_bwd(a->dy, a->y, L.dU, L.sdu, N, R, To * V, s));
+    HIP_TRY(launch_bn_grads_out(L.sdu, L.sdu, nullptr, R, a->dbWt, a->dbr ? a->dbr : a->dbWt,
+                                nullptr, s));
   }
-  HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
 
   // Temporal conv data-gradient: dZ = conv^T(dU)
   {
@@ -414,14 +521,24 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   // Temporal conv weight-gradient: dWt[co][ci][q] = sum dU[co] * Z[ci](shifted)
   {
-    WgradParams w = make_wgrad_taps(d, L.dU, a->Z, L.slab);
+    WgradParams w = make_wgrad_taps(d, L.dU, res ? a->Za : a->Z, L.slab);
     HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * R * 9, a->dWt, 0, R, 1, R, s));
   }
-  // Spatial conv backward. Recompute G = BN1(x) A^T, then
+  if (res) {
+    // BN2 + ReLU backward over Z (residual block, st_graphconv.py:76-77): dZ in place
+    HIP_TRY(launch_bn_relu_bwd_reduce(L.dZ, a->Z, mean2, invstd2, a->g2, a->b2, N, R, T * V,
+                                      L.sg, L.sgu, s));
+    HIP_TRY(launch_bn_relu_bwd_apply(L.dZ, a->Z, mean2, invstd2, a->g2, a->b2, L.sg, L.sgu,
+                                     L.dZ, L.sdu, N, R, T * V, s));
+    HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, nullptr, R, a->dg2, a->db2, nullptr, s));
+  }
+  // Spatial conv backward. Recompute G = f(BN1(x)) A^T (f = ReLU in the
+  // residual block), then
   //   dW' = dZ G^T (split-K), H_k = W_k^T dZ, dxhat = sum_k H_k A_k,
-  //   dA = sum H_k^T BN1(x) + bias part, dbW = sum dZ rowsum(A_k).
-  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, s));
+  //   dA = sum H_k^T f(BN1(x)) + bias part, dbW = sum dZ rowsum(A_k).
+  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, res,
+                            s));
   {
     WgradParams w = make_wgrad(d, L.dZ, (int64_t)R * T * V, R, T, L.G, (int64_t)K * C * T * V,
                                K * C, T, 1, 1, 0, L.slab);
@@ -454,11 +571,46 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_conv_gemm(p, s));
   }
   HIP_TRY(launch_spatial_dx(L.H, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
-                            L.sdn, N, C, T, V, K, d->need_dx, s));
+                            L.sdn, N, C, T, V, K, d->need_dx, res, s));
   HIP_TRY(launch_bn_grads_out(L.sd, L.sdn, nullptr, C, a->dg1, a->db1, nullptr, s));
+  // residual path gradient (added to dx after the BN1 backward)
+  const float *add = nullptr;
+  if (res && !projection(d)) add = L.dU;  // identity: d(res) = dU
+  if (projection(d)) {
+    // dWr[co][ci] = sum dU[co](m) x[ci](s*m)
+    WgradParams w = make_wgrad(d, L.dU, (int64_t)R * To * V, R, To, a->x, (int64_t)C * T * V, C,
+                               T, 1, d->stride, 0, L.slab);
+    HIP_TRY(launch_wgrad(w, s));
+    HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * C, a->dWr, 0, R, 1, C, s));
+    if (d->need_dx) {  // Rg[ci](s*m) = sum_co Wr[co][ci] dU[co](m); other frames 0
+      HIP_TRY(hipMemsetAsync(L.Rg, 0, sizeof(float) * (size_t)N * C * T * V, s));
+      ConvGemmParams p = conv_base(d, L.wpk);
+      p.in = L.dU;
+      p.w = a->Wr;
+      p.out = L.Rg;
+      p.in_bstride = (int64_t)R * To * V;
+      p.out_bstride = (int64_t)C * T * V;
+      p.w_sr = 1;
+      p.w_sc = C;
+      p.w_sq = 0;
+      p.C = R;
+      p.R = C;
+      p.NQ = 1;
+      p.s_in = 1;
+      p.off = 0;
+      p.s_out = d->stride;
+      p.p_out = 0;
+      p.M = To;
+      p.T_src = To;
+      p.T_dst = T;
+      conv_tiles(p);
+      HIP_TRY(launch_conv_gemm(p, s));
+      add = L.Rg;
+    }
+  }
   if (d->need_dx)
-    HIP_TRY(launch_bn1_bwd_apply(a->dx, a->x, mean1, invstd1, a->g1, L.sd, L.sdn, N, C, T * V,
-                                 (int64_t)N * T * V, s));
+    HIP_TRY(launch_bn1_bwd_apply(a->dx, a->x, mean1, invstd1, a->g1, L.sd, L.sdn, add, N, C,
+                                 T * V, (int64_t)N * T * V, s));
   return STGCN_OK;
 }
 

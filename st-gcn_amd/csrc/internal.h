@@ -31,6 +31,9 @@ struct ConvGemmParams {
   int V, FT;  // joints; frames per tile (FT*V <= kTileCols)
   int n_mtiles, n_rtiles, N;
   int Cpad;  // set by launch_conv_gemm
+  // epilogue extras (residual block): out = f(acc + bias + res), f = ReLU if relu_out
+  const float *res;  // same layout and clip stride as out, or null
+  int relu_out;
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -54,6 +57,7 @@ hipError_t launch_wgrad(const WgradParams &p, hipStream_t s);
 // wgrad_sp_kc(CT) columns): sets CT, n_rtiles, n_jtiles, n_mtiles (chunks per
 // clip), S. Requires s_in = 1, off = 0, M = T_src.
 void plan_wgrad_sp(WgradParams &p);
+bool wgrad_sp_applies(const WgradParams &p);
 inline int wgrad_sp_kc(int CT) { return CT == 64 ? 64 : 32; }
 // Temporal-conv weight gradient (NQ = 9) with taps-inner tiles; n_jtiles
 // counts channel blocks of wgrad_taps_cb(p) channels. Slab = (R, C, 9).
@@ -92,18 +96,23 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     double *sdu, int N, int C, int L, hipStream_t s);
 hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
                                float *dgamma, float *dbeta, float *dbias, hipStream_t s);
+// add (same layout as dx, or null) is added after the BN1 backward (residual path)
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean,
                                 const float *invstd, const float *g, const double *sd,
-                                const double *sdn, int N, int C, int L, int64_t M,
-                                hipStream_t s);
+                                const double *sdn, const float *add, int N, int C, int L,
+                                int64_t M, hipStream_t s);
+// dout = dy * (y > 0) (the final ReLU of the residual block), sum[c] += sum dout
+hipError_t launch_relu_bwd(const float *dy, const float *y, float *dout, double *sum, int N,
+                           int C, int L, hipStream_t s);
 
 // Spatial (graph) helpers.
 hipError_t launch_pack_w(const float *W, float *Wpk, int K, int R, int C, hipStream_t s);
 hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K, int R, int V,
                           hipStream_t s);
+// G = f(BN1(x)) A^T with f = identity, or ReLU when relu != 0 (residual block)
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
-                             int C, int T, int V, int K, hipStream_t s);
+                             int C, int T, int V, int K, int relu, hipStream_t s);
 hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out,
                          hipStream_t s);
 hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K,
@@ -111,6 +120,7 @@ hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *
 hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b,
                              const float *A, float *dx, float *dA, double *sd, double *sdn,
-                             int N, int C, int T, int V, int K, int write_dx, hipStream_t s);
+                             int N, int C, int T, int V, int K, int write_dx, int relu,
+                             hipStream_t s);
 
 }  // namespace stgcn

@@ -248,6 +248,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
       if (rok && cok[j]) {
         float val = acc[j][i] + br;
         if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
+        if (p.res) val += p.res[(int64_t)n * p.out_bstride + row * ostride + ocol[j]];
+        if (p.relu_out) val = fmaxf(val, 0.f);
         outN[row * ostride + ocol[j]] = val;
         s += val;
         sq += (double)val * val;
@@ -412,6 +414,8 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
   const __amdgpu_buffer_rsrc_t rs_b = make_rsrc(p.bias_r ? p.bias_r : p.out, p.bias_r ? p.R : 0);
   const __amdgpu_buffer_rsrc_t rs_bv =
       make_rsrc(p.bias_rv ? p.bias_rv : p.out, p.bias_rv ? (int64_t)p.R * V : 0);
+  const __amdgpu_buffer_rsrc_t rs_res = make_rsrc(
+      p.res ? p.res + (int64_t)n * p.out_bstride : p.out, p.res ? p.out_bstride : 0);
   int ocol[4], cv[4];
   bool cok[4];
 #pragma unroll
@@ -445,8 +449,11 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
           float val = acc[j][i] + br;
           val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                                rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o,
-                                                ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB, 0, 0);
+          const int off = ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB;
+          if (p.res)
+            val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, off, 0, 0));
+          if (p.relu_out) val = fmaxf(val, 0.f);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o, off, 0, 0);
           if constexpr (STATS) {
             const double dv = ok ? (double)val : 0.0;
             s += dv;
@@ -1286,15 +1293,19 @@ static hipError_t launch_wgrad_sp(const WgradParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
+bool wgrad_sp_applies(const WgradParams &p) {
+  return p.NQ == 1 && p.s_in == 1 && p.off == 0 && p.M == p.T_src;
+}
+
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s) {
-  if (p.NQ == 1) {
-    if (p.s_in != 1 || p.off != 0 || p.M != p.T_src) return hipErrorInvalidValue;
-    return launch_wgrad_sp(p, s);
-  }
+  if (wgrad_sp_applies(p)) return launch_wgrad_sp(p, s);
   if (!wgrad_supported(p)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const size_t lds = wgrad_lds_bytes(p);
   switch (p.NQ) {
+    case 1:  // strided 1x1 (residual projection)
+      hipLaunchKernelGGL((k_wgrad<1, 128>), dim3(nblk), dim3(256), lds, s, p);
+      break;
     case 9:
       hipLaunchKernelGGL((k_wgrad<9, 192>), dim3(nblk), dim3(256), lds, s, p);
       break;
@@ -1372,7 +1383,7 @@ __device__ __forceinline__ void vst(float *p, const float (&v)[N]) {
 
 static int slice_vec(int L, std::initializer_list<const void *> ptrs) {
   int vec = L % 4 == 0 ? 4 : (L % 2 == 0 ? 2 : 1);
-  for (const void *q : ptrs)
+  for (const void *q : ptrs)  // (null pointers are aligned)
     while (vec > 1 && ((uintptr_t)q & (4 * vec - 1)) != 0) vec >>= 1;
   return vec;
 }
@@ -1561,8 +1572,8 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x,
                                                        const float *mean, const float *invstd,
                                                        const float *g, const double *sd,
-                                                       const double *sdn, int C, int L,
-                                                       double invM) {
+                                                       const double *sdn, const float *add,
+                                                       int C, int L, double invM) {
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c];
@@ -1573,15 +1584,50 @@ __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x
     vld<VEC>(dx + base + i, d);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) d[j] = a * (d[j] - md - (xv[j] - mu) * is * mdn);
+    if (add) {
+      float r[VEC];
+      vld<VEC>(add + base + i, r);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) d[j] += r[j];
+    }
     vst<VEC>(dx + base + i, d);
   }
 }
 
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean, const float *invstd,
-                                const float *g, const double *sd, const double *sdn, int N, int C,
-                                int L, int64_t M, hipStream_t s) {
-  STGCN_VEC_LAUNCH(k_bn1_bwd_apply, slice_vec(L, {dx, x}), dim3(C, N), dx, x, mean, invstd, g,
-                   sd, sdn, C, L, 1.0 / (double)M);
+                                const float *g, const double *sd, const double *sdn,
+                                const float *add, int N, int C, int L, int64_t M, hipStream_t s) {
+  STGCN_VEC_LAUNCH(k_bn1_bwd_apply, slice_vec(L, {dx, x, add}), dim3(C, N), dx, x, mean, invstd,
+                   g, sd, sdn, add, C, L, 1.0 / (double)M);
+  return hipGetLastError();
+}
+
+// dout = dy * (y > 0) for the residual block's final ReLU (st_graphconv.py:105),
+// with the per-channel sum of dout (the temporal and projection bias grads).
+template <int VEC>
+__global__ __launch_bounds__(256) void k_relu_bwd(const float *dy, const float *y, float *dout,
+                                                  double *sum, int C, int L) {
+  __shared__ double red[8];
+  const int c = blockIdx.x, n = blockIdx.y;
+  const int64_t base = ((int64_t)n * C + c) * L;
+  double s = 0.0;
+  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+    float d[VEC], yv[VEC];
+    vld<VEC>(dy + base + i, d);
+    vld<VEC>(y + base + i, yv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      s += d[j];
+    }
+    vst<VEC>(dout + base + i, d);
+  }
+  block_sum2_atomic<256>(s, 0.0, sum + c, nullptr, red);
+}
+
+hipError_t launch_relu_bwd(const float *dy, const float *y, float *dout, double *sum, int N,
+                           int C, int L, hipStream_t s) {
+  STGCN_VEC_LAUNCH(k_relu_bwd, slice_vec(L, {dy, y, dout}), dim3(C, N), dy, y, dout, sum, C, L);
   return hipGetLastError();
 }
 
@@ -1631,7 +1677,7 @@ constexpr int kGatherTC = 32;  // frames per gather block
 __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float *mean,
                                                     const float *invstd, const float *g,
                                                     const float *b, const float *A, float *G,
-                                                    int C, int T, int V, int K) {
+                                                    int C, int T, int V, int K, int relu) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *As = smem;                 // [K][V][V]
   float *xs = smem + K * V * V;     // [TC][V]
@@ -1645,7 +1691,10 @@ __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float 
     __syncthreads();
     const float *src = x + ((int64_t)n * C + ci) * L + (int64_t)t0 * V;
     const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
-    for (int i = threadIdx.x; i < tc * V; i += 256) xs[i] = (src[i] - mu) * a + be;
+    for (int i = threadIdx.x; i < tc * V; i += 256) {
+      const float t = (src[i] - mu) * a + be;
+      xs[i] = relu ? fmaxf(t, 0.f) : t;
+    }
     __syncthreads();
     for (int o = threadIdx.x; o < nout; o += 256) {
       const int k = o / (tc * V);
@@ -1660,235 +1709,11 @@ __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float 
   }
 }
 
-// ---------------------------------------------------------------------------
-// Joint-axis (V) contractions, one workgroup per (channel ci, clip n) slice,
-// one thread per frame row, the row's V-wide math fully unrolled (template V).
-// A is pinned in LDS with rows padded to VP (multiple of 4) and read with
-// 16-byte broadcast loads (every lane of a wave reads the same A element).
-// Slices are loaded with coalesced loads into LDS first; frames are processed
-// in chunks of TC rows.
-// ---------------------------------------------------------------------------
+// Joint-axis (V) kernels: rows padded to VP (multiple of 4) for 16-byte LDS reads.
 template <int V>
 struct JointCfg {
   static constexpr int VP = (V + 3) & ~3;
 };
-
-// G[n][k*C+ci][t][v] = sum_w A[k][v][w] * BN1(x)[n][ci][t][w]
-template <int V>
-__global__ __launch_bounds__(256) void k_gather2(const float *__restrict__ x,
-                                                 const float *__restrict__ mean,
-                                                 const float *__restrict__ invstd,
-                                                 const float *__restrict__ g,
-                                                 const float *__restrict__ b,
-                                                 const float *__restrict__ A, float *G, int C,
-                                                 int T, int K, int TC) {
-  constexpr int VP = JointCfg<V>::VP;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float *As = smem;              // [K][V][VP]
-  float *Xs = As + K * V * VP;   // [TC][VP] BN1(x)
-  float *Os = Xs + TC * VP;      // [TC*V] output staging (coalesced stores)
-  const int ci = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
-  for (int i = tid; i < K * V * VP; i += nt) {
-    const int kv = i / VP, w = i - kv * VP;
-    As[i] = w < V ? A[kv * V + w] : 0.f;
-  }
-  const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
-  const float *xs = x + ((int64_t)n * C + ci) * T * V;
-  for (int t0 = 0; t0 < T; t0 += TC) {
-    const int tc = min(TC, T - t0);
-    __syncthreads();
-    for (int e = tid; e < tc * V; e += nt) {
-      const int r = e / V, w = e - r * V;
-      Xs[r * VP + w] = (xs[(int64_t)t0 * V + e] - mu) * a + be;
-    }
-    __syncthreads();
-    float xr[VP];
-    const int row = tid;
-    if (row < tc) {
-#pragma unroll
-      for (int w4 = 0; w4 < VP; w4 += 4) {
-        const float4 q = *reinterpret_cast<const float4 *>(Xs + row * VP + w4);
-        xr[w4] = q.x;
-        xr[w4 + 1] = q.y;
-        xr[w4 + 2] = q.z;
-        xr[w4 + 3] = q.w;
-      }
-    }
-    for (int k = 0; k < K; ++k) {
-      if (row < tc) {
-        const float *Ak = As + k * V * VP;
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          float acc = 0.f;
-#pragma unroll
-          for (int w4 = 0; w4 < VP; w4 += 4) {
-            const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
-            acc = fmaf(q.x, xr[w4], acc);
-            if (w4 + 1 < V) acc = fmaf(q.y, xr[w4 + 1], acc);
-            if (w4 + 2 < V) acc = fmaf(q.z, xr[w4 + 2], acc);
-            if (w4 + 3 < V) acc = fmaf(q.w, xr[w4 + 3], acc);
-          }
-          Os[row * V + v] = acc;
-        }
-      }
-      __syncthreads();
-      float *gout = G + (((int64_t)n * K + k) * C + ci) * T * V + (int64_t)t0 * V;
-      for (int e = tid; e < tc * V; e += nt) gout[e] = Os[e];
-      __syncthreads();
-    }
-  }
-}
-
-// Per (ci, n) slice, for every frame row t:
-//   dxhat[t][w] = sum_k sum_v H[k*C+ci][t][v] * A[k][v][w]   (-> dx, if write_dx)
-//   sd[ci] += sum dxhat, sdn[ci] += sum dxhat * xnorm       (BN1 backward)
-//   dA[k][v][w] += sum_t H[k*C+ci][t][v] * BN1(x)[t][w]
-// dA is a V x V output with the slice's rows as reduction: an MFMA GEMM
-// (v_mfma_f32_32x32x2_f32, v and w padded to 32-tiles); the 4 waves split the
-// rows, their partial tiles are summed through LDS once per workgroup.
-template <int V>
-__global__ __launch_bounds__(256) void k_spatial_bwd2(
-    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
-    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
-    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int TC, int write_dx) {
-  constexpr int VP = JointCfg<V>::VP;
-  constexpr int NT = (V + 31) / 32;      // 32-tiles along v and along w
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ double red[8];
-  float *As = smem;                 // [K][V][VP]
-  float *Hs = As + K * V * VP;      // [K][TC][V]
-  float *XRs = Hs + K * TC * V;     // [TC][VP] raw x
-  float *Os = XRs + TC * VP;        // [TC*V] dx staging (coalesced stores)
-  const int ci = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, nt = blockDim.x;
-  const int lane = tid & 63, wave = tid >> 6, hi = lane >> 5, lo = lane & 31;
-  for (int i = tid; i < K * V * VP; i += nt) {
-    const int kv = i / VP, w = i - kv * VP;
-    As[i] = w < V ? A[kv * V + w] : 0.f;
-  }
-  const float mu = mean[ci], is = invstd[ci], be = b[ci], a = is * g[ci];
-  const int64_t xo = ((int64_t)n * C + ci) * T * V;
-  double s = 0.0, sn = 0.0;
-  floatx16 dacc[3][NT][NT];  // K <= 3
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-#pragma unroll
-    for (int p2 = 0; p2 < NT; ++p2)
-#pragma unroll
-      for (int q2 = 0; q2 < NT; ++q2)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dacc[k][p2][q2][i] = 0.f;
-  for (int t0 = 0; t0 < T; t0 += TC) {
-    const int tc = min(TC, T - t0);
-    __syncthreads();
-    for (int e = tid; e < tc * V; e += nt) {
-      const int r = e / V, w = e - r * V;
-      XRs[r * VP + w] = x[xo + (int64_t)t0 * V + e];
-    }
-    for (int k = 0; k < K; ++k) {
-      const float *hk = H + (((int64_t)n * K + k) * C + ci) * T * V + (int64_t)t0 * V;
-      for (int e = tid; e < tc * V; e += nt) Hs[k * TC * V + e] = hk[e];
-    }
-    __syncthreads();
-    for (int row = tid; row < tc; row += nt) {
-      float acc[VP];
-#pragma unroll
-      for (int w = 0; w < VP; ++w) acc[w] = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float *hr = Hs + (k * TC + row) * V;
-        const float *Ak = As + k * V * VP;
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          const float h = hr[v];
-#pragma unroll
-          for (int w4 = 0; w4 < VP; w4 += 4) {
-            const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
-            acc[w4] = fmaf(h, q.x, acc[w4]);
-            acc[w4 + 1] = fmaf(h, q.y, acc[w4 + 1]);
-            acc[w4 + 2] = fmaf(h, q.z, acc[w4 + 2]);
-            acc[w4 + 3] = fmaf(h, q.w, acc[w4 + 3]);
-          }
-        }
-      }
-#pragma unroll
-      for (int w = 0; w < V; ++w) {
-        const float xn = (XRs[row * VP + w] - mu) * is;
-        s += acc[w];
-        sn += (double)acc[w] * xn;
-        Os[row * V + w] = acc[w];
-      }
-    }
-    __syncthreads();
-    if (write_dx) {
-      float *dxo = dx + xo + (int64_t)t0 * V;
-      for (int e = tid; e < tc * V; e += nt) dxo[e] = Os[e];
-    }
-    // dA partial on MFMA: A-frag H[k][row][v], B-frag BN1(x)[row][w]; wave w
-    // takes row pairs kk = wave, wave + 4, ... (rows 2kk + hi).
-    const int nk = (tc + 1) / 2;
-    for (int k = 0; k < K; ++k) {
-      const float *hk = Hs + k * TC * V;
-      for (int kk = wave; kk < nk; kk += 4) {
-        const int r = 2 * kk + hi;
-        const bool rok = r < tc;
-#pragma unroll
-        for (int p2 = 0; p2 < NT; ++p2) {
-          const int v = p2 * 32 + lo;
-          const float av = (rok && v < V) ? hk[r * V + v] : 0.f;
-#pragma unroll
-          for (int q2 = 0; q2 < NT; ++q2) {
-            const int w = q2 * 32 + lo;
-            const float bw = (rok && w < V) ? (XRs[r * VP + w] - mu) * a + be : 0.f;
-            if (k == 0) dacc[0][p2][q2] = mfma32(av, bw, dacc[0][p2][q2]);
-            else if (k == 1) dacc[1][p2][q2] = mfma32(av, bw, dacc[1][p2][q2]);
-            else dacc[2][p2][q2] = mfma32(av, bw, dacc[2][p2][q2]);
-          }
-        }
-      }
-    }
-  }
-  // sum the 4 waves' dA tiles in LDS (reuse the staging area), one atomic each
-  __syncthreads();
-  float *dred = smem;  // [K][NT*32][NT*32]
-  const int DW = NT * 32;
-  for (int i = tid; i < K * DW * DW; i += nt) dred[i] = 0.f;
-  __syncthreads();
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int p2 = 0; p2 < NT; ++p2)
-#pragma unroll
-      for (int q2 = 0; q2 < NT; ++q2)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-          const int w = q2 * 32 + lo;
-          const float val = k == 0 ? dacc[0][p2][q2][i] : (k == 1 ? dacc[1][p2][q2][i]
-                                                                   : dacc[2][p2][q2][i]);
-          if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, val);  // LDS atomic
-        }
-  __syncthreads();
-  for (int i = tid; i < K * V * V; i += nt) {
-    const int k = i / (V * V), rem = i - k * V * V, v = rem / V, w = rem - v * V;
-    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
-  }
-  // BN1 partial sums (the block size is a multiple of 64)
-  s = wave_sum(s);
-  sn = wave_sum(sn);
-  if ((tid & 63) == 0) {
-    red[tid >> 6] = s;
-    red[4 + (tid >> 6)] = sn;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double a0 = 0.0, a1 = 0.0;
-    for (int w = 0; w < nt / 64; ++w) {
-      a0 += red[w];
-      a1 += red[4 + w];
-    }
-    atomicAdd(sd + ci, a0);
-    atomicAdd(sdn + ci, a1);
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Flat row-parallel joint kernels: one thread per (n, ci, t) row of the whole
@@ -1902,7 +1727,7 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
                                                  const float *__restrict__ g,
                                                  const float *__restrict__ b,
                                                  const float *__restrict__ A, float *G, int C,
-                                                 int T, int K, int64_t rows) {
+                                                 int T, int K, int64_t rows, int relu) {
   constexpr int VP = JointCfg<V>::VP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *As = smem;  // [K][V][VP]
@@ -1922,7 +1747,10 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
   const float *xr = x + r * V;
   float xv[VP];
 #pragma unroll
-  for (int w = 0; w < VP; ++w) xv[w] = w < V ? (xr[w] - mu) * a + be : 0.f;
+  for (int w = 0; w < VP; ++w) {
+    const float t = w < V ? (xr[w] - mu) * a + be : 0.f;
+    xv[w] = relu ? fmaxf(t, 0.f) : t;
+  }
   for (int k = 0; k < K; ++k) {
     float *gout = G + ((n * K + k) * C + ci) * (int64_t)T * V + (int64_t)t * V;
     const float *Ak = As + k * V * VP;
@@ -1955,7 +1783,7 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
                                                  const float *__restrict__ g,
                                                  const float *__restrict__ b,
                                                  const float *__restrict__ A, float *G, int C,
-                                                 int T, int K, int64_t rows) {
+                                                 int T, int K, int64_t rows, int relu) {
   constexpr int VP = JointCfg<V>::VP;
   constexpr int BF = 256 * V;  // floats of a block (a multiple of 256: V DMA rounds)
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1982,7 +1810,10 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
   __syncthreads();
   float xv[VP];
 #pragma unroll
-  for (int w = 0; w < VP; ++w) xv[w] = w < V ? (xs[tid * V + w] - mu) * a + be : 0.f;
+  for (int w = 0; w < VP; ++w) {
+    const float t = w < V ? (xs[tid * V + w] - mu) * a + be : 0.f;
+    xv[w] = relu ? fmaxf(t, 0.f) : t;
+  }
   for (int k = 0; k < K; ++k) {
     const float *Ak = As + k * V * VP;
     if (k > 0) __syncthreads();  // previous partition's stores have read os
@@ -2006,7 +1837,7 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
   }
 }
 
-// Flat-row spatial backward (see k_spatial_bwd2 for the math). Per block:
+// Flat-row spatial backward (the math: see k_spatial_dx). Per block:
 // dx rows, BN1 sums reduced per channel segment in LDS (rows are sorted by
 // channel), dA over the block's rows on MFMA, wave partials summed in LDS.
 template <int V>
@@ -2014,7 +1845,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx) {
+    int K, int64_t rows, int write_dx, int relu) {
   constexpr int VP = JointCfg<V>::VP;
   constexpr int NT = (V + 31) / 32;
   constexpr int MAXSEG = 32;
@@ -2078,10 +1909,12 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
 #pragma unroll
     for (int w = 0; w < V; ++w) {
       const float xn = (xv[w] - mu) * is;
+      const float bn = (xv[w] - mu) * a + be;
+      if (relu && bn <= 0.f) acc[w] = 0.f;  // ReLU'(BN1(x))
       s += acc[w];
       sn = fmaf(acc[w], xn, sn);
       if (write_dx) dxr[w] = acc[w];
-      XBs[tid * VP + w] = (xv[w] - mu) * a + be;
+      XBs[tid * VP + w] = relu ? fmaxf(bn, 0.f) : bn;
     }
   } else {
     for (int k = 0; k < K; ++k)
@@ -2159,181 +1992,6 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
   }
 }
 
-// k_spatial_bwd4: k_spatial_bwd3 as a persistent, double-buffered kernel with
-// coalesced block traffic. Row blocks (RB rows, contiguous in x, dx and, per
-// partition k, in H: the host checks that no block crosses a clip) are
-// striped over the grid; the H planes and x of block i+1 arrive by 16-byte
-// LDS-DMA while block i is processed, dx leaves through LDS as float4 stores.
-// Per row: dx = sum_k H_k A_k and the BN1 partial sums (per channel segment);
-// dA = sum_rows H_k^T BN1(x) on MFMA, accumulated in LDS over all blocks of
-// the workgroup and added to global memory once at the end.
-template <int V>
-__global__ __launch_bounds__(256) void k_spatial_bwd4(
-    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
-    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
-    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx) {
-  constexpr int VP = JointCfg<V>::VP;
-  constexpr int NT = (V + 31) / 32;
-  constexpr int MAXSEG = 32;
-  constexpr int DW = NT * 32;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
-  const int RB = blockDim.x;
-  const int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
-  const int BUF = (K + 1) * PL;               // one buffer: K H planes + x plane
-  float *As = smem + 2 * BUF;                 // [K][V][VP]
-  float *dred = As + K * V * VP;              // [K][DW][DW]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hi = lane >> 5, lo = lane & 31;
-  const int nw = RB / 64;
-  const int64_t CT = (int64_t)C * T;
-  const int nblocks = (int)(rows / RB);
-  const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
-
-  auto stage = [&](int blk, float *buf) {
-    const int64_t r0 = (int64_t)blk * RB;
-    const int64_t n0 = r0 / CT, rem0 = r0 - n0 * CT;
-    const int nd = PL / 256;  // DMA rounds per plane
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + r0 * V, (int64_t)RB * V);
-    for (int i = wave; i < nd; i += nw)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + K * PL + i * 256, 16,
-                                               (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
-    for (int k = 0; k < K; ++k) {
-      const __amdgpu_buffer_rsrc_t rh =
-          make_rsrc(H + ((n0 * K + k) * CT + rem0) * V, (int64_t)RB * V);
-      for (int i = wave; i < nd; i += nw)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, buf + k * PL + i * 256, 16,
-                                                 (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
-    }
-  };
-
-  for (int i = tid; i < K * V * VP; i += RB) {
-    const int kv = i / VP, w = i - kv * VP;
-    As[i] = w < V ? A[kv * V + w] : 0.f;
-  }
-  for (int i = tid; i < K * DW * DW; i += RB) dred[i] = 0.f;
-  int blk = blockIdx.x;
-  if (blk < nblocks) stage(blk, smem);
-  for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
-    float *buf = smem + (it & 1) * BUF;
-    float *Hs = buf, *xs = buf + K * PL;
-    if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
-    __syncthreads();  // block blk staged (vmcnt(0)); previous block fully retired
-    if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * BUF);
-    const int64_t r0 = (int64_t)blk * RB;
-    const int64_t n0 = r0 / CT, rem0 = r0 - n0 * CT;
-    const int rem = (int)(rem0 + tid);
-    const int ci = rem / T;
-    const int64_t cfirst = n0 * C + rem0 / T;  // global (n*C + ci) of row r0
-    const int seg = (int)(n0 * C + ci - cfirst);
-    float acc[VP];
-    float s = 0.f, sn = 0.f;
-    {
-      const float mu = mean[ci], is = invstd[ci];
-      const float a = is * g[ci], be = b[ci];
-      float xv[V];
-#pragma unroll
-      for (int w = 0; w < V; ++w) xv[w] = xs[tid * V + w];
-#pragma unroll
-      for (int w = 0; w < VP; ++w) acc[w] = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float *hr = Hs + k * PL + tid * V;
-        const float *Ak = As + k * V * VP;
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          const float h = hr[v];
-#pragma unroll
-          for (int w4 = 0; w4 < VP; w4 += 4) {
-            const float4 q = *reinterpret_cast<const float4 *>(Ak + v * VP + w4);
-            acc[w4] = fmaf(h, q.x, acc[w4]);
-            acc[w4 + 1] = fmaf(h, q.y, acc[w4 + 1]);
-            acc[w4 + 2] = fmaf(h, q.z, acc[w4 + 2]);
-            acc[w4 + 3] = fmaf(h, q.w, acc[w4 + 3]);
-          }
-        }
-      }
-#pragma unroll
-      for (int w = 0; w < V; ++w) {
-        const float xn = (xv[w] - mu) * is;
-        s += acc[w];
-        sn = fmaf(acc[w], xn, sn);
-        xs[tid * V + w] = (xv[w] - mu) * a + be;  // BN1(x), own row only
-      }
-    }
-    // BN1 partial sums per channel segment
-    if (seg_lds) {
-      atomicAdd(&seg_s[seg], (double)s);
-      atomicAdd(&seg_n[seg], (double)sn);
-    } else {
-      atomicAdd(sd + ci, (double)s);
-      atomicAdd(sdn + ci, (double)sn);
-    }
-    __syncthreads();  // BN1(x) rows and segment sums complete
-    if (seg_lds && tid < MAXSEG) {
-      const int64_t gc = cfirst + tid;  // global (n*C + ci)
-      const int64_t rlast = r0 + RB - 1;
-      const int64_t glast = (rlast / CT) * C + (int)((rlast % CT) / T);
-      if (gc <= glast) {
-        const int cc = (int)(gc % C);
-        atomicAdd(sd + cc, seg_s[tid]);
-        atomicAdd(sdn + cc, seg_n[tid]);
-      }
-    }
-    // dA partials on MFMA (wave takes row pairs kk = wave, +nw, ...), into LDS
-    const int nk = RB / 2;
-    for (int k = 0; k < K; ++k) {
-      floatx16 dacc[NT][NT];
-#pragma unroll
-      for (int p2 = 0; p2 < NT; ++p2)
-#pragma unroll
-        for (int q2 = 0; q2 < NT; ++q2)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) dacc[p2][q2][i] = 0.f;
-      const float *hk = Hs + k * PL;
-      for (int kk = wave; kk < nk; kk += nw) {
-        const int rr = 2 * kk + hi;
-#pragma unroll
-        for (int p2 = 0; p2 < NT; ++p2) {
-          const int v = p2 * 32 + lo;
-          const float av = v < V ? hk[rr * V + v] : 0.f;
-#pragma unroll
-          for (int q2 = 0; q2 < NT; ++q2) {
-            const int w = q2 * 32 + lo;
-            const float bw = w < V ? xs[rr * V + w] : 0.f;
-            dacc[p2][q2] = mfma32(av, bw, dacc[p2][q2]);
-          }
-        }
-      }
-#pragma unroll
-      for (int p2 = 0; p2 < NT; ++p2)
-#pragma unroll
-        for (int q2 = 0; q2 < NT; ++q2)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-            const int w = q2 * 32 + lo;
-            if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, dacc[p2][q2][i]);
-          }
-    }
-    if (write_dx) {
-      __syncthreads();  // H plane 0 no longer read
-#pragma unroll
-      for (int w = 0; w < V; ++w) Hs[tid * V + w] = acc[w];
-      __syncthreads();
-      float *dst = dx + r0 * V;
-      for (int e = tid; e < RB * V / 4; e += RB)
-        *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(Hs + e * 4);
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < K * V * V; i += RB) {
-    const int k = i / (V * V), rm = i - k * V * V, v = rm / V, w = rm - v * V;
-    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
-  }
-}
-
 // k_spatial_bwd5: the spatial backward with both joint contractions on MFMA.
 // Persistent and double-buffered like k_spatial_bwd4 (row blocks of RB rows,
 // contiguous in x, dx and per partition in H; H planes and x by 16-byte
@@ -2349,7 +2007,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx) {
+    int K, int64_t rows, int write_dx, int relu) {
   constexpr int VH = (V + 1) / 2;           // MFMA k-steps over v
   constexpr int NT = (V + 31) / 32;         // 32-column output tiles over w
   constexpr int DW = NT * 32;
@@ -2481,10 +2139,16 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
       for (int j = 0; j < (V + TPR - 1) / TPR; ++j) {
         const int w = part + j * TPR;
         if (w < V) {
-          const float xv = xs[rl * V + w], d = dxs[rl * V + w];
+          const float xv = xs[rl * V + w];
+          float d = dxs[rl * V + w];
+          const float bn = (xv - mu) * a + be;
+          if (relu && bn <= 0.f) {  // ReLU'(BN1(x))
+            d = 0.f;
+            dxs[rl * V + w] = 0.f;
+          }
           s += d;
           sn = fmaf(d, (xv - mu) * is, sn);
-          xs[rl * V + w] = (xv - mu) * a + be;
+          xs[rl * V + w] = relu ? fmaxf(bn, 0.f) : bn;
         }
       }
       const int seg0 = __builtin_amdgcn_readfirstlane(seg);
@@ -2572,14 +2236,14 @@ template <int V, int RB, int KT>
 static bool launch_bwd5(const float *H, const float *x, const float *mean, const float *invstd,
                         const float *g, const float *b, const float *A, float *dx, float *dA,
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
-                        int write_dx, hipStream_t s) {
+                        int write_dx, int relu, hipStream_t s) {
   const size_t lds = bwd5_lds<V, RB>(K);
   if (lds > 160 * 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
   const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 512))));
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
   if (K != KT) return false;
   hipLaunchKernelGGL((k_spatial_bwd5<V, RB, KT>), grid, dim3(256), lds, s, H, x, mean, invstd, g,
-                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx);
+                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
   return true;
 }
 
@@ -2589,20 +2253,11 @@ static int bwd3_rows(int V, int K) {
   return (K * V + VP) * 4 * 256 <= 48 * 1024 ? 256 : 64;
 }
 
-static int joint_tc(int V, int K, int bytes_per_row_extra) {
-  // rows per chunk: as many as fit ~48 KB of LDS, multiple of 64, <= 256
-  const int VP = (V + 3) & ~3;
-  const int per_row = (K * V + VP + V + bytes_per_row_extra) * 4;
-  int tc = (48 * 1024 - K * V * VP * 4) / per_row;
-  tc = tc / 64 * 64;
-  return tc < 64 ? 64 : (tc > 256 ? 256 : tc);
-}
-
 static bool joint_fast(int V) { return V == 18 || V == 25 || V == 50; }
 
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
-                             int C, int T, int V, int K, hipStream_t s) {
+                             int C, int T, int V, int K, int relu, hipStream_t s) {
   static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
   const size_t lds4 = sizeof(float) * ((size_t)2 * 256 * V + (size_t)K * V * ((V + 3) & ~3));
   if (!joint3 && joint_fast(V) && ((int64_t)C * T) % 256 == 0 && ((uintptr_t)x & 15) == 0 &&
@@ -2610,11 +2265,11 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
     const int64_t rows = (int64_t)N * C * T;
     const dim3 grid4((unsigned)(rows / 256));
     if (V == 18)
-      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
     else if (V == 25)
-      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
     else
-      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
     return hipGetLastError();
   }
   if (joint_fast(V)) {
@@ -2623,30 +2278,16 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
     const size_t lds3 = sizeof(float) * (size_t)K * V * VP;
     const dim3 grid3((unsigned)((rows + 255) / 256));
     if (V == 18)
-      hipLaunchKernelGGL(k_gather3<18>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+      hipLaunchKernelGGL(k_gather3<18>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
     else if (V == 25)
-      hipLaunchKernelGGL(k_gather3<25>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
+      hipLaunchKernelGGL(k_gather3<25>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
     else
-      hipLaunchKernelGGL(k_gather3<50>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows);
-    return hipGetLastError();
-  }
-  if (false) {
-    const int VP = (V + 3) & ~3;
-    const int TC = joint_tc(V, 0, 0);
-    const int nt = 256;
-    const size_t lds = sizeof(float) * ((size_t)K * V * VP + (size_t)TC * VP + (size_t)TC * V);
-    const dim3 grid(C, N);
-    if (V == 18)
-      hipLaunchKernelGGL(k_gather2<18>, grid, dim3(nt), lds, s, x, mean, invstd, g, b, A, G, C, T, K, TC);
-    else if (V == 25)
-      hipLaunchKernelGGL(k_gather2<25>, grid, dim3(nt), lds, s, x, mean, invstd, g, b, A, G, C, T, K, TC);
-    else
-      hipLaunchKernelGGL(k_gather2<50>, grid, dim3(nt), lds, s, x, mean, invstd, g, b, A, G, C, T, K, TC);
+      hipLaunchKernelGGL(k_gather3<50>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
     return hipGetLastError();
   }
   const size_t lds = sizeof(float) * ((size_t)K * V * V + kGatherTC * V);
   hipLaunchKernelGGL(k_gather_fwd, dim3((T + kGatherTC - 1) / kGatherTC, N), dim3(256), lds, s, x,
-                     mean, invstd, g, b, A, G, C, T, V, K);
+                     mean, invstd, g, b, A, G, C, T, V, K, relu);
   return hipGetLastError();
 }
 
@@ -2719,7 +2360,7 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
                                                     const float *g, const float *b,
                                                     const float *A, float *dx, float *dA,
                                                     double *sd, double *sdn, int C, int T, int V,
-                                                    int K, int write_dx) {
+                                                    int K, int write_dx, int relu) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ double red[8];
   const int KVV = K * V * V;
@@ -2740,7 +2381,10 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
     __syncthreads();
     const int64_t xo = ((int64_t)n * C + ci) * L + (int64_t)t0 * V;
     const float mu = mean[ci], is = invstd[ci], a = is * g[ci], be = b[ci];
-    for (int i = tid; i < tc * V; i += 256) xb[i] = (x[xo + i] - mu) * a + be;
+    for (int i = tid; i < tc * V; i += 256) {
+      const float t = (x[xo + i] - mu) * a + be;
+      xb[i] = relu ? fmaxf(t, 0.f) : t;
+    }
     for (int i = tid; i < K * tc * V; i += 256) {
       const int k = i / (tc * V), rem = i - k * tc * V;
       Hs[k * kDxTC * V + rem] = H[(((int64_t)n * K + k) * C + ci) * L + (int64_t)t0 * V + rem];
@@ -2757,6 +2401,7 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
         for (int v = 0; v < V; ++v) acc = fmaf(hr[v], ac[v * V], acc);
       }
       const float xn = (x[xo + o] - mu) * is;
+      if (relu && (x[xo + o] - mu) * a + be <= 0.f) acc = 0.f;  // ReLU'(BN1(x))
       if (write_dx) dx[xo + o] = acc;
       s += acc;
       sn += (double)acc * xn;
@@ -2777,16 +2422,16 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
 hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b, const float *A,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
-                             int V, int K, int write_dx, hipStream_t s) {
+                             int V, int K, int write_dx, int relu, hipStream_t s) {
   static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
-  static const bool joint4 = env_flag("STGCN_JOINT4");  // A/B measurement only
   const bool aligned = ((int64_t)N * C * T * V) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
                        ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0;
-  if (!joint3 && !joint4 && aligned && K <= 3 && K * ((V + 1) / 2) * ((V + 31) / 32) <= 48) {
+  if (!joint3 && aligned && K <= 3 && K * ((V + 1) / 2) * ((V + 31) / 32) <= 48) {
     const int64_t rows = (int64_t)N * C * T;
     bool done = false;
 #define STGCN_BWD5(VV, RR, KK)                                                              \
-  launch_bwd5<VV, RR, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, s)
+  launch_bwd5<VV, RR, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, \
+                          relu, s)
     // partitions K: 1 (uniform), 2 (distance), 3 (spatial) labelling
     if (V == 18)
       done = STGCN_BWD5(18, 128, 1) || STGCN_BWD5(18, 64, 1) || STGCN_BWD5(18, 128, 2) ||
@@ -2799,33 +2444,6 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
 #undef STGCN_BWD5
     if (done) return hipGetLastError();
   }
-  if (!joint3 && joint_fast(V) && K <= 3 && aligned) {
-    const int VP = (V + 3) & ~3;
-    const int RB = (K + 1) * V * 256 * 4 <= 40 * 1024 ? 256 : 64;
-    const int64_t CT = (int64_t)C * T;
-    if (CT % RB == 0) {
-      const int64_t rows = (int64_t)N * CT;
-      const int PL = (RB * V + 255) / 256 * 256;
-      const int DW = (V + 31) / 32 * 32;
-      const size_t lds = sizeof(float) * ((size_t)2 * (K + 1) * PL + (size_t)K * V * VP +
-                                          (size_t)K * DW * DW);
-      // persistent grid: the workgroups that fit on the chip at once
-      const int per_cu = std::max(1, std::min(8 / (RB / 64), (int)((160 * 1024) / lds)));
-      const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
-      if (lds > 160 * 1024) {
-        // too large double-buffered (V = 50 with K = 3): k_spatial_bwd3 below
-      } else if (V == 18)
-        hipLaunchKernelGGL(k_spatial_bwd4<18>, grid, dim3(RB), lds, s, H, x, mean, invstd, g, b, A,
-                           dx, dA, sd, sdn, C, T, K, rows, write_dx);
-      else if (V == 25)
-        hipLaunchKernelGGL(k_spatial_bwd4<25>, grid, dim3(RB), lds, s, H, x, mean, invstd, g, b, A,
-                           dx, dA, sd, sdn, C, T, K, rows, write_dx);
-      else
-        hipLaunchKernelGGL(k_spatial_bwd4<50>, grid, dim3(RB), lds, s, H, x, mean, invstd, g, b, A,
-                           dx, dA, sd, sdn, C, T, K, rows, write_dx);
-      if (lds <= 160 * 1024) return hipGetLastError();
-    }
-  }
   if (joint_fast(V) && K <= 3) {
     const int VP = (V + 3) & ~3;
     const int RB = bwd3_rows(V, K);
@@ -2836,39 +2454,19 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
     const dim3 grid3((unsigned)((rows + RB - 1) / RB));
     if (V == 18)
       hipLaunchKernelGGL(k_spatial_bwd3<18>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, rows, write_dx);
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
     else if (V == 25)
       hipLaunchKernelGGL(k_spatial_bwd3<25>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, rows, write_dx);
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
     else
       hipLaunchKernelGGL(k_spatial_bwd3<50>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, rows, write_dx);
-    return hipGetLastError();
-  }
-  if (false) {
-    const int VP = (V + 3) & ~3;
-    const int TC = joint_tc(V, K, 0);
-    const int nt = 256;  // dA quad ownership assumes 256 threads
-    const int DW = (V + 31) / 32 * 32;
-    const size_t lds = sizeof(float) * std::max((size_t)K * V * VP + (size_t)K * TC * V +
-                                                    (size_t)TC * VP + (size_t)TC * V,
-                                                (size_t)K * DW * DW);
-    const dim3 grid(C, N);
-    if (V == 18)
-      hipLaunchKernelGGL(k_spatial_bwd2<18>, grid, dim3(nt), lds, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, TC, write_dx);
-    else if (V == 25)
-      hipLaunchKernelGGL(k_spatial_bwd2<25>, grid, dim3(nt), lds, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, TC, write_dx);
-    else
-      hipLaunchKernelGGL(k_spatial_bwd2<50>, grid, dim3(nt), lds, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, TC, write_dx);
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
     return hipGetLastError();
   }
   if (K * V * V > 8192) return hipErrorInvalidValue;
   const size_t lds = sizeof(float) * (2 * (size_t)K * V * V + kDxTC * V + (size_t)K * kDxTC * V);
   hipLaunchKernelGGL(k_spatial_dx, dim3((T + kDxTC - 1) / kDxTC, N), dim3(256), lds, s, H, x,
-                     mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, V, K, write_dx);
+                     mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, V, K, write_dx, relu);
   return hipGetLastError();
 }
 

@@ -1,10 +1,12 @@
-"""``StgcnBlockFn`` — the fused ST-GCN block as a torch.autograd.Function.
+"""``StgcnBlockFn`` / ``StgcnResBlockFn`` — the fused ST-GCN block as
+torch.autograd.Functions.
 
 Forward and backward are single calls into libstgcn_hip.so
 (``stgcn_block_fwd`` / ``stgcn_block_bwd``) on the current HIP stream. The
-math is that of ``SpatialTemporalConv.forward`` (non-residual, no dropout,
-src/network/st_graphconv.py:97-109 with SpatialConv :139-152) and of its
-autograd backward (driven by lightning_model.py:199-205).
+math is that of ``SpatialTemporalConv.forward`` (src/network/st_graphconv.py:
+97-109 for the default block, the residual block :60-82 with apply_residual
+:24-28; SpatialConv :139-152; no dropout) and of its autograd backward
+(driven by lightning_model.py:199-205).
 """
 import ctypes
 
@@ -19,11 +21,12 @@ def _f32c(t, name):
     return t
 
 
-def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1, gamma=9):
+def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1, gamma=9,
+              residual=False):
     N, C_in, T, V = x_shape
     T_out = (T + 2 * pad - gamma) // stride + 1
     return hip_lib.Desc(N, C_in, C_out, T, T_out, V, K, gamma, stride, pad, eps, momentum,
-                        int(training), int(need_dx), 0)
+                        int(training), int(need_dx), hip_lib.F_RESIDUAL if residual else 0)
 
 
 class StgcnBlockFn(torch.autograd.Function):
@@ -57,7 +60,8 @@ class StgcnBlockFn(torch.autograd.Function):
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
-            x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats)])
+            x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats,
+            None, None, None)])
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2)
@@ -82,10 +86,86 @@ class StgcnBlockFn(torch.autograd.Function):
         ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
         args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
             dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
-            grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2)])
+            grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
+            None, None, None, None, None)])
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))
         dA, dW, dbW, dWt = grads
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
+                None, None, None, None, None, None, None, None, None)
+
+
+class StgcnResBlockFn(torch.autograd.Function):
+    """The full pre-activation residual block (st_graphconv.py:60-82, then the
+    ReLU of :105):  y = ReLU(Conv9x1(ReLU(BN2(SpatialConv(ReLU(BN1(x)))))) + R(x)).
+
+    forward(x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br, rm1, rv1, rm2, rv2,
+            stride, pad, eps, momentum, training) -> y
+    R = identity when Wr is None (C_in == C_out, stride 1), else the 1x1
+    projection Conv2d (Wr, br) with temporal stride. Backward returns the
+    gradients of x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br.
+    """
+
+    @staticmethod
+    def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br, rm1, rv1, rm2, rv2,
+                stride, pad, eps, momentum, training):
+        lib = hip_lib.lib()
+        x = x.contiguous()
+        names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
+                 "rm1", "rv1", "rm2", "rv2")
+        for t, n in zip((x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2), names):
+            _f32c(t, n)
+        if Wr is not None:
+            _f32c(Wr, "Wr")
+            _f32c(br, "br")
+        N, C_in, T, V = x.shape
+        K = A.shape[0]
+        C_out = Wt.shape[0]
+        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training, residual=True)
+        hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
+        if (Wr is None) != (C_in == C_out and stride == 1):
+            raise RuntimeError("residual projection weights must be given iff shapes differ")
+        dev = x.device
+        y = torch.empty((N, C_out, desc.T_out, V), device=dev, dtype=torch.float32)
+        Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
+        Za = torch.empty_like(Z)
+        stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
+        nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
+        ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
+            x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, None, stats,
+            Wr, br, Za)])
+        hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
+                                          hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
+        ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr)
+        ctx.cfg = (stride, pad, eps, momentum, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = hip_lib.lib()
+        x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr = ctx.saved_tensors
+        stride, pad, eps, momentum, training = ctx.cfg
+        need_dx = bool(ctx.needs_input_grad[0])
+        dy = dy.contiguous()
+        C_out = Wt.shape[0]
+        desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
+                         need_dx=need_dx, residual=True)
+        dev = x.device
+        dx = torch.empty_like(x) if need_dx else None
+        dA, dW, dbW, dWt = (torch.empty_like(t) for t in (A, W, bW, Wt))
+        dbWt = torch.empty(C_out, device=dev, dtype=torch.float32)
+        dg1, db1, dg2, db2 = (torch.empty_like(t) for t in (g1, b1, g2, b2))
+        dWr = torch.empty_like(Wr) if Wr is not None else None
+        dbr = torch.empty(C_out, device=dev, dtype=torch.float32) if Wr is not None else None
+        nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
+        ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
+            dy, x, Z, None, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
+            dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
+            Wr, Za, y, dWr, dbr)])
+        hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
+                                          hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
+        return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2, dWr, dbr,
                 None, None, None, None, None, None, None, None, None)

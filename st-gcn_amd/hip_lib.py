@@ -16,7 +16,8 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libstgcn_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
+F_RESIDUAL = 1  # stgcn_desc_t.flags
 
 _c_int = ctypes.c_int32
 _c_float = ctypes.c_float
@@ -34,13 +35,15 @@ class Desc(ctypes.Structure):
 class FwdArgs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in (
         "x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
-        "rm1", "rv1", "rm2", "rv2", "y", "Z", "U", "stats")]
+        "rm1", "rv1", "rm2", "rv2", "y", "Z", "U", "stats",
+        "Wr", "br", "Za")]  # ABI 2: residual block
 
 
 class BwdArgs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in (
         "dy", "x", "Z", "U", "stats", "A", "W", "bW", "Wt", "g1", "b1", "g2", "b2",
-        "dx", "dA", "dW", "dbW", "dWt", "dbWt", "dg1", "db1", "dg2", "db2")]
+        "dx", "dA", "dW", "dbW", "dWt", "dbWt", "dg1", "db1", "dg2", "db2",
+        "Wr", "Za", "y", "dWr", "dbr")]  # ABI 2: residual block
 
 
 # Every symbol include/stgcn_hip.h declares (checked by tests/test_capi.py).

@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fused import StgcnBlockFn
+from .fused import StgcnBlockFn, StgcnResBlockFn
 
 
 class SpatialConv(nn.Module):
@@ -40,9 +40,9 @@ class SpatialConv(nn.Module):
 class SpatialTemporalConv(nn.Module):
     """Reference: st_graphconv.py:4-109 (same arguments, children, state_dict).
 
-    Accelerated: the non-residual block, training and eval mode. Dropout
-    (p > 0, training) is applied after the fused block with torch's dropout.
-    The residual variant is not implemented on the HIP path yet and raises.
+    Accelerated: the default and the residual block (full pre-activation,
+    st_graphconv.py:60-82), training and eval mode. Dropout (p > 0, training)
+    is applied after the fused block with torch's dropout.
     """
 
     def __init__(self, C_in, C_out, A, gamma, temporal_stride, temporal_padding,
@@ -73,8 +73,6 @@ class SpatialTemporalConv(nn.Module):
         self.pad = temporal_padding
 
     def forward(self, f_in):
-        if self.residual:
-            raise NotImplementedError("residual ST-GCN block is not implemented on the HIP path")
         bn1, bn2 = self.batch_n, self.batch_n_2
         if bn1.momentum is None or bn2.momentum is None:
             raise NotImplementedError("BatchNorm momentum=None (cumulative average)")
@@ -84,11 +82,21 @@ class SpatialTemporalConv(nn.Module):
             bn2.num_batches_tracked.add_(1)
         sc = self.spatialConv
         x = f_in.float()
-        y = StgcnBlockFn.apply(
-            x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
-            self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
-            bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-            self.stride, self.pad, bn1.eps, bn1.momentum, training)
+        if self.residual:
+            proj = self.apply_residual if isinstance(self.apply_residual, nn.Conv2d) else None
+            y = StgcnResBlockFn.apply(
+                x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
+                self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
+                proj.weight if proj is not None else None,
+                proj.bias if proj is not None else None,
+                bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
+                self.stride, self.pad, bn1.eps, bn1.momentum, training)
+        else:
+            y = StgcnBlockFn.apply(
+                x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
+                self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
+                bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
+                self.stride, self.pad, bn1.eps, bn1.momentum, training)
         if self.dropout is None:
             return y
         return F.dropout(y, self.dropout.p, training=training)

@@ -26,10 +26,10 @@ def test_header_declares_entry_points(pkg):
     assert _header_functions() == sorted(pkg.hip_lib.EXPORTED)
 
 
-def test_library_exports_every_header_symbol(lib):
+def test_library_exports_every_header_symbol(pkg, lib):
     for name in _header_functions():
         assert hasattr(lib, name), name
-    assert lib.stgcn_abi_version() == 1
+    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 2
 
 
 def _desc(pkg, **kw):
@@ -41,7 +41,9 @@ def _desc(pkg, **kw):
 
 def test_check_desc_accepts_north_star_shapes(pkg, lib):
     for kw in (dict(), dict(C_in=3), dict(C_in=64, C_out=128, stride=2, T_out=150),
-               dict(V=25, K=3), dict(V=50, K=3, C_in=256, C_out=256, T=75, T_out=75)):
+               dict(V=25, K=3), dict(V=50, K=3, C_in=256, C_out=256, T=75, T_out=75),
+               dict(flags=1), dict(flags=1, C_in=64, C_out=128, stride=2, T_out=150),
+               dict(flags=1, V=25, K=3, C_in=3)):
         d = _desc(pkg, **kw)
         assert lib.stgcn_check_desc(ctypes.byref(d)) == 0, kw
         assert lib.stgcn_fwd_workspace_bytes(ctypes.byref(d)) > 0
@@ -49,7 +51,7 @@ def test_check_desc_accepts_north_star_shapes(pkg, lib):
 
 
 @pytest.mark.parametrize("kw,code", [
-    (dict(flags=1), -2), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
+    (dict(flags=2), -2), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
     (dict(T_out=299), -1), (dict(N=0), -1), (dict(V=300), -2)])
 def test_check_desc_rejects(pkg, lib, kw, code):
     d = _desc(pkg, **kw)
@@ -63,6 +65,14 @@ def test_null_arguments_fail_without_touching_gpu(pkg, lib):
     args = pkg.hip_lib.FwdArgs()
     assert lib.stgcn_block_fwd(ctypes.byref(d), ctypes.byref(args), None, 0, None) == -1
     assert b"null" in lib.stgcn_last_error()
+
+
+def test_residual_null_projection_fails(pkg, lib):
+    """A projection residual block (C_in != C_out) needs Wr / br / Za."""
+    d = _desc(pkg, flags=1, C_in=32)
+    args = pkg.hip_lib.FwdArgs(*([ctypes.c_void_p(256)] * 18))  # dummy non-null core args
+    assert lib.stgcn_block_fwd(ctypes.byref(d), ctypes.byref(args), None, 0, None) == -1
+    assert b"residual" in lib.stgcn_last_error()
 
 
 def test_cpu_tensors_fail_loudly(pkg):

@@ -8,7 +8,9 @@ reference's own error for that tensor ("no worse than the reference"). The
 latter happens for BN-heavy small batches (T=1) and for large-N bias-type
 gradients (sums of ~1e5 cancelling terms). The temporal-conv bias gradient is
 analytically zero (BN2 follows the conv) and is checked with an absolute
-tolerance instead.
+tolerance instead (non-residual block only: in the residual block it is a real
+gradient). Residual blocks (full pre-activation, st_graphconv.py:60-82) use
+the same gates.
 """
 import numpy as np
 import pytest
@@ -29,16 +31,21 @@ DEV = "cuda:0"
 def _run_hip(pkg, arrays, x, g, need_dx=True):
     """Fused block fwd+bwd on the GPU; returns the oracle-style result dict."""
     p, b = ref_cpu.block_params_from_arrays(arrays, dtype=torch.float32, requires_grad=False)
-    stride = int(arrays["meta"][2])
+    stride, residual = int(arrays["meta"][2]), bool(arrays["meta"][7])
     cu = {k: v.to(DEV).contiguous().requires_grad_(True) for k, v in p.items()}
     bu = {k: v.to(DEV).clone() for k, v in b.items() if "num_batches" not in k}
     xd = x.to(DEV).float().contiguous().requires_grad_(need_dx)
-    y = pkg.fused.StgcnBlockFn.apply(
-        xd, cu["spatialConv.A"], cu["spatialConv.W.weight"], cu["spatialConv.W.bias"],
-        cu["temporalConv.weight"], cu["temporalConv.bias"], cu["batch_n.weight"],
-        cu["batch_n.bias"], cu["batch_n_2.weight"], cu["batch_n_2.bias"],
-        bu["batch_n.running_mean"], bu["batch_n.running_var"],
-        bu["batch_n_2.running_mean"], bu["batch_n_2.running_var"], stride, 4, 1e-5, 0.1, True)
+    common = (xd, cu["spatialConv.A"], cu["spatialConv.W.weight"], cu["spatialConv.W.bias"],
+              cu["temporalConv.weight"], cu["temporalConv.bias"], cu["batch_n.weight"],
+              cu["batch_n.bias"], cu["batch_n_2.weight"], cu["batch_n_2.bias"])
+    running = (bu["batch_n.running_mean"], bu["batch_n.running_var"],
+               bu["batch_n_2.running_mean"], bu["batch_n_2.running_var"])
+    if residual:
+        y = pkg.fused.StgcnResBlockFn.apply(
+            *common, cu.get("apply_residual.weight"), cu.get("apply_residual.bias"), *running,
+            stride, 4, 1e-5, 0.1, True)
+    else:
+        y = pkg.fused.StgcnBlockFn.apply(*common, *running, stride, 4, 1e-5, 0.1, True)
     y.backward(g.to(DEV).float())
     torch.cuda.synchronize()
     out = {"y": y.detach().cpu()}
@@ -71,17 +78,18 @@ def _compare(got, want, residual=False, tol=TOL, floor=None):
     assert not bad, "; ".join(f"{k}: {e:.2e} > {l:.1e}" for k, e, l in bad)
 
 
-@pytest.mark.parametrize("fixture", [f for f in block_fixtures() if not f.startswith("block_res")])
+@pytest.mark.parametrize("fixture", block_fixtures())
 def test_block_matches_reference_fixture(pkg, fixture):
     ref = load_npz(fixture)
+    residual = bool(ref["meta"][7])
     x = torch.from_numpy(ref["x"])
     g = torch.from_numpy(ref["g"])
     got = _run_hip(pkg, ref, x, g)
     want64, floor = _oracle(ref, got)
-    _compare(got, want64, floor=floor)
+    _compare(got, want64, residual=residual, floor=floor)
     # and against the reference's own fp32 outputs (its rounding included)
     _compare(got, {k: torch.from_numpy(v) for k, v in ref.items()
-                   if k == "y" or k.startswith("grad.")}, tol=5e-5)
+                   if k == "y" or k.startswith("grad.")}, residual=residual, tol=5e-5)
 
 
 # ReLU ties: a pre-ReLU value within fp32 rounding of 0 can land on either
@@ -106,24 +114,25 @@ def _oracle(arrays, got):
     return want, floor
 
 
-def _random_case(pkg, C_in, C_out, stride, V, K, N, T, seed=0):
-    return _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed)
+def _random_case(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=False):
+    return _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed, residual)
 
 
-def _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed=0):
+def _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=False):
     gr = pkg.graph
     strat = 0 if K == 1 else 2
     A = gr.get_normalized_adjacency_matrices(strat, 1, distances=gr.synthetic_distances(V),
                                              graph=gr.graph_for(V))
     torch.manual_seed(seed)
-    blk = pkg.SpatialTemporalConv(C_in, C_out, A, 9, stride, 4, dropout_rate=0)
+    blk = pkg.SpatialTemporalConv(C_in, C_out, A, 9, stride, 4, dropout_rate=0,
+                                  residual=residual)
     gen = torch.Generator().manual_seed(seed + 3)
     with torch.no_grad():
         for bn in (blk.batch_n, blk.batch_n_2):
             bn.weight.copy_(1.0 + 0.1 * torch.randn(bn.weight.shape, generator=gen))
             bn.bias.copy_(0.1 * torch.randn(bn.bias.shape, generator=gen))
     arrays = {"param." + k: v.detach().numpy() for k, v in blk.state_dict().items()}
-    arrays["meta"] = np.array([C_in, C_out, stride, V, strat, N, T, 0])
+    arrays["meta"] = np.array([C_in, C_out, stride, V, strat, N, T, int(residual)])
     x = torch.randn(N, C_in, T, V, generator=torch.Generator().manual_seed(seed + 1))
     T_out = (T - 1) // stride + 1
     g = torch.randn(N, C_out, T_out, V, generator=torch.Generator().manual_seed(seed + 2))
@@ -201,4 +210,68 @@ def test_eval_mode_uses_running_stats(pkg):
     want = ref_cpu.block_forward(x.double(), p64, b64, 2, training=False, dtype=torch.float64)
     assert rel_to_max(y.cpu().numpy(), want.numpy()) < TOL
     for k in bu:  # eval mode leaves running stats untouched
+        assert torch.equal(bu[k].cpu(), b[k])
+
+
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T   (residual block, st_graphconv.py:60-82)
+    (64, 64, 1, 18, 1, 3, 40),      # identity residual
+    (64, 128, 2, 18, 1, 2, 37),     # projection, stride 2, odd T
+    (3, 64, 1, 18, 1, 3, 45),       # projection, stride 1 (channels differ)
+    (128, 128, 1, 25, 3, 2, 30),    # identity, K=3
+    (64, 128, 2, 25, 3, 2, 33),     # projection, K=3
+    (64, 64, 1, 50, 3, 2, 17),      # identity, V=50
+    (5, 7, 2, 18, 1, 2, 9),         # odd channel counts, projection stride 2
+])
+def test_residual_block_matches_oracle_random(pkg, case):
+    C_in, C_out, stride, V, K, N, T = case
+    arrays, x, g = _random_case(pkg, C_in, C_out, stride, V, K, N, T, residual=True)
+    got = _run_hip(pkg, arrays, x, g)
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, residual=True, floor=floor)
+
+
+def test_residual_block_without_dx(pkg):
+    arrays, x, g = _random_case(pkg, 3, 64, 2, 18, 1, 2, 30, residual=True)
+    got = _run_hip(pkg, arrays, x, g, need_dx=False)
+    want, floor = _oracle(arrays, got)
+    want.pop("grad.x")
+    _compare(got, want, residual=True, floor=floor)
+
+
+def test_residual_full_size_block(pkg):
+    """cfg2 L4 shape (64 -> 128, stride 2, projection) at N=16, T=300."""
+    arrays, x, g = _random_case(pkg, 64, 128, 2, 18, 1, 16, 300, seed=5, residual=True)
+    got = _run_hip(pkg, arrays, x, g)
+    for k, v in got.items():
+        assert torch.isfinite(v).all(), k
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, residual=True, floor=floor)
+
+
+def test_residual_eval_mode(pkg):
+    arrays, x, _ = _random_case(pkg, 64, 128, 2, 18, 1, 2, 21, residual=True)
+    p, b = ref_cpu.block_params_from_arrays(arrays, dtype=torch.float32, requires_grad=False)
+    gen = torch.Generator().manual_seed(12)
+    for k in b:
+        if "running_mean" in k:
+            b[k] = 0.1 * torch.randn(b[k].shape, generator=gen)
+        elif "running_var" in k:
+            b[k] = 0.5 + torch.rand(b[k].shape, generator=gen)
+    cu = {k: v.to(DEV) for k, v in p.items()}
+    bu = {k: v.to(DEV).clone() for k, v in b.items() if "num_batches" not in k}
+    with torch.no_grad():
+        y = pkg.fused.StgcnResBlockFn.apply(
+            x.to(DEV), cu["spatialConv.A"], cu["spatialConv.W.weight"], cu["spatialConv.W.bias"],
+            cu["temporalConv.weight"], cu["temporalConv.bias"], cu["batch_n.weight"],
+            cu["batch_n.bias"], cu["batch_n_2.weight"], cu["batch_n_2.bias"],
+            cu["apply_residual.weight"], cu["apply_residual.bias"],
+            bu["batch_n.running_mean"], bu["batch_n.running_var"],
+            bu["batch_n_2.running_mean"], bu["batch_n_2.running_var"], 2, 4, 1e-5, 0.1, False)
+    p64 = {k: v.double() for k, v in p.items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
+    want = ref_cpu.block_forward(x.double(), p64, b64, 2, residual=True, training=False,
+                                 dtype=torch.float64)
+    assert rel_to_max(y.cpu().numpy(), want.numpy()) < TOL
+    for k in bu:
         assert torch.equal(bu[k].cpu(), b[k])
