@@ -120,6 +120,31 @@ def kernel_roofline(pkg, device, cfg, iters=10):
     return kinds, symbols
 
 
+def per_block_rates(model, cfg, device, iters=5):
+    """per-block clips/s (fwd+bwd of one block, L0..L9) at the
+    bench batch, timed with events after the main measurement."""
+    out, c, t = {}, cfg["C"], cfg["T"]
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    for i, (ci, co, tin, s) in enumerate(stack_layers(cfg)):
+        blk = model.conv[i]
+        x = torch.randn(cfg["N"], ci, tin, cfg["V"], generator=gen).to(device)
+        x.requires_grad_(i > 0)
+        tout = (tin - 1) // s + 1
+        g = torch.randn(cfg["N"], co, tout, cfg["V"], generator=gen).to(device)
+        for _ in range(2):
+            blk(x).backward(g)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            blk(x).backward(g)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        out[f"L{i}"] = round(cfg["N"] / (ms * 1e-3), 1)
+    model.zero_grad(set_to_none=True)
+    return out
+
+
 def traffic_from_profiles(symbol):
     """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC pass
     (profiles/pmc_*.json: FETCH_SIZE doubled per the gfx950 correction +
@@ -210,6 +235,7 @@ def main():
             "loss": round(float(loss.item()), 5),
         }
         if not args.no_roofline:
+            out["per_block_clips_s"] = per_block_rates(model, cfg, device)
             kinds, symbols = kernel_roofline(pkg, device, cfg)
             sym = max(symbols, key=lambda k: symbols[k][0])
             ms_tot, fl_tot, nl = symbols[sym]

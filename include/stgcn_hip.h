@@ -90,6 +90,9 @@ typedef struct stgcn_fwd_args {
   /* ABI 2 (residual block; null otherwise) */
   const float *Wr, *br;                 /* apply_residual Conv2d (projection) */
   float *Za;                            /* saved: ReLU(BN2(Z)) N,C_out,T,V    */
+  /* ABI 2, optional: keep the joint contraction G = f(BN1(x)) A^T
+   * (N, K*C_in, T, V) for the backward instead of recomputing it */
+  float *G;
 } stgcn_fwd_args_t;
 
 /* Backward arguments: the gradients of every input of the forward. */
@@ -104,6 +107,7 @@ typedef struct stgcn_bwd_args {
   const float *Wr;                      /* projection weight or null          */
   const float *Za, *y;                  /* saved by the forward               */
   float *dWr, *dbr;                     /* projection gradients or null       */
+  const float *G;                       /* optional: G kept by the forward    */
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);

@@ -376,11 +376,11 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     Wz = L.Wpk;
   }
   // (residual block: SpatialConv sees ReLU(BN1(x)), st_graphconv.py:72-74)
-  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, res,
-                            s));
+  float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
+  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s));
   {
     ConvGemmParams p = conv_base(d, L.wpk);
-    p.in = L.G;
+    p.in = G;
     p.w = Wz;
     p.out = a->Z;
     p.bias_rv = L.biasZ;
@@ -537,10 +537,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   // residual block), then
   //   dW' = dZ G^T (split-K), H_k = W_k^T dZ, dxhat = sum_k H_k A_k,
   //   dA = sum H_k^T f(BN1(x)) + bias part, dbW = sum dZ rowsum(A_k).
-  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, res,
-                            s));
+  const float *G = a->G;  // kept by the forward, else recomputed
+  if (!G) {
+    HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, res,
+                              s));
+    G = L.G;
+  }
   {
-    WgradParams w = make_wgrad(d, L.dZ, (int64_t)R * T * V, R, T, L.G, (int64_t)K * C * T * V,
+    WgradParams w = make_wgrad(d, L.dZ, (int64_t)R * T * V, R, T, G, (int64_t)K * C * T * V,
                                K * C, T, 1, 1, 0, L.slab);
     HIP_TRY(launch_wgrad(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));

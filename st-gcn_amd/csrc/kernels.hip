@@ -2313,39 +2313,89 @@ __global__ __launch_bounds__(256) void k_sum_nt(const float *X, int C, int T, in
   }
 }
 
+// k_sum_nt with float4 loads: 4*A consecutive floats per pass, A = the
+// largest multiple of the float4 period of V (V / gcd(4, V)) <= 256, so each
+// thread's 4 lanes keep fixed joints v = (4*tid + u) % V across passes; the
+// per-thread fp64 partials are then folded per joint through LDS.
+__global__ __launch_bounds__(256) void k_sum_nt4(const float *X, int C, int T, int V,
+                                                 double *out) {
+  __shared__ double part[1024];
+  const int c = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const int L = T * V;
+  const int per = V / (V % 4 == 0 ? 4 : (V % 2 == 0 ? 2 : 1));  // float4 period
+  const int A = 256 / per * per;                                 // active threads
+  const float4 *src = reinterpret_cast<const float4 *>(X + ((int64_t)n * C + c) * L);
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (tid < A) {
+    for (int f = tid; f < L / 4; f += A) {
+      const float4 q = src[f];
+      a0 += q.x;
+      a1 += q.y;
+      a2 += q.z;
+      a3 += q.w;
+    }
+  }
+  part[4 * tid] = a0;
+  part[4 * tid + 1] = a1;
+  part[4 * tid + 2] = a2;
+  part[4 * tid + 3] = a3;
+  __syncthreads();
+  if (tid < V) {
+    double acc = 0.0;
+    for (int p = tid; p < 4 * A; p += V) acc += part[p];  // 4*A is a multiple of V
+    atomicAdd(out + c * V + tid, acc);
+  }
+}
+
 hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out, hipStream_t s) {
+  if (((int64_t)T * V) % 4 == 0 && ((uintptr_t)X & 15) == 0 && V <= 256) {
+    hipLaunchKernelGGL(k_sum_nt4, dim3(C, N), dim3(256), 0, s, X, C, T, V, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_sum_nt, dim3(C, N), dim3(256), 0, s, X, C, T, V, out);
   return hipGetLastError();
 }
 
 // dbW[k*R+co] = sum_v SdZ[co][v] * rowsum(A_k)[v]
 // dA[k][v][w]  = sum_co bW[k*R+co] * SdZ[co][v]      (bias part of dA; all w)
-__global__ void k_spatial_small(const double *SdZ, const float *A, const float *bW, int K, int R,
-                                int V, float *dbW, float *dA) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < K * R) {
-    const int k = idx / R, co = idx - k * R;
-    double s = 0.0;
-    for (int v = 0; v < V; ++v) {
-      double ra = 0.0;
-      for (int w = 0; w < V; ++w) ra += A[((int64_t)k * V + v) * V + w];
-      s += SdZ[co * V + v] * ra;
-    }
-    dbW[idx] = (float)s;
+// One block per partition k; V <= 90 (K*V*V <= 8192, checked by the C-ABI).
+__global__ __launch_bounds__(256) void k_spatial_small(const double *SdZ, const float *A,
+                                                       const float *bW, int K, int R, int V,
+                                                       float *dbW, float *dA) {
+  __shared__ double rs[128], part[256];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  for (int v = tid; v < V; v += 256) {
+    double ra = 0.0;
+    for (int w = 0; w < V; ++w) ra += A[((int64_t)k * V + v) * V + w];
+    rs[v] = ra;
   }
-  if (idx < K * V) {
-    const int k = idx / V, v = idx - k * V;
-    double s = 0.0;
-    for (int co = 0; co < R; ++co) s += (double)bW[k * R + co] * SdZ[co * V + v];
-    for (int w = 0; w < V; ++w) dA[((int64_t)k * V + v) * V + w] = (float)s;
+  __syncthreads();
+  for (int co = tid; co < R; co += 256) {
+    double acc = 0.0;
+    for (int v = 0; v < V; ++v) acc += SdZ[co * V + v] * rs[v];
+    dbW[k * R + co] = (float)acc;
   }
+  // bias part of dA: thread (v, j) sums co = j, j + P, ... (P = 256 / V parts)
+  const int P = 256 / V;
+  const int v = tid % V, j = tid / V;
+  double acc = 0.0;
+  if (j < P)
+    for (int co = j; co < R; co += P) acc += (double)bW[k * R + co] * SdZ[co * V + v];
+  part[tid] = acc;
+  __syncthreads();
+  if (tid < V) {
+    double t = 0.0;
+    for (int jj = 0; jj < P; ++jj) t += part[jj * V + tid];
+    rs[tid] = t;  // rowsums no longer needed
+  }
+  __syncthreads();
+  for (int i = tid; i < V * V; i += 256) dA[(int64_t)k * V * V + i] = (float)rs[i / V];
 }
 
 hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K, int R,
                                 int V, float *dbW, float *dA, hipStream_t s) {
-  const int n = K * R > K * V ? K * R : K * V;
-  hipLaunchKernelGGL(k_spatial_small, dim3((n + 255) / 256), dim3(256), 0, s, SdZ, A, bW, K, R, V,
-                     dbW, dA);
+  if (V > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_spatial_small, dim3(K), dim3(256), 0, s, SdZ, A, bW, K, R, V, dbW, dA);
   return hipGetLastError();
 }
 

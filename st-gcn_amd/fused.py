@@ -29,6 +29,16 @@ def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1
                         int(training), int(need_dx), hip_lib.F_RESIDUAL if residual else 0)
 
 
+def _keep_g(ctx, x, K):
+    """Buffer for the joint contraction G (N, K*C_in, T, V) when a backward
+    will run (the forward writes it once; the backward then skips recomputing
+    it), else None (eval / no-grad: the library uses its workspace)."""
+    if not (torch.is_grad_enabled() or any(ctx.needs_input_grad)):
+        return None
+    N, C, T, V = x.shape
+    return torch.empty((N, K * C, T, V), device=x.device, dtype=torch.float32)
+
+
 class StgcnBlockFn(torch.autograd.Function):
     """forward(x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
                stride, pad, eps, momentum, training) -> y
@@ -57,21 +67,22 @@ class StgcnBlockFn(torch.autograd.Function):
         Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
         U = torch.empty_like(y)
         stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
+        G = _keep_g(ctx, x, K)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats,
-            None, None, None)])
+            None, None, None, G)])
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
-        ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2)
+        ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = hip_lib.lib()
-        x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2 = ctx.saved_tensors
+        x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G = ctx.saved_tensors
         stride, pad, eps, momentum, training = ctx.cfg
         need_dx = bool(ctx.needs_input_grad[0])
         dy = dy.contiguous()
@@ -87,7 +98,7 @@ class StgcnBlockFn(torch.autograd.Function):
         args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
             dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
-            None, None, None, None, None)])
+            None, None, None, None, None, G)])
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))
@@ -131,21 +142,22 @@ class StgcnResBlockFn(torch.autograd.Function):
         Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
         Za = torch.empty_like(Z)
         stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
+        G = _keep_g(ctx, x, K)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, None, stats,
-            Wr, br, Za)])
+            Wr, br, Za, G)])
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
-        ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr)
+        ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         lib = hip_lib.lib()
-        x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr = ctx.saved_tensors
+        x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr, G = ctx.saved_tensors
         stride, pad, eps, momentum, training = ctx.cfg
         need_dx = bool(ctx.needs_input_grad[0])
         dy = dy.contiguous()
@@ -164,7 +176,7 @@ class StgcnResBlockFn(torch.autograd.Function):
         args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
             dy, x, Z, None, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-            Wr, Za, y, dWr, dbr)])
+            Wr, Za, y, dWr, dbr, G)])
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2, dWr, dbr,
