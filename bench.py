@@ -90,7 +90,7 @@ def kernel_roofline(pkg, device, cfg, iters=10):
     """Per-kernel timing with HIP events on the launch stream (the library's
     stgcn_time_kernel entry point, same launch parameters as the block), over
     every layer of the stack. Returns {kind: (total_ms, total_flops, launches)}
-    and the same aggregated per kernel symbol (rocprof names: k_tconv<9,4,V,1>
+    and the same aggregated per kernel symbol (rocprof names: k_tconv<9,2,V,1>
     = temporal forward + data-grad of the stride-1 layers)."""
     import ctypes
     hl = pkg.hip_lib
@@ -113,8 +113,8 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             del scratch
             add(kinds, kind, ms.value, fl.value, 1)
             V = cfg["V"]
-            sym = {0: f"k_tconv<9,4,{V},{s}>",
-                   1: f"k_tconv<9,4,{V},1>" if s == 1 else f"k_tconv<5|4,4,{V},1>",
+            sym = {0: f"k_tconv<9,2,{V},{s}>",
+                   1: f"k_tconv<9,2,{V},1>" if s == 1 else f"k_tconv<5|4,2,{V},1>",
                    2: f"k_wgrad_taps<{V},{s}>", 3: f"k_tconv<1,8,{V},1>"}[which]
             add(symbols, sym, ms.value, fl.value, 1 if (which != 1 or s == 1) else 2)
     return kinds, symbols

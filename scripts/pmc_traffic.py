@@ -57,7 +57,7 @@ def main(src, dst):
         out["calibration_k_bn_stats"] = {
             "algorithmic_read_bytes": round(alg), "fetch_size_bytes": round(fs),
             "fetch_over_algorithmic": round(fs / alg, 3)}
-    # bench.py keys its dominant kernel as k_tconv<9,4,V,1> (the same short names)
+    # bench.py keys its dominant kernel as k_tconv<9,2,V,1> (the same short names)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out.get("calibration_k_bn_stats"), indent=1))
     for k, v in out["hbm_bytes_per_launch"].items():

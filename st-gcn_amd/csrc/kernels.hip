@@ -305,6 +305,17 @@ struct ConvGeo {
   static constexpr int WLAST = (WSZ % 256) / 4;       // lanes of a partial last row (0: full)
   static constexpr int NS = CK / 2 * NQ;              // MFMA k-steps per chunk
   static_assert(CK % 2 == 0 && WSZ % 4 == 0, "k-steps pair channels; 16-byte weight pieces");
+  // ring-buffered staging: the chunk's DMA rows (WROWS 16-byte weight rows,
+  // then input rows) are dealt round-robin to the 4 waves, padded with extra
+  // input rows (zero-filled, never read) so every wave issues DPW DMAs.
+  static constexpr int DPW = (WROWS + IROWS + 3) / 4;   // DMAs per wave per chunk
+  static constexpr int IROWS_P = 4 * DPW - WROWS;       // input rows incl. padding
+  static constexpr int WBUF = WROWS * 256, IBUF = IROWS_P * 64;
+  static constexpr int BUF = WBUF + IBUF;               // floats per ring slot
+  // ring depth: 3 slots for the temporal taps (chunk compute ~ DMA latency),
+  // 2 for the short spatial chunks (measured)
+  static constexpr int STAGES = NQ == 1 ? 2 : 3;
+  static_assert((STAGES - 2) * DPW < 64, "vmcnt range");
 };
 
 template <int NQ, int CK, int V, int SIN>
@@ -320,8 +331,6 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
   const int mt = bid % p.n_mtiles;
   const int n = bid / p.n_mtiles;
   const int r0 = rt * kTileRows, m0 = mt * G::FT;
-  float *Ws0 = smem, *Ws1 = smem + G::WSZ;
-  float *Is0 = smem + 2 * G::WSZ, *Is1 = smem + 2 * G::WSZ + G::ISZ;
   const int cstride = p.T_src * V;
   const int g0 = (SIN * m0 + p.off) * V;
   const float *inN = p.in + (int64_t)n * p.in_bstride;
@@ -337,29 +346,37 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
     const int mf = col / V;
     bb[j] = hi * G::SP + (col < G::NCOLS ? SIN * mf * V + (col - mf * V) : 0);
   }
-  unsigned voff[G::NI];  // input DMA byte offsets (relative to the chunk's first channel)
+  // DMA slot k of this wave: row d = 4k + wave; d < WROWS: weight row d
+  // (16 B/lane), else input row d - WROWS (4 B/lane, byte offset voff[k]
+  // relative to the chunk's first channel; kOOB outside the image)
+  unsigned voff[G::DPW];
 #pragma unroll
-  for (int i = 0; i < G::NI; ++i) {
-    const int e = (i * 4 + wave) * 64 + lane;
+  for (int k = 0; k < G::DPW; ++k) {
+    const int d = 4 * k + wave;
+    const int e = (d - G::WROWS) * 64 + lane;
     const int c = e / G::SP, o = e - c * G::SP;
     const int g = g0 + o;
-    const bool ok = c < CK && o < G::SPAN && g >= 0 && g < cstride;
-    voff[i] = ok ? (unsigned)(c * cstride + g) * 4u : kOOB;
+    const bool ok = d >= G::WROWS && c < CK && o < G::SPAN && g >= 0 && g < cstride;
+    voff[k] = ok ? (unsigned)(c * cstride + g) * 4u : kOOB;
   }
   const __amdgpu_buffer_rsrc_t rs_w = make_rsrc(wblk, (int64_t)p.Cpad * NQ * 64);
   auto stage = [&](int chunk, float *Ws, float *Is) {
-#pragma unroll
-    for (int k = 0; k < (G::WROWS + 3) / 4; ++k) {
-      const int r = k * 4 + wave;
-      if (r < G::WROWS && (G::WLAST == 0 || r < G::WROWS - 1 || lane < G::WLAST))
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs_w, Ws + r * 256, 16, (unsigned)(chunk * G::WSZ + r * 256 + lane * 4) * 4u, 0, 0, 0);
-    }
     const __amdgpu_buffer_rsrc_t rs_in =
         make_rsrc(inN + (int64_t)chunk * CK * cstride, (int64_t)(p.C - chunk * CK) * cstride);
 #pragma unroll
-    for (int i = 0; i < G::NI; ++i)
-      if (i * 4 + wave < G::IROWS) blds_f32(rs_in, voff[i], Is + (i * 4 + wave) * 64);
+    for (int k = 0; k < G::DPW; ++k) {
+      const int d = 4 * k + wave;  // wave-uniform
+      if (d < G::WROWS) {
+        // a partial last weight row still issues (OOB lanes: zero) so that every
+        // wave's DMA count stays DPW
+        const bool lane_ok = G::WLAST == 0 || d < G::WROWS - 1 || lane < G::WLAST;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs_w, Ws + d * 256, 16,
+            lane_ok ? (unsigned)(chunk * G::WSZ + d * 256 + lane * 4) * 4u : kOOB, 0, 0, 0);
+      } else {
+        blds_f32(rs_in, voff[k], Is + (d - G::WROWS) * 64);
+      }
+    }
   };
 
   floatx16 acc[4];
@@ -368,13 +385,25 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 
-  stage(0, Ws0, Is0);
-  __syncthreads();
-  for (int chunk = 0; chunk < nchunks; ++chunk) {
-    const bool odd = chunk & 1;
-    const float *Ws = odd ? Ws1 : Ws0;
-    const float *Is = odd ? Is1 : Is0;
-    if (chunk + 1 < nchunks) stage(chunk + 1, odd ? Ws0 : Ws1, odd ? Is0 : Is1);
+  // STAGES-slot ring: chunks c+1 .. c+STAGES-1 are in flight while chunk c
+  // computes. Each wave waits only for its own DMAs of chunk c (vmcnt counts
+  // retire in order), then one barrier publishes the chunk (a fenced
+  // __syncthreads would drain the whole ring).
+  constexpr int S = G::STAGES;
+  auto wbuf = [&](int slot) { return smem + slot * G::BUF; };
+  auto ibuf = [&](int slot) { return smem + slot * G::BUF + G::WBUF; };
+#pragma unroll
+  for (int c = 0; c < S - 1; ++c)
+    if (c < nchunks) stage(c, wbuf(c), ibuf(c));
+  auto body = [&](int chunk, auto slot_c) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    if (S == 3 && chunk + 1 < nchunks)  // chunk c+1 may stay in flight
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((S - 2) * G::DPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (chunk + S - 1 < nchunks)
+      stage(chunk + S - 1, wbuf((SLOT + S - 1) % S), ibuf((SLOT + S - 1) % S));
+    const float *Ws = wbuf(SLOT), *Is = ibuf(SLOT);
     const float *wp = Ws + hi * NQ * 64 + mi * 32 + lo;
     const float *ib0 = Is + bb[0], *ib1 = Is + bb[1], *ib2 = Is + bb[2], *ib3 = Is + bb[3];
     constexpr int PD = 2;  // operands are read PD k-steps ahead of their MFMAs
@@ -403,8 +432,15 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();  // retires this wave's LDS-DMA (vmcnt(0)) and publishes the next chunk
+  };
+  static_assert(S == 2 || S == 3, "ring depth");
+  for (int chunk = 0; chunk < nchunks; chunk += S) {
+    body(chunk, std::integral_constant<int, 0>{});
+    if (chunk + 1 < nchunks) body(chunk + 1, std::integral_constant<int, 1>{});
+    if constexpr (S == 3)
+      if (chunk + 2 < nchunks) body(chunk + 2, std::integral_constant<int, 2 % S>{});
   }
+  asm volatile("s_barrier" ::: "memory");  // every wave done reading the ring (LDS reuse)
 
   // Epilogue: bias, store, optional per-row BN statistics (fp64). Buffer
   // loads/stores with 32-bit offsets; masked elements get offset kOOB (loads
@@ -517,12 +553,12 @@ static bool tconv_specialised(const ConvGemmParams &p) {
   return p.s_in == 1 && (p.NQ == 1 || p.NQ == 4 || p.NQ == 5 || p.NQ == 9);
 }
 
-// Channels per reduction chunk. Specialised kernels: 8 for the spatial GEMM,
-// 4 for the temporal taps (small LDS images: 4-5 workgroups per CU; measured
-// against 16/32 and 6/8 with scripts/ck_sweep.sh).
+// Channels per reduction chunk. Specialised kernels: 8 for the spatial GEMM
+// (2-slot ring), 2 for the temporal taps (3-slot ring, 27 KB of LDS: 4
+// workgroups per CU); measured against 16/32 and 4/6/8 (scripts/ck_sweep.sh).
 static int conv_ck(const ConvGemmParams &p) {
   if (!tconv_specialised(p)) return p.NQ == 1 ? 32 : 8;
-  return p.NQ == 1 ? 8 : 4;
+  return p.NQ == 1 ? 8 : 2;
 }
 
 int conv_gemm_cpad(const ConvGemmParams &p) {
@@ -539,7 +575,13 @@ int conv_gemm_span(const ConvGemmParams &p) { return (p.s_in * (p.FT - 1) + p.NQ
 size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
   const int CK = conv_ck(p);
   const size_t stage = sizeof(float) * 2 * ((size_t)CK * p.NQ * 64 + round64(CK * (conv_gemm_span(p) | 1)));
-  if (tconv_specialised(p)) return stage;  // stats partials (2 KiB) reuse the staging area
+  if (tconv_specialised(p)) {  // ring of ConvGeo::STAGES slots; stats partials (2 KiB) reuse it
+    const int WROWS = (CK * p.NQ * 64 + 255) / 256;
+    const int IROWS = round64(CK * (conv_gemm_span(p) | 1)) / 64;
+    const int DPW = (WROWS + IROWS + 3) / 4;
+    const int stages = p.NQ == 1 ? 2 : 3;
+    return sizeof(float) * stages * ((size_t)WROWS * 256 + (size_t)(4 * DPW - WROWS) * 64);
+  }
   const size_t stats = sizeof(double) * 4 * 16 * 2 * 64;  // k_conv_gemm epilogue buffer
   return stage > stats ? stage : stats;
 }
@@ -574,7 +616,7 @@ static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t ld
   if constexpr (NQ == 1) {
     if (CK == 8) return launch_tconv_v<NQ, 8>(p, nblk, lds, s);
   } else {
-    if (CK == 4) return launch_tconv_v<NQ, 4>(p, nblk, lds, s);
+    if (CK == 2) return launch_tconv_v<NQ, 2>(p, nblk, lds, s);
   }
   return false;
 }
