@@ -93,6 +93,11 @@ typedef struct stgcn_fwd_args {
   /* ABI 2, optional: keep the joint contraction G = f(BN1(x)) A^T
    * (N, K*C_in, T, V) for the backward instead of recomputing it */
   float *G;
+  /* ABI 2, optional stack chaining (training): x_stats = [sum(C_in), sumsq(C_in)]
+   * of x over (n,t,v) in fp64 (produced by the previous block's y_stats: the
+   * BN1 statistics pass is skipped); y_stats (out) = the same for y (C_out). */
+  const double *x_stats;
+  double *y_stats;
 } stgcn_fwd_args_t;
 
 /* Backward arguments: the gradients of every input of the forward. */
@@ -108,6 +113,15 @@ typedef struct stgcn_bwd_args {
   const float *Za, *y;                  /* saved by the forward               */
   float *dWr, *dbr;                     /* projection gradients or null       */
   const float *G;                       /* optional: G kept by the forward    */
+  /* optional stack chaining (non-residual blocks):
+   * dy_sums = [sum dy*m, sum dy*m*uhat] (2*C_out, fp64) of this block's
+   * ReLU+BN2 backward, produced by the next block (its reduction pass is
+   * skipped); prev_g2/prev_b2 = BN2 affine of the (non-residual) block that
+   * produced x, prev_sums (out, 2*C_in) = that block's dy_sums, computed while
+   * writing dx (needs need_dx). */
+  const double *dy_sums;
+  const float *prev_g2, *prev_b2;
+  double *prev_sums;
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);

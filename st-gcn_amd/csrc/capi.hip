@@ -251,7 +251,8 @@ static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
   float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
   HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * T * V, d->eps, d->momentum,
                              d->training, a->rm2, a->rv2, mean2, invstd2, s));
-  HIP_TRY(launch_bn_relu_fwd(a->Z, mean2, invstd2, a->g2, a->b2, a->Za, N, R, T * V, s));
+  HIP_TRY(launch_bn_relu_fwd(a->Z, mean2, invstd2, a->g2, a->b2, a->Za, N, R, T * V, nullptr,
+                             nullptr, s));
   const float *resid = a->x;
   if (projection(d)) {  // apply_residual: Conv2d(C_in, C_out, 1, stride (s,1)) (:27)
     ConvGemmParams p = conv_base(d, L.wpk);
@@ -285,6 +286,11 @@ static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
   p.bias_r = a->bWt;
   p.res = resid;
   p.relu_out = 1;
+  if (d->training && a->y_stats) {  // next block's BN1 statistics from the epilogue
+    HIP_TRY(hipMemsetAsync(a->y_stats, 0, sizeof(double) * 2 * R, s));
+    p.stat_sum = a->y_stats;
+    p.stat_sq = a->y_stats + R;
+  }
   p.in_bstride = (int64_t)R * T * V;
   p.out_bstride = (int64_t)R * To * V;
   p.w_sr = (int64_t)R * 9;
@@ -365,9 +371,16 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
 
   HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
   // BN1 statistics of the block input (st_graphconv.py:98)
-  if (d->training) HIP_TRY(launch_bn_stats(a->x, N, C, T * V, L.s1, L.q1, s));
-  HIP_TRY(launch_bn_finalize(L.s1, L.q1, C, (int64_t)N * T * V, d->eps, d->momentum,
-                             d->training, a->rm1, a->rv1, mean1, invstd1, s));
+  // (the caller may hand over the previous block's y statistics: x_stats)
+  const double *xs1 = L.s1, *xq1 = L.q1;
+  if (d->training && a->x_stats) {
+    xs1 = a->x_stats;
+    xq1 = a->x_stats + C;
+  } else if (d->training) {
+    HIP_TRY(launch_bn_stats(a->x, N, C, T * V, L.s1, L.q1, s));
+  }
+  HIP_TRY(launch_bn_finalize(xs1, xq1, C, (int64_t)N * T * V, d->eps, d->momentum, d->training,
+                             a->rm1, a->rv1, mean1, invstd1, s));
   // Spatial graph conv (st_graphconv.py:139-152) in the form (1).
   HIP_TRY(launch_bias_rv(a->A, a->bW, L.biasZ, K, R, V, s));
   const float *Wz = a->W;
@@ -440,7 +453,10 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   // BN2 (st_graphconv.py:100) + ReLU (:105)
   HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * To * V, d->eps, d->momentum,
                              d->training, a->rm2, a->rv2, mean2, invstd2, s));
-  HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, s));
+  double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
+  if (ys) HIP_TRY(hipMemsetAsync(ys, 0, sizeof(double) * 2 * R, s));
+  HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
+                             ys ? ys + R : nullptr, s));
   return STGCN_OK;
 }
 
@@ -455,6 +471,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     return fail(STGCN_E_INVALID, "null tensor argument");
   if (res && (!a->Za || !a->y || (projection(d) && (!a->Wr || !a->dWr || !a->dbr))))
     return fail(STGCN_E_INVALID, "residual block: null Za / y / projection tensors");
+  if (res && a->dy_sums)
+    return fail(STGCN_E_INVALID, "dy_sums applies to the non-residual block only");
   if (!d->training) return fail(STGCN_E_UNSUPPORTED, "backward in eval mode is not implemented");
   const BwdLayout L = bwd_layout(d, workspace);
   if (!workspace || workspace_bytes < L.total)
@@ -466,12 +484,19 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 
   HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
   if (!res) {
-    // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias)
-    HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
-                                      L.sg, L.sgu, s));
-    HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, L.sg, L.sgu,
-                                     L.dU, L.sdu, N, R, To * V, s));
-    HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
+    // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias); the
+    // reduction comes from the next block when it was chained (dy_sums)
+    const double *sg = L.sg, *sgu = L.sgu;
+    if (a->dy_sums) {
+      sg = a->dy_sums;
+      sgu = a->dy_sums + R;
+    } else {
+      HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
+                                        L.sg, L.sgu, s));
+    }
+    HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
+                                     L.sdu, N, R, To * V, s));
+    HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
     // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
     // temporal and projection bias grads are its per-channel sums
@@ -612,9 +637,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       add = L.Rg;
     }
   }
-  if (d->need_dx)
+  if (d->need_dx) {
+    const bool chain = a->prev_g2 && a->prev_b2 && a->prev_sums;
+    if (chain) HIP_TRY(hipMemsetAsync(a->prev_sums, 0, sizeof(double) * 2 * C, s));
     HIP_TRY(launch_bn1_bwd_apply(a->dx, a->x, mean1, invstd1, a->g1, L.sd, L.sdn, add, N, C,
-                                 T * V, (int64_t)N * T * V, s));
+                                 T * V, (int64_t)N * T * V, chain ? a->prev_g2 : nullptr,
+                                 chain ? a->prev_b2 : nullptr, chain ? a->prev_sums : nullptr,
+                                 s));
+  }
   return STGCN_OK;
 }
 

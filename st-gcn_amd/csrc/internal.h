@@ -83,9 +83,10 @@ hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, dou
 hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M,
                               float eps, float momentum, int training, float *rm, float *rv,
                               float *mean_out, float *invstd_out, hipStream_t s);
+// y = ReLU(BN(U)); ysum/ysq (or null): per-channel sum / sum of squares of y
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
-                              hipStream_t s);
+                              double *ysum, double *ysq, hipStream_t s);
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b,
                                      int N, int C, int L, double *sg, double *sgu,
@@ -97,10 +98,12 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
 hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
                                float *dgamma, float *dbeta, float *dbias, hipStream_t s);
 // add (same layout as dx, or null) is added after the BN1 backward (residual path)
+// pg2/pb2/psum (or null): also the previous block's ReLU+BN2 backward sums
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean,
                                 const float *invstd, const float *g, const double *sd,
                                 const double *sdn, const float *add, int N, int C, int L,
-                                int64_t M, hipStream_t s);
+                                int64_t M, const float *pg2, const float *pb2, double *psum,
+                                hipStream_t s);
 // dout = dy * (y > 0) (the final ReLU of the residual block), sum[c] += sum dout
 hipError_t launch_relu_bwd(const float *dy, const float *y, float *dout, double *sum, int N,
                            int C, int L, hipStream_t s);

@@ -1495,13 +1495,18 @@ hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_
   return hipGetLastError();
 }
 
+// y = ReLU(BN(U)); optionally (ysum != null) also the per-channel sum and sum
+// of squares of y (fp64): the next block's BN1 batch statistics.
 template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
                                                      const float *invstd, const float *g,
-                                                     const float *b, float *y, int C, int L) {
+                                                     const float *b, float *y, int C, int L,
+                                                     double *ysum, double *ysq) {
+  __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], a = invstd[c] * g[c], be = b[c];
+  double s = 0.0, q = 0.0;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float v[VEC];
     vld<VEC>(U + base + i, v);
@@ -1509,16 +1514,19 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
     for (int j = 0; j < VEC; ++j) {
       const float t = (v[j] - mu) * a + be;
       v[j] = t > 0.f ? t : 0.f;
+      s += (double)v[j];
+      q += (double)v[j] * (double)v[j];
     }
     vst<VEC>(y + base + i, v);
   }
+  if (ysum) block_sum2_atomic<256>(s, q, ysum + c, ysq + c, red);
 }
 
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
-                              hipStream_t s) {
+                              double *ysum, double *ysq, hipStream_t s) {
   STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, N), U, mean, invstd, g, b, y, C,
-                   L);
+                   L, ysum, ysq);
   return hipGetLastError();
 }
 
@@ -1610,16 +1618,25 @@ hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double
 }
 
 // dx = g*invstd * (dxhat - sum(dxhat)/M - xnorm * sum(dxhat*xnorm)/M), in place.
+// Optionally (pg2 != null) also the previous block's ReLU+BN2 backward sums:
+// x = ReLU(g2*uhat + b2) of that block, so its ReLU mask is x > 0 and
+// uhat = (x - b2) / g2 there; with dy_prev = dx:
+//   psum[c] += sum dx * [x > 0],  psum[C + c] += sum dx * [x > 0] * uhat.
 template <int VEC>
 __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x,
                                                        const float *mean, const float *invstd,
                                                        const float *g, const double *sd,
                                                        const double *sdn, const float *add,
-                                                       int C, int L, double invM) {
+                                                       int C, int L, double invM,
+                                                       const float *pg2, const float *pb2,
+                                                       double *psum) {
+  __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c];
   const float md = (float)(sd[c] * invM), mdn = (float)(sdn[c] * invM);
+  const float pg = pg2 ? pg2[c] : 1.f, pb = pg2 ? pb2[c] : 0.f;
+  double s = 0.0, q = 0.0;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float xv[VEC], d[VEC];
     vld<VEC>(x + base + i, xv);
@@ -1633,14 +1650,24 @@ __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x
       for (int j = 0; j < VEC; ++j) d[j] += r[j];
     }
     vst<VEC>(dx + base + i, d);
+    if (pg2) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (xv[j] > 0.f) {
+          s += d[j];
+          q += (double)d[j] * (double)((xv[j] - pb) / pg);
+        }
+    }
   }
+  if (pg2) block_sum2_atomic<256>(s, q, psum + c, psum + C + c, red);
 }
 
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean, const float *invstd,
                                 const float *g, const double *sd, const double *sdn,
-                                const float *add, int N, int C, int L, int64_t M, hipStream_t s) {
+                                const float *add, int N, int C, int L, int64_t M,
+                                const float *pg2, const float *pb2, double *psum, hipStream_t s) {
   STGCN_VEC_LAUNCH(k_bn1_bwd_apply, slice_vec(L, {dx, x, add}), dim3(C, N), dx, x, mean, invstd,
-                   g, sd, sdn, add, C, L, 1.0 / (double)M);
+                   g, sd, sdn, add, C, L, 1.0 / (double)M, pg2, pb2, psum);
   return hipGetLastError();
 }
 

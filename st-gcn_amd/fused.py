@@ -9,6 +9,7 @@ math is that of ``SpatialTemporalConv.forward`` (src/network/st_graphconv.py:
 (driven by lightning_model.py:199-205).
 """
 import ctypes
+import weakref
 
 import torch
 
@@ -27,6 +28,54 @@ def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1
     T_out = (T + 2 * pad - gamma) // stride + 1
     return hip_lib.Desc(N, C_in, C_out, T, T_out, V, K, gamma, stride, pad, eps, momentum,
                         int(training), int(need_dx), hip_lib.F_RESIDUAL if residual else 0)
+
+
+class Link:
+    """Hand-over between two chained blocks in backward: the later block
+    computes the earlier block's ReLU+BN2 backward sums while writing its dx
+    (``sums``); the earlier block uses them only if the gradient it receives is
+    that very dx tensor, unmodified (``dx_ref`` / ``dx_version``)."""
+
+    def __init__(self):
+        self.sums = None
+        self.dx_ref = None
+        self.dx_version = None
+
+    def valid_for(self, dy):
+        return (self.sums is not None and self.dx_ref is not None and self.dx_ref() is dy
+                and dy._version == self.dx_version)
+
+
+class ChainCtx:
+    """Per-block chaining arguments (see network.StackChain): x_stats / y_stats
+    (fp64 [sum, sumsq] per channel of the block input / output), the Link to
+    the previous block (``in_link``, with its BN2 affine ``prev_g2/prev_b2``)
+    and to the next one (``out_link``)."""
+
+    def __init__(self, x_stats=None, y_stats=None, in_link=None, out_link=None, prev_g2=None,
+                 prev_b2=None):
+        self.x_stats, self.y_stats = x_stats, y_stats
+        self.in_link, self.out_link = in_link, out_link
+        self.prev_g2, self.prev_b2 = prev_g2, prev_b2
+
+
+def _chain_bwd_args(cc, dy, need_dx, C_in, dev):
+    """(dy_sums, prev_g2, prev_b2, prev_sums) for stgcn_block_bwd."""
+    if cc is None:
+        return None, None, None, None
+    dy_sums = cc.out_link.sums if (cc.out_link is not None and cc.out_link.valid_for(dy)) \
+        else None
+    if cc.in_link is not None and need_dx:
+        prev_sums = torch.empty(2 * C_in, device=dev, dtype=torch.float64)
+        return dy_sums, cc.prev_g2, cc.prev_b2, prev_sums
+    return dy_sums, None, None, None
+
+
+def _chain_publish(cc, prev_sums, dx):
+    if prev_sums is not None:
+        cc.in_link.sums = prev_sums
+        cc.in_link.dx_ref = weakref.ref(dx)
+        cc.in_link.dx_version = dx._version
 
 
 def _keep_g(ctx, x, K):
@@ -49,7 +98,7 @@ class StgcnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training):
+                stride, pad, eps, momentum, training, cc=None):
         lib = hip_lib.lib()
         x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
@@ -72,11 +121,12 @@ class StgcnBlockFn(torch.autograd.Function):
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats,
-            None, None, None, G)])
+            None, None, None, G, cc and cc.x_stats, cc and cc.y_stats)])
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
+        ctx.cc = cc
         return y
 
     @staticmethod
@@ -89,6 +139,7 @@ class StgcnBlockFn(torch.autograd.Function):
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
                          need_dx=need_dx)
+        dy_sums, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], x.device)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
         dbWt = torch.empty(C_out, device=x.device, dtype=torch.float32)
@@ -98,13 +149,14 @@ class StgcnBlockFn(torch.autograd.Function):
         args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
             dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
-            None, None, None, None, None, G)])
+            None, None, None, None, None, G, dy_sums, pg2, pb2, psums)])
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))
+        _chain_publish(ctx.cc, psums, dx)
         dA, dW, dbW, dWt = grads
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 class StgcnResBlockFn(torch.autograd.Function):
@@ -120,7 +172,7 @@ class StgcnResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training):
+                stride, pad, eps, momentum, training, cc=None):
         lib = hip_lib.lib()
         x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
@@ -147,11 +199,12 @@ class StgcnResBlockFn(torch.autograd.Function):
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, None, stats,
-            Wr, br, Za, G)])
+            Wr, br, Za, G, cc and cc.x_stats, cc and cc.y_stats)])
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
+        ctx.cc = cc
         return y
 
     @staticmethod
@@ -171,13 +224,15 @@ class StgcnResBlockFn(torch.autograd.Function):
         dg1, db1, dg2, db2 = (torch.empty_like(t) for t in (g1, b1, g2, b2))
         dWr = torch.empty_like(Wr) if Wr is not None else None
         dbr = torch.empty(C_out, device=dev, dtype=torch.float32) if Wr is not None else None
+        _, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], dev)
         nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
             dy, x, Z, None, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-            Wr, Za, y, dWr, dbr, G)])
+            Wr, Za, y, dWr, dbr, G, None, pg2, pb2, psums)])
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
+        _chain_publish(ctx.cc, psums, dx)
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2, dWr, dbr,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)

@@ -36,16 +36,18 @@ class FwdArgs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in (
         "x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
         "rm1", "rv1", "rm2", "rv2", "y", "Z", "U", "stats",
-        "Wr", "br", "Za",  # ABI 2: residual block
-        "G")]              # ABI 2: optional kept joint contraction
+        "Wr", "br", "Za",        # ABI 2: residual block
+        "G",                     # ABI 2: optional kept joint contraction
+        "x_stats", "y_stats")]   # ABI 2: optional stack chaining
 
 
 class BwdArgs(ctypes.Structure):
     _fields_ = [(n, _vp) for n in (
         "dy", "x", "Z", "U", "stats", "A", "W", "bW", "Wt", "g1", "b1", "g2", "b2",
         "dx", "dA", "dW", "dbW", "dWt", "dbWt", "dg1", "db1", "dg2", "db2",
-        "Wr", "Za", "y", "dWr", "dbr",  # ABI 2: residual block
-        "G")]                           # ABI 2: optional kept joint contraction
+        "Wr", "Za", "y", "dWr", "dbr",         # ABI 2: residual block
+        "G",                                   # ABI 2: optional kept joint contraction
+        "dy_sums", "prev_g2", "prev_b2", "prev_sums")]  # ABI 2: optional stack chaining
 
 
 # Every symbol include/stgcn_hip.h declares (checked by tests/test_capi.py).

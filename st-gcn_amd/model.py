@@ -7,7 +7,7 @@ NTVC -> permute -> 10 blocks -> avg_pool2d over (T, V) -> Linear.
 import torch
 import torch.nn as nn
 
-from .network import SpatialTemporalConv
+from .network import SpatialTemporalConv, StackChain
 
 # (C_out, temporal stride) per block, lightning_model.py:65-86.
 LAYERS = [(64, 1), (64, 1), (64, 1), (64, 1), (128, 2), (128, 1), (128, 1),
@@ -29,7 +29,10 @@ class STGCNStack(nn.Module):
         self.fc_layer = nn.Linear(256, nr_classes).float()
 
     def forward_nctv(self, x):
-        x = self.conv(x)
+        # same as self.conv(x), with cross-block fusion (network.StackChain)
+        chain = StackChain() if self.training else None
+        for blk in self.conv:
+            x = blk(x, chain=chain)
         # global average pool over (T, V) (lightning_model.py:105): a mean over
         # the contiguous T*V axis; ROCm's avg_pool2d with a (T, V) window is a
         # slow generic kernel (1.7 ms at N=128), the reduction is ~20 us.

@@ -13,7 +13,24 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fused import StgcnBlockFn, StgcnResBlockFn
+from .fused import ChainCtx, Link, StgcnBlockFn, StgcnResBlockFn
+
+
+class StackChain:
+    """Cross-block fusion state for one forward pass of a block stack
+    (``model.STGCNStack`` passes one; a drop-in user of single blocks does not
+    need it). When block i+1's input is exactly block i's output (same tensor,
+    unmodified), block i+1 takes its BN1 batch statistics from block i's output
+    pass instead of re-reading x, and in backward computes block i's ReLU+BN2
+    reduction while writing its dx. Any other input (dropout in between, user
+    code, eval mode) breaks the chain and both blocks fall back to their own
+    passes: results are the same either way."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.y, self.y_version, self.y_stats, self.link, self.g2b2 = None, None, None, None, None
 
 
 class SpatialConv(nn.Module):
@@ -72,7 +89,8 @@ class SpatialTemporalConv(nn.Module):
         self.stride = temporal_stride
         self.pad = temporal_padding
 
-    def forward(self, f_in):
+    def forward(self, f_in, chain=None):
+        """``chain``: optional ``StackChain`` (not part of the reference API)."""
         bn1, bn2 = self.batch_n, self.batch_n_2
         if bn1.momentum is None or bn2.momentum is None:
             raise NotImplementedError("BatchNorm momentum=None (cumulative average)")
@@ -82,6 +100,16 @@ class SpatialTemporalConv(nn.Module):
             bn2.num_batches_tracked.add_(1)
         sc = self.spatialConv
         x = f_in.float()
+        cc = None
+        if chain is not None and training and self.dropout is None:
+            cc = ChainCtx(y_stats=torch.empty(2 * self.temporalConv.out_channels,
+                                              device=x.device, dtype=torch.float64),
+                          out_link=None if self.residual else Link())
+            if chain.y is not None and x is chain.y and x._version == chain.y_version:
+                cc.x_stats = chain.y_stats
+                if chain.link is not None:
+                    cc.in_link = chain.link
+                    cc.prev_g2, cc.prev_b2 = chain.g2b2
         if self.residual:
             proj = self.apply_residual if isinstance(self.apply_residual, nn.Conv2d) else None
             y = StgcnResBlockFn.apply(
@@ -90,13 +118,20 @@ class SpatialTemporalConv(nn.Module):
                 proj.weight if proj is not None else None,
                 proj.bias if proj is not None else None,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc)
         else:
             y = StgcnBlockFn.apply(
                 x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
                 self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc)
+        if chain is not None:
+            if cc is None:
+                chain.reset()
+            else:
+                chain.y, chain.y_version, chain.y_stats = y, y._version, cc.y_stats
+                chain.link = cc.out_link
+                chain.g2b2 = None if self.residual else (bn2.weight, bn2.bias)
         if self.dropout is None:
             return y
         return F.dropout(y, self.dropout.p, training=training)

@@ -70,3 +70,43 @@ def test_stack_cfg1_matches_reference(pkg):
     for k, v in model.state_dict().items():
         if "running" in k:
             assert rel_to_max(v.cpu().numpy(), ref["after." + k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("residual", [False, True])
+def test_stack_chain_matches_unchained(pkg, residual):
+    """Cross-block fusion (network.StackChain: BN1 stats from the previous
+    block's output pass, the previous block's ReLU+BN2 reduction from the next
+    block's dx pass) gives the same results as running the blocks one by one."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    torch.manual_seed(3)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 10, A, residual=residual).cuda().train()
+        m2 = pkg.STGCNStack(3, 10, A, residual=residual).cuda().train()
+    m2.load_state_dict(m1.state_dict())
+    x = torch.randn(6, 3, 40, 18, generator=torch.Generator().manual_seed(4)).cuda()
+    lab = torch.randint(0, 10, (6,), generator=torch.Generator().manual_seed(5)).cuda()
+    out1 = m1.forward_nctv(x)                      # chained
+    h = x
+    for blk in m2.conv:                            # unchained
+        h = blk(h)
+    out2 = m2.fc_layer(h.flatten(2).mean(dim=2))
+    torch.nn.functional.cross_entropy(out1, lab).backward()
+    torch.nn.functional.cross_entropy(out2, lab).backward()
+    torch.cuda.synchronize()
+    assert rel_to_max(out1.detach().cpu().numpy(), out2.detach().cpu().numpy()) < 1e-5
+    # dA of the deep blocks is a small difference of large terms (BN makes the
+    # loss invariant to A's scale: |dA| ~ 1e-11 here) -- gated looser
+    bad = []
+    for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
+        if np.abs(gb).max() == 0:
+            continue
+        tol = 2e-3 if k.endswith("spatialConv.A") else 1e-4
+        err = rel_to_max(ga, gb)
+        if err > tol:
+            bad.append(f"{k}: {err:.2e} > {tol:.0e}")
+    assert not bad, "; ".join(bad)
+    for (k, a), (_, b) in zip(m1.named_buffers(), m2.named_buffers()):
+        if a.is_floating_point():
+            assert rel_to_max(a.cpu().numpy(), b.cpu().numpy()) < 1e-5, k
