@@ -98,6 +98,11 @@ typedef struct stgcn_fwd_args {
    * BN1 statistics pass is skipped); y_stats (out) = the same for y (C_out). */
   const double *x_stats;
   double *y_stats;
+  /* ABI 2, optional fused dropout on y (training only; st_graphconv.py:53-58,
+   * :107-109): element e of y is kept iff splitmix64(seed + e * 0x9E3779B97F4A7C15)
+   * >> 32 >= dropout_p * 2^32, then scaled by 1/(1 - dropout_p). 0: no dropout. */
+  float dropout_p;
+  uint64_t seed;
 } stgcn_fwd_args_t;
 
 /* Backward arguments: the gradients of every input of the forward. */
@@ -122,6 +127,8 @@ typedef struct stgcn_bwd_args {
   const double *dy_sums;
   const float *prev_g2, *prev_b2;
   double *prev_sums;
+  float dropout_p;                      /* the forward's dropout (same seed)  */
+  uint64_t seed;
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);

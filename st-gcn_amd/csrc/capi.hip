@@ -58,6 +58,16 @@ size_t wpk_floats(const stgcn_desc_t *d) {
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }
 int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
 bool residual(const stgcn_desc_t *d) { return (d->flags & STGCN_F_RESIDUAL) != 0; }
+// the fused dropout of a call (training and 0 < p < 1; p >= 1: everything dropped)
+Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
+  Dropout dr;
+  if (!d->training || !(p > 0.f)) return dr;
+  dr.seed = seed;
+  const double t = (double)p * 4294967296.0;
+  dr.thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  dr.scale = p < 1.f ? (float)(1.0 / (1.0 - (double)p)) : 0.f;
+  return dr;
+}
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {
   return residual(d) && (d->C_in != d->C_out || d->stride != 1);
@@ -252,7 +262,7 @@ static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
   HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * T * V, d->eps, d->momentum,
                              d->training, a->rm2, a->rv2, mean2, invstd2, s));
   HIP_TRY(launch_bn_relu_fwd(a->Z, mean2, invstd2, a->g2, a->b2, a->Za, N, R, T * V, nullptr,
-                             nullptr, s));
+                             nullptr, Dropout(), s));
   const float *resid = a->x;
   if (projection(d)) {  // apply_residual: Conv2d(C_in, C_out, 1, stride (s,1)) (:27)
     ConvGemmParams p = conv_base(d, L.wpk);
@@ -286,6 +296,7 @@ static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
   p.bias_r = a->bWt;
   p.res = resid;
   p.relu_out = 1;
+  p.drop = make_dropout(d, a->dropout_p, a->seed);
   if (d->training && a->y_stats) {  // next block's BN1 statistics from the epilogue
     HIP_TRY(hipMemsetAsync(a->y_stats, 0, sizeof(double) * 2 * R, s));
     p.stat_sum = a->y_stats;
@@ -456,7 +467,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
   if (ys) HIP_TRY(hipMemsetAsync(ys, 0, sizeof(double) * 2 * R, s));
   HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
-                             ys ? ys + R : nullptr, s));
+                             ys ? ys + R : nullptr, make_dropout(d, a->dropout_p, a->seed), s));
   return STGCN_OK;
 }
 
@@ -473,6 +484,9 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     return fail(STGCN_E_INVALID, "residual block: null Za / y / projection tensors");
   if (res && a->dy_sums)
     return fail(STGCN_E_INVALID, "dy_sums applies to the non-residual block only");
+  const Dropout drop = make_dropout(d, a->dropout_p, a->seed);
+  if (drop.thresh && a->dy_sums)
+    return fail(STGCN_E_INVALID, "dy_sums cannot be combined with dropout");
   if (!d->training) return fail(STGCN_E_UNSUPPORTED, "backward in eval mode is not implemented");
   const BwdLayout L = bwd_layout(d, workspace);
   if (!workspace || workspace_bytes < L.total)
@@ -492,15 +506,16 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       sgu = a->dy_sums + R;
     } else {
       HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
-                                        L.sg, L.sgu, s));
+                                        L.sg, L.sgu, drop, s));
     }
     HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
-                                     L.sdu, N, R, To * V, s));
+                                     L.sdu, N, R, To * V, drop, s));
     HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
     // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
     // temporal and projection bias grads are its per-channel sums
-    HIP_TRY(launch_relu_bwd(a->dy, a->y, L.dU, L.sdu, N, R, To * V, s));
+    HIP_TRY(launch_relu_bwd(a->dy, a->y, L.dU, L.sdu, N, R, To * V, drop.thresh ? drop.scale : 1.f,
+                            s));
     HIP_TRY(launch_bn_grads_out(L.sdu, L.sdu, nullptr, R, a->dbWt, a->dbr ? a->dbr : a->dbWt,
                                 nullptr, s));
   }
@@ -553,9 +568,9 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   if (res) {
     // BN2 + ReLU backward over Z (residual block, st_graphconv.py:76-77): dZ in place
     HIP_TRY(launch_bn_relu_bwd_reduce(L.dZ, a->Z, mean2, invstd2, a->g2, a->b2, N, R, T * V,
-                                      L.sg, L.sgu, s));
+                                      L.sg, L.sgu, Dropout(), s));
     HIP_TRY(launch_bn_relu_bwd_apply(L.dZ, a->Z, mean2, invstd2, a->g2, a->b2, L.sg, L.sgu,
-                                     L.dZ, L.sdu, N, R, T * V, s));
+                                     L.dZ, L.sdu, N, R, T * V, Dropout(), s));
     HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, nullptr, R, a->dg2, a->db2, nullptr, s));
   }
   // Spatial conv backward. Recompute G = f(BN1(x)) A^T (f = ReLU in the

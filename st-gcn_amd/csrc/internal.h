@@ -5,6 +5,25 @@
 
 namespace stgcn {
 
+// Fused dropout (st_graphconv.py:53-58, :107-109): element e of the block
+// output is kept iff hash(seed, e) >= thresh (thresh = p * 2^32) and then
+// scaled by 1/(1-p). thresh == 0: no dropout. The hash (splitmix64 of
+// seed + e * golden ratio) is counter-based: the backward regenerates the
+// mask instead of storing it.
+struct Dropout {
+  uint64_t seed = 0;
+  uint32_t thresh = 0;
+  float scale = 1.f;
+};
+
+__host__ __device__ inline bool dropout_keep(const Dropout &d, uint64_t e) {
+  uint64_t z = d.seed + e * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32) >= d.thresh;
+}
+
 constexpr int kTileRows = 64;   // output rows per workgroup (2 MFMA 32-row tiles)
 constexpr int kTileCols = 256;  // max (frames x V) columns per workgroup (8 MFMA 32-col tiles)
 
@@ -34,6 +53,7 @@ struct ConvGemmParams {
   // epilogue extras (residual block): out = f(acc + bias + res), f = ReLU if relu_out
   const float *res;  // same layout and clip stride as out, or null
   int relu_out;
+  Dropout drop;      // applied after relu_out (element index = flat index in out)
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -86,15 +106,16 @@ hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_
 // y = ReLU(BN(U)); ysum/ysq (or null): per-channel sum / sum of squares of y
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
-                              double *ysum, double *ysq, hipStream_t s);
+                              double *ysum, double *ysq, Dropout drop, hipStream_t s);
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b,
-                                     int N, int C, int L, double *sg, double *sgu,
+                                     int N, int C, int L, double *sg, double *sgu, Dropout drop,
                                      hipStream_t s);
 hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU,
-                                    double *sdu, int N, int C, int L, hipStream_t s);
+                                    double *sdu, int N, int C, int L, Dropout drop,
+                                    hipStream_t s);
 hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
                                float *dgamma, float *dbeta, float *dbias, hipStream_t s);
 // add (same layout as dx, or null) is added after the BN1 backward (residual path)
@@ -105,8 +126,9 @@ hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean,
                                 int64_t M, const float *pg2, const float *pb2, double *psum,
                                 hipStream_t s);
 // dout = dy * (y > 0) (the final ReLU of the residual block), sum[c] += sum dout
+// (with dropout: y is the dropped output; dout = dy * scale where y > 0)
 hipError_t launch_relu_bwd(const float *dy, const float *y, float *dout, double *sum, int N,
-                           int C, int L, hipStream_t s);
+                           int C, int L, float scale, hipStream_t s);
 
 // Spatial (graph) helpers.
 hipError_t launch_pack_w(const float *W, float *Wpk, int K, int R, int C, hipStream_t s);

@@ -250,6 +250,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
         if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
         if (p.res) val += p.res[(int64_t)n * p.out_bstride + row * ostride + ocol[j]];
         if (p.relu_out) val = fmaxf(val, 0.f);
+        if (p.drop.thresh)
+          val = dropout_keep(p.drop, (uint64_t)n * p.out_bstride + row * ostride + ocol[j])
+                    ? val * p.drop.scale
+                    : 0.f;
         outN[row * ostride + ocol[j]] = val;
         s += val;
         sq += (double)val * val;
@@ -489,6 +493,10 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
           if (p.res)
             val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, off, 0, 0));
           if (p.relu_out) val = fmaxf(val, 0.f);
+          if (p.drop.thresh && ok)
+            val = dropout_keep(p.drop, (uint64_t)n * p.out_bstride + row * ostride + ocol[j])
+                      ? val * p.drop.scale
+                      : 0.f;
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o, off, 0, 0);
           if constexpr (STATS) {
             const double dv = ok ? (double)val : 0.0;
@@ -1501,7 +1509,7 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
                                                      const float *invstd, const float *g,
                                                      const float *b, float *y, int C, int L,
-                                                     double *ysum, double *ysq) {
+                                                     double *ysum, double *ysq, Dropout drop) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
@@ -1514,6 +1522,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
     for (int j = 0; j < VEC; ++j) {
       const float t = (v[j] - mu) * a + be;
       v[j] = t > 0.f ? t : 0.f;
+      if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
       s += (double)v[j];
       q += (double)v[j] * (double)v[j];
     }
@@ -1524,9 +1533,9 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
 
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
-                              double *ysum, double *ysq, hipStream_t s) {
+                              double *ysum, double *ysq, Dropout drop, hipStream_t s) {
   STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, N), U, mean, invstd, g, b, y, C,
-                   L, ysum, ysq);
+                   L, ysum, ysq, drop);
   return hipGetLastError();
 }
 
@@ -1535,7 +1544,8 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
                                                             const float *mean,
                                                             const float *invstd, const float *g,
                                                             const float *b, int C, int L,
-                                                            double *sg, double *sgu) {
+                                                            double *sg, double *sgu,
+                                                            Dropout drop) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
@@ -1545,6 +1555,11 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
     float u[VEC], d[VEC];
     vld<VEC>(U + base + i, u);
     vld<VEC>(dy + base + i, d);
+    if (drop.thresh) {  // gradient through the fused dropout
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        d[j] = dropout_keep(drop, base + i + j) ? d[j] * drop.scale : 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       if ((u[j] - mu) * a + be > 0.f) {
@@ -1558,9 +1573,10 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
 
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b, int N,
-                                     int C, int L, double *sg, double *sgu, hipStream_t s) {
+                                     int C, int L, double *sg, double *sgu, Dropout drop,
+                                     hipStream_t s) {
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_reduce, slice_vec(L, {dy, U}), dim3(C, N), dy, U, mean, invstd,
-                   g, b, C, L, sg, sgu);
+                   g, b, C, L, sg, sgu, drop);
   return hipGetLastError();
 }
 
@@ -1568,7 +1584,7 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
     const float *dy, const float *U, const float *mean, const float *invstd, const float *g,
     const float *b, const double *sg, const double *sgu, float *dU, double *sdu, int C, int L,
-    double invM) {
+    double invM, Dropout drop) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
@@ -1579,6 +1595,11 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
     float u[VEC], d[VEC], o[VEC];
     vld<VEC>(U + base + i, u);
     vld<VEC>(dy + base + i, d);
+    if (drop.thresh) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        d[j] = dropout_keep(drop, base + i + j) ? d[j] * drop.scale : 0.f;
+    }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
       const float uh = (u[j] - mu) * is;
@@ -1594,10 +1615,10 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
 hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU, double *sdu,
-                                    int N, int C, int L, hipStream_t s) {
+                                    int N, int C, int L, Dropout drop, hipStream_t s) {
   const double invM = 1.0 / ((double)N * L);
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_apply, slice_vec(L, {dy, U, dU}), dim3(C, N), dy, U, mean,
-                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM);
+                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop);
   return hipGetLastError();
 }
 
@@ -1675,7 +1696,7 @@ hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean, co
 // with the per-channel sum of dout (the temporal and projection bias grads).
 template <int VEC>
 __global__ __launch_bounds__(256) void k_relu_bwd(const float *dy, const float *y, float *dout,
-                                                  double *sum, int C, int L) {
+                                                  double *sum, int C, int L, float scale) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
@@ -1686,7 +1707,7 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float *dy, const float *
     vld<VEC>(y + base + i, yv);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-      d[j] = yv[j] > 0.f ? d[j] : 0.f;
+      d[j] = yv[j] > 0.f ? d[j] * scale : 0.f;
       s += d[j];
     }
     vst<VEC>(dout + base + i, d);
@@ -1695,8 +1716,9 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float *dy, const float *
 }
 
 hipError_t launch_relu_bwd(const float *dy, const float *y, float *dout, double *sum, int N,
-                           int C, int L, hipStream_t s) {
-  STGCN_VEC_LAUNCH(k_relu_bwd, slice_vec(L, {dy, y, dout}), dim3(C, N), dy, y, dout, sum, C, L);
+                           int C, int L, float scale, hipStream_t s) {
+  STGCN_VEC_LAUNCH(k_relu_bwd, slice_vec(L, {dy, y, dout}), dim3(C, N), dy, y, dout, sum, C, L,
+                   scale);
   return hipGetLastError();
 }
 

@@ -78,6 +78,21 @@ def _chain_publish(cc, prev_sums, dx):
         cc.in_link.dx_version = dx._version
 
 
+def _dropout_seed(drop, training):
+    """Seed of this call's fused dropout, drawn from torch's default generator
+    (so torch.manual_seed reproduces it); 0 when inactive."""
+    if not (training and drop > 0):
+        return 0
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def _args(cls, ptrs, drop, seed):
+    a = cls(*ptrs)
+    a.dropout_p = float(drop)
+    a.seed = seed
+    return a
+
+
 def _keep_g(ctx, x, K):
     """Buffer for the joint contraction G (N, K*C_in, T, V) when a backward
     will run (the forward writes it once; the backward then skips recomputing
@@ -98,12 +113,13 @@ class StgcnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training, cc=None):
+                stride, pad, eps, momentum, training, cc=None, drop=0.0):
         lib = hip_lib.lib()
         x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
                  "rm1", "rv1", "rm2", "rv2")
         tensors = (x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2)
+        seed = _dropout_seed(drop, training)
         for t, n in zip(tensors, names):
             _f32c(t, n)
         N, C_in, T, V = x.shape
@@ -119,14 +135,15 @@ class StgcnBlockFn(torch.autograd.Function):
         G = _keep_g(ctx, x, K)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-        args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
+        args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats,
-            None, None, None, G, cc and cc.x_stats, cc and cc.y_stats)])
+            None, None, None, G, cc and cc.x_stats, cc and cc.y_stats)], drop, seed)
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
         ctx.cc = cc
+        ctx.drop = (drop, seed)
         return y
 
     @staticmethod
@@ -146,17 +163,17 @@ class StgcnBlockFn(torch.autograd.Function):
         dg1, db1, dg2, db2 = (torch.empty_like(t) for t in (g1, b1, g2, b2))
         nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
-        args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
+        args = _args(hip_lib.BwdArgs, [hip_lib.ptr(t) for t in (
             dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
-            None, None, None, None, None, G, dy_sums, pg2, pb2, psums)])
+            None, None, None, None, None, G, dy_sums, pg2, pb2, psums)], *ctx.drop)
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))
         _chain_publish(ctx.cc, psums, dx)
         dA, dW, dbW, dWt = grads
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-                None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)
 
 
 class StgcnResBlockFn(torch.autograd.Function):
@@ -172,9 +189,10 @@ class StgcnResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training, cc=None):
+                stride, pad, eps, momentum, training, cc=None, drop=0.0):
         lib = hip_lib.lib()
         x = x.contiguous()
+        seed = _dropout_seed(drop, training)
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
                  "rm1", "rv1", "rm2", "rv2")
         for t, n in zip((x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2), names):
@@ -197,14 +215,15 @@ class StgcnResBlockFn(torch.autograd.Function):
         G = _keep_g(ctx, x, K)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-        args = hip_lib.FwdArgs(*[hip_lib.ptr(t) for t in (
+        args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, None, stats,
-            Wr, br, Za, G, cc and cc.x_stats, cc and cc.y_stats)])
+            Wr, br, Za, G, cc and cc.x_stats, cc and cc.y_stats)], drop, seed)
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
         ctx.cc = cc
+        ctx.drop = (drop, seed)
         return y
 
     @staticmethod
@@ -227,12 +246,12 @@ class StgcnResBlockFn(torch.autograd.Function):
         _, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], dev)
         nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-        args = hip_lib.BwdArgs(*[hip_lib.ptr(t) for t in (
+        args = _args(hip_lib.BwdArgs, [hip_lib.ptr(t) for t in (
             dy, x, Z, None, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-            Wr, Za, y, dWr, dbr, G, None, pg2, pb2, psums)])
+            Wr, Za, y, dWr, dbr, G, None, pg2, pb2, psums)], *ctx.drop)
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         _chain_publish(ctx.cc, psums, dx)
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2, dWr, dbr,
-                None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None)

@@ -38,7 +38,8 @@ class FwdArgs(ctypes.Structure):
         "rm1", "rv1", "rm2", "rv2", "y", "Z", "U", "stats",
         "Wr", "br", "Za",        # ABI 2: residual block
         "G",                     # ABI 2: optional kept joint contraction
-        "x_stats", "y_stats")]   # ABI 2: optional stack chaining
+        "x_stats", "y_stats")    # ABI 2: optional stack chaining
+    ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)]  # ABI 2: fused dropout
 
 
 class BwdArgs(ctypes.Structure):
@@ -47,7 +48,8 @@ class BwdArgs(ctypes.Structure):
         "dx", "dA", "dW", "dbW", "dWt", "dbWt", "dg1", "db1", "dg2", "db2",
         "Wr", "Za", "y", "dWr", "dbr",         # ABI 2: residual block
         "G",                                   # ABI 2: optional kept joint contraction
-        "dy_sums", "prev_g2", "prev_b2", "prev_sums")]  # ABI 2: optional stack chaining
+        "dy_sums", "prev_g2", "prev_b2", "prev_sums")  # ABI 2: optional stack chaining
+    ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)]  # ABI 2: fused dropout
 
 
 # Every symbol include/stgcn_hip.h declares (checked by tests/test_capi.py).

@@ -11,7 +11,6 @@ forward raises.
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .fused import ChainCtx, Link, StgcnBlockFn, StgcnResBlockFn
 
@@ -58,8 +57,9 @@ class SpatialTemporalConv(nn.Module):
     """Reference: st_graphconv.py:4-109 (same arguments, children, state_dict).
 
     Accelerated: the default and the residual block (full pre-activation,
-    st_graphconv.py:60-82), training and eval mode. Dropout (p > 0, training)
-    is applied after the fused block with torch's dropout.
+    st_graphconv.py:60-82), training and eval mode, with dropout (p > 0,
+    training) fused into the block's output pass (counter-based mask,
+    regenerated in backward; a different random stream from torch's).
     """
 
     def __init__(self, C_in, C_out, A, gamma, temporal_stride, temporal_padding,
@@ -100,11 +100,14 @@ class SpatialTemporalConv(nn.Module):
             bn2.num_batches_tracked.add_(1)
         sc = self.spatialConv
         x = f_in.float()
+        drop = self.dropout.p if (self.dropout is not None and training) else 0.0
         cc = None
-        if chain is not None and training and self.dropout is None:
+        if chain is not None and training:
+            # (the backward link derives this block's ReLU mask from its output:
+            # not with dropout on that output, nor for the residual block)
             cc = ChainCtx(y_stats=torch.empty(2 * self.temporalConv.out_channels,
                                               device=x.device, dtype=torch.float64),
-                          out_link=None if self.residual else Link())
+                          out_link=None if (self.residual or drop > 0) else Link())
             if chain.y is not None and x is chain.y and x._version == chain.y_version:
                 cc.x_stats = chain.y_stats
                 if chain.link is not None:
@@ -118,13 +121,13 @@ class SpatialTemporalConv(nn.Module):
                 proj.weight if proj is not None else None,
                 proj.bias if proj is not None else None,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop)
         else:
             y = StgcnBlockFn.apply(
                 x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
                 self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop)
         if chain is not None:
             if cc is None:
                 chain.reset()
@@ -132,6 +135,4 @@ class SpatialTemporalConv(nn.Module):
                 chain.y, chain.y_version, chain.y_stats = y, y._version, cc.y_stats
                 chain.link = cc.out_link
                 chain.g2b2 = None if self.residual else (bn2.weight, bn2.bias)
-        if self.dropout is None:
-            return y
-        return F.dropout(y, self.dropout.p, training=training)
+        return y  # dropout (p > 0, training) is fused into the block's output pass

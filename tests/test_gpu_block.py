@@ -275,3 +275,98 @@ def test_residual_eval_mode(pkg):
     assert rel_to_max(y.cpu().numpy(), want.numpy()) < TOL
     for k in bu:
         assert torch.equal(bu[k].cpu(), b[k])
+
+
+# --- fused dropout (st_graphconv.py:50-54, :107-108) -----------------------
+# The HIP block draws its keep mask from a counter-based hash of the flat NCTV
+# output index (splitmix64, internal.h dropout_keep); torch's Philox stream is
+# not reproducible outside torch, and any two dropout implementations differ
+# in their random stream. Parity: the oracle differentiated through the SAME
+# mask (relu mask x keep / (1-p)) -- everything else must match exactly as in
+# the dropout-free tests -- and the mask is checked for its distribution.
+
+
+def _keep_mask(seed, shape, p):
+    e = np.arange(int(np.prod(shape)), dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + e * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    thresh = min(int(p * 2.0 ** 32), 2 ** 32 - 1)
+    return torch.from_numpy(((z >> np.uint64(32)) >= np.uint64(thresh)).reshape(shape))
+
+
+def _run_hip_dropout(pkg, arrays, x, g, drop):
+    torch.manual_seed(1234)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item())   # fused._dropout_seed's draw
+    torch.manual_seed(1234)
+    p, b = ref_cpu.block_params_from_arrays(arrays, dtype=torch.float32, requires_grad=False)
+    stride, residual = int(arrays["meta"][2]), bool(arrays["meta"][7])
+    cu = {k: v.to(DEV).contiguous().requires_grad_(True) for k, v in p.items()}
+    bu = {k: v.to(DEV).clone() for k, v in b.items() if "num_batches" not in k}
+    xd = x.to(DEV).float().contiguous().requires_grad_(True)
+    common = (xd, cu["spatialConv.A"], cu["spatialConv.W.weight"], cu["spatialConv.W.bias"],
+              cu["temporalConv.weight"], cu["temporalConv.bias"], cu["batch_n.weight"],
+              cu["batch_n.bias"], cu["batch_n_2.weight"], cu["batch_n_2.bias"])
+    running = (bu["batch_n.running_mean"], bu["batch_n.running_var"],
+               bu["batch_n_2.running_mean"], bu["batch_n_2.running_var"])
+    if residual:
+        y = pkg.fused.StgcnResBlockFn.apply(
+            *common, cu.get("apply_residual.weight"), cu.get("apply_residual.bias"), *running,
+            stride, 4, 1e-5, 0.1, True, None, drop)
+    else:
+        y = pkg.fused.StgcnBlockFn.apply(*common, *running, stride, 4, 1e-5, 0.1, True,
+                                         None, drop)
+    y.backward(g.to(DEV).float())
+    torch.cuda.synchronize()
+    out = {"y": y.detach().cpu(), "grad.x": xd.grad.cpu()}
+    for k, t in cu.items():
+        out["grad." + k] = t.grad.cpu()
+    for k, t in bu.items():
+        out["after." + k] = t.cpu()
+    return out, seed
+
+
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T, residual, p
+    (64, 64, 1, 18, 1, 3, 40, False, 0.5),     # specialised conv + bn_relu_fwd dropout
+    (64, 128, 2, 18, 1, 2, 37, False, 0.2),
+    (5, 7, 1, 18, 1, 2, 9, False, 0.5),        # generic conv, partial tiles
+    (64, 64, 1, 18, 1, 3, 40, True, 0.5),      # dropout in the tconv epilogue
+    (64, 128, 2, 25, 3, 2, 33, True, 0.3),     # projection residual, NTU graph
+    (3, 64, 1, 50, 3, 2, 20, False, 0.9),
+])
+def test_block_dropout_matches_oracle(pkg, case):
+    *shape, residual, drop = case
+    C_in, C_out, stride, V, K, N, T = shape
+    arrays, x, g = _random_case(pkg, C_in, C_out, stride, V, K, N, T, seed=5,
+                                residual=residual)
+    got, seed = _run_hip_dropout(pkg, arrays, x, g, drop)
+    keep = _keep_mask(seed, tuple(got["y"].shape), drop)
+    # mask statistics: the fraction kept is 1-p (binomial, 6 sigma)
+    n = keep.numel()
+    assert abs(keep.double().mean().item() - (1 - drop)) < 6 * (drop * (1 - drop) / n) ** 0.5
+    y = got["y"]
+    assert (y[~keep] == 0).all(), "dropped elements must be 0"
+    pre = ref_cpu.block_pre_relu(arrays)
+    relu = y > 0
+    kflips = keep & (relu != (pre > 0))
+    if kflips.any():
+        assert pre[kflips].abs().max().item() < TIE, "ReLU mask differs away from a tie"
+    mask = (keep & relu).double() / (1 - drop)
+    want = ref_cpu.block_step(arrays, dtype=torch.float64, relu_mask=mask)
+    ref32 = ref_cpu.block_step(arrays, dtype=torch.float32, relu_mask=mask.float())
+    floor = {k: rel_to_max(ref32[k].detach().double().numpy(), v.detach().double().numpy())
+             for k, v in want.items() if k in ref32 and "num_batches" not in k}
+    _compare(got, want, residual=residual, floor=floor)
+
+
+def test_block_dropout_seed_reproducible(pkg):
+    """Same torch seed -> same mask; different seed -> different mask."""
+    arrays, x, g = _random_case(pkg, 64, 64, 1, 18, 1, 2, 30, seed=2)
+    a, sa = _run_hip_dropout(pkg, arrays, x, g, 0.5)
+    b, sb = _run_hip_dropout(pkg, arrays, x, g, 0.5)
+    assert sa == sb and torch.equal(a["y"], b["y"])
+    assert not torch.equal(_keep_mask(sa, (2, 64, 30, 18), 0.5),
+                           _keep_mask(sa + 1, (2, 64, 30, 18), 0.5))

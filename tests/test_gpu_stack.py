@@ -72,21 +72,24 @@ def test_stack_cfg1_matches_reference(pkg):
             assert rel_to_max(v.cpu().numpy(), ref["after." + k]) < 1e-4, k
 
 
-@pytest.mark.parametrize("residual", [False, True])
-def test_stack_chain_matches_unchained(pkg, residual):
+@pytest.mark.parametrize("residual,drop", [(False, 0), (True, 0), (False, 0.5), (True, 0.3)])
+def test_stack_chain_matches_unchained(pkg, residual, drop):
     """Cross-block fusion (network.StackChain: BN1 stats from the previous
     block's output pass, the previous block's ReLU+BN2 reduction from the next
-    block's dx pass) gives the same results as running the blocks one by one."""
+    block's dx pass) gives the same results as running the blocks one by one,
+    with and without the fused dropout (same per-block seeds in both runs)."""
     gr = pkg.graph
     A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
     torch.manual_seed(3)
     with contextlib.redirect_stdout(io.StringIO()):
-        m1 = pkg.STGCNStack(3, 10, A, residual=residual).cuda().train()
-        m2 = pkg.STGCNStack(3, 10, A, residual=residual).cuda().train()
+        m1 = pkg.STGCNStack(3, 10, A, dropout_rate=drop, residual=residual).cuda().train()
+        m2 = pkg.STGCNStack(3, 10, A, dropout_rate=drop, residual=residual).cuda().train()
     m2.load_state_dict(m1.state_dict())
     x = torch.randn(6, 3, 40, 18, generator=torch.Generator().manual_seed(4)).cuda()
     lab = torch.randint(0, 10, (6,), generator=torch.Generator().manual_seed(5)).cuda()
+    torch.manual_seed(9)
     out1 = m1.forward_nctv(x)                      # chained
+    torch.manual_seed(9)
     h = x
     for blk in m2.conv:                            # unchained
         h = blk(h)
