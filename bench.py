@@ -25,19 +25,43 @@ sys.path.insert(0, ROOT)
 
 from stgcn_loader import load  # noqa: E402
 
-CFG = dict(N=128, C=3, T=300, V=18, K=1, classes=400)
-MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+# BASELINE.json configs (SURVEY.md §8 "Per-config inputs"); the default bench
+# line is cfg2. cfg3 / cfg5 use the spatial-configuration partitioning (K=3,
+# strategy 2 with synthetic distances) and bf16 channel GEMMs (fp32 accumulate,
+# fp32 tensors); cfg4 is cfg2 data-parallel (run with --gpus N).
+CONFIGS = {
+    "cfg2": dict(N=128, C=3, T=300, V=18, K=1, classes=400, bf16=False,
+                 desc="cfg2 Kinetics-skeleton shape: 10-block ST-GCN stack fwd+bwd+CE+Adam, "
+                      "V=18, T=300, K=1 (uni), 400 classes"),
+    "cfg3": dict(N=128, C=3, T=300, V=25, K=3, classes=60, bf16=True,
+                 desc="cfg3 NTU-RGB+D shape: 10-block ST-GCN stack fwd+bwd+CE+Adam, V=25, "
+                      "T=300, K=3 (spatial), 60 classes, bf16 channel GEMMs"),
+    "cfg5": dict(N=128, C=3, T=300, V=50, K=3, classes=60, bf16=True,
+                 desc="cfg5 2-person stacked graph: 10-block ST-GCN stack fwd+bwd+CE+Adam, "
+                      "V=50, T=300, K=3 (spatial), 60 classes, bf16 channel GEMMs"),
+}
+CFG = CONFIGS["cfg2"]
+MFMA_F32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
-def build_model(pkg, cfg, device):
+def adjacency(pkg, cfg):
     gr = pkg.graph
-    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(cfg["V"]))
+    if cfg["K"] == 1:
+        return gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(cfg["V"]))
+    return gr.get_normalized_adjacency_matrices(
+        2, 1, distances=gr.synthetic_distances(cfg["V"]), graph=gr.graph_for(cfg["V"]))
+
+
+def build_model(pkg, cfg, device):
+    A = adjacency(pkg, cfg)
     torch.manual_seed(0)
     import io
     import contextlib
     with contextlib.redirect_stdout(io.StringIO()):
-        model = pkg.STGCNStack(cfg["C"], cfg["classes"], A)
+        model = pkg.STGCNStack(cfg["C"], cfg["classes"], A,
+                               gemm_dtype=torch.bfloat16 if cfg["bf16"] else torch.float32)
     return model.to(device)
 
 
@@ -48,8 +72,7 @@ def cpu_baseline(cfg, seconds=12.0):
     pkg = load()
     threads = max(1, min(16, os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    gr = pkg.graph
-    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(cfg["V"]))
+    A = adjacency(pkg, cfg)
     p, b = ref_cpu.init_stack_params(cfg["C"], cfg["classes"], A, seed=0)
     p = {k: v.clone().requires_grad_(True) for k, v in p.items()}
     st = ref_cpu.Stack(p, b)
@@ -70,7 +93,8 @@ def cpu_baseline(cfg, seconds=12.0):
     return {"value": round(n * iters / dt, 3), "unit": "clips/s", "cores": threads,
             "kind": "port",
             "sample": f"oracle/ref_cpu.py fp32 stack fwd+bwd+loss, N={n} clips x {iters} iters "
-                      f"(T=300, V=18, K=1, 400 classes), {threads} threads, {dt:.1f}s"}
+                      f"(T={cfg['T']}, V={cfg['V']}, K={cfg['K']}, {cfg['classes']} classes), "
+                      f"{threads} threads, {dt:.1f}s"}
 
 
 # cfg2 stack layers (lightning_model.py:65-86): (C_in, C_out, T_in, stride)
@@ -102,7 +126,8 @@ def kernel_roofline(pkg, device, cfg, iters=10):
         d[key] = (t[0] + ms, t[1] + fl, t[2] + n)
 
     for ci, co, t, s in stack_layers(cfg):
-        d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True)
+        d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
+                                bf16=cfg["bf16"])
         for which, kind in KERNEL_KINDS.items():
             nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
             scratch = torch.randn(nbytes // 4 + 1, device=device)
@@ -113,9 +138,14 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             del scratch
             add(kinds, kind, ms.value, fl.value, 1)
             V = cfg["V"]
-            sym = {0: f"k_tconv<9,2,{V},{s}>",
-                   1: f"k_tconv<9,2,{V},1>" if s == 1 else f"k_tconv<5|4,2,{V},1>",
-                   2: f"k_wgrad_taps<{V},{s}>", 3: f"k_tconv<1,8,{V},1>"}[which]
+            if cfg["bf16"]:
+                sym = {0: f"k_conv_bf16<9,16,{V},{s}>",
+                       1: f"k_conv_bf16<9,16,{V},1>" if s == 1 else f"k_conv_bf16<5|4,16,{V},1>",
+                       2: f"k_wgrad_bf16<9,{V},{s}>", 3: f"k_conv_bf16<1,32,{V},1>"}[which]
+            else:
+                sym = {0: f"k_tconv<9,2,{V},{s}>",
+                       1: f"k_tconv<9,2,{V},1>" if s == 1 else f"k_tconv<5|4,2,{V},1>",
+                       2: f"k_wgrad_taps<{V},{s}>", 3: f"k_tconv<1,8,{V},1>"}[which]
             add(symbols, sym, ms.value, fl.value, 1 if (which != 1 or s == 1) else 2)
     return kinds, symbols
 
@@ -166,6 +196,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=CFG["N"], help="clips per GPU")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
+                    help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
@@ -178,7 +210,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     pkg = load()
-    cfg = dict(CFG, N=args.batch)
+    cfg = dict(CONFIGS[args.config], N=args.batch)
 
     model = build_model(pkg, cfg, device)
     params = [p for p in model.parameters()]
@@ -226,9 +258,9 @@ def main():
             "value": round(clips, 2), "unit": "clips/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (random N(0,1) skeletons, random labels)",
-            "config": {"workload": "cfg2 Kinetics-skeleton shape: 10-block ST-GCN stack "
-                                   "fwd+bwd+CE+Adam, V=18, T=300, K=1 (uni), 400 classes",
+            "dtype": "bf16" if cfg["bf16"] else "fp32",
+            "data": "synthetic (random N(0,1) skeletons, random labels)",
+            "config": {"workload": cfg["desc"],
                        "per_gpu_batch": cfg["N"], "global_batch": cfg["N"] * world,
                        "seq_len": cfg["T"], "parallelism": f"dp{world}"},
             "model_tflops": round(clips * gf_clip / 1e3, 2),
@@ -241,10 +273,11 @@ def main():
             ms_tot, fl_tot, nl = symbols[sym]
             ach = fl_tot / (ms_tot * 1e-3) / 1e12
             traffic = traffic_from_profiles(sym)
+            peak = MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else MFMA_F32_PEAK_TFLOPS
             out["roofline"] = {
                 "kernel": sym, "bound": "mfma", "achieved": round(ach, 2),
-                "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": traffic,
                 "avg_launch_ms": round(ms_tot / nl, 4), "launches_per_step": nl,
                 "per_kind_tflops": {k: round(v[1] / (v[0] * 1e-3) / 1e12, 1)
                                     for k, v in kinds.items()},

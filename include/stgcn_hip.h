@@ -50,6 +50,11 @@ extern "C" {
 
 /* stgcn_desc_t.flags */
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
+#define STGCN_F_BF16 2     /* channel GEMMs (W, temporal conv fwd/dgrad/wgrad, projection)
+                            * on bf16 MFMA: operands rounded to bf16, fp32 accumulate;
+                            * tensors stay fp32, A / BatchNorm stay fp32 (BASELINE cfg3/5).
+                            * Applies for V in {18, 25, 50} and reductions over >= 16
+                            * channels; other GEMMs run the fp32 kernels. */
 
 enum {
   STGCN_OK = 0,
@@ -68,7 +73,7 @@ typedef struct stgcn_desc {
   float momentum;      /* BatchNorm momentum 0.1                             */
   int32_t training;    /* 1: batch statistics + running-stat update          */
   int32_t need_dx;     /* backward: write dx (0 for the network's first block)*/
-  int32_t flags;       /* 0 or STGCN_F_RESIDUAL                              */
+  int32_t flags;       /* STGCN_F_RESIDUAL | STGCN_F_BF16 (or 0)             */
 } stgcn_desc_t;
 
 /* Forward arguments. Saved tensors (Z, U, stats; residual: Z, Za, y, stats)

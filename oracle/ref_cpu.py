@@ -59,19 +59,55 @@ def _bn(x, p, b, prefix, training, momentum, eps):
     return y
 
 
-def spatial_conv(x, A, W, bW):
+def _bf16(t):
+    """Round to bf16 (nearest even) and back to t's dtype."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _Bf16Conv(torch.autograd.Function):
+    """Conv2d whose GEMM operands are rounded to bf16 in forward (input,
+    weight) and backward (grad_output and the saved rounded operands), with
+    the accumulation in the tensors' own dtype: the reference's conv as it
+    runs with bf16 channel GEMMs (BASELINE cfg3 / cfg5). Used only to measure
+    the reference's own error in that precision (the parity tests' floor)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad):
+        xr, wr = _bf16(x), _bf16(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.cfg = (stride, pad, b is not None)
+        return F.conv2d(xr, wr, b, stride=stride, padding=pad)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xr, wr = ctx.saved_tensors
+        stride, pad, has_b = ctx.cfg
+        gr = _bf16(gy)
+        dx = torch.nn.grad.conv2d_input(xr.shape, wr, gr, stride=stride, padding=pad)
+        dw = torch.nn.grad.conv2d_weight(xr, wr.shape, gr, stride=stride, padding=pad)
+        db = gy.sum(dim=(0, 2, 3)) if has_b else None
+        return dx, dw, db, None, None
+
+
+def _conv(x, w, b, stride=(1, 1), padding=(0, 0), gemm_bf16=False):
+    if gemm_bf16:
+        return _Bf16Conv.apply(x, w, b, stride, padding)
+    return F.conv2d(x, w, b, stride=stride, padding=padding)
+
+
+def spatial_conv(x, A, W, bW, gemm_bf16=False):
     """st_graphconv.py:139-152."""
     N, _, T, V = x.shape
     K = A.shape[0]
     C_out = W.shape[0] // K
-    y = F.conv2d(x, W, bW)
+    y = _conv(x, W, bW, gemm_bf16=gemm_bf16)
     y = y.view(N, K, C_out, T, V)
     return torch.einsum("kvw,nkctw->nctv", A, y)
 
 
 def block_forward(x, p, b, stride, pad=4, residual=False, training=True,
                   momentum=0.1, eps=1e-5, dtype=torch.float32, relu_mask=None,
-                  return_pre_relu=False):
+                  return_pre_relu=False, gemm_bf16=False, inner_mask=None):
     """One SpatialTemporalConv step. ``p``: parameter tensors keyed by the
     reference's state_dict names (BLOCK_PARAM_NAMES [+ apply_residual.*]);
     ``b``: running buffers (updated in place when ``training``).
@@ -79,28 +115,32 @@ def block_forward(x, p, b, stride, pad=4, residual=False, training=True,
     ``relu_mask`` (optional, 0/1 tensor shaped like the output): use this
     mask for the final ReLU instead of ``f > 0`` — used by the parity tests to
     differentiate through the SAME subgradient choice as the implementation
-    under test at ReLU ties (|pre-ReLU| below fp32 resolution)."""
+    under test at ReLU ties (|pre-ReLU| below fp32 resolution).
+
+    ``gemm_bf16``: run the convolutions with bf16-rounded operands
+    (``_Bf16Conv``), everything else unchanged. ``inner_mask`` (residual
+    block): the same as ``relu_mask`` for the inner ReLU after BN2 (:77)."""
     x = x.to(dtype)
     A = p["spatialConv.A"]
     if residual:
         res = x.clone()
         f = _bn(x, p, b, "batch_n", training, momentum, eps)
         f = F.relu(f.clone())
-        f = spatial_conv(f, A, p["spatialConv.W.weight"], p["spatialConv.W.bias"])
+        f = spatial_conv(f, A, p["spatialConv.W.weight"], p["spatialConv.W.bias"], gemm_bf16)
         f = _bn(f, p, b, "batch_n_2", training, momentum, eps)
-        f = F.relu(f.clone())
-        f = F.conv2d(f, p["temporalConv.weight"], p["temporalConv.bias"],
-                     stride=(stride, 1), padding=(pad, 0))
+        f = F.relu(f.clone()) if inner_mask is None else f * inner_mask.to(f.dtype)
+        f = _conv(f, p["temporalConv.weight"], p["temporalConv.bias"],
+                  stride=(stride, 1), padding=(pad, 0), gemm_bf16=gemm_bf16)
         if "apply_residual.weight" in p:
-            f = f + F.conv2d(res, p["apply_residual.weight"], p["apply_residual.bias"],
-                             stride=(stride, 1))
+            f = f + _conv(res, p["apply_residual.weight"], p["apply_residual.bias"],
+                          stride=(stride, 1), gemm_bf16=gemm_bf16)
         else:
             f = f + res
     else:
         f = _bn(x, p, b, "batch_n", training, momentum, eps)
-        f = spatial_conv(f, A, p["spatialConv.W.weight"], p["spatialConv.W.bias"])
-        f = F.conv2d(f, p["temporalConv.weight"], p["temporalConv.bias"],
-                     stride=(stride, 1), padding=(pad, 0))
+        f = spatial_conv(f, A, p["spatialConv.W.weight"], p["spatialConv.W.bias"], gemm_bf16)
+        f = _conv(f, p["temporalConv.weight"], p["temporalConv.bias"],
+                  stride=(stride, 1), padding=(pad, 0), gemm_bf16=gemm_bf16)
         f = _bn(f, p, b, "batch_n_2", training, momentum, eps)
     if return_pre_relu:
         return f
@@ -124,7 +164,7 @@ def block_params_from_arrays(arrays, prefix="param.", dtype=torch.float32, requi
     return p, b
 
 
-def block_step(arrays, dtype=torch.float64, relu_mask=None):
+def block_step(arrays, dtype=torch.float64, relu_mask=None, gemm_bf16=False, inner_mask=None):
     """Run fwd+bwd of one block fixture on the oracle; returns a dict with
     the same keys the fixture stores (y, grad.*, after.*)."""
     meta = arrays["meta"]
@@ -132,7 +172,8 @@ def block_step(arrays, dtype=torch.float64, relu_mask=None):
     p, b = block_params_from_arrays(arrays, dtype=dtype)
     x = torch.as_tensor(arrays["x"]).to(dtype).requires_grad_(True)
     g = torch.as_tensor(arrays["g"]).to(dtype)
-    y = block_forward(x, p, b, stride, residual=residual, dtype=dtype, relu_mask=relu_mask)
+    y = block_forward(x, p, b, stride, residual=residual, dtype=dtype, relu_mask=relu_mask,
+                      gemm_bf16=gemm_bf16, inner_mask=inner_mask)
     (y * g).sum().backward()
     out = {"y": y.detach(), "grad.x": x.grad}
     for k, t in p.items():

@@ -58,6 +58,7 @@ size_t wpk_floats(const stgcn_desc_t *d) {
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }
 int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
 bool residual(const stgcn_desc_t *d) { return (d->flags & STGCN_F_RESIDUAL) != 0; }
+bool bf16(const stgcn_desc_t *d) { return (d->flags & STGCN_F_BF16) != 0; }
 // the fused dropout of a call (training and 0 < p < 1; p >= 1: everything dropped)
 Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
   Dropout dr;
@@ -115,6 +116,7 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   w.N = d->N;
   w.S = wgrad_splits(w.n_rtiles * w.n_jtiles, d->N * w.n_mtiles);
   if (wgrad_sp_applies(w)) plan_wgrad_sp(w);
+  if (bf16(d)) plan_wgrad_bf16(w);  // k_wgrad_bf16 where it covers the shape
   return w;
 }
 
@@ -144,6 +146,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
   w.n_jtiles = (R + wgrad_taps_cb(w) - 1) / wgrad_taps_cb(w);
   const int tiles = w.n_rtiles * w.n_jtiles;
   w.S = std::max(1, std::min((256 + tiles - 1) / tiles, d->N * w.n_mtiles));
+  if (bf16(d)) plan_wgrad_bf16(w);
   return w;
 }
 
@@ -216,6 +219,7 @@ ConvGemmParams conv_base(const stgcn_desc_t *d, float *wpk) {
   p.V = d->V;
   p.FT = conv_ft(d->V);
   p.N = d->N;
+  p.bf16 = bf16(d);
   return p;
 }
 
@@ -231,7 +235,7 @@ static bool geometry_supported(const stgcn_desc_t *d) {
   const int R = d->C_out, C = d->C_in, K = d->K;
   WgradParams w1 = make_wgrad_taps(d, nullptr, nullptr, nullptr);
   WgradParams w2 = make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
-  if (!wgrad_taps_supported(w1) || !wgrad_supported(w2)) return false;
+  if (!(w1.bf16 || wgrad_taps_supported(w1)) || !(w2.bf16 || wgrad_supported(w2))) return false;
   ConvGemmParams p = conv_base(d, nullptr);
   p.NQ = 9;
   p.s_in = d->stride;
@@ -247,7 +251,8 @@ static bool geometry_supported(const stgcn_desc_t *d) {
     p.C = C;
     WgradParams w3 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, C, d->T, 1, d->stride, 0,
                                 nullptr);
-    if (!conv_gemm_supported(p) || !(wgrad_sp_applies(w3) || wgrad_supported(w3))) return false;
+    if (!conv_gemm_supported(p) || !(w3.bf16 || wgrad_sp_applies(w3) || wgrad_supported(w3)))
+      return false;
   }
   return true;
 }
@@ -334,7 +339,8 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   if (!d) return fail(STGCN_E_INVALID, "null descriptor");
   if (d->N <= 0 || d->C_in <= 0 || d->C_out <= 0 || d->T <= 0 || d->V <= 0 || d->K <= 0)
     return fail(STGCN_E_INVALID, "non-positive dimension");
-  if ((d->flags & ~STGCN_F_RESIDUAL) != 0) return fail(STGCN_E_UNSUPPORTED, "unknown flags");
+  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16)) != 0)
+    return fail(STGCN_E_UNSUPPORTED, "unknown flags");
   if (d->gamma != 9 || d->pad != 4)
     return fail(STGCN_E_UNSUPPORTED, "only gamma=9, pad=4 (the reference default)");
   if (d->stride != 1 && d->stride != 2) return fail(STGCN_E_UNSUPPORTED, "stride must be 1 or 2");

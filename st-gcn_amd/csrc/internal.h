@@ -54,6 +54,8 @@ struct ConvGemmParams {
   const float *res;  // same layout and clip stride as out, or null
   int relu_out;
   Dropout drop;      // applied after relu_out (element index = flat index in out)
+  int bf16;          // 1: operands rounded to bf16 on v_mfma_f32_32x32x16_bf16 (fp32
+                     // accumulate, fp32 in/out), where k_conv_bf16 covers the shape
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -69,9 +71,22 @@ struct WgradParams {
   int V, FT;
   int n_mtiles, n_rtiles, n_jtiles, S, N;
   int CT;  // k_wgrad_sp (NQ = 1): output columns per workgroup (64 or 128)
+  int bf16;  // set by plan_wgrad_bf16: run k_wgrad_bf16 (bf16 operands, fp32 accumulate)
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
+// bf16 path (kernels_bf16.hip): the reference's graphs (V = 18, 25, 50) with
+// the fp32 path's tile plan (FT = kTileCols / V); launch_conv_gemm dispatches here
+// when p.bf16 and conv_bf16_supported(p).
+bool conv_bf16_supported(const ConvGemmParams &p);
+size_t conv_bf16_lds_bytes(const ConvGemmParams &p);
+hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s);
+// Re-plans a weight gradient (NQ = 9 temporal taps or NQ = 1) for k_wgrad_bf16
+// (sets FT, n_mtiles, n_rtiles, n_jtiles, S, bf16 = 1) when the shape is
+// covered; returns false (w unchanged) otherwise. launch_wgrad / launch_wgrad_taps
+// dispatch to launch_wgrad_bf16 when w.bf16.
+bool plan_wgrad_bf16(WgradParams &w);
+hipError_t launch_wgrad_bf16(const WgradParams &p, hipStream_t s);
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s);
 // Plan of the NQ = 1 weight gradient (plain split-K GEMM over (n, t*V) chunks of
 // wgrad_sp_kc(CT) columns): sets CT, n_rtiles, n_jtiles, n_mtiles (chunks per

@@ -1,0 +1,583 @@
+// bf16 GEMM kernels of libstgcn_hip.so (STGCN_F_BF16) — gfx950 only.
+//
+// The channel contractions of the block (spatial 1x1 conv, (9,1) temporal conv
+// forward / data-grad / weight-grad, residual projection) on
+// v_mfma_f32_32x32x16_bf16: operands rounded to bf16 (RNE) while they are
+// staged into LDS, fp32 accumulation, fp32 tensors in HBM (the block's
+// interface and every other kernel stay fp32; the joint contractions with A
+// and BatchNorm are fp32 / fp64 as in the fp32 path). This is the "bf16
+// channel GEMMs with fp32 accumulate and fp32 A" configuration of
+// BASELINE.json cfg3 / cfg5 (SURVEY.md §8c tolerance 2e-2).
+//
+// Operand fragments of v_mfma_f32_32x32x16_bf16 (lane l, r = l & 31,
+// h = l >> 5): A[row r][k = 8h + j], B[k = 8h + j][col r], j = 0..7 — eight
+// consecutive k per lane, so each LDS image keeps the reduction index
+// innermost: the conv GEMM stages its input window position-major with the
+// chunk's channels contiguous ([pos][channel], 16-byte slots, odd slot pitch),
+// the weight gradient stages both operands row-major over (frame, joint)
+// positions with the joint axis padded to a multiple of 4.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "device_common.h"
+#include "internal.h"
+
+namespace stgcn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// two floats -> one dword of two bf16 (round to nearest even, v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+__device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t rs, unsigned voff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0));
+}
+
+// ---------------------------------------------------------------------------
+// k_conv_bf16: the ConvGemmParams GEMM (see internal.h) on bf16 MFMA.
+// Workgroup = 4 waves, tile = 64 rows x FT*V columns (FT = kTileCols / V, the
+// fp32 plan), wave w: rows (w&1)*32..+31, column tiles (w>>1)*4..+3.
+// k-step = one tap q x 16 channels of the chunk (CK channels per chunk):
+//   A fragment: packed weights [q][channel octet][64 rows][8] (one ds_read_b128),
+//   B fragment: the input window [position][CK channels] at position
+//               colpos + q*V (one ds_read_b128; slot pitch CK/8 + 1 is odd,
+//               so any 16 lanes of consecutive positions are conflict-free).
+// Staging: the weights (already bf16 in HBM, wpk) move by 16-byte LDS-DMA;
+// the window is loaded as fp32 dwords (consecutive lanes = consecutive
+// positions of one channel: coalesced), converted, and written as 16-byte
+// [position][8 channels] pieces. Two LDS buffers; chunk i+1's loads are in
+// flight under chunk i's MFMAs; one barrier per chunk.
+// ---------------------------------------------------------------------------
+template <int NQ, int CK, int V, int SIN>
+struct ConvBf16Geo {
+  static constexpr int FT = kTileCols / V;
+  static constexpr int NCOLS = FT * V;
+  static constexpr int SPAN = (SIN * (FT - 1) + NQ) * V;  // window positions
+  static constexpr int OCT = CK / 8;                      // channel octets per position
+  static constexpr int SLOTS = OCT + 1;                   // 16-byte slots per position (odd)
+  static constexpr int IMG = SPAN * SLOTS * 16;           // bytes
+  static constexpr int WCH = NQ * OCT * 1024;             // bytes of one packed weight chunk
+  static constexpr int BUF = WCH + IMG;
+  static constexpr int NIT = SPAN * OCT;                  // (position, octet) staging items
+  static constexpr int IPT = (NIT + 255) / 256;           // items per thread
+  static constexpr int WDMA = NQ * OCT;                   // 1 KiB DMA rows per weight chunk
+  static_assert(CK % 16 == 0 && (SLOTS & 1), "k-step = 16 channels; odd slot pitch");
+};
+
+template <int NQ, int CK, int V, int SIN>
+__global__ __launch_bounds__(256, 2) void k_conv_bf16(ConvGemmParams p) {
+  using G = ConvBf16Geo<NQ, CK, V, SIN>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid % p.n_rtiles;
+  bid /= p.n_rtiles;
+  const int mt = bid % p.n_mtiles;
+  const int n = bid / p.n_mtiles;
+  const int r0 = rt * kTileRows, m0 = mt * G::FT;
+  const int cstride = p.T_src * V;
+  const int g0 = (SIN * m0 + p.off) * V;
+  const float *inN = p.in + (int64_t)n * p.in_bstride;
+  const int nchunks = (p.C + CK - 1) / CK;
+  const char *wblk = reinterpret_cast<const char *>(p.wpk) + (int64_t)rt * nchunks * G::WCH;
+  const int mi = wave & 1, nj0 = (wave >> 1) * 4;
+
+  // per-lane byte offsets of the A fragment and the 4 B fragments (tap 0, octet h)
+  const int ao = (hi * 64 + mi * 32 + lo) * 16;
+  int bo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    const int mf = col / V;
+    const int cp = col < G::NCOLS ? SIN * mf * V + (col - mf * V) : 0;
+    bo[j] = (cp * G::SLOTS + hi) * 16;
+  }
+  // staging items of this thread: (octet o, window position pp); byte offset of
+  // channel 8o, position g0 + pp relative to the chunk's first channel
+  unsigned voff[G::IPT];
+  int loff[G::IPT];
+#pragma unroll
+  for (int k = 0; k < G::IPT; ++k) {
+    const int e = k * 256 + tid;
+    const int o = e / G::SPAN, pp = e - o * G::SPAN;
+    const int g = g0 + pp;
+    const bool ok = e < G::NIT && g >= 0 && g < cstride;
+    voff[k] = ok ? (unsigned)(o * 8 * cstride + g) * 4u : kOOB;
+    loff[k] = e < G::NIT ? (pp * G::SLOTS + o) * 16 : -1;
+  }
+  const __amdgpu_buffer_rsrc_t rs_w =
+      make_rsrc(reinterpret_cast<const float *>(wblk), (int64_t)nchunks * G::WCH / 4);
+  float st[G::IPT][8];
+  auto load_img = [&](int chunk) {
+    const __amdgpu_buffer_rsrc_t rs =
+        make_rsrc(inN + (int64_t)chunk * CK * cstride, (int64_t)(p.C - chunk * CK) * cstride);
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) st[k][j] = ld_f32(rs, voff[k] + (unsigned)(j * cstride * 4));
+  };
+  auto dma_w = [&](int chunk, char *dst) {
+    for (int d = wave; d < G::WDMA; d += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, dst + d * 1024, 16,
+                                               (unsigned)(chunk * G::WCH + d * 1024 + lane * 16),
+                                               0, 0, 0);
+  };
+  auto write_img = [&](char *dst) {
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+      if (loff[k] >= 0) {
+        uint4 v;
+        v.x = pk_bf16(st[k][0], st[k][1]);
+        v.y = pk_bf16(st[k][2], st[k][3]);
+        v.z = pk_bf16(st[k][4], st[k][5]);
+        v.w = pk_bf16(st[k][6], st[k][7]);
+        *reinterpret_cast<uint4 *>(dst + loff[k]) = v;
+      }
+  };
+
+  floatx16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+
+  dma_w(0, lds);
+  load_img(0);
+  write_img(lds + G::WCH);
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    __syncthreads();  // chunk's weights (DMA) and window (all waves) are in LDS
+    char *cur = lds + (chunk & 1) * G::BUF;
+    char *nxt = lds + ((chunk + 1) & 1) * G::BUF;
+    const bool more = chunk + 1 < nchunks;
+    if (more) {
+      dma_w(chunk + 1, nxt);
+      load_img(chunk + 1);
+    }
+    const char *wa = cur + ao;
+    const char *ib = cur + G::WCH;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int o2 = 0; o2 < G::OCT / 2; ++o2) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8 *>(wa + (q * G::OCT + 2 * o2) * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x8 b = *reinterpret_cast<const bf16x8 *>(
+              ib + bo[j] + (q * V * G::SLOTS + 2 * o2) * 16);
+          acc[j] = mfma_bf16(a, b, acc[j]);
+        }
+      }
+    if (more) write_img(nxt + G::WCH);
+  }
+  __syncthreads();  // every wave done with the buffers (the epilogue reuses LDS)
+  conv_tile_epilogue<V, G::NCOLS>(p, acc, n, r0, m0, smem);
+}
+
+// Packs w[r*w_sr + c*w_sc + q*w_sq] as bf16 into
+// wpk[rt][chunk][q][octet][64 rows][8] (zero padded rows and channels).
+__global__ void k_pack_conv_w_bf16(const float *w, __bf16 *wpk, int R, int C, int NQ, int CK,
+                                   int nch, int64_t w_sr, int64_t w_sc, int64_t w_sq,
+                                   int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int jj = (int)(idx & 7);
+  int64_t t = idx >> 3;
+  const int rl = (int)(t & 63);
+  t >>= 6;
+  const int oct = CK / 8;
+  const int o = (int)(t % oct);
+  t /= oct;
+  const int q = (int)(t % NQ);
+  t /= NQ;
+  const int ch = (int)(t % nch);
+  const int rt = (int)(t / nch);
+  const int r = rt * 64 + rl, c = ch * CK + o * 8 + jj;
+  float v = 0.f;
+  if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
+  wpk[idx] = (__bf16)v;
+}
+
+static int conv_bf16_ck(int NQ) { return NQ == 1 ? 32 : 16; }
+
+bool conv_bf16_supported(const ConvGemmParams &p) {
+  // a reduction over fewer than 16 channels (the first block's C_in = 3: the
+  // spatial GEMM over K*3 channels, the 1x1 projection) stays on the fp32
+  // path: a bf16 k-step is 16 channels (mostly padding there), and rounding
+  // the smooth joint-averaged G of a 3-channel input costs the most precision
+  if (p.C < 16) return false;
+  if (p.V != 18 && p.V != 25 && p.V != 50) return false;
+  if (p.FT != kTileCols / p.V) return false;
+  if (p.s_in == 2) return p.NQ == 9 || p.NQ == 1;
+  return p.s_in == 1 && (p.NQ == 1 || p.NQ == 4 || p.NQ == 5 || p.NQ == 9);
+}
+
+size_t conv_bf16_lds_bytes(const ConvGemmParams &p) {
+  const int CK = conv_bf16_ck(p.NQ);
+  const int span = (p.s_in * (p.FT - 1) + p.NQ) * p.V;
+  const size_t buf = (size_t)p.NQ * (CK / 8) * 1024 + (size_t)span * (CK / 8 + 1) * 16;
+  return std::max(2 * buf, (size_t)2048);
+}
+
+template <int NQ, int V, int SIN>
+static bool launch_cb_if(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
+  if (p.V != V || p.s_in != SIN) return false;
+  constexpr int CK = NQ == 1 ? 32 : 16;
+  hipLaunchKernelGGL((k_conv_bf16<NQ, CK, V, SIN>), dim3(nblk), dim3(256), lds, s, p);
+  return true;
+}
+
+template <int NQ, int SIN>
+static bool launch_cb_v(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
+  return launch_cb_if<NQ, 18, SIN>(p, nblk, lds, s) || launch_cb_if<NQ, 25, SIN>(p, nblk, lds, s) ||
+         launch_cb_if<NQ, 50, SIN>(p, nblk, lds, s);
+}
+
+hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s) {
+  if (!conv_bf16_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  const int CK = conv_bf16_ck(p.NQ);
+  const int nch = (p.C + CK - 1) / CK;
+  {
+    const int64_t total = (int64_t)p.n_rtiles * nch * CK * p.NQ * 64;
+    hipLaunchKernelGGL(k_pack_conv_w_bf16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       s, p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, CK, nch, p.w_sr,
+                       p.w_sc, p.w_sq, total);
+  }
+  const int nblk = p.N * p.n_mtiles * p.n_rtiles;
+  const size_t lds = conv_bf16_lds_bytes(p);
+  bool done = false;
+  if (p.s_in == 2) {
+    done = p.NQ == 9 ? launch_cb_v<9, 2>(p, nblk, lds, s) : launch_cb_v<1, 2>(p, nblk, lds, s);
+  } else {
+    switch (p.NQ) {
+      case 1: done = launch_cb_v<1, 1>(p, nblk, lds, s); break;
+      case 4: done = launch_cb_v<4, 1>(p, nblk, lds, s); break;
+      case 5: done = launch_cb_v<5, 1>(p, nblk, lds, s); break;
+      case 9: done = launch_cb_v<9, 1>(p, nblk, lds, s); break;
+    }
+  }
+  return done ? hipGetLastError() : hipErrorInvalidValue;
+}
+
+// ---------------------------------------------------------------------------
+// k_wgrad_bf16: the WgradParams weight gradient (internal.h) on bf16 MFMA,
+//   slab[split][r][c*NQ + q] = sum_{items of split} sum_{m,v} P[n,r,m,v] Q[n,c,SIN*m+q+off,v]
+// NQ = 9 (temporal taps) or 1 (spatial W, residual projection). Output tile
+// 64 rows x CB channels x NQ taps; waves = (row half) x (32-channel block) x
+// (tap group: taps 0-4 / 5-8 for NQ = 9). Work item = (clip n, FT frames of P);
+// the split-K over items is S-way (grid = tiles x S), items s, s+S, ...
+// The reduction index is the (frame, joint) position with the joint axis
+// padded to Vp = round4(V) (P's pad positions are zero, so Q's are don't-care).
+// k-step s (16 positions): lane half h takes the position 4-groups 2s, 2s+1 of
+// frame half h (frames h*FT/2 ..): eight consecutive positions of P (one
+// ds_read_b128) and, per tap, two 4-position runs of Q at frame SIN*m + q
+// (two ds_read_b64; row pitches = 4 mod 8 elements: conflict-free).
+// Staging: thread t owns position group (t mod PG) of rows t/PG, t/PG + RS, ...
+// (PG groups per row, RS = NTH / PG rows per pass), fp32 dword loads through
+// a buffer resource (kOOB -> 0 outside the tensor, the halo and the row tail),
+// converted and written as 8-byte pieces; double-buffered, one barrier per item.
+// ---------------------------------------------------------------------------
+template <int NQ, int V, int SIN, int FT, int CB>
+struct WgBf16Geo {
+  static constexpr int Vp = (V + 3) & ~3;
+  static constexpr int G4 = Vp / 4;
+  static constexpr int KP = FT * Vp;  // P positions per item
+  static constexpr int KSTEPS = KP / 16;
+  static constexpr int HF = FT / 2;
+  static constexpr int PPITCH = KP + 8;  // elements; PPITCH/8 odd: ds_read_b128 conflict-free
+  static constexpr int QF = SIN * (FT - 1) + NQ;  // Q frames per item
+  static constexpr int QP0 = QF * Vp;
+  static constexpr int QPITCH = QP0 % 8 == 0 ? QP0 + 4 : QP0;  // = 4 mod 8 (b64 conflict-free)
+  // tap groups: NQ = 9 -> 2 groups (taps 0-4, 5-8) at CB = 64, 4 groups
+  // (0-2, 3-4, 5-6, 7-8) at CB = 32: 8 waves either way
+  static constexpr int TG = NQ == 9 ? (CB == 64 ? 2 : 4) : 1;
+  static constexpr int NTMAX = NQ == 9 ? (TG == 2 ? 5 : 3) : 1;
+  static constexpr int NW = 2 * (CB / 32) * TG;
+  static constexpr int NTH = NW * 64;
+  static constexpr int PBYTES = (64 * PPITCH * 2 + 15) / 16 * 16;
+  static constexpr int QBYTES = (CB * QPITCH * 2 + 15) / 16 * 16;
+  static constexpr int BUF = PBYTES + QBYTES;
+  // staging: P: PGR = FT*G4 groups per row, RSP rows per pass, NPP passes
+  static constexpr int PGR = FT * G4;
+  static constexpr int RSP = NTH / PGR;
+  static constexpr int NPP = (64 + RSP - 1) / RSP;
+  static constexpr int QGR = QF * G4;
+  static constexpr int RSQ = NTH / QGR;
+  static constexpr int NPQ = (CB + RSQ - 1) / RSQ;
+  static constexpr int NPASS = NPP + NPQ;
+  static constexpr int NPART = KSTEPS >= 4 ? 4 : 2;  // staging parts per item
+  static constexpr int PPART = (NPASS + NPART - 1) / NPART;
+  static_assert(KP % 16 == 0 && FT % 2 == 0 && PPITCH % 16 == 8, "k-step geometry");
+  static_assert(RSP >= 1 && RSQ >= 1, "a row of position groups fits the workgroup");
+};
+
+template <int NQ, int V, int SIN, int FT, int CB>
+__global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgrad_bf16(WgradParams p) {
+  using G = WgBf16Geo<NQ, V, SIN, FT, CB>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid % p.S;
+  bid /= p.S;
+  const int jt = bid % p.n_jtiles;
+  const int rt = bid / p.n_jtiles;
+  const int r0 = rt * 64, c0 = jt * CB;
+  const int mi = wave & 1;
+  const int cj = (wave >> 1) % (CB / 32);
+  const int tq = wave / (2 * (CB / 32));
+  // first tap and tap count of this wave's group
+  const int q0 = G::TG == 2 ? 5 * tq : (G::TG == 4 ? (tq ? 1 + 2 * tq : 0) : 0);
+  const int nitems = p.N * p.n_mtiles;
+
+  // lane bases (elements) of the A (P) and B (Q) fragments
+  const int pa = (mi * 32 + lo) * G::PPITCH + hi * G::HF * G::Vp;
+  const int qb = (cj * 32 + lo) * G::QPITCH + hi * SIN * G::HF * G::Vp + q0 * G::Vp;
+
+  // staging geometry of this thread
+  const int pg = tid % G::PGR, prow = tid / G::PGR;  // prow >= RSP: idle in P staging
+  const int pf = pg / G::G4, pv = (pg % G::G4) * 4;
+  const int qg = tid % G::QGR, qrow = tid / G::QGR;
+  const int qf = qg / G::G4, qv = (qg % G::G4) * 4;
+  const int MV = p.M * V, TV = p.T_src * V;
+  // Staging passes: pass k < NPP loads 4 joints of P row prow + k*RSP, pass
+  // NPP + k 4 joints of Q row qrow + k*RSQ. An item's passes are issued in
+  // NPART parts, each loaded under one NPART-th of the previous item's k-steps
+  // and written right after them (fewer staging registers).
+  struct ItemRef {
+    __amdgpu_buffer_rsrc_t rp, rq;
+    bool fok, tok;
+    int pbase, qbase;  // element offsets of (row 0 of the tile, frame m0 / t0)
+  };
+  auto item_ref = [&](int item) {
+    ItemRef ir;
+    const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * FT;
+    ir.rp = make_rsrc(p.P + (int64_t)n * p.p_bstride, p.p_bstride);
+    ir.rq = make_rsrc(p.Q + (int64_t)n * p.q_bstride, p.q_bstride);
+    ir.fok = prow < G::RSP && m0 + pf < p.M;
+    const int t = SIN * m0 + p.off + qf;
+    ir.tok = qrow < G::RSQ && t >= 0 && t < p.T_src;
+    ir.pbase = (m0 + pf) * V + pv;
+    ir.qbase = t * V + qv;
+    return ir;
+  };
+  float st[G::PPART][4];
+  auto load_part = [&](const ItemRef &ir, auto part_c) {
+    constexpr int PART = decltype(part_c)::value;
+#pragma unroll
+    for (int i = 0; i < G::PPART; ++i) {
+      const int k = PART * G::PPART + i;
+      if (k < G::NPP) {
+        const int r = r0 + prow + k * G::RSP;
+        const bool ok = ir.fok && prow + k * G::RSP < 64 && r < p.R;
+        const unsigned base = ok ? (unsigned)(r * MV + ir.pbase) * 4u : kOOB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          st[i][j] = (pv + j < V) ? ld_f32(ir.rp, base + 4u * j) : 0.f;  // pad joints: 0
+      } else if (k < G::NPP + G::NPQ) {
+        const int kq = k - G::NPP;
+        const int c = c0 + qrow + kq * G::RSQ;
+        const bool ok = ir.tok && qrow + kq * G::RSQ < CB && c < p.C;
+        const unsigned base = ok ? (unsigned)(c * TV + ir.qbase) * 4u : kOOB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st[i][j] = ld_f32(ir.rq, base + 4u * j);
+      }
+    }
+  };
+  auto write_part = [&](char *buf, auto part_c) {
+    constexpr int PART = decltype(part_c)::value;
+#pragma unroll
+    for (int i = 0; i < G::PPART; ++i) {
+      const int k = PART * G::PPART + i;
+      uint2 v;
+      v.x = pk_bf16(st[i][0], st[i][1]);
+      v.y = pk_bf16(st[i][2], st[i][3]);
+      if (k < G::NPP) {
+        if (prow < G::RSP && prow + k * G::RSP < 64)
+          *reinterpret_cast<uint2 *>(buf + ((prow + k * G::RSP) * G::PPITCH + pf * G::Vp + pv) * 2) = v;
+      } else if (k < G::NPP + G::NPQ) {
+        const int kq = k - G::NPP;
+        if (qrow < G::RSQ && qrow + kq * G::RSQ < CB)
+          *reinterpret_cast<uint2 *>(buf + G::PBYTES +
+                                     ((qrow + kq * G::RSQ) * G::QPITCH + qf * G::Vp + qv) * 2) = v;
+      }
+    }
+  };
+
+  constexpr int NTMAX = G::NTMAX;
+
+  // k-loop with the operands of step s+1 read (LDS) under the MFMAs of step s
+  auto compute = [&](floatx16 *acc, const char *buf, auto nt_c, auto s0_c, auto s1_c) {
+    constexpr int NT = decltype(nt_c)::value;
+    constexpr int S0 = decltype(s0_c)::value, S1 = decltype(s1_c)::value;
+    const __bf16 *P = reinterpret_cast<const __bf16 *>(buf) + pa;
+    const __bf16 *Q = reinterpret_cast<const __bf16 *>(buf + G::PBYTES) + qb;
+    bf16x8 a[2], b[2][NT];
+    auto ld = [&](int s, int set) {
+      a[set] = *reinterpret_cast<const bf16x8 *>(P + 8 * s);
+      // position 4-groups 2s, 2s+1 of the frame half: Q frame SIN*m + tap, joint v0
+      const int ga = 2 * s, gb = 2 * s + 1;
+      const int oa = SIN * (ga / G::G4) * G::Vp + (ga % G::G4) * 4;
+      const int ob = SIN * (gb / G::G4) * G::Vp + (gb % G::G4) * 4;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const bf16x4 b0 = *reinterpret_cast<const bf16x4 *>(Q + oa + t * G::Vp);
+        const bf16x4 b1 = *reinterpret_cast<const bf16x4 *>(Q + ob + t * G::Vp);
+        b[set][t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    ld(S0, 0);
+#pragma unroll
+    for (int s = S0; s < S1; ++s) {
+      if (s + 1 < S1) ld(s + 1, (s + 1 - S0) & 1);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = mfma_bf16(a[(s - S0) & 1], b[(s - S0) & 1][t], acc[t]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // one item: part j of the next item's staging is loaded under the j-th
+  // slice of this item's k-steps and written after it
+  auto item_body = [&](floatx16 *acc, const char *cur, char *nxt, bool more, const ItemRef &nir,
+                       auto nt_c) {
+    auto part = [&](auto j_c) {
+      constexpr int J = decltype(j_c)::value;
+      constexpr int S0 = J * G::KSTEPS / G::NPART, S1 = (J + 1) * G::KSTEPS / G::NPART;
+      if (more) load_part(nir, j_c);
+      compute(acc, cur, nt_c, std::integral_constant<int, S0>{}, std::integral_constant<int, S1>{});
+      if (more) write_part(nxt, j_c);
+    };
+    part(std::integral_constant<int, 0>{});
+    part(std::integral_constant<int, 1>{});
+    if constexpr (G::NPART == 4) {
+      part(std::integral_constant<int, 2>{});
+      part(std::integral_constant<int, 3>{});
+    }
+  };
+
+  int item = split;
+  if (item < nitems) {
+    const ItemRef ir = item_ref(item);
+    load_part(ir, std::integral_constant<int, 0>{});
+    write_part(lds, std::integral_constant<int, 0>{});
+    load_part(ir, std::integral_constant<int, 1>{});
+    write_part(lds, std::integral_constant<int, 1>{});
+    if constexpr (G::NPART == 4) {
+      load_part(ir, std::integral_constant<int, 2>{});
+      write_part(lds, std::integral_constant<int, 2>{});
+      load_part(ir, std::integral_constant<int, 3>{});
+      write_part(lds, std::integral_constant<int, 3>{});
+    }
+  }
+  // the item loop and the slab store, instantiated per tap count of the wave
+  // (a wave-uniform branch outside the loop: the accumulators of the two
+  // variants never meet)
+  auto run = [&](auto nt_c) {
+    constexpr int NT = decltype(nt_c)::value;
+    floatx16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    for (int it = 0, itm = item; itm < nitems; ++it, itm += p.S) {
+      __syncthreads();
+      const char *cur = lds + (it & 1) * G::BUF;
+      char *nxt = lds + ((it + 1) & 1) * G::BUF;
+      const bool more = itm + p.S < nitems;
+      const ItemRef nir = item_ref(more ? itm + p.S : itm);
+      item_body(acc, cur, nxt, more, nir, nt_c);
+    }
+    // partial tile -> slab[split][r][c*NQ + q]
+    float *slab = p.slab + (int64_t)split * p.R * p.C * NQ;
+    const int c = c0 + cj * 32 + lo;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        if (r < p.R && c < p.C) slab[((int64_t)r * p.C + c) * NQ + q0 + t] = acc[t][i];
+      }
+  };
+  if (tq == 0)  // the first tap group has the most taps
+    run(std::integral_constant<int, NTMAX>{});
+  else
+    run(std::integral_constant<int, (NTMAX > 1 ? NTMAX - 1 : 1)>{});
+}
+
+// Tile plans (FT, CB) per (NQ, V, SIN): double-buffered images within 160 KiB.
+struct WgBf16Plan {
+  int FT, CB;
+};
+
+static bool wgrad_bf16_plan(const WgradParams &w, WgBf16Plan &pl) {
+  if (w.V != 18 && w.V != 25 && w.V != 50) return false;
+  if (w.s_in != 1 && w.s_in != 2) return false;
+  if (w.NQ == 9) {
+    if (w.off != -4) return false;
+    pl.FT = w.V == 18 ? 8 : 4;
+    pl.CB = w.V == 50 ? 32 : 64;
+  } else if (w.NQ == 1) {
+    if (w.off != 0) return false;
+    pl.FT = 4;
+    pl.CB = 64;
+  } else {
+    return false;
+  }
+  return true;
+}
+
+bool plan_wgrad_bf16(WgradParams &w) {
+  WgBf16Plan pl;
+  if (!wgrad_bf16_plan(w, pl)) return false;
+  w.FT = pl.FT;
+  w.n_mtiles = (w.M + pl.FT - 1) / pl.FT;
+  w.n_rtiles = (w.R + 63) / 64;
+  w.n_jtiles = (w.C + pl.CB - 1) / pl.CB;
+  const int tiles = w.n_rtiles * w.n_jtiles;
+  const int target = w.NQ == 9 ? 256 : 512;
+  w.S = std::max(1, std::min((target + tiles - 1) / tiles, w.N * w.n_mtiles));
+  w.bf16 = 1;
+  return true;
+}
+
+template <int NQ, int V, int SIN, int FT, int CB>
+static bool launch_wb_if(const WgradParams &p, hipStream_t s) {
+  if (p.V != V || p.s_in != SIN || p.FT != FT) return false;
+  using G = WgBf16Geo<NQ, V, SIN, FT, CB>;
+  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  hipLaunchKernelGGL((k_wgrad_bf16<NQ, V, SIN, FT, CB>), dim3(nblk), dim3(G::NTH), 2 * G::BUF, s,
+                     p);
+  return true;
+}
+
+hipError_t launch_wgrad_bf16(const WgradParams &p, hipStream_t s) {
+  if (!p.bf16) return hipErrorInvalidValue;
+  bool done = false;
+  if (p.NQ == 9) {
+    done = launch_wb_if<9, 18, 1, 8, 64>(p, s) || launch_wb_if<9, 18, 2, 8, 64>(p, s) ||
+           launch_wb_if<9, 25, 1, 4, 64>(p, s) || launch_wb_if<9, 25, 2, 4, 64>(p, s) ||
+           launch_wb_if<9, 50, 1, 4, 32>(p, s) || launch_wb_if<9, 50, 2, 4, 32>(p, s);
+  } else if (p.NQ == 1) {
+    done = launch_wb_if<1, 18, 1, 4, 64>(p, s) || launch_wb_if<1, 18, 2, 4, 64>(p, s) ||
+           launch_wb_if<1, 25, 1, 4, 64>(p, s) || launch_wb_if<1, 25, 2, 4, 64>(p, s) ||
+           launch_wb_if<1, 50, 1, 4, 64>(p, s) || launch_wb_if<1, 50, 2, 4, 64>(p, s);
+  }
+  return done ? hipGetLastError() : hipErrorInvalidValue;
+}
+
+}  // namespace stgcn

@@ -23,11 +23,12 @@ def _f32c(t, name):
 
 
 def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1, gamma=9,
-              residual=False):
+              residual=False, bf16=False):
     N, C_in, T, V = x_shape
     T_out = (T + 2 * pad - gamma) // stride + 1
+    flags = (hip_lib.F_RESIDUAL if residual else 0) | (hip_lib.F_BF16 if bf16 else 0)
     return hip_lib.Desc(N, C_in, C_out, T, T_out, V, K, gamma, stride, pad, eps, momentum,
-                        int(training), int(need_dx), hip_lib.F_RESIDUAL if residual else 0)
+                        int(training), int(need_dx), flags)
 
 
 class Link:
@@ -113,7 +114,7 @@ class StgcnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training, cc=None, drop=0.0):
+                stride, pad, eps, momentum, training, cc=None, drop=0.0, bf16=False):
         lib = hip_lib.lib()
         x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
@@ -125,7 +126,7 @@ class StgcnBlockFn(torch.autograd.Function):
         N, C_in, T, V = x.shape
         K = A.shape[0]
         C_out = Wt.shape[0]
-        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training)
+        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training, bf16=bf16)
         hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
         dev = x.device
         y = torch.empty((N, C_out, desc.T_out, V), device=dev, dtype=torch.float32)
@@ -142,6 +143,7 @@ class StgcnBlockFn(torch.autograd.Function):
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
+        ctx.bf16 = bf16
         ctx.cc = cc
         ctx.drop = (drop, seed)
         return y
@@ -155,7 +157,7 @@ class StgcnBlockFn(torch.autograd.Function):
         dy = dy.contiguous()
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
-                         need_dx=need_dx)
+                         need_dx=need_dx, bf16=ctx.bf16)
         dy_sums, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], x.device)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
@@ -173,7 +175,7 @@ class StgcnBlockFn(torch.autograd.Function):
         _chain_publish(ctx.cc, psums, dx)
         dA, dW, dbW, dWt = grads
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-                None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 class StgcnResBlockFn(torch.autograd.Function):
@@ -189,7 +191,7 @@ class StgcnResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training, cc=None, drop=0.0):
+                stride, pad, eps, momentum, training, cc=None, drop=0.0, bf16=False):
         lib = hip_lib.lib()
         x = x.contiguous()
         seed = _dropout_seed(drop, training)
@@ -203,7 +205,8 @@ class StgcnResBlockFn(torch.autograd.Function):
         N, C_in, T, V = x.shape
         K = A.shape[0]
         C_out = Wt.shape[0]
-        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training, residual=True)
+        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training, residual=True,
+                         bf16=bf16)
         hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
         if (Wr is None) != (C_in == C_out and stride == 1):
             raise RuntimeError("residual projection weights must be given iff shapes differ")
@@ -222,6 +225,7 @@ class StgcnResBlockFn(torch.autograd.Function):
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
+        ctx.bf16 = bf16
         ctx.cc = cc
         ctx.drop = (drop, seed)
         return y
@@ -235,7 +239,7 @@ class StgcnResBlockFn(torch.autograd.Function):
         dy = dy.contiguous()
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
-                         need_dx=need_dx, residual=True)
+                         need_dx=need_dx, residual=True, bf16=ctx.bf16)
         dev = x.device
         dx = torch.empty_like(x) if need_dx else None
         dA, dW, dbW, dWt = (torch.empty_like(t) for t in (A, W, bW, Wt))
@@ -254,4 +258,4 @@ class StgcnResBlockFn(torch.autograd.Function):
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         _chain_publish(ctx.cc, psums, dx)
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2, dWr, dbr,
-                None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None)

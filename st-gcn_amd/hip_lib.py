@@ -18,6 +18,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libstgcn_hip.so")
 ABI_VERSION = 2
 F_RESIDUAL = 1  # stgcn_desc_t.flags
+F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 
 _c_int = ctypes.c_int32
 _c_float = ctypes.c_float

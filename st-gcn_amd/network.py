@@ -63,8 +63,14 @@ class SpatialTemporalConv(nn.Module):
     """
 
     def __init__(self, C_in, C_out, A, gamma, temporal_stride, temporal_padding,
-                 dropout_rate=0.5, residual=False):
+                 dropout_rate=0.5, residual=False, gemm_dtype=torch.float32):
         super().__init__()
+        if gemm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("gemm_dtype must be torch.float32 or torch.bfloat16")
+        # (not in the reference) arithmetic of the channel GEMMs: bf16 rounds the
+        # GEMM operands to bf16 on the bf16 matrix cores (fp32 accumulate; tensors,
+        # parameters, A and BatchNorm stay fp32) — BASELINE cfg3 / cfg5
+        self.gemm_dtype = gemm_dtype
         if residual:
             if C_in == C_out and temporal_stride == 1:
                 self.apply_residual = lambda x: x
@@ -101,6 +107,7 @@ class SpatialTemporalConv(nn.Module):
         sc = self.spatialConv
         x = f_in.float()
         drop = self.dropout.p if (self.dropout is not None and training) else 0.0
+        bf16 = getattr(self, "gemm_dtype", torch.float32) == torch.bfloat16
         cc = None
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:
@@ -121,13 +128,13 @@ class SpatialTemporalConv(nn.Module):
                 proj.weight if proj is not None else None,
                 proj.bias if proj is not None else None,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop, bf16)
         else:
             y = StgcnBlockFn.apply(
                 x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
                 self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop, bf16)
         if chain is not None:
             if cc is None:
                 chain.reset()
