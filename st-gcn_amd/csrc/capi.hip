@@ -49,7 +49,7 @@ int wgrad_ft(int V) { return std::max(1, 80 / V); }
 
 // Upper bound of the packed-weight scratch any conv_gemm launch of this block needs.
 size_t wpk_floats(const stgcn_desc_t *d) {
-  const int rows = std::max(d->C_out, d->C_in);
+  const int rows = std::max(d->C_out, d->K * d->C_in);  // (stacked H GEMM: K*C_in rows)
   const int red = std::max(d->C_out, d->K * d->C_in);
   // reduction padded to a whole number of chunks for any chunk size <= 32
   return (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32 + 32) * 9;
@@ -153,6 +153,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
 struct BwdLayout {
   double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
   float *dU, *dZ, *G, *H, *slab, *wpk;
+  float *Wpk;  // W' = [W_0 | ... | W_{K-1}] (C_out, K*C_in) for the stacked H GEMM
   float *Rg;  // residual projection data-grad (N, C_in, T, V)
   size_t dbl_bytes, total;
 };
@@ -184,6 +185,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   }
   L.slab = c.take<float>(slab);
   L.wpk = c.take<float>(wpk_floats(d));
+  L.Wpk = c.take<float>((size_t)R * K * C);
   L.total = c.off;
   return L;
 }
@@ -597,18 +599,25 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s));
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
-  for (int k = 0; k < K; ++k) {
+  {
+    // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
+    // the channels of H_k): dZ is read once instead of K times
+    const float *Wz = a->W;
+    if (K > 1) {
+      HIP_TRY(launch_pack_w(a->W, L.Wpk, K, R, C, s));
+      Wz = L.Wpk;
+    }
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.dZ;
-    p.w = a->W + (int64_t)k * R * C;
-    p.out = L.H + (int64_t)k * C * T * V;
+    p.w = Wz;
+    p.out = L.H;
     p.in_bstride = (int64_t)R * T * V;
     p.out_bstride = (int64_t)K * C * T * V;
     p.w_sr = 1;
-    p.w_sc = C;
+    p.w_sc = (int64_t)K * C;
     p.w_sq = 0;
     p.C = R;
-    p.R = C;
+    p.R = K * C;
     p.NQ = 1;
     p.s_in = 1;
     p.off = 0;

@@ -2176,6 +2176,319 @@ static bool launch_bwd5(const float *H, const float *x, const float *mean, const
   return true;
 }
 
+// k_spatial_bwd6: k_spatial_bwd5 for joint counts above 32 (two 32-column
+// output tiles, V = 50: the two-person graph) with up to 3 partitions, where
+// bwd5's register-resident B operand (all column tiles) and LDS dA accumulator
+// do not fit. RB = 64 rows per block (2 row tiles x 2 column tiles of dx =
+// one MFMA tile per wave, so a wave keeps only its column tile of A_k as the B
+// operand: K * V/2 VGPRs), and the K x 2 x 2 dA tiles are dealt to the 4 waves
+// (K tiles each) and stay in registers for the whole persistent loop, flushed
+// once by global atomics. Staging, BN1 sums and the dx store as in bwd5.
+template <int V, int KMAX>
+__global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
+    const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
+    const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
+    const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
+    int K, int64_t rows, int write_dx, int relu) {
+  constexpr int RB = 64;
+  constexpr int VH = (V + 1) / 2;  // MFMA k-steps over v
+  static_assert(V > 32 && V <= 64, "two 32-column tiles");
+  constexpr int MAXSEG = 32;
+  constexpr int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
+  const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
+  float *dxs = smem + 2 * BUF;   // [RB][V]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int CT = C * T;
+  const int nblocks = (int)(rows / RB);
+  const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
+  const int rt = wave & 1, ct = wave >> 1;  // this wave's dx tile
+
+  // B operand of the dx GEMM for column tile ct: A_k[v = 2s + hi][w = 32ct + lo]
+  float Bm[KMAX][VH];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+    for (int s2 = 0; s2 < VH; ++s2) {
+      const int v = 2 * s2 + hi, w = 32 * ct + lo;
+      Bm[k][s2] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
+    }
+
+  auto stage = [&](int blk, float *buf) {
+    const int r0 = blk * RB;
+    const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    constexpr int ND = PL / 256;
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + (int64_t)r0 * V, (int64_t)RB * V);
+    for (int i = wave; i < ND; i += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + K * PL + i * 256, 16,
+                                               (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+    for (int k = 0; k < K; ++k) {
+      const __amdgpu_buffer_rsrc_t rh =
+          make_rsrc(H + ((int64_t)(n0 * K + k) * CT + rem0) * V, (int64_t)RB * V);
+      for (int i = wave; i < ND; i += 4)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, buf + k * PL + i * 256, 16,
+                                                 (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+    }
+  };
+
+  // dA tiles of this wave: j = wave + 4i (i < KMAX) -> (k = j / 4, p2 = (j / 2) & 1, q2 = j & 1)
+  floatx16 dacc[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dacc[i][e] = 0.f;
+
+  int blk = blockIdx.x;
+  if (blk < nblocks) stage(blk, smem);
+  for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
+    float *buf = smem + (it & 1) * BUF;
+    float *Hs = buf, *xs = buf + K * PL;
+    if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
+    __syncthreads();  // block blk staged (vmcnt(0)); previous block fully retired
+    if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * BUF);
+    const int r0 = blk * RB;
+    const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    const int cfirst = n0 * C + rem0 / T;
+    {  // dx tile (rt, ct)
+      floatx16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {
+          const float *hr = Hs + k * PL + (rt * 32 + lo) * V + hi;
+#pragma unroll
+          for (int s2 = 0; s2 < VH; ++s2) {
+            const float av = (2 * s2 + hi < V) ? hr[2 * s2] : 0.f;
+            acc = mfma32(av, Bm[k][s2], acc);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        const int w = 32 * ct + lo;
+        if (w < V) dxs[row * V + w] = acc[i];
+      }
+    }
+    __syncthreads();  // dx tile complete
+    {  // per row (4 threads each): BN1 sums, BN1(x) in place (see bwd5)
+      constexpr int TPR = 256 / RB;
+      const int rl = tid / TPR, part = tid % TPR;
+      const int rem = rem0 + rl;
+      const int ci = rem / T;
+      const int seg = n0 * C + ci - cfirst;
+      const float mu = mean[ci], is = invstd[ci];
+      const float a = is * g[ci], be = b[ci];
+      float s = 0.f, sn = 0.f;
+#pragma unroll
+      for (int j = 0; j < (V + TPR - 1) / TPR; ++j) {
+        const int w = part + j * TPR;
+        if (w < V) {
+          const float xv = xs[rl * V + w];
+          float d = dxs[rl * V + w];
+          const float bn = (xv - mu) * a + be;
+          if (relu && bn <= 0.f) {
+            d = 0.f;
+            dxs[rl * V + w] = 0.f;
+          }
+          s += d;
+          sn = fmaf(d, (xv - mu) * is, sn);
+          xs[rl * V + w] = relu ? fmaxf(bn, 0.f) : bn;
+        }
+      }
+      const int seg0 = __builtin_amdgcn_readfirstlane(seg);
+      if (__builtin_amdgcn_ballot_w64(seg != seg0) == 0) {
+        const double ws = wave_sum((double)s), wn = wave_sum((double)sn);
+        if (lane == 0) {
+          if (seg_lds) {
+            atomicAdd(&seg_s[seg0], ws);
+            atomicAdd(&seg_n[seg0], wn);
+          } else {
+            atomicAdd(sd + ci, ws);
+            atomicAdd(sdn + ci, wn);
+          }
+        }
+      } else if (seg_lds) {
+        atomicAdd(&seg_s[seg], (double)s);
+        atomicAdd(&seg_n[seg], (double)sn);
+      } else {
+        atomicAdd(sd + ci, (double)s);
+        atomicAdd(sdn + ci, (double)sn);
+      }
+    }
+    __syncthreads();  // BN1(x) rows and segment sums complete
+    if (seg_lds && tid < MAXSEG) {
+      const int gc = cfirst + tid;
+      const int rlast = r0 + RB - 1;
+      const int glast = (rlast / CT) * C + (rlast % CT) / T;
+      if (gc <= glast) {
+        const int cc = gc % C;
+        atomicAdd(sd + cc, seg_s[tid]);
+        atomicAdd(sdn + cc, seg_n[tid]);
+      }
+    }
+    // dA tiles: dA_k[v in p2][w in q2] += sum_rows H_k[row][v] BN1(x)[row][w]
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      const int j = wave + 4 * i;
+      const int k = j >> 2, p2 = (j >> 1) & 1, q2 = j & 1;
+      if (k < K) {
+        const float *hk = Hs + k * PL;
+        const int cv = p2 * 32 + lo, cw = q2 * 32 + lo;
+#pragma unroll 8
+        for (int s2 = 0; s2 < RB / 2; ++s2) {
+          const int rr = 2 * s2 + hi;
+          const float av = cv < V ? hk[rr * V + cv] : 0.f;
+          const float bw = cw < V ? xs[rr * V + cw] : 0.f;
+          dacc[i] = mfma32(av, bw, dacc[i]);
+        }
+      }
+    }
+    if (write_dx) {
+      float *dst = dx + (int64_t)r0 * V;
+      for (int e = tid; e < RB * V / 4; e += 256)
+        *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(dxs + e * 4);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int j = wave + 4 * i;
+    const int k = j >> 2, p2 = (j >> 1) & 1, q2 = j & 1;
+    if (k < K) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int v = p2 * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        const int w = q2 * 32 + lo;
+        if (v < V && w < V) atomicAdd(dA + (k * V + v) * V + w, dacc[i][e]);
+      }
+    }
+  }
+}
+
+template <int V, int KT>
+static bool launch_bwd6(const float *H, const float *x, const float *mean, const float *invstd,
+                        const float *g, const float *b, const float *A, float *dx, float *dA,
+                        double *sd, double *sdn, int C, int T, int K, int64_t rows,
+                        int write_dx, int relu, hipStream_t s) {
+  constexpr int RB = 64;
+  constexpr int PL = (RB * V + 255) / 256 * 256;
+  const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 1) * PL);
+  if (K != KT || lds > 160 * 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31)
+    return false;
+  const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256));
+  hipLaunchKernelGGL((k_spatial_bwd6<V, KT>), grid, dim3(256), lds, s, H, x, mean, invstd, g, b,
+                     A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
+  return true;
+}
+
+// k_gather_mfma: G_k = f(BN1(x)) A_k^T on the fp32 matrix cores (joint counts
+// 25 and 50 with 3 partitions, where k_gather4's one-row-per-thread VALU
+// contraction is the slow part). Persistent, x row blocks double-buffered by
+// LDS-DMA; block = RB = 128 / NT rows = 4 MFMA tiles (32 rows x one 32-joint
+// column tile), one per wave. A-operand: f(BN1(x))[row][w] computed once per
+// block from the staged rows (per-lane row constants); B-operand: the wave's
+// column tile of A_k^T (B[w][v] = A_k[v][w]) resident in VGPRs. The K output
+// tiles leave through LDS as float4 stores (each partition's block of G is
+// contiguous).
+template <int V, int KMAX>
+__global__ __launch_bounds__(256, 2) void k_gather_mfma(
+    const float *__restrict__ x, const float *__restrict__ mean, const float *__restrict__ invstd,
+    const float *__restrict__ g, const float *__restrict__ b, const float *__restrict__ A,
+    float *G, int C, int T, int K, int64_t rows, int relu) {
+  constexpr int NT = (V + 31) / 32;
+  constexpr int RB = 128 / NT;
+  constexpr int NRT = RB / 32;
+  constexpr int VH = (V + 1) / 2;
+  constexpr int PL = (RB * V + 255) / 256 * 256;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *obuf = smem + 2 * PL;  // [K][PL]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int CT = C * T;
+  const int nblocks = (int)(rows / RB);
+  const int rt = wave % NRT, ct = wave / NRT;
+  float Bm[KMAX][VH];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+    for (int s2 = 0; s2 < VH; ++s2) {
+      const int w = 2 * s2 + hi, v = 32 * ct + lo;
+      Bm[k][s2] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
+    }
+  auto stage = [&](int blk, float *buf) {
+    constexpr int ND = PL / 256;
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + (int64_t)blk * RB * V, (int64_t)RB * V);
+    for (int i = wave; i < ND; i += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + i * 256, 16,
+                                               (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
+  };
+  int blk = blockIdx.x;
+  if (blk < nblocks) stage(blk, smem);
+  for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
+    const float *xs = smem + (it & 1) * PL;
+    __syncthreads();  // block staged; previous block's stores done with obuf
+    if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * PL);
+    const int r0 = blk * RB;
+    const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
+    const int row = rt * 32 + lo;
+    const int ci = (rem0 + row) / T;
+    const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
+    float fv[VH];
+#pragma unroll
+    for (int s2 = 0; s2 < VH; ++s2) {
+      const int w = 2 * s2 + hi;
+      const float t = w < V ? (xs[row * V + w] - mu) * a + be : 0.f;
+      fv[s2] = w < V ? (relu ? fmaxf(t, 0.f) : t) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        floatx16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < VH; ++s2) acc = mfma32(fv[s2], Bm[k][s2], acc);
+        float *ok = obuf + k * PL;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int v = 32 * ct + lo;
+          if (v < V) ok[r * V + v] = acc[i];
+        }
+      }
+    }
+    __syncthreads();  // output tiles complete
+    for (int k = 0; k < K; ++k) {
+      float *dst = G + ((int64_t)(n0 * K + k) * CT + rem0) * V;
+      const float *src = obuf + k * PL;
+      for (int e = tid; e < RB * V / 4; e += 256)
+        *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(src + e * 4);
+    }
+  }
+}
+
+template <int V, int KT>
+static bool launch_gather_mfma(const float *x, const float *mean, const float *invstd,
+                               const float *g, const float *b, const float *A, float *G, int C,
+                               int T, int K, int64_t rows, int relu, hipStream_t s) {
+  constexpr int NT = (V + 31) / 32;
+  constexpr int RB = 128 / NT;
+  constexpr int PL = (RB * V + 255) / 256 * 256;
+  if (K != KT || ((int64_t)C * T) % RB != 0 || (RB * V) % 4 != 0 || rows >= (int64_t)1 << 31)
+    return false;
+  const size_t lds = sizeof(float) * (size_t)(2 + K) * PL;
+  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / (lds + 512))));
+  const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
+  hipLaunchKernelGGL((k_gather_mfma<V, KT>), grid, dim3(256), lds, s, x, mean, invstd, g, b, A, G,
+                     C, T, K, rows, relu);
+  return true;
+}
+
 static int bwd3_rows(int V, int K) {
   // rows per block: 256 when the per-row LDS footprint is small, else 64
   const int VP = (V + 3) & ~3;
@@ -2188,6 +2501,16 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, int relu, hipStream_t s) {
   static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
+  if (!joint3 && K > 1 && (V == 25 || V == 50) && ((uintptr_t)x & 15) == 0 &&
+      ((uintptr_t)G & 15) == 0) {  // partitioned graphs: contraction on MFMA
+    const int64_t rows = (int64_t)N * C * T;
+    const bool done =
+        V == 25 ? (launch_gather_mfma<25, 2>(x, mean, invstd, g, b, A, G, C, T, K, rows, relu, s) ||
+                   launch_gather_mfma<25, 3>(x, mean, invstd, g, b, A, G, C, T, K, rows, relu, s))
+                : (launch_gather_mfma<50, 2>(x, mean, invstd, g, b, A, G, C, T, K, rows, relu, s) ||
+                   launch_gather_mfma<50, 3>(x, mean, invstd, g, b, A, G, C, T, K, rows, relu, s));
+    if (done) return hipGetLastError();
+  }
   const size_t lds4 = sizeof(float) * ((size_t)2 * 256 * V + (size_t)K * V * ((V + 3) & ~3));
   if (!joint3 && joint_fast(V) && ((int64_t)C * T) % 256 == 0 && ((uintptr_t)x & 15) == 0 &&
       ((uintptr_t)G & 15) == 0 && lds4 <= 160 * 1024) {
@@ -2421,6 +2744,15 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
     else if (V == 50)
       done = STGCN_BWD5(50, 64, 1) || STGCN_BWD5(50, 64, 2) || STGCN_BWD5(50, 64, 3);
 #undef STGCN_BWD5
+    if (done) return hipGetLastError();
+  }
+  if (!joint3 && aligned && V == 50 && K <= 3) {  // two-person graph, 2 or 3 partitions
+    const int64_t rows = (int64_t)N * C * T;
+    bool done = false;
+#define STGCN_BWD6(KK) \
+  launch_bwd6<50, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, s)
+    done = STGCN_BWD6(1) || STGCN_BWD6(2) || STGCN_BWD6(3);
+#undef STGCN_BWD6
     if (done) return hipGetLastError();
   }
   if (joint_fast(V) && K <= 3) {
