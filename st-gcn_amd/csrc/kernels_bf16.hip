@@ -519,6 +519,132 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
     run(std::integral_constant<int, (NTMAX > 1 ? NTMAX - 1 : 1)>{});
 }
 
+// ---------------------------------------------------------------------------
+// k_wgrad_gemm_bf16: the NQ = 1, stride-1 weight gradient (the spatial
+// dW' = dZ G^T) as a plain split-K GEMM over the contiguous (t, v) positions of
+// each clip row: slab[split][r][c] = sum_{items} sum_{l in chunk} P[n][r][l] Q[n][c][l].
+// A bandwidth-bound GEMM (every P row is re-read by C/TC column tiles, every Q
+// row by R/TR row tiles): big tiles (TR x TC = 128 x 256, 8 waves of 64 x 64)
+// for reuse, operands staged in fp32 by LDS-DMA straight from HBM (no staging
+// registers, coalesced rows; 16-byte pieces when rows are 16-byte aligned),
+// rounded to bf16 when the MFMA fragments are read (2 x ds_read_b128 + 4
+// v_cvt_pk_bf16_f32 per fragment). Item = (clip, KC = 32 positions);
+// double-buffered; the WGs of one split are adjacent in the (XCD-remapped)
+// grid so they share the split's chunks in L2.
+// ---------------------------------------------------------------------------
+template <int TR, int TC>
+struct WgGemmGeo {
+  static constexpr int KC = 32, PITCH = KC + 4;  // floats (PITCH/4 odd: b128 conflict-free)
+  static constexpr int PSZ = TR * PITCH, QSZ = TC * PITCH, BUF = PSZ + QSZ;  // floats
+  static constexpr int NWR = TR / 64, NWC = TC / 64, NW = NWR * NWC;
+  static constexpr int NTH = NW * 64;
+};
+
+template <int TR, int TC, bool X4>
+__global__ __launch_bounds__((WgGemmGeo<TR, TC>::NTH), 1) void k_wgrad_gemm_bf16(WgradParams p) {
+  using G = WgGemmGeo<TR, TC>;
+  constexpr int GF = X4 ? 4 : 1;                              // floats per lane per DMA
+  constexpr int ROUNDS = (G::BUF / GF + G::NTH - 1) / G::NTH;  // DMA rounds per wave
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = p.n_rtiles * p.n_jtiles;
+  const int tile = bid % ntiles;
+  const int split = bid / ntiles;
+  const int ct = tile % p.n_jtiles, rt = tile / p.n_jtiles;
+  const int L = p.M * p.V;
+  const int r0 = rt * TR, c0 = ct * TC;
+  const int prow_lim = min(TR, p.R - r0), qrow_lim = min(TC, p.C - c0);
+  const int total = p.N * p.n_mtiles;
+  const int per = (total + p.S - 1) / p.S;
+  const int it0 = split * per, it1 = min(total, it0 + per);
+
+  // DMA round i of this wave fills image floats [((i*NW + wave)*64 + lane)*GF, +GF);
+  // the image is P rows [0, TR) then Q rows, PITCH floats each
+  int goff[ROUNDS], gcol[ROUNDS];
+#pragma unroll
+  for (int i = 0; i < ROUNDS; ++i) {
+    const int pos = ((i * G::NW + wave) * 64 + lane) * GF;
+    const int row = pos / G::PITCH, col = pos - row * G::PITCH;
+    const bool isq = row >= TR;
+    const int rr = isq ? row - TR : row;
+    gcol[i] = col;
+    goff[i] = (pos < G::BUF && col < G::KC && rr < (isq ? qrow_lim : prow_lim)) ? rr * L + col : -1;
+  }
+  auto stage = [&](int it, float *buf) {
+    const int n = it / p.n_mtiles, kc = it - n * p.n_mtiles;
+    const int l0 = kc * G::KC, lrem = L - l0;
+    const __amdgpu_buffer_rsrc_t rs_p = make_rsrc(
+        p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * L + l0, (int64_t)prow_lim * L - l0);
+    const __amdgpu_buffer_rsrc_t rs_q = make_rsrc(
+        p.Q + (int64_t)n * p.q_bstride + (int64_t)c0 * L + l0, (int64_t)qrow_lim * L - l0);
+#pragma unroll
+    for (int i = 0; i < ROUNDS; ++i) {
+      const int base = (i * G::NW + wave) * 64 * GF;  // wave-uniform
+      if (base < G::BUF) {
+        const bool isq = base >= G::PSZ;  // rounds never straddle P and Q (PSZ % (64*GF) == 0)
+        const bool ok = goff[i] >= 0 && gcol[i] < lrem;
+        const unsigned voff = ok ? (unsigned)goff[i] * 4u : kOOB;
+        if constexpr (X4)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(isq ? rs_q : rs_p, buf + base, 16, voff, 0, 0, 0);
+        else
+          blds_f32(isq ? rs_q : rs_p, voff, buf + base);
+      }
+    }
+  };
+  const int wr = wave / G::NWC, wc = wave % G::NWC;  // this wave's 64 x 64 sub-tile
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  auto frag = [&](const float *src) {  // 8 consecutive fp32 -> bf16x8
+    bf16x8 f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) f[u] = (__bf16)src[u];
+    return f;
+  };
+  float *buf0 = smem, *buf1 = smem + G::BUF;
+  if (it0 < it1) stage(it0, buf0);
+  __syncthreads();
+  for (int it = it0; it < it1; ++it) {
+    const bool odd = (it - it0) & 1;
+    const float *cur = odd ? buf1 : buf0;
+    if (it + 1 < it1) stage(it + 1, odd ? buf0 : buf1);
+    const float *pa = cur + (wr * 64 + lo) * G::PITCH + 8 * hi;
+    const float *qb = cur + G::PSZ + (wc * 64 + lo) * G::PITCH + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < G::KC / 16; ++s) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = frag(pa + i * 32 * G::PITCH + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = frag(qb + j * 32 * G::PITCH + 16 * s);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf16(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();  // retires this wave's LDS-DMA and publishes the next chunk
+  }
+  float *slab = p.slab + (int64_t)split * p.R * p.C;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c0 + wc * 64 + j * 32 + lo;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = r0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        if (r < p.R && c < p.C) slab[(int64_t)r * p.C + c] = acc[i][j][e];
+      }
+    }
+}
+
 // Tile plans (FT, CB) per (NQ, V, SIN): double-buffered images within 160 KiB.
 struct WgBf16Plan {
   int FT, CB;
@@ -542,6 +668,19 @@ static bool wgrad_bf16_plan(const WgradParams &w, WgBf16Plan &pl) {
 }
 
 bool plan_wgrad_bf16(WgradParams &w) {
+  if (w.NQ == 1 && w.s_in == 1 && w.off == 0 && w.M == w.T_src) {
+    // plain split-K GEMM over contiguous positions (k_wgrad_gemm_bf16); FT = 0
+    // marks the plan, CT = rows per tile (128 | 64), columns per tile 256
+    w.FT = 0;
+    w.CT = w.R > 64 ? 128 : 64;
+    w.n_mtiles = (w.M * w.V + 31) / 32;
+    w.n_rtiles = (w.R + w.CT - 1) / w.CT;
+    w.n_jtiles = (w.C + 255) / 256;
+    const int tiles = w.n_rtiles * w.n_jtiles;
+    w.S = std::max(1, std::min((256 + tiles - 1) / tiles, w.N * w.n_mtiles));
+    w.bf16 = 1;
+    return true;
+  }
   WgBf16Plan pl;
   if (!wgrad_bf16_plan(w, pl)) return false;
   w.FT = pl.FT;
@@ -565,8 +704,27 @@ static bool launch_wb_if(const WgradParams &p, hipStream_t s) {
   return true;
 }
 
+template <int TR, bool X4>
+static void launch_wgg(const WgradParams &p, int nblk, hipStream_t s) {
+  using G = WgGemmGeo<TR, 256>;
+  hipLaunchKernelGGL((k_wgrad_gemm_bf16<TR, 256, X4>), dim3(nblk), dim3(G::NTH),
+                     2 * G::BUF * sizeof(float), s, p);
+}
+
 hipError_t launch_wgrad_bf16(const WgradParams &p, hipStream_t s) {
   if (!p.bf16) return hipErrorInvalidValue;
+  if (p.NQ == 1 && p.FT == 0) {
+    const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+    const int64_t L = (int64_t)p.M * p.V;
+    const bool x4 = L % 4 == 0 && p.p_bstride % 4 == 0 && p.q_bstride % 4 == 0 &&
+                    ((uintptr_t)p.P & 15) == 0 && ((uintptr_t)p.Q & 15) == 0;
+    if (p.CT == 128) {
+      if (x4) launch_wgg<128, true>(p, nblk, s); else launch_wgg<128, false>(p, nblk, s);
+    } else {
+      if (x4) launch_wgg<64, true>(p, nblk, s); else launch_wgg<64, false>(p, nblk, s);
+    }
+    return hipGetLastError();
+  }
   bool done = false;
   if (p.NQ == 9) {
     done = launch_wb_if<9, 18, 1, 8, 64>(p, s) || launch_wb_if<9, 18, 2, 8, 64>(p, s) ||
