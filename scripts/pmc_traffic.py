@@ -51,7 +51,10 @@ def main(src, dst):
                              "launches": len(cs["FETCH_SIZE"])}
     stats = [k for k in out["raw_kib"] if k.startswith("k_bn_stats")]
     if stats:
-        alg = sum(128 * c * t * 18 * 4 for c, t in LAYER_IN) / len(LAYER_IN)
+        # with stack chaining only block 0 runs its own BN1 statistics pass
+        # (the other blocks take them from the previous block's output pass):
+        # one launch per step reading the 3-channel input once
+        alg = 128 * LAYER_IN[0][0] * LAYER_IN[0][1] * 18 * 4
         n = sum(out["raw_kib"][k]["launches"] for k in stats)
         fs = sum(out["raw_kib"][k]["FETCH_SIZE"] * out["raw_kib"][k]["launches"] for k in stats) * 1024 / n
         out["calibration_k_bn_stats"] = {
