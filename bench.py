@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[1]): Kinetics-skeleton
 shape, synthetic input (N, 3, 300, 18) NCTV per GPU with N=128, V=18, uni
 labelling (K=1), 400 classes, fp32. One step = forward of the 10-block stack
-(fused HIP blocks) + avg-pool/FC head + cross-entropy + backward + (N>1) RCCL
-gradient all-reduce + Adam update. Inputs are resident in HBM before timing.
+(fused HIP blocks) + avg-pool/FC head + cross-entropy (fused HIP head) +
+backward + (N>1) RCCL gradient all-reduce + Adam update (FusedAdam: one HIP
+launch; --torch-ops for torch's head / loss / Adam). Inputs are resident in HBM before timing.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
      (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
@@ -200,6 +201,8 @@ def main():
                     help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--torch-ops", action="store_true",
+                    help="head + cross entropy + Adam from torch instead of the HIP library")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,7 +217,9 @@ def main():
 
     model = build_model(pkg, cfg, device)
     params = [p for p in model.parameters()]
-    opt = torch.optim.Adam(params, lr=1e-3)
+    # FusedAdam: torch.optim.Adam semantics, one libstgcn_hip launch per step
+    opt = (torch.optim.Adam(params, lr=1e-3) if args.torch_ops
+           else pkg.FusedAdam(params, lr=1e-3))
     dp = pkg.dp.GradAllReduce(model, world) if world > 1 else None
     gen = torch.Generator(device="cpu").manual_seed(1 + rank)
     x = torch.randn(cfg["N"], cfg["C"], cfg["T"], cfg["V"], generator=gen).to(device)
@@ -222,8 +227,10 @@ def main():
 
     def step():
         opt.zero_grad(set_to_none=True)
-        logits = model.forward_nctv(x)
-        loss = torch.nn.functional.cross_entropy(logits, labels)
+        if args.torch_ops:
+            loss = torch.nn.functional.cross_entropy(model.forward_nctv(x), labels)
+        else:  # fused HIP head: avg-pool + Linear + cross entropy
+            loss, _ = model.forward_loss(x, labels)
         loss.backward()
         if dp is not None:
             dp.synchronize()

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 2
+#define STGCN_ABI_VERSION 3
 
 /* stgcn_desc_t.flags */
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
@@ -159,6 +159,52 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a,
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which);
 int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t scratch_bytes,
                       int iters, void *stream, float *avg_ms, double *flops);
+
+/* ---------------------------------------------------------------------------
+ * ABI 3: training-step ops around the stack.
+ *
+ * Classification head: global average pool over (T, V) + Linear + cross
+ * entropy (lightning_model.py:105-107 avg_pool2d + fc_layer, :202
+ * F.cross_entropy with mean reduction). y is the last block's output
+ * (N, C, L = T*V); W (classes, C), bias (classes), labels int64 (N).
+ * stgcn_head_fwd writes pooled (N, C), logits (N, classes), lossv (N, per-clip
+ * loss) and loss (1, the mean). stgcn_head_bwd takes dloss (1) and writes
+ * dlogits (N, classes, scratch), dpooled (N, C, scratch), dy (N, C, L: the
+ * gradient of y), dW, dbias. Deterministic (no atomics).
+ */
+typedef struct stgcn_head_desc {
+  int32_t N, C, L, classes;
+} stgcn_head_desc_t;
+
+int stgcn_head_fwd(const stgcn_head_desc_t *d, const float *y, const float *W, const float *bias,
+                   const int64_t *labels, float *pooled, float *logits, float *lossv, float *loss,
+                   void *stream);
+int stgcn_head_bwd(const stgcn_head_desc_t *d, const float *pooled, const float *logits,
+                   const float *W, const int64_t *labels, const float *dloss, float *dlogits,
+                   float *dpooled, float *dy, float *dW, float *dbias, void *stream);
+
+/* Multi-tensor Adam (torch.optim.Adam, amsgrad=False, maximize=False;
+ * lightning_model.py:196-197): ONE launch updates every tensor of a table.
+ * stgcn_adam_build_table fills a HOST buffer (stgcn_adam_table_bytes; pinned
+ * memory, so the caller can copy it to the device asynchronously) with the
+ * tensor list and its chunk prefix sums and returns the chunk count;
+ * stgcn_adam_step reads the DEVICE copy, with the 1-based step count; the
+ * hyper-parameters are doubles (Python floats): 1 - beta and the bias
+ * corrections are formed in double and rounded to float, as torch does. */
+typedef struct stgcn_adam_tensor {
+  float *param;
+  const float *grad;
+  float *exp_avg;
+  float *exp_avg_sq;
+  int64_t numel;
+} stgcn_adam_tensor_t;
+
+size_t stgcn_adam_table_bytes(int ntensors);
+int stgcn_adam_build_table(const stgcn_adam_tensor_t *tensors, int ntensors, void *host_table,
+                           size_t table_bytes, int64_t *total_chunks);
+int stgcn_adam_step(const void *dev_table, int ntensors, int64_t total_chunks, double lr,
+                    double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                    void *stream);
 
 #ifdef __cplusplus
 }

@@ -33,6 +33,14 @@ int fail(int code, const std::string &msg) {
   return code;
 }
 
+}  // namespace
+
+namespace stgcn {
+void set_last_error(const std::string &msg) { g_err = msg; }
+}  // namespace stgcn
+
+namespace {
+
 #define HIP_TRY(expr)                                                                      \
   do {                                                                                     \
     hipError_t e_ = (expr);                                                                \

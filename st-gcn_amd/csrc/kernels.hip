@@ -249,7 +249,10 @@ struct ConvGeo {
   static constexpr int BUF = WBUF + IBUF;               // floats per ring slot
   // ring depth: 3 slots for the temporal taps (chunk compute ~ DMA latency),
   // 2 for the short spatial chunks (measured)
-  static constexpr int STAGES = NQ == 1 ? 2 : 3;
+#ifndef STGCN_STAGES1
+#define STGCN_STAGES1 2
+#endif
+  static constexpr int STAGES = NQ == 1 ? STGCN_STAGES1 : 3;
   static_assert((STAGES - 2) * DPW < 64, "vmcnt range");
 };
 
@@ -399,9 +402,12 @@ static bool tconv_specialised(const ConvGemmParams &p) {
 // Channels per reduction chunk. Specialised kernels: 8 for the spatial GEMM
 // (2-slot ring), 2 for the temporal taps (3-slot ring, 27 KB of LDS: 4
 // workgroups per CU); measured against 16/32 and 4/6/8 (scripts/ck_sweep.sh).
+#ifndef STGCN_CK1
+#define STGCN_CK1 8
+#endif
 static int conv_ck(const ConvGemmParams &p) {
   if (!tconv_specialised(p)) return p.NQ == 1 ? 32 : 8;
-  return p.NQ == 1 ? 8 : 2;
+  return p.NQ == 1 ? STGCN_CK1 : 2;
 }
 
 int conv_gemm_cpad(const ConvGemmParams &p) {
@@ -422,7 +428,7 @@ size_t conv_gemm_lds_bytes(const ConvGemmParams &p) {
     const int WROWS = (CK * p.NQ * 64 + 255) / 256;
     const int IROWS = round64(CK * (conv_gemm_span(p) | 1)) / 64;
     const int DPW = (WROWS + IROWS + 3) / 4;
-    const int stages = p.NQ == 1 ? 2 : 3;
+    const int stages = p.NQ == 1 ? STGCN_STAGES1 : 3;
     return sizeof(float) * stages * ((size_t)WROWS * 256 + (size_t)(4 * DPW - WROWS) * 64);
   }
   const size_t stats = sizeof(double) * 4 * 16 * 2 * 64;  // k_conv_gemm epilogue buffer
@@ -457,7 +463,7 @@ template <int NQ>
 static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t lds,
                             hipStream_t s) {
   if constexpr (NQ == 1) {
-    if (CK == 8) return launch_tconv_v<NQ, 8>(p, nblk, lds, s);
+    if (CK == STGCN_CK1) return launch_tconv_v<NQ, STGCN_CK1>(p, nblk, lds, s);
   } else {
     if (CK == 2) return launch_tconv_v<NQ, 2>(p, nblk, lds, s);
   }

@@ -16,7 +16,9 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libstgcn_hip.so")
-ABI_VERSION = 2
+if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in-tree only
+    LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
+ABI_VERSION = 3
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 
@@ -53,11 +55,21 @@ class BwdArgs(ctypes.Structure):
     ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)]  # ABI 2: fused dropout
 
 
+class HeadDesc(ctypes.Structure):  # ABI 3
+    _fields_ = [("N", _c_int), ("C", _c_int), ("L", _c_int), ("classes", _c_int)]
+
+
+class AdamTensor(ctypes.Structure):  # ABI 3
+    _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp),
+                ("numel", ctypes.c_int64)]
+
+
 # Every symbol include/stgcn_hip.h declares (checked by tests/test_capi.py).
 EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_fwd_workspace_bytes", "stgcn_bwd_workspace_bytes",
             "stgcn_block_fwd", "stgcn_block_bwd", "stgcn_time_kernel_bytes",
-            "stgcn_time_kernel")
+            "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
+            "stgcn_adam_build_table", "stgcn_adam_step")
 
 _LIB = None
 
@@ -88,6 +100,18 @@ def load_library(path=LIB_PATH):
                                       ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_float),
                                       ctypes.POINTER(ctypes.c_double)]
     lib.stgcn_time_kernel.restype = ctypes.c_int
+    lib.stgcn_head_fwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 8 + [_vp]
+    lib.stgcn_head_fwd.restype = ctypes.c_int
+    lib.stgcn_head_bwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 10 + [_vp]
+    lib.stgcn_head_bwd.restype = ctypes.c_int
+    lib.stgcn_adam_table_bytes.argtypes = [ctypes.c_int]
+    lib.stgcn_adam_table_bytes.restype = ctypes.c_size_t
+    lib.stgcn_adam_build_table.argtypes = [ctypes.POINTER(AdamTensor), ctypes.c_int, _vp,
+                                           ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]
+    lib.stgcn_adam_build_table.restype = ctypes.c_int
+    lib.stgcn_adam_step.argtypes = [_vp, ctypes.c_int, ctypes.c_int64] + \
+        [ctypes.c_double] * 5 + [ctypes.c_int64, _vp]
+    lib.stgcn_adam_step.restype = ctypes.c_int
     if lib.stgcn_abi_version() != ABI_VERSION:
         raise RuntimeError("libstgcn_hip.so ABI version mismatch; rebuild it")
     return lib

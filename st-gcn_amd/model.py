@@ -8,6 +8,7 @@ import torch
 import torch.nn as nn
 
 from .network import SpatialTemporalConv, StackChain
+from .train_ops import StgcnHeadFn
 
 # (C_out, temporal stride) per block, lightning_model.py:65-86.
 LAYERS = [(64, 1), (64, 1), (64, 1), (64, 1), (128, 2), (128, 1), (128, 1),
@@ -44,6 +45,16 @@ class STGCNStack(nn.Module):
     def forward(self, x):
         """x: (N, T, V, C_in) as in L_STGCN.forward (lightning_model.py:101)."""
         return self.forward_nctv(x.permute(0, 3, 1, 2))
+
+    def forward_loss(self, x, labels):
+        """Training step's forward with the fused HIP head: x (N, C_in, T, V)
+        NCTV, labels int64 (N) -> (mean cross-entropy loss, logits); the same
+        arithmetic as F.cross_entropy(self.forward_nctv(x), labels)
+        (lightning_model.py:105-107, :202)."""
+        chain = StackChain() if self.training else None
+        for blk in self.conv:
+            x = blk(x, chain=chain)
+        return StgcnHeadFn.apply(x, self.fc_layer.weight, self.fc_layer.bias, labels)
 
 
 def flops_per_clip(C_in, T, V, K, nr_classes, gamma=9):

@@ -1,0 +1,139 @@
+"""The training-step ops around the block stack on the HIP library (SURVEY.md
+§8(f) row 1): the classification head (global average pool over (T, V) +
+Linear + cross entropy; lightning_model.py:105-107 and the loss of
+training_step :202) as one autograd Function, and ``FusedAdam``, a drop-in for
+``torch.optim.Adam`` (lightning_model.py:196-197) whose step is ONE kernel
+launch over every parameter (same hyper-parameters, same per-parameter state
+names ``step`` / ``exp_avg`` / ``exp_avg_sq``, so state_dicts interchange).
+No CPU fallback: both raise without the HIP library / a GPU.
+"""
+import ctypes
+
+import torch
+
+from . import hip_lib
+
+
+def _check_f32(t, name):
+    if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+        raise RuntimeError(f"{name}: expected a contiguous float32 GPU tensor")
+
+
+class StgcnHeadFn(torch.autograd.Function):
+    """forward(y (N,C,T,V), W (classes,C), b (classes), labels int64 (N)) ->
+    (loss (scalar, mean cross entropy), logits (N, classes), non-differentiable).
+    Same arithmetic as ``F.cross_entropy(fc_layer(avg_pool2d(y, (T,V)).view(N,C)), labels)``."""
+
+    @staticmethod
+    def forward(ctx, y, W, b, labels):
+        lib = hip_lib.lib()
+        y = y.contiguous()
+        for t, n in ((y, "y"), (W, "W"), (b, "b")):
+            _check_f32(t, n)
+        if labels.dtype != torch.int64 or not labels.is_cuda:
+            raise RuntimeError("labels: expected an int64 GPU tensor")
+        labels = labels.contiguous()
+        N, C = y.shape[0], y.shape[1]
+        L = y[0, 0].numel()
+        classes = W.shape[0]
+        if W.shape[1] != C or b.shape[0] != classes or labels.shape[0] != N:
+            raise RuntimeError("head: shape mismatch between y, W, b and labels")
+        d = hip_lib.HeadDesc(N, C, L, classes)
+        dev = y.device
+        pooled = torch.empty((N, C), device=dev, dtype=torch.float32)
+        logits = torch.empty((N, classes), device=dev, dtype=torch.float32)
+        lossv = torch.empty(N, device=dev, dtype=torch.float32)
+        loss = torch.empty((), device=dev, dtype=torch.float32)
+        hip_lib.check(lib.stgcn_head_fwd(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
+            y, W, b, labels, pooled, logits, lossv, loss)], hip_lib.stream_handle(dev)))
+        ctx.save_for_backward(pooled, logits, W, labels)
+        ctx.shape = y.shape
+        ctx.mark_non_differentiable(logits)
+        return loss, logits
+
+    @staticmethod
+    def backward(ctx, dloss, _dlogits):
+        lib = hip_lib.lib()
+        pooled, logits, W, labels = ctx.saved_tensors
+        N, C = pooled.shape
+        classes = W.shape[0]
+        dev = pooled.device
+        L = 1
+        for s in ctx.shape[2:]:
+            L *= s
+        d = hip_lib.HeadDesc(N, C, L, classes)
+        dloss = dloss.reshape(1).float().contiguous()
+        dlogits = torch.empty((N, classes), device=dev, dtype=torch.float32)
+        dpooled = torch.empty((N, C), device=dev, dtype=torch.float32)
+        dy = torch.empty(ctx.shape, device=dev, dtype=torch.float32)
+        dW = torch.empty_like(W)
+        db = torch.empty(classes, device=dev, dtype=torch.float32)
+        hip_lib.check(lib.stgcn_head_bwd(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
+            pooled, logits, W, labels, dloss, dlogits, dpooled, dy, dW, db)],
+            hip_lib.stream_handle(dev)))
+        return dy, dW, db, None
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, maximize=False, fp32 parameters on one
+    device) with the update as one libstgcn_hip launch per step. The tensor
+    table (pointers of param / grad / exp_avg / exp_avg_sq) is rebuilt on the
+    host only when a pointer changed (e.g. grads re-allocated after
+    zero_grad(set_to_none=True)) and copied to the device asynchronously from
+    pinned memory."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
+                 amsgrad=False):
+        if amsgrad:
+            raise NotImplementedError("FusedAdam: amsgrad")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._key = None
+        self._dev_table = None
+        self._chunks = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = hip_lib.lib()
+        for group in self.param_groups:
+            plist = [p for p in group["params"] if p.grad is not None]
+            if not plist:
+                continue
+            for p in plist:
+                _check_f32(p, "param")
+                _check_f32(p.grad, "grad")
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] = st["step"] + 1  # (not in place: loaded state may share it)
+            steps = {int(self.state[p]["step"].item()) for p in plist}
+            if len(steps) != 1:
+                raise RuntimeError("FusedAdam: parameters of a group at different steps")
+            step = steps.pop()
+            tabs = [hip_lib.AdamTensor(p.data_ptr(), p.grad.data_ptr(),
+                                       self.state[p]["exp_avg"].data_ptr(),
+                                       self.state[p]["exp_avg_sq"].data_ptr(), p.numel())
+                    for p in plist]
+            key = tuple((t.param, t.grad, t.exp_avg, t.exp_avg_sq, t.numel) for t in tabs)
+            dev = plist[0].device
+            if key != self._key:
+                n = len(tabs)
+                nbytes = lib.stgcn_adam_table_bytes(n)
+                host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+                chunks = ctypes.c_int64(0)
+                arr = (hip_lib.AdamTensor * n)(*tabs)
+                hip_lib.check(lib.stgcn_adam_build_table(arr, n, ctypes.c_void_p(host.data_ptr()),
+                                                         nbytes, ctypes.byref(chunks)))
+                self._dev_table = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                self._dev_table.copy_(host, non_blocking=True)
+                self._key, self._chunks, self._n = key, chunks.value, n
+            b1, b2 = group["betas"]
+            hip_lib.check(lib.stgcn_adam_step(
+                hip_lib.ptr(self._dev_table), self._n, self._chunks, group["lr"], b1, b2,
+                group["eps"], group["weight_decay"], step, hip_lib.stream_handle(dev)))
+        return loss
