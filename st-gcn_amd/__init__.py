@@ -5,10 +5,10 @@ Drop-in for the reference's ``src/network`` module API
 forward/backward run on hand-written gfx950 HIP kernels behind a C-ABI
 library (``include/stgcn_hip.h``). Import via ``stgcn_loader.load()``.
 """
-from . import graph, hip_lib, fused, network, model, dp, train_ops  # noqa: F401
+from . import graph, hip_lib, fused, network, model, dp, train_ops, data  # noqa: F401
 from .network import SpatialConv, SpatialTemporalConv  # noqa: F401
 from .model import STGCNStack, flops_per_clip  # noqa: F401
 from .train_ops import FusedAdam, StgcnHeadFn  # noqa: F401
 
-__all__ = ["graph", "hip_lib", "fused", "network", "model", "train_ops", "SpatialConv",
+__all__ = ["graph", "hip_lib", "fused", "network", "model", "train_ops", "data", "SpatialConv",
            "SpatialTemporalConv", "STGCNStack", "flops_per_clip", "FusedAdam", "StgcnHeadFn"]

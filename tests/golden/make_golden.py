@@ -18,6 +18,13 @@ Outputs (small .npz files next to this script):
                   running stats after the step.
   stack_cfg1.npz  full L_STGCN (src/lightning_model.py) cfg1 plumbing case:
                   logits, loss, param checksums and sampled grads.
+  data_pipeline.npz  host input pipeline:
+                  src/data/util.py loopy_pad_collate_fn on a ragged batch,
+                  src/data/augmentation.py augment_data under fixed
+                  np.random seeds, src/data/calculate_distances.py on
+                  synthetic (T, 25, 3) .npy clips written to a temp dir.
+
+  --only data     regenerate data_pipeline.npz only.
 """
 import argparse
 import os
@@ -195,14 +202,57 @@ def make_stack_cfg1(lightning_model, adjacency):
     np.savez_compressed(os.path.join(HERE, "stack_cfg1.npz"), **rec)
 
 
+def make_data_pipeline(util, augmentation, calc):
+    rec = {}
+    rng = np.random.default_rng(7)
+    # ragged batch of (1, T_i, 25, 2) clips with int labels (loopy_pad_collate_fn)
+    lens = [5, 9, 3, 9, 1]
+    batch = []
+    for i, t in enumerate(lens):
+        x = rng.standard_normal((1, t, 25, 2))
+        rec[f"collate_in_{i}"] = x
+        batch.append((x, np.array([i % 6])))
+    xx, labels = util.loopy_pad_collate_fn(batch)
+    rec["collate_out_x"] = xx.numpy()
+    rec["collate_out_labels"] = labels.numpy()
+    # augment_data under fixed global-RNG seeds (np.random, as the reference uses)
+    seqs = rng.standard_normal((4, 20, 25, 2)) * 50 + 100
+    rec["augment_in"] = seqs
+    for seed in range(6):
+        np.random.seed(seed)
+        rec[f"augment_out_seed{seed}"] = augmentation.augment_data(seqs)
+    # calculate_distances over synthetic clips (T, 25, 3): x, y, confidence
+    with tempfile.TemporaryDirectory() as d:
+        os.makedirs(os.path.join(d, "data"))
+        names = []
+        for i, t in enumerate((7, 12, 4)):
+            clip = rng.standard_normal((t, 25, 3)) * 30 + 200
+            np.save(os.path.join(d, "data", f"clip{i}.npy"), clip)
+            rec[f"dist_clip{i}"] = clip
+        names = os.listdir(os.path.join(d, "data"))
+        out = os.path.join(d, "distances.npy")
+        calc.calculate_distances(V=25, dataset_dir=os.path.join(d, "data"), output_file=out)
+        rec["dist_out"] = np.load(out)
+        rec["dist_listdir_order"] = np.array([int(n[4]) for n in names])
+    np.savez_compressed(os.path.join(HERE, "data_pipeline.npz"), **rec)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("reference", nargs="?", default="/root/reference")
+    ap.add_argument("--only", choices=["data"], default=None)
     args = ap.parse_args()
     _install_stubs()
     sys.path.insert(0, os.path.join(args.reference, "src"))
     import io
     import contextlib
+    if args.only == "data":
+        sys.path.insert(0, os.path.join(args.reference, "src", "data"))
+        with contextlib.redirect_stdout(io.StringIO()):
+            from data import util, augmentation, calculate_distances  # noqa: E402
+        make_data_pipeline(util, augmentation, calculate_distances)
+        print("wrote data_pipeline.npz to", HERE)
+        return
     with contextlib.redirect_stdout(io.StringIO()):
         from data import adjacency  # noqa: E402
         from network import st_graphconv  # noqa: E402
