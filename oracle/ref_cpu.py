@@ -199,13 +199,14 @@ class Stack:
     def __init__(self, params, buffers, residual=False):
         self.p, self.b, self.residual = params, buffers, residual
 
-    def forward(self, x_ntvc, training=True, dtype=torch.float32):
+    def forward(self, x_ntvc, training=True, dtype=torch.float32, gemm_bf16=False):
         x = x_ntvc.to(dtype).permute(0, 3, 1, 2)
         for i, (_, s) in enumerate(LAYERS):
             pre = f"conv.{i}."
             p = {k[len(pre):]: v for k, v in self.p.items() if k.startswith(pre)}
             b = {k[len(pre):]: v for k, v in self.b.items() if k.startswith(pre)}
-            x = block_forward(x, p, b, s, residual=self.residual, training=training, dtype=dtype)
+            x = block_forward(x, p, b, s, residual=self.residual, training=training, dtype=dtype,
+                              gemm_bf16=gemm_bf16)
             for k, v in b.items():
                 self.b[pre + k] = v
         V = x.shape[3]
