@@ -254,6 +254,21 @@ struct ConvGeo {
 #endif
   static constexpr int STAGES = NQ == 1 ? STGCN_STAGES1 : 3;
   static_assert((STAGES - 2) * DPW < 64, "vmcnt range");
+  // Input stride 2: each channel's window is stored de-interleaved, even
+  // frames first (NFE of them) then odd frames, so output column (mf, v) at
+  // tap q reads position TAPOFF(q) + mf*V + v: consecutive columns hit
+  // consecutive words (the interleaved layout read 2- to 3-way bank conflicts).
+  static constexpr int NF = SPAN / V;                  // window frames
+  static constexpr int NFE = (NF + 1) / 2;             // even frames
+  static __host__ __device__ constexpr int tapoff(int q) {
+    return SIN == 2 ? (q & 1) * NFE * V + (q >> 1) * V : q * V;
+  }
+  // window position (de-interleaved layout) -> frame offset within the window
+  static __host__ __device__ constexpr int src_pos(int o) {
+    return SIN != 2 ? o
+                    : (o < NFE * V ? 2 * (o / V) * V + o % V
+                                   : (2 * ((o - NFE * V) / V) + 1) * V + (o - NFE * V) % V);
+  }
 };
 
 template <int NQ, int CK, int V, int SIN>
@@ -282,7 +297,7 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
   for (int j = 0; j < 4; ++j) {
     const int col = (nj0 + j) * 32 + lo;
     const int mf = col / V;
-    bb[j] = hi * G::SP + (col < G::NCOLS ? SIN * mf * V + (col - mf * V) : 0);
+    bb[j] = hi * G::SP + (col < G::NCOLS ? (SIN == 2 ? col : SIN * mf * V + (col - mf * V)) : 0);
   }
   // DMA slot k of this wave: row d = 4k + wave; d < WROWS: weight row d
   // (16 B/lane), else input row d - WROWS (4 B/lane, byte offset voff[k]
@@ -293,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
     const int d = 4 * k + wave;
     const int e = (d - G::WROWS) * 64 + lane;
     const int c = e / G::SP, o = e - c * G::SP;
-    const int g = g0 + o;
+    const int g = g0 + (o < G::SPAN ? G::src_pos(o) : o);
     const bool ok = d >= G::WROWS && c < CK && o < G::SPAN && g >= 0 && g < cstride;
     voff[k] = ok ? (unsigned)(c * cstride + g) * 4u : kOOB;
   }
@@ -348,7 +363,7 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
     float a[PD + 1], b[PD + 1][4];
     auto ld = [&](int s, int set) {
       const int cp = s / NQ, q = s - cp * NQ;
-      const int bo = 2 * cp * G::SP + q * V;
+      const int bo = 2 * cp * G::SP + G::tapoff(q);
       a[set] = wp[(2 * cp * NQ + q) * 64];
       b[set][0] = ib0[bo];
       b[set][1] = ib1[bo];
@@ -405,9 +420,12 @@ static bool tconv_specialised(const ConvGemmParams &p) {
 #ifndef STGCN_CK1
 #define STGCN_CK1 8
 #endif
+#ifndef STGCN_CK45
+#define STGCN_CK45 2
+#endif
 static int conv_ck(const ConvGemmParams &p) {
   if (!tconv_specialised(p)) return p.NQ == 1 ? 32 : 8;
-  return p.NQ == 1 ? STGCN_CK1 : 2;
+  return p.NQ == 1 ? STGCN_CK1 : (p.NQ == 4 || p.NQ == 5) ? STGCN_CK45 : 2;
 }
 
 int conv_gemm_cpad(const ConvGemmParams &p) {
@@ -464,6 +482,8 @@ static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t ld
                             hipStream_t s) {
   if constexpr (NQ == 1) {
     if (CK == STGCN_CK1) return launch_tconv_v<NQ, STGCN_CK1>(p, nblk, lds, s);
+  } else if constexpr (NQ == 4 || NQ == 5) {
+    if (CK == STGCN_CK45) return launch_tconv_v<NQ, STGCN_CK45>(p, nblk, lds, s);
   } else {
     if (CK == 2) return launch_tconv_v<NQ, 2>(p, nblk, lds, s);
   }
