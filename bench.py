@@ -208,9 +208,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; STGCN_DIST_BACKEND=gloo (with more ranks than GPUs:
+    # ranks share devices round-robin) only rehearses the multi-rank path on a
+    # one-GPU box, the real run is RCCL ("nccl") over xGMI
+    backend = os.environ.get("STGCN_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     pkg = load()
     cfg = dict(CONFIGS[args.config], N=args.batch)
