@@ -44,6 +44,9 @@ CONFIGS = {
 CFG = CONFIGS["cfg2"]
 MFMA_F32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix (= vector) peak
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense (no sparsity)
+# fp32 work on the bf16 matrix cores by exact 3-way operand splits: six bf16
+# MFMAs per fp32 product (kernels_x3.hip), so the fp32-work ceiling is 1/6 of BF16
+X3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0
 
 
@@ -62,7 +65,8 @@ def build_model(pkg, cfg, device):
     import contextlib
     with contextlib.redirect_stdout(io.StringIO()):
         model = pkg.STGCNStack(cfg["C"], cfg["classes"], A,
-                               gemm_dtype=torch.bfloat16 if cfg["bf16"] else torch.float32)
+                               gemm_dtype=torch.bfloat16 if cfg["bf16"] else torch.float32,
+                               f32_gemm=cfg.get("f32_gemm", "mfma"))
     return model.to(device)
 
 
@@ -127,8 +131,9 @@ def kernel_roofline(pkg, device, cfg, iters=10):
         d[key] = (t[0] + ms, t[1] + fl, t[2] + n)
 
     for ci, co, t, s in stack_layers(cfg):
+        x3 = cfg.get("f32_gemm") == "bf16x3" and not cfg["bf16"]
         d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
-                                bf16=cfg["bf16"])
+                                bf16=cfg["bf16"], f32x3=x3)
         for which, kind in KERNEL_KINDS.items():
             nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
             scratch = torch.randn(nbytes // 4 + 1, device=device)
@@ -143,6 +148,10 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 sym = {0: f"k_conv_bf16<9,16,{V},{s}>",
                        1: f"k_conv_bf16<9,16,{V},1>" if s == 1 else f"k_conv_bf16<5|4,16,{V},1>",
                        2: f"k_wgrad_bf16<9,{V},{s}>", 3: f"k_conv_bf16<1,32,{V},1>"}[which]
+            elif x3 and V in (18, 25):
+                sym = {0: f"k_conv_x3<9,3,{V}>" if s == 1 else f"k_tconv<9,2,{V},{s}>",
+                       1: f"k_conv_x3<9,3,{V}>" if s == 1 else f"k_conv_x3<5|4,{V}>",
+                       2: f"k_wgrad_taps<{V},{s}>", 3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
                        1: f"k_tconv<9,2,{V},1>" if s == 1 else f"k_tconv<5|4,2,{V},1>",
@@ -201,6 +210,9 @@ def main():
                     help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3"], default="mfma",
+                    help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma) or "
+                         "as exact 3-way bf16 operand splits (bf16x3; fp32 accuracy)")
     ap.add_argument("--torch-ops", action="store_true",
                     help="head + cross entropy + Adam from torch instead of the HIP library")
     args = ap.parse_args()
@@ -221,7 +233,7 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
     pkg = load()
-    cfg = dict(CONFIGS[args.config], N=args.batch)
+    cfg = dict(CONFIGS[args.config], N=args.batch, f32_gemm=args.f32_gemm)
 
     model = build_model(pkg, cfg, device)
     params = [p for p in model.parameters()]
@@ -277,7 +289,11 @@ def main():
             "data": "synthetic (random N(0,1) skeletons, random labels)",
             "config": {"workload": cfg["desc"],
                        "per_gpu_batch": cfg["N"], "global_batch": cfg["N"] * world,
-                       "seq_len": cfg["T"], "parallelism": f"dp{world}"},
+                       "seq_len": cfg["T"], "parallelism": f"dp{world}",
+                       "channel_gemm": ("bf16 operands, fp32 accumulate" if cfg["bf16"] else
+                                        "fp32: temporal conv fwd/data-grad as exact 3-way bf16 "
+                                        "splits (6 MFMAs, fp32-gated), rest fp32 MFMA"
+                                        if cfg["f32_gemm"] == "bf16x3" else "fp32 MFMA")},
             "model_tflops": round(clips * gf_clip / 1e3, 2),
             "loss": round(float(loss.item()), 5),
         }
@@ -288,7 +304,8 @@ def main():
             ms_tot, fl_tot, nl = symbols[sym]
             ach = fl_tot / (ms_tot * 1e-3) / 1e12
             traffic = traffic_from_profiles(sym)
-            peak = MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else MFMA_F32_PEAK_TFLOPS
+            peak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
+                    X3_PEAK_TFLOPS if sym.startswith("k_conv_x3") else MFMA_F32_PEAK_TFLOPS)
             out["roofline"] = {
                 "kernel": sym, "bound": "mfma", "achieved": round(ach, 2),
                 "peak": peak, "unit": "TFLOP/s",

@@ -55,6 +55,12 @@ extern "C" {
                             * tensors stay fp32, A / BatchNorm stay fp32 (BASELINE cfg3/5).
                             * Applies for V in {18, 25, 50} and reductions over >= 16
                             * channels; other GEMMs run the fp32 kernels. */
+#define STGCN_F_F32X3 4    /* fp32 channel GEMMs on the bf16 matrix cores by exact 3-way
+                            * operand splits (x = h + m + l, six partial products, fp32
+                            * accumulate): fp32-GEMM accuracy at up to 2.67x the fp32
+                            * MFMA rate. Applies to the stride-1 temporal conv forward
+                            * and data-grad for V in {18, 25} over >= 16 channels; other
+                            * GEMMs run the fp32 kernels. Exclusive with STGCN_F_BF16. */
 
 enum {
   STGCN_OK = 0,

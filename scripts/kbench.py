@@ -24,7 +24,8 @@ if os.environ.get("KB_SHAPES"):
     shapes = [shapes[int(i)] for i in os.environ["KB_SHAPES"].split(",")]
 for label, ci, co, T, s in shapes:
     d = pkg.fused.make_desc((128, ci, T, V), co, K, s, 4, 1e-5, 0.1, True,
-                            bf16=os.environ.get("KB_BF16") == "1")
+                            bf16=os.environ.get("KB_BF16") == "1",
+                            f32x3=os.environ.get("KB_X3") == "1")
     row = []
     for which in which_set:
         nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)

@@ -60,13 +60,16 @@ size_t wpk_floats(const stgcn_desc_t *d) {
   const int rows = std::max(d->C_out, d->K * d->C_in);  // (stacked H GEMM: K*C_in rows)
   const int red = std::max(d->C_out, d->K * d->C_in);
   // reduction padded to a whole number of chunks for any chunk size <= 32
-  return (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32 + 32) * 9;
+  const size_t n = (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32 + 32) * 9;
+  // STGCN_F_F32X3: three bf16 planes of the weights (1.5x the fp32 floats)
+  return (d->flags & STGCN_F_F32X3) ? 2 * n : n;
 }
 
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }
 int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
 bool residual(const stgcn_desc_t *d) { return (d->flags & STGCN_F_RESIDUAL) != 0; }
 bool bf16(const stgcn_desc_t *d) { return (d->flags & STGCN_F_BF16) != 0; }
+bool f32x3(const stgcn_desc_t *d) { return (d->flags & STGCN_F_F32X3) != 0; }
 // the fused dropout of a call (training and 0 < p < 1; p >= 1: everything dropped)
 Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
   Dropout dr;
@@ -229,7 +232,7 @@ ConvGemmParams conv_base(const stgcn_desc_t *d, float *wpk) {
   p.V = d->V;
   p.FT = conv_ft(d->V);
   p.N = d->N;
-  p.bf16 = bf16(d);
+  p.bf16 = bf16(d) ? 1 : (f32x3(d) ? 3 : 0);
   return p;
 }
 
@@ -349,8 +352,10 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   if (!d) return fail(STGCN_E_INVALID, "null descriptor");
   if (d->N <= 0 || d->C_in <= 0 || d->C_out <= 0 || d->T <= 0 || d->V <= 0 || d->K <= 0)
     return fail(STGCN_E_INVALID, "non-positive dimension");
-  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16)) != 0)
+  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16 | STGCN_F_F32X3)) != 0)
     return fail(STGCN_E_UNSUPPORTED, "unknown flags");
+  if ((d->flags & STGCN_F_BF16) && (d->flags & STGCN_F_F32X3))
+    return fail(STGCN_E_INVALID, "STGCN_F_BF16 and STGCN_F_F32X3 are exclusive");
   if (d->gamma != 9 || d->pad != 4)
     return fail(STGCN_E_UNSUPPORTED, "only gamma=9, pad=4 (the reference default)");
   if (d->stride != 1 && d->stride != 2) return fail(STGCN_E_UNSUPPORTED, "stride must be 1 or 2");

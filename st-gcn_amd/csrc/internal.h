@@ -55,7 +55,8 @@ struct ConvGemmParams {
   int relu_out;
   Dropout drop;      // applied after relu_out (element index = flat index in out)
   int bf16;          // 1: operands rounded to bf16 on v_mfma_f32_32x32x16_bf16 (fp32
-                     // accumulate, fp32 in/out), where k_conv_bf16 covers the shape
+                     // accumulate, fp32 in/out), where k_conv_bf16 covers the shape;
+                     // 3: fp32 GEMM as exact 3-way bf16 splits (k_conv_x3) where covered
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -81,6 +82,12 @@ hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
 bool conv_bf16_supported(const ConvGemmParams &p);
 size_t conv_bf16_lds_bytes(const ConvGemmParams &p);
 hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s);
+// fp32 via exact bf16 splits (kernels_x3.hip): stride-1 temporal conv forward /
+// data-grad (NQ = 9, 5, 4) for V = 18, 25 over >= 16 channels; launch_conv_gemm
+// dispatches here when p.bf16 == 3 and conv_x3_supported(p).
+bool conv_x3_supported(const ConvGemmParams &p);
+size_t conv_x3_wpk_bytes(const ConvGemmParams &p);
+hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s);
 // Re-plans a weight gradient (NQ = 9 temporal taps or NQ = 1) for k_wgrad_bf16
 // (sets FT, n_mtiles, n_rtiles, n_jtiles, S, bf16 = 1) when the shape is
 // covered; returns false (w unchanged) otherwise. launch_wgrad / launch_wgrad_taps

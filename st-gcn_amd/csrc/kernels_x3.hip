@@ -1,0 +1,420 @@
+// fp32 temporal-conv GEMMs on the bf16 matrix cores by exact operand splitting
+// (STGCN_F_F32X3) — gfx950 only.
+//
+// gfx950 runs fp32 MFMA (v_mfma_f32_32x32x2_f32) at 157 TF/s and bf16 MFMA
+// (v_mfma_f32_32x32x16_bf16) at 2.5 PF/s. Every fp32 value splits EXACTLY into
+// three bf16 (round-to-nearest-even at each step):
+//   h = bf16(x),  m = bf16(x - h),  l = bf16(x - h - m),   x == h + m + l
+// (x - h and x - h - m are exact fp32 differences; the last residual holds at
+// most 7 significant bits, so l is exact). A product then expands into nine
+// bf16 x bf16 products, each exact in the fp32 accumulator's input; the six
+// with weight >= 2^-16 are kept:
+//   a*b ~= ah*bh + ah*bm + am*bh + ah*bl + am*bm + al*bh
+// The three dropped terms (am*bl, al*bm, al*bl) are below 2^-23 |a||b| — the
+// size of one fp32 rounding — so each output carries fp32-GEMM error (fp32
+// accumulation as in v_mfma_f32_32x32x2_f32), and the block is gated at the
+// fp32 tolerance (1e-5 rel-to-max vs fp64). Six bf16 MFMAs
+// (6 x 32 cycles) replace the eight fp32 MFMAs (8 x 64 cycles) of one
+// 32x32x16 step: a 2.67x higher ceiling, 417 TF/s of fp32 work.
+//
+// k_conv_x3<NQ, TG, V>: the ConvGemmParams GEMM (internal.h) for the stride-1
+// temporal conv forward (NQ = 9) and data-gradient (NQ = 9; stride-2 phases
+// NQ = 5 / 4). Tile = 64 rows x FT*V columns as in k_tconv / k_conv_bf16 (same
+// epilogue). Workgroup = 8 waves, two per SIMD: wave w computes rows
+// (w&1)*32..+31 of column tiles ((w>>1)&1)*4 + (w>>2)*2 + {0,1}, with the h*h
+// products and the five small cross terms in separate accumulators. Chunk =
+// 16 channels = one k-step per tap; a chunk runs in NQ/TG steps of TG taps.
+//   Weights: pre-split by k_pack_conv_w_x3 into [chunk][tap group][plane][tap]
+//            [octet][64 rows][8] bf16 (6 KiB per tap), moved per step by
+//            16-byte LDS-DMA, double-buffered.
+//   Window:  [position][plane*2 + octet] 16-byte slots, pitch 7 slots (odd:
+//            ds_read_b128 of 16 consecutive positions is conflict-free),
+//            double-buffered; chunk c+1 is loaded as fp32 dwords (coalesced
+//            along positions) in chunk c's first step, split and written in its
+//            last one. Staging is dealt evenly over the 8 waves (no wave-
+//            dependent branches: they would make the compiler copy and wait).
+// One barrier per step; weights prefetched two steps ahead where LDS allows.
+// LDS: 3 x TG x 6 KiB + 2 x SPAN x 112 B (142.6 KiB at V = 18, NQ = 9): one
+// workgroup per CU, two waves per SIMD.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+#include "internal.h"
+
+#ifndef STGCN_X3_EXP  // timing experiments only (bits skip work; results wrong)
+#define STGCN_X3_EXP 0
+#endif
+
+namespace stgcn {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ floatx16 mfma_x(bf16x8_t a, bf16x8_t b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ __forceinline__ unsigned pk2(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float lo_f(unsigned w) { return __builtin_bit_cast(float, w << 16); }
+__device__ __forceinline__ float hi_f(unsigned w) {
+  return __builtin_bit_cast(float, w & 0xffff0000u);
+}
+
+// exact 3-way split of two floats into packed (h, m, l) bf16 pairs
+__device__ __forceinline__ void split2(float a, float b, unsigned &h, unsigned &m, unsigned &l) {
+  h = pk2(a, b);
+  const float ra = a - lo_f(h), rb = b - hi_f(h);
+  m = pk2(ra, rb);
+  l = pk2(ra - lo_f(m), rb - hi_f(m));
+}
+
+// Waits until at most NA VMEM operations are in flight, naming the 16 window
+// staging registers (so no consumer of them is scheduled above the wait).
+template <int NA>
+__device__ __forceinline__ void wait_img(float (&st)[2][8]) {
+  asm volatile("s_waitcnt vmcnt(%16)"
+               : "+v"(st[0][0]), "+v"(st[0][1]), "+v"(st[0][2]), "+v"(st[0][3]),
+                 "+v"(st[0][4]), "+v"(st[0][5]), "+v"(st[0][6]), "+v"(st[0][7]),
+                 "+v"(st[1][0]), "+v"(st[1][1]), "+v"(st[1][2]), "+v"(st[1][3]),
+                 "+v"(st[1][4]), "+v"(st[1][5]), "+v"(st[1][6]), "+v"(st[1][7])
+               : "n"(NA)
+               : "memory");
+}
+
+template <int NQ, int TG, int V>
+struct ConvX3Geo {
+  static constexpr int CK = 16;                   // channels per chunk (one k-step)
+  static constexpr int FT = kTileCols / V;
+  static constexpr int NCOLS = FT * V;
+  static constexpr int SPAN = (FT - 1 + NQ) * V;  // window positions (stride 1)
+  static constexpr int SLOTS = 7;                 // 6 (plane, octet) slots + 1 pad
+  static constexpr int IMG = SPAN * SLOTS * 16;   // window bytes
+  static constexpr int NG = NQ / TG;              // steps per chunk
+  static constexpr int WST = 3 * TG * 2 * 1024;   // packed weight bytes per step
+  static constexpr int WDMA = WST / 1024;         // 1 KiB DMA pieces per step
+  // weight ring: 3 step buffers (prefetch distance 2) where LDS allows
+  static constexpr int NWB = 3 * WST + 2 * IMG <= 160 * 1024 ? 3 : 2;
+  static constexpr int PD = NWB - 1;
+  static constexpr int LDS = NWB * WST + 2 * IMG;
+  static constexpr int NIT = SPAN * 2;            // (position, octet) staging items
+  static constexpr int IPT = (NIT + 511) / 512;   // staging items per thread
+  static constexpr int DPW = (WDMA + 7) / 8;      // DMA pieces per wave and step (max)
+  static constexpr int DPWMIN = WDMA / 8;         // ... issued by every wave
+  // vmcnt allowance at step g's barrier (DMA(s) must have landed): the VMEM
+  // operations every wave issued after DMA(s) in steady state — the pieces of
+  // the PD-1 later weight steps and the window loads of the chunk-start steps
+  // among the PD steps before s (fewer before that: the wait is conservative)
+  static constexpr int wait_n(int g) {
+    int n = (PD - 1) * DPWMIN;
+    for (int k = 1; k <= PD; ++k)
+      if (((g - k) % NG + NG) % NG == 0) n += IPT * 8;
+    return n;
+  }
+  static_assert(NQ % TG == 0, "whole tap groups");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(4096 + 4 * 2 * 64 * 16 * 4 <= LDS, "epilogue hand-over fits");
+};
+
+template <int NQ, int TG, int V>
+__global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
+  using G = ConvX3Geo<NQ, TG, V>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  char *const wbuf0 = lds, *const win0 = lds + G::NWB * G::WST;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave >> 2;
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid % p.n_rtiles;
+  bid /= p.n_rtiles;
+  const int mt = bid % p.n_mtiles;
+  const int n = bid / p.n_mtiles;
+  const int r0 = rt * kTileRows, m0 = mt * G::FT;
+  const int cstride = p.T_src * V;
+  const int g0 = (m0 + p.off) * V;
+  const float *inN = p.in + (int64_t)n * p.in_bstride;
+  const int nchunks = (p.C + G::CK - 1) / G::CK;
+  const int nsteps = nchunks * G::NG;
+  const char *wblk = reinterpret_cast<const char *>(p.wpk) + (int64_t)rt * nsteps * G::WST;
+  const int mi = wave & 1, nj0 = ((wave >> 1) & 1) * 4 + half * 2;
+
+  // A fragment (plane 0, tap 0, octet hi) and B fragments (tap 0, plane 0, octet hi)
+  const int ao = (hi * 64 + mi * 32 + lo) * 16;
+  int bo[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    bo[j] = ((col < G::NCOLS ? col : 0) * G::SLOTS + hi) * 16;
+  }
+  // window staging items (octet o, position pp), dealt over all 8 waves
+  unsigned voff[G::IPT];
+  int loff[G::IPT];
+#pragma unroll
+  for (int k = 0; k < G::IPT; ++k) {
+    const int e = k * 512 + tid;
+    const int o = e / G::SPAN, pp = e - o * G::SPAN;
+    const int g = g0 + pp;
+    const bool ok = e < G::NIT && g >= 0 && g < cstride;
+    voff[k] = ok ? (unsigned)(o * 8 * cstride + g) * 4u : kOOB;
+    loff[k] = e < G::NIT ? (pp * G::SLOTS + o) * 16 : -1;
+  }
+  float st[G::IPT][8];
+  // Window loads as inline asm too (the compiler neither waits for them nor
+  // counts them; a compiler-counted load here would make hipcc wait vmcnt(0)
+  // -- including the weight DMA issued after it -- before the write). Their
+  // completion is waited for by wait_img, which names every destination.
+  static_assert(G::IPT == 2, "wait_img names 16 staging registers");
+  auto load_img = [&](int chunk) {
+    // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
+    const int64_t rem = (int64_t)(p.C - chunk * G::CK) * cstride * 4;
+    const uint64_t src = reinterpret_cast<uint64_t>(inN + (int64_t)chunk * G::CK * cstride);
+    const int4v rs = {(int)(uint32_t)src, (int)((src >> 32) & 0xffff),
+                      (int)(rem > 0x7fffffff ? 0x7fffffff : (rem > 0 ? rem : 0)), 0x00020000};
+    asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                     : "=v"(st[k][j])
+                     : "v"(voff[k] + (unsigned)(j * cstride * 4)), "s"(rs)
+                     : "memory");
+  };
+  auto write_img = [&](char *win) {
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+      if (loff[k] >= 0) {
+        uint4 h, m, l;
+        split2(st[k][0], st[k][1], h.x, m.x, l.x);
+        split2(st[k][2], st[k][3], h.y, m.y, l.y);
+        split2(st[k][4], st[k][5], h.z, m.z, l.z);
+        split2(st[k][6], st[k][7], h.w, m.w, l.w);
+        *reinterpret_cast<uint4 *>(win + loff[k]) = h;
+        *reinterpret_cast<uint4 *>(win + loff[k] + 32) = m;
+        *reinterpret_cast<uint4 *>(win + loff[k] + 64) = l;
+      }
+  };
+  // Weight DMA as inline asm: hipcc treats an LDS-DMA builtin as a pending LDS
+  // write and waits for it (vmcnt) before the next ds_read of ANY buffer, which
+  // would drain the prefetch every step. Its completion is counted by hand
+  // (the s_waitcnt before each step's barrier).
+  const uint64_t wsrc = reinterpret_cast<uint64_t>(wblk);
+  const int4v rsw = {(int)(uint32_t)wsrc, (int)((wsrc >> 32) & 0xffff), nsteps * G::WST,
+                     0x00020000};
+  const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(wbuf0);
+  auto dma_w = [&](int step, int buf) {
+#pragma unroll
+    for (int i = 0; i < G::DPW; ++i) {
+      const int d = i * 8 + wave;
+      if (d < G::WDMA) {
+        const unsigned voffw = (unsigned)(step * G::WST + d * 1024 + lane * 16);
+        const unsigned m0v = lds0 + (unsigned)(buf * G::WST + d * 1024);
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(m0v), "v"(voffw), "s"(rsw)
+            : "memory");
+      }
+    }
+  };
+
+  // acc: the h*h products; acl: the five small cross terms (<= 2^-8 of acc),
+  // accumulated apart so their roundings stay 2^-8 smaller; summed at the end
+  floatx16 acc[4], acl[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = acl[j][i] = 0.f;
+
+  struct Frag {
+    bf16x8_t a[3], b[3][2];
+  };
+  auto ld = [&](const char *wa, const char *win, int qq, int q, Frag &f) {
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      f.a[pl] = *reinterpret_cast<const bf16x8_t *>(wa + ((pl * TG + qq) * 2) * 1024);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        f.b[pl][j] =
+            *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * V * G::SLOTS + 2 * pl) * 16);
+  };
+  auto mm = [&](const Frag &f) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j] = mfma_x(f.a[0], f.b[0][j], acc[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[0], f.b[1][j], acl[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[1], f.b[0][j], acl[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[0], f.b[2][j], acl[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[1], f.b[1][j], acl[j]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[2], f.b[0][j], acl[j]);
+  };
+
+#pragma unroll
+  for (int d = 0; d < G::PD; ++d)
+    if (d < nsteps) dma_w(d, d);
+  load_img(0);
+  wait_img<0>(st);
+  write_img(win0);
+  for (int c = 0; c < nchunks; ++c) {
+    const char *win = win0 + (c & 1) * G::IMG;
+#pragma unroll
+    for (int g = 0; g < G::NG; ++g) {
+      const int s = c * G::NG + g;
+      // step s's weights: each wave waits for its own DMA pieces (issued PD
+      // steps earlier; later pieces and window loads stay in flight), then the
+      // barrier publishes them and chunk c's window (written in the previous
+      // chunk's last step)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::wait_n(g)) : "memory");
+      if (!(STGCN_X3_EXP & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const char *wa = wbuf0 + (s % G::NWB) * G::WST + ao;
+      Frag f[2];
+      ld(wa, win, 0, g * TG, f[0]);
+      // next step's weights and (first step) chunk c+1's window, issued after
+      // this step's first fragment reads (a compiler wait placed before those
+      // reads then finds no load of ours in flight). The window load is
+      // unconditional: chunk == nchunks loads zeros and is never read.
+      if (!(STGCN_X3_EXP & 2) && s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
+      if (!(STGCN_X3_EXP & 4) && g == 0) load_img(c + 1);
+#pragma unroll
+      for (int qq = 0; qq < TG; ++qq) {
+        if (qq + 1 < TG) {
+          // tap qq+1's 9 fragment reads among tap qq's 12 MFMAs
+          ld(wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) & 1]);
+          mm(f[qq & 1]);
+#pragma unroll
+          for (int i = 0; i < 9; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        } else {
+          mm(f[qq & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (!(STGCN_X3_EXP & 1) && g == G::NG - 1) {
+        // issued after the loads (step g = 0): the weight pieces of steps 1..NG-1
+        wait_img<(G::NG - 1) * G::DPWMIN>(st);
+        write_img(win0 + ((c + 1) & 1) * G::IMG);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j] += acl[j];
+  // hand-over: waves 4-7 give their two column tiles to waves 0-3 (same rows,
+  // next two tiles), which run the shared 4-wave epilogue
+  float *ho = smem + 1024 + (wave & 3) * 2 * 64 * 16;
+  __syncthreads();  // every wave is done with the buffers
+  if (half == 1) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ho[(j * 16 + i) * 64 + lane] = acc[j][i];
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[2 + j][i] = ho[(j * 16 + i) * 64 + lane];
+    conv_tile_epilogue<V, G::NCOLS>(p, acc, n, r0, m0, smem);
+  } else if (p.stat_sum) {
+    __syncthreads();  // the epilogue's one barrier (statistics)
+  }
+}
+
+// Packs w[r*w_sr + c*w_sc + q*w_sq] split into three bf16 planes:
+// wpk[rt][chunk][tap group][plane][tap in group][octet][64 rows][8] (zero
+// padded rows and channels), so one step's weights are one contiguous run.
+__global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int NQ, int TG,
+                                 int nch, int64_t w_sr, int64_t w_sc, int64_t w_sq,
+                                 int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int jj = (int)(idx & 7);
+  int64_t t = idx >> 3;
+  const int rl = (int)(t & 63);
+  t >>= 6;
+  const int o = (int)(t & 1);
+  t >>= 1;
+  const int qq = (int)(t % TG);
+  t /= TG;
+  const int pl = (int)(t % 3);
+  t /= 3;
+  const int NG = NQ / TG;
+  const int g = (int)(t % NG);
+  t /= NG;
+  const int ch = (int)(t % nch);
+  const int rt = (int)(t / nch);
+  const int r = rt * 64 + rl, c = ch * 16 + o * 8 + jj, q = g * TG + qq;
+  float v = 0.f;
+  if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
+  const __bf16 h = (__bf16)v;
+  const float r1 = v - (float)h;
+  const __bf16 m = (__bf16)r1;
+  const __bf16 l = (__bf16)(r1 - (float)m);
+  wpk[idx] = pl == 0 ? h : (pl == 1 ? m : l);
+}
+
+static int x3_tg(int NQ) { return NQ == 9 ? 3 : NQ; }
+
+bool conv_x3_supported(const ConvGemmParams &p) {
+  if (p.C < 16 || p.s_in != 1) return false;
+  if (p.V != 18 && p.V != 25) return false;
+  if (p.FT != kTileCols / p.V) return false;
+  return p.NQ == 9 || p.NQ == 5 || p.NQ == 4;
+}
+
+size_t conv_x3_wpk_bytes(const ConvGemmParams &p) {
+  return (size_t)p.n_rtiles * ((p.C + 15) / 16) * 3 * p.NQ * 16 * 64 * 2;
+}
+
+template <int NQ, int V>
+static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
+  if (p.V != V) return false;
+  constexpr int TG = NQ == 9 ? 3 : NQ;
+  constexpr int lds = ConvX3Geo<NQ, TG, V>::LDS;
+  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V>), dim3(nblk), dim3(512), lds, s, p);
+  return true;
+}
+
+template <int NQ>
+static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
+  return launch_cx_if<NQ, 18>(p, nblk, s) || launch_cx_if<NQ, 25>(p, nblk, s);
+}
+
+hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
+  if (!conv_x3_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  const int nch = (p.C + 15) / 16;
+  {
+    const int64_t total = (int64_t)p.n_rtiles * nch * 3 * p.NQ * 2 * 64 * 8;
+    hipLaunchKernelGGL(k_pack_conv_w_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                       p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, x3_tg(p.NQ), nch,
+                       p.w_sr, p.w_sc, p.w_sq, total);
+  }
+  const int nblk = p.N * p.n_mtiles * p.n_rtiles;
+  bool done = false;
+  switch (p.NQ) {
+    case 4: done = launch_cx_v<4>(p, nblk, s); break;
+    case 5: done = launch_cx_v<5>(p, nblk, s); break;
+    case 9: done = launch_cx_v<9>(p, nblk, s); break;
+  }
+  return done ? hipGetLastError() : hipErrorInvalidValue;
+}
+
+}  // namespace stgcn

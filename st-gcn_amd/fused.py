@@ -23,12 +23,21 @@ def _f32c(t, name):
 
 
 def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1, gamma=9,
-              residual=False, bf16=False):
+              residual=False, bf16=False, f32x3=False):
     N, C_in, T, V = x_shape
     T_out = (T + 2 * pad - gamma) // stride + 1
-    flags = (hip_lib.F_RESIDUAL if residual else 0) | (hip_lib.F_BF16 if bf16 else 0)
+    flags = ((hip_lib.F_RESIDUAL if residual else 0) | (hip_lib.F_BF16 if bf16 else 0)
+             | (hip_lib.F_F32X3 if f32x3 else 0))
     return hip_lib.Desc(N, C_in, C_out, T, T_out, V, K, gamma, stride, pad, eps, momentum,
                         int(training), int(need_dx), flags)
+
+
+def _gemm_flags(gemm):
+    """Channel-GEMM arithmetic of a block: "fp32" (fp32 MFMA), "f32x3" (fp32 via
+    exact 3-way bf16 operand splits, STGCN_F_F32X3), "bf16" (STGCN_F_BF16)."""
+    if gemm not in ("fp32", "f32x3", "bf16"):
+        raise ValueError(f"unknown gemm mode {gemm!r}")
+    return {"bf16": gemm == "bf16", "f32x3": gemm == "f32x3"}
 
 
 class Link:
@@ -114,7 +123,7 @@ class StgcnBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training, cc=None, drop=0.0, bf16=False):
+                stride, pad, eps, momentum, training, cc=None, drop=0.0, gemm="fp32"):
         lib = hip_lib.lib()
         x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
@@ -126,7 +135,8 @@ class StgcnBlockFn(torch.autograd.Function):
         N, C_in, T, V = x.shape
         K = A.shape[0]
         C_out = Wt.shape[0]
-        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training, bf16=bf16)
+        desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training,
+                         **_gemm_flags(gemm))
         hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
         dev = x.device
         y = torch.empty((N, C_out, desc.T_out, V), device=dev, dtype=torch.float32)
@@ -143,7 +153,7 @@ class StgcnBlockFn(torch.autograd.Function):
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
-        ctx.bf16 = bf16
+        ctx.gemm = gemm
         ctx.cc = cc
         ctx.drop = (drop, seed)
         return y
@@ -157,7 +167,7 @@ class StgcnBlockFn(torch.autograd.Function):
         dy = dy.contiguous()
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
-                         need_dx=need_dx, bf16=ctx.bf16)
+                         need_dx=need_dx, **_gemm_flags(ctx.gemm))
         dy_sums, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], x.device)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
@@ -191,7 +201,7 @@ class StgcnResBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, Wr, br, rm1, rv1, rm2, rv2,
-                stride, pad, eps, momentum, training, cc=None, drop=0.0, bf16=False):
+                stride, pad, eps, momentum, training, cc=None, drop=0.0, gemm="fp32"):
         lib = hip_lib.lib()
         x = x.contiguous()
         seed = _dropout_seed(drop, training)
@@ -206,7 +216,7 @@ class StgcnResBlockFn(torch.autograd.Function):
         K = A.shape[0]
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, K, stride, pad, eps, momentum, training, residual=True,
-                         bf16=bf16)
+                         **_gemm_flags(gemm))
         hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
         if (Wr is None) != (C_in == C_out and stride == 1):
             raise RuntimeError("residual projection weights must be given iff shapes differ")
@@ -225,7 +235,7 @@ class StgcnResBlockFn(torch.autograd.Function):
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, Za, y, stats, A, W, bW, Wt, g1, b1, g2, b2, Wr, G)
         ctx.cfg = (stride, pad, eps, momentum, training)
-        ctx.bf16 = bf16
+        ctx.gemm = gemm
         ctx.cc = cc
         ctx.drop = (drop, seed)
         return y
@@ -239,7 +249,8 @@ class StgcnResBlockFn(torch.autograd.Function):
         dy = dy.contiguous()
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
-                         need_dx=need_dx, residual=True, bf16=ctx.bf16)
+                         need_dx=need_dx, residual=True,
+                         **_gemm_flags(ctx.gemm))
         dev = x.device
         dx = torch.empty_like(x) if need_dx else None
         dA, dW, dbW, dWt = (torch.empty_like(t) for t in (A, W, bW, Wt))

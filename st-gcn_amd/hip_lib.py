@@ -21,6 +21,7 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
 ABI_VERSION = 3
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
+F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
 
 _c_int = ctypes.c_int32
 _c_float = ctypes.c_float

@@ -17,7 +17,7 @@ LAYERS = [(64, 1), (64, 1), (64, 1), (64, 1), (128, 2), (128, 1), (128, 1),
 
 class STGCNStack(nn.Module):
     def __init__(self, C_in, nr_classes, A, gamma=9, dropout_rate=0, residual=False,
-                 gemm_dtype=torch.float32):
+                 gemm_dtype=torch.float32, f32_gemm="mfma"):
         super().__init__()
         pad = (gamma - 1) // 2
         self.K, self.V = A.shape[0], A.shape[1]
@@ -26,7 +26,7 @@ class STGCNStack(nn.Module):
         for co, s in LAYERS:
             blocks.append(SpatialTemporalConv(c, co, A, gamma, s, pad,
                                               dropout_rate=dropout_rate, residual=residual,
-                                              gemm_dtype=gemm_dtype))
+                                              gemm_dtype=gemm_dtype, f32_gemm=f32_gemm))
             c = co
         self.conv = nn.Sequential(*blocks).float()
         self.fc_layer = nn.Linear(256, nr_classes).float()

@@ -63,10 +63,18 @@ class SpatialTemporalConv(nn.Module):
     """
 
     def __init__(self, C_in, C_out, A, gamma, temporal_stride, temporal_padding,
-                 dropout_rate=0.5, residual=False, gemm_dtype=torch.float32):
+                 dropout_rate=0.5, residual=False, gemm_dtype=torch.float32,
+                 f32_gemm="mfma"):
         super().__init__()
         if gemm_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("gemm_dtype must be torch.float32 or torch.bfloat16")
+        if f32_gemm not in ("mfma", "bf16x3"):
+            raise ValueError("f32_gemm must be 'mfma' or 'bf16x3'")
+        # (not in the reference) how fp32 channel GEMMs run: "mfma" on the fp32
+        # matrix cores, "bf16x3" as exact 3-way bf16 operand splits with six
+        # partial products on the bf16 matrix cores (fp32-GEMM accuracy,
+        # STGCN_F_F32X3; the stride-1 temporal conv forward and data-grad)
+        self.f32_gemm = f32_gemm
         # (not in the reference) arithmetic of the channel GEMMs: bf16 rounds the
         # GEMM operands to bf16 on the bf16 matrix cores (fp32 accumulate; tensors,
         # parameters, A and BatchNorm stay fp32) — BASELINE cfg3 / cfg5
@@ -107,7 +115,10 @@ class SpatialTemporalConv(nn.Module):
         sc = self.spatialConv
         x = f_in.float()
         drop = self.dropout.p if (self.dropout is not None and training) else 0.0
-        bf16 = getattr(self, "gemm_dtype", torch.float32) == torch.bfloat16
+        if getattr(self, "gemm_dtype", torch.float32) == torch.bfloat16:
+            gemm = "bf16"
+        else:
+            gemm = "f32x3" if getattr(self, "f32_gemm", "mfma") == "bf16x3" else "fp32"
         cc = None
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:
@@ -128,13 +139,13 @@ class SpatialTemporalConv(nn.Module):
                 proj.weight if proj is not None else None,
                 proj.bias if proj is not None else None,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop, bf16)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop, gemm)
         else:
             y = StgcnBlockFn.apply(
                 x, sc.A, sc.W.weight, sc.W.bias, self.temporalConv.weight,
                 self.temporalConv.bias, bn1.weight, bn1.bias, bn2.weight, bn2.bias,
                 bn1.running_mean, bn1.running_var, bn2.running_mean, bn2.running_var,
-                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop, bf16)
+                self.stride, self.pad, bn1.eps, bn1.momentum, training, cc, drop, gemm)
         if chain is not None:
             if cc is None:
                 chain.reset()

@@ -28,8 +28,9 @@ TOL_RUNNING = 1e-5
 DEV = "cuda:0"
 
 
-def _run_hip(pkg, arrays, x, g, need_dx=True):
-    """Fused block fwd+bwd on the GPU; returns the oracle-style result dict."""
+def _run_hip(pkg, arrays, x, g, need_dx=True, gemm="fp32"):
+    """Fused block fwd+bwd on the GPU; returns the oracle-style result dict.
+    gemm: channel-GEMM arithmetic ("fp32", "f32x3", "bf16"; fused._gemm_flags)."""
     p, b = ref_cpu.block_params_from_arrays(arrays, dtype=torch.float32, requires_grad=False)
     stride, residual = int(arrays["meta"][2]), bool(arrays["meta"][7])
     cu = {k: v.to(DEV).contiguous().requires_grad_(True) for k, v in p.items()}
@@ -43,9 +44,10 @@ def _run_hip(pkg, arrays, x, g, need_dx=True):
     if residual:
         y = pkg.fused.StgcnResBlockFn.apply(
             *common, cu.get("apply_residual.weight"), cu.get("apply_residual.bias"), *running,
-            stride, 4, 1e-5, 0.1, True)
+            stride, 4, 1e-5, 0.1, True, None, 0.0, gemm)
     else:
-        y = pkg.fused.StgcnBlockFn.apply(*common, *running, stride, 4, 1e-5, 0.1, True)
+        y = pkg.fused.StgcnBlockFn.apply(*common, *running, stride, 4, 1e-5, 0.1, True,
+                                         None, 0.0, gemm)
     y.backward(g.to(DEV).float())
     torch.cuda.synchronize()
     out = {"y": y.detach().cpu()}

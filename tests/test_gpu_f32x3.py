@@ -1,0 +1,73 @@
+"""GPU parity of the fp32 block with STGCN_F_F32X3: the stride-1 temporal conv
+forward / data-grad GEMMs as exact 3-way bf16 operand splits with six partial
+products on the bf16 matrix cores (st-gcn_amd/csrc/kernels_x3.hip).
+
+The mode claims fp32-GEMM accuracy, so it is held to the SAME gate as the fp32
+MFMA path (test_gpu_block.py): rel-to-max error vs the fp64
+oracle below 1e-5 per output and gradient (or below twice the fp32 reference's
+own error where that is larger), ReLU ties as there. Each case also checks the
+split kernels ran: the output is not bit-identical to the fp32 MFMA path's.
+"""
+import pytest
+import torch
+
+from conftest import block_fixtures, load_npz
+from test_gpu_block import _compare, _oracle, _random_case, _run_hip
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(pkg, arrays, x, g, residual=False, need_dx=True):
+    got = _run_hip(pkg, arrays, x, g, need_dx=need_dx, gemm="f32x3")
+    want, floor = _oracle(arrays, got)
+    if not need_dx:
+        want.pop("grad.x")
+    _compare(got, want, residual=residual, floor=floor)
+    return got
+
+
+@pytest.mark.parametrize("fixture", [f for f in block_fixtures()])
+def test_f32x3_block_fixture(pkg, fixture):
+    ref = load_npz(fixture)
+    _check(pkg, ref, torch.from_numpy(ref["x"]), torch.from_numpy(ref["g"]),
+           residual=bool(ref["meta"][7]))
+
+
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T, residual
+    (64, 64, 1, 18, 1, 4, 64, False),     # cfg2 L1 shape: fwd + dgrad on k_conv_x3<9,18>
+    (64, 128, 2, 18, 1, 3, 37, False),    # stride 2: dgrad phases k_conv_x3<5|4,18>
+    (128, 256, 2, 18, 1, 2, 30, False),   # 4 row tiles, 8 channel chunks
+    (256, 256, 1, 18, 1, 2, 19, False),   # 16 chunks, ragged T
+    (3, 64, 1, 18, 1, 3, 45, False),      # C_in = 3: spatial GEMM stays fp32 MFMA
+    (24, 40, 1, 18, 1, 2, 23, False),     # partial channel chunk (24 = 16 + 8), partial rows
+    (64, 64, 1, 25, 3, 2, 40, False),     # V = 25 (k_conv_x3<9,25>), K = 3
+    (64, 128, 2, 25, 3, 2, 33, False),
+    (64, 64, 1, 50, 3, 2, 17, False),     # V = 50: not covered -> fp32 MFMA kernels
+    (64, 64, 2, 18, 1, 1, 1, False),      # T = 1
+    (64, 64, 1, 18, 1, 3, 40, True),      # residual, identity
+    (64, 128, 2, 18, 1, 2, 37, True),     # residual, projection
+])
+def test_f32x3_block_random(pkg, case):
+    *shape, residual = case
+    arrays, x, g = _random_case(pkg, *shape, residual=residual)
+    got = _check(pkg, arrays, x, g, residual=residual)
+    C_in, C_out, stride, V = shape[:4]
+    if V in (18, 25) and C_out >= 16 and shape[6] > 1:
+        # stride 1: the forward runs k_conv_x3; stride 2: the data-grad phases
+        key = "y" if stride == 1 else "grad.x"
+        ref = _run_hip(pkg, arrays, x, g, gemm="fp32")
+        assert not torch.equal(got[key], ref[key]), "split kernels did not run"
+
+
+def test_f32x3_full_size_block(pkg):
+    """cfg2 L1 shape at N=32, T=300 (the bench layer) at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, 64, 64, 1, 18, 1, 32, 300, seed=7)
+    got = _check(pkg, arrays, x, g)
+    for k, v in got.items():
+        assert torch.isfinite(v).all(), k
+
+
+def test_f32x3_without_dx(pkg):
+    arrays, x, g = _random_case(pkg, 3, 64, 1, 18, 1, 2, 30)
+    _check(pkg, arrays, x, g, need_dx=False)
