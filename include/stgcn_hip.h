@@ -58,9 +58,9 @@ extern "C" {
 #define STGCN_F_F32X3 4    /* fp32 channel GEMMs on the bf16 matrix cores by exact 3-way
                             * operand splits (x = h + m + l, six partial products, fp32
                             * accumulate): fp32-GEMM accuracy at up to 2.67x the fp32
-                            * MFMA rate. Applies to the stride-1 temporal conv forward
-                            * and data-grad for V in {18, 25} over >= 16 channels; other
-                            * GEMMs run the fp32 kernels. Exclusive with STGCN_F_BF16. */
+                            * MFMA rate. Applies to the temporal conv forward (stride 1
+                            * and 2) and data-grad for V in {18, 25} over >= 16 channels;
+                            * other GEMMs run the fp32 kernels. Exclusive with STGCN_F_BF16. */
 
 enum {
   STGCN_OK = 0,

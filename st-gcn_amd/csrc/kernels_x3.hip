@@ -76,34 +76,39 @@ __device__ __forceinline__ void split2(float a, float b, unsigned &h, unsigned &
 
 // Waits until at most NA VMEM operations are in flight, naming the 16 window
 // staging registers (so no consumer of them is scheduled above the wait).
+#define X3_ST8(k)                                                                         \
+  "+v"(st[k][0]), "+v"(st[k][1]), "+v"(st[k][2]), "+v"(st[k][3]), "+v"(st[k][4]),       \
+      "+v"(st[k][5]), "+v"(st[k][6]), "+v"(st[k][7])
 template <int NA>
 __device__ __forceinline__ void wait_img(float (&st)[2][8]) {
-  asm volatile("s_waitcnt vmcnt(%16)"
-               : "+v"(st[0][0]), "+v"(st[0][1]), "+v"(st[0][2]), "+v"(st[0][3]),
-                 "+v"(st[0][4]), "+v"(st[0][5]), "+v"(st[0][6]), "+v"(st[0][7]),
-                 "+v"(st[1][0]), "+v"(st[1][1]), "+v"(st[1][2]), "+v"(st[1][3]),
-                 "+v"(st[1][4]), "+v"(st[1][5]), "+v"(st[1][6]), "+v"(st[1][7])
-               : "n"(NA)
-               : "memory");
+  asm volatile("s_waitcnt vmcnt(%16)" : X3_ST8(0), X3_ST8(1) : "n"(NA) : "memory");
 }
+template <int NA>
+__device__ __forceinline__ void wait_img(float (&st)[3][8]) {
+  asm volatile("s_waitcnt vmcnt(%24)" : X3_ST8(0), X3_ST8(1), X3_ST8(2) : "n"(NA) : "memory");
+}
+#undef X3_ST8
 
-template <int NQ, int TG, int V>
+template <int NQ, int TG, int V, int SIN>
 struct ConvX3Geo {
   static constexpr int CK = 16;                   // channels per chunk (one k-step)
   static constexpr int FT = kTileCols / V;
   static constexpr int NCOLS = FT * V;
-  static constexpr int SPAN = (FT - 1 + NQ) * V;  // window positions (stride 1)
+  static constexpr int SPAN = (SIN * (FT - 1) + NQ) * V;  // window positions
   static constexpr int SLOTS = 7;                 // 6 (plane, octet) slots + 1 pad
   static constexpr int IMG = SPAN * SLOTS * 16;   // window bytes
   static constexpr int NG = NQ / TG;              // steps per chunk
   static constexpr int WST = 3 * TG * 2 * 1024;   // packed weight bytes per step
   static constexpr int WDMA = WST / 1024;         // 1 KiB DMA pieces per step
   // weight ring: 3 step buffers (prefetch distance 2) where LDS allows
-  static constexpr int NWB = 3 * WST + 2 * IMG <= 160 * 1024 ? 3 : 2;
+  // window double-buffered where LDS allows (else written between two barriers)
+  static constexpr int NWIN = 3 * WST + 2 * IMG <= 160 * 1024 ? 2 : 1;
+  static constexpr int NWB = 3 * WST + NWIN * IMG <= 160 * 1024 ? 3 : 2;
   static constexpr int PD = NWB - 1;
-  static constexpr int LDS = NWB * WST + 2 * IMG;
+  static constexpr int LDS = NWB * WST + NWIN * IMG;
   static constexpr int NIT = SPAN * 2;            // (position, octet) staging items
   static constexpr int IPT = (NIT + 511) / 512;   // staging items per thread
+  static_assert(IPT == 2 || IPT == 3, "wait_img overloads");
   static constexpr int DPW = (WDMA + 7) / 8;      // DMA pieces per wave and step (max)
   static constexpr int DPWMIN = WDMA / 8;         // ... issued by every wave
   // vmcnt allowance at step g's barrier (DMA(s) must have landed): the VMEM
@@ -121,9 +126,9 @@ struct ConvX3Geo {
   static_assert(4096 + 4 * 2 * 64 * 16 * 4 <= LDS, "epilogue hand-over fits");
 };
 
-template <int NQ, int TG, int V>
+template <int NQ, int TG, int V, int SIN>
 __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
-  using G = ConvX3Geo<NQ, TG, V>;
+  using G = ConvX3Geo<NQ, TG, V, SIN>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   char *const wbuf0 = lds, *const win0 = lds + G::NWB * G::WST;
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   const int n = bid / p.n_mtiles;
   const int r0 = rt * kTileRows, m0 = mt * G::FT;
   const int cstride = p.T_src * V;
-  const int g0 = (m0 + p.off) * V;
+  const int g0 = (SIN * m0 + p.off) * V;
   const float *inN = p.in + (int64_t)n * p.in_bstride;
   const int nchunks = (p.C + G::CK - 1) / G::CK;
   const int nsteps = nchunks * G::NG;
@@ -151,7 +156,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = (nj0 + j) * 32 + lo;
-    bo[j] = ((col < G::NCOLS ? col : 0) * G::SLOTS + hi) * 16;
+    const int mf = col / V;
+    const int cp = col < G::NCOLS ? SIN * mf * V + (col - mf * V) : 0;
+    bo[j] = (cp * G::SLOTS + hi) * 16;
   }
   // window staging items (octet o, position pp), dealt over all 8 waves
   unsigned voff[G::IPT];
@@ -170,7 +177,6 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   // counts them; a compiler-counted load here would make hipcc wait vmcnt(0)
   // -- including the weight DMA issued after it -- before the write). Their
   // completion is waited for by wait_img, which names every destination.
-  static_assert(G::IPT == 2, "wait_img names 16 staging registers");
   auto load_img = [&](int chunk) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
     const int64_t rem = (int64_t)(p.C - chunk * G::CK) * cstride * 4;
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   wait_img<0>(st);
   write_img(win0);
   for (int c = 0; c < nchunks; ++c) {
-    const char *win = win0 + (c & 1) * G::IMG;
+    const char *win = win0 + (G::NWIN == 2 ? (c & 1) * G::IMG : 0);
 #pragma unroll
     for (int g = 0; g < G::NG; ++g) {
       const int s = c * G::NG + g;
@@ -310,7 +316,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
       if (!(STGCN_X3_EXP & 1) && g == G::NG - 1) {
         // issued after the loads (step g = 0): the weight pieces of steps 1..NG-1
         wait_img<(G::NG - 1) * G::DPWMIN>(st);
-        write_img(win0 + ((c + 1) & 1) * G::IMG);
+        if (G::NWIN == 1)  // single window: every wave is done reading chunk c's
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        write_img(win0 + (G::NWIN == 2 ? ((c + 1) & 1) * G::IMG : 0));
       }
     }
   }
@@ -374,28 +382,32 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
 static int x3_tg(int NQ) { return NQ == 9 ? 3 : NQ; }
 
 bool conv_x3_supported(const ConvGemmParams &p) {
-  if (p.C < 16 || p.s_in != 1) return false;
+  if (p.C < 16) return false;
   if (p.V != 18 && p.V != 25) return false;
   if (p.FT != kTileCols / p.V) return false;
-  return p.NQ == 9 || p.NQ == 5 || p.NQ == 4;
+  if (p.s_in == 2) return p.NQ == 9;  // stride-2 forward
+  return p.s_in == 1 && (p.NQ == 9 || p.NQ == 5 || p.NQ == 4);
 }
 
 size_t conv_x3_wpk_bytes(const ConvGemmParams &p) {
   return (size_t)p.n_rtiles * ((p.C + 15) / 16) * 3 * p.NQ * 16 * 64 * 2;
 }
 
-template <int NQ, int V>
+template <int NQ, int V, int SIN>
 static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
-  if (p.V != V) return false;
+  if (p.V != V || p.s_in != SIN) return false;
   constexpr int TG = NQ == 9 ? 3 : NQ;
-  constexpr int lds = ConvX3Geo<NQ, TG, V>::LDS;
-  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V>), dim3(nblk), dim3(512), lds, s, p);
+  constexpr int lds = ConvX3Geo<NQ, TG, V, SIN>::LDS;
+  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN>), dim3(nblk), dim3(512), lds, s, p);
   return true;
 }
 
 template <int NQ>
 static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
-  return launch_cx_if<NQ, 18>(p, nblk, s) || launch_cx_if<NQ, 25>(p, nblk, s);
+  if (launch_cx_if<NQ, 18, 1>(p, nblk, s) || launch_cx_if<NQ, 25, 1>(p, nblk, s)) return true;
+  if constexpr (NQ == 9)
+    return launch_cx_if<NQ, 18, 2>(p, nblk, s) || launch_cx_if<NQ, 25, 2>(p, nblk, s);
+  return false;
 }
 
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
