@@ -158,6 +158,9 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
   const int tiles = w.n_rtiles * w.n_jtiles;
   w.S = std::max(1, std::min((256 + tiles - 1) / tiles, d->N * w.n_mtiles));
   if (bf16(d)) plan_wgrad_bf16(w);
+  // k_wgrad_x3 where it covers the shape (its S x R x C x 9 slab fits the fp32
+  // plan's: twice the tiles, half the splits)
+  if (f32x3(d)) plan_wgrad_x3(w);
   return w;
 }
 

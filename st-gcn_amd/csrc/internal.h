@@ -72,7 +72,8 @@ struct WgradParams {
   int V, FT;
   int n_mtiles, n_rtiles, n_jtiles, S, N;
   int CT;  // k_wgrad_sp (NQ = 1): output columns per workgroup (64 or 128)
-  int bf16;  // set by plan_wgrad_bf16: run k_wgrad_bf16 (bf16 operands, fp32 accumulate)
+  int bf16;  // set by plan_wgrad_bf16: run k_wgrad_bf16 (bf16 operands, fp32 accumulate);
+             // 3: set by plan_wgrad_x3 (fp32 via exact bf16 splits, k_wgrad_x3)
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
@@ -88,6 +89,11 @@ hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s);
 bool conv_x3_supported(const ConvGemmParams &p);
 size_t conv_x3_wpk_bytes(const ConvGemmParams &p);
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s);
+// Re-plans the temporal weight gradient (NQ = 9, stride 1, V = 18) for
+// k_wgrad_x3 (sets FT, tiles, S, bf16 = 3); false (w unchanged) otherwise.
+// launch_wgrad_taps dispatches to launch_wgrad_x3 when w.bf16 == 3.
+bool plan_wgrad_x3(WgradParams &w);
+hipError_t launch_wgrad_x3(const WgradParams &p, hipStream_t s);
 // Re-plans a weight gradient (NQ = 9 temporal taps or NQ = 1) for k_wgrad_bf16
 // (sets FT, n_mtiles, n_rtiles, n_jtiles, S, bf16 = 1) when the shape is
 // covered; returns false (w unchanged) otherwise. launch_wgrad / launch_wgrad_taps

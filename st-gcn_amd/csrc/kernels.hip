@@ -981,6 +981,7 @@ bool wgrad_taps_supported(const WgradParams &p) {
 }
 
 hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s) {
+  if (p.bf16 == 3) return launch_wgrad_x3(p, s);
   if (p.bf16) return launch_wgrad_bf16(p, s);
   if (!wgrad_taps_supported(p)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;

@@ -52,6 +52,7 @@ namespace stgcn {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef int int4v __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ floatx16 mfma_x(bf16x8_t a, bf16x8_t b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -427,6 +428,238 @@ hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
     case 9: done = launch_cx_v<9>(p, nblk, s); break;
   }
   return done ? hipGetLastError() : hipErrorInvalidValue;
+}
+
+}  // namespace stgcn
+
+namespace stgcn {
+
+// ---------------------------------------------------------------------------
+// k_wgrad_x3<V, SIN>: the temporal-conv weight gradient (WgradParams, NQ = 9,
+// off = -4) in fp32 via the same exact 3-way bf16 splits, six products per
+// fp32 product, h*h and cross terms in separate accumulators:
+//   slab[split][r][c*9 + q] = sum_{items of split} sum_{m,v} P[n,r,m,v] Q[n,c,SIN*m+q-4,v]
+// Output tile 64 rows x 32 channels x 9 taps; 8 waves = (row half) x (tap
+// group: taps 0-2, 3-4, 5-6, 7-8; waves w and w+4 share a SIMD, so every SIMD
+// carries 5 or 4 taps). Work item = (clip, FT = 4 frames of P); each split
+// takes a contiguous run of items (consecutive frame tiles: the Q halo of the
+// next item is L2-hot). Reduction index = (frame, joint) with the joint axis
+// padded to Vp = round4(V) (P's pad positions are 0). k-step = 16 positions:
+// lane half h takes 4-groups 2s, 2s+1 of frame half h: A = one ds_read_b128 per
+// plane, B per tap = two ds_read_b64 per plane (row pitches 8 mod 16 / 4 mod 8
+// elements: conflict-free). Images: 3 planes each of P [64][KP] and Q
+// [32][QF*Vp], double-buffered (157.5 KiB at V = 18); the next item is loaded
+// into registers (4-joint groups, fp32 dwords) under this item's MFMAs, split
+// and written after them; one barrier per item.
+// ---------------------------------------------------------------------------
+template <int V, int SIN>
+struct WgX3Geo {
+  static constexpr int Vp = (V + 3) & ~3;
+  static constexpr int G4 = Vp / 4;
+  static constexpr int FT = 4;
+  static constexpr int KP = FT * Vp;
+  static constexpr int KSTEPS = KP / 16;
+  static constexpr int HF = FT / 2;
+  static constexpr int PPITCH = KP + 8;
+  static constexpr int QF = SIN * (FT - 1) + 9;
+  static constexpr int QP0 = QF * Vp;
+  static constexpr int QPITCH = QP0 % 8 == 0 ? QP0 + 4 : QP0;
+  static constexpr int CB = 32;
+  static constexpr int PPL = 64 * PPITCH * 2;  // bytes per P plane
+  static constexpr int QPL = CB * QPITCH * 2;  // bytes per Q plane
+  static constexpr int BUF = 3 * (PPL + QPL);
+  static constexpr int LDS = 2 * BUF;
+  static constexpr int PG = FT * G4;  // 4-joint groups per P row
+  static constexpr int QG = QF * G4;  // ... per Q row
+  static constexpr int NGRP = 64 * PG + CB * QG;
+  static constexpr int GPT = (NGRP + 511) / 512;
+  static_assert(KP % 16 == 0 && PPITCH % 16 == 8 && QPITCH % 8 == 4, "conflict-free pitches");
+  static_assert(PPL % 16 == 0 && QPL % 16 == 0, "plane alignment");
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+};
+
+template <int V, int SIN>
+__global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
+  using G = WgX3Geo<V, SIN>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int jt = bid % p.n_jtiles;
+  bid /= p.n_jtiles;
+  const int rt = bid % p.n_rtiles;
+  const int split = bid / p.n_rtiles;
+  const int r0 = rt * 64, c0 = jt * G::CB;
+  const int mi = wave & 1, tq = wave >> 1;
+  const int q0 = tq ? 1 + 2 * tq : 0;
+  const int total = p.N * p.n_mtiles;
+  const int per = (total + p.S - 1) / p.S;
+  const int it0 = split * per, it1 = min(total, it0 + per);
+  const int MV = p.M * V, TV = p.T_src * V;
+
+  // staging groups of this thread: P (row, frame, joint group) or Q (channel, ...)
+  int grow[G::GPT], gfr[G::GPT], gv0[G::GPT], gl[G::GPT];
+  bool isq[G::GPT];
+#pragma unroll
+  for (int k = 0; k < G::GPT; ++k) {
+    int e = k * 512 + tid;
+    isq[k] = e >= 64 * G::PG;
+    if (isq[k]) e -= 64 * G::PG;
+    const int per_row = isq[k] ? G::QG : G::PG;
+    const int row = e / per_row, g = e - row * per_row;
+    grow[k] = row;
+    gfr[k] = g / G::G4;
+    gv0[k] = (g % G::G4) * 4;
+    const bool live = isq[k] ? row < G::CB : true;
+    // LDS byte offset within a plane (-1: no group)
+    gl[k] = (!live || (isq[k] && e >= G::CB * G::QG)) ? -1
+            : isq[k] ? (row * G::QPITCH + gfr[k] * G::Vp + gv0[k]) * 2
+                     : (row * G::PPITCH + gfr[k] * G::Vp + gv0[k]) * 2;
+  }
+  float st[G::GPT][4];
+  auto load_item = [&](int item) {
+    const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * G::FT;
+    const __amdgpu_buffer_rsrc_t rp = make_rsrc(p.P + (int64_t)n * p.p_bstride, p.p_bstride);
+    const __amdgpu_buffer_rsrc_t rq = make_rsrc(p.Q + (int64_t)n * p.q_bstride, p.q_bstride);
+#pragma unroll
+    for (int k = 0; k < G::GPT; ++k) {
+      unsigned base;
+      if (isq[k]) {
+        const int c = c0 + grow[k], t = SIN * m0 + p.off + gfr[k];
+        const bool ok = gl[k] >= 0 && c < p.C && t >= 0 && t < p.T_src;
+        base = ok ? (unsigned)(c * TV + t * V + gv0[k]) * 4u : kOOB;
+      } else {
+        const int r = r0 + grow[k], m = m0 + gfr[k];
+        const bool ok = gl[k] >= 0 && r < p.R && m < p.M;
+        base = ok ? (unsigned)(r * MV + m * V + gv0[k]) * 4u : kOOB;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const unsigned off = gv0[k] + j < V ? base + 4u * j : kOOB;  // pad joints: 0
+        st[k][j] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(isq[k] ? rq : rp, off, 0, 0));
+      }
+    }
+  };
+  auto write_item = [&](char *buf) {
+#pragma unroll
+    for (int k = 0; k < G::GPT; ++k)
+      if (gl[k] >= 0) {
+        uint2 h, m, l;
+        split2(st[k][0], st[k][1], h.x, m.x, l.x);
+        split2(st[k][2], st[k][3], h.y, m.y, l.y);
+        char *dst = buf + (isq[k] ? 3 * G::PPL : 0) + gl[k];
+        const int pl = isq[k] ? G::QPL : G::PPL;
+        *reinterpret_cast<uint2 *>(dst) = h;
+        *reinterpret_cast<uint2 *>(dst + pl) = m;
+        *reinterpret_cast<uint2 *>(dst + 2 * pl) = l;
+      }
+  };
+
+  // lane bases (elements) of the A (P) and B (Q) fragments in plane 0
+  const int pa = (mi * 32 + lo) * G::PPITCH + hi * G::HF * G::Vp;
+  const int qb = lo * G::QPITCH + hi * SIN * G::HF * G::Vp + q0 * G::Vp;
+
+  auto run = [&](auto nt_c) {
+    constexpr int NT = decltype(nt_c)::value;
+    floatx16 acc[NT], acl[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = acl[t][i] = 0.f;
+    struct Frag {
+      bf16x8_t a[3], b[3][NT];
+    };
+    auto ld = [&](const char *buf, int s, Frag &f) {
+      const __bf16 *P = reinterpret_cast<const __bf16 *>(buf) + pa + 8 * s;
+      const int ga = 2 * s, gb = 2 * s + 1;
+      const int oa = SIN * (ga / G::G4) * G::Vp + (ga % G::G4) * 4;
+      const int ob = SIN * (gb / G::G4) * G::Vp + (gb % G::G4) * 4;
+      const __bf16 *Q = reinterpret_cast<const __bf16 *>(buf + 3 * G::PPL) + qb;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        f.a[pl] = *reinterpret_cast<const bf16x8_t *>(P + pl * (G::PPL / 2));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const __bf16 *Qp = Q + pl * (G::QPL / 2) + t * G::Vp;
+          const bf16x4_t b0 = *reinterpret_cast<const bf16x4_t *>(Qp + oa);
+          const bf16x4_t b1 = *reinterpret_cast<const bf16x4_t *>(Qp + ob);
+          f.b[pl][t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+    };
+    auto mm = [&](const Frag &f) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mfma_x(f.a[0], f.b[0][t], acc[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0], f.b[1][t], acl[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[1], f.b[0][t], acl[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0], f.b[2][t], acl[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[1], f.b[1][t], acl[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[2], f.b[0][t], acl[t]);
+    };
+    for (int it = it0; it < it1; ++it) {
+      const char *cur = lds + ((it - it0) & 1) * G::BUF;
+      char *nxt = lds + ((it - it0 + 1) & 1) * G::BUF;
+      // next item (the last iteration reloads its own item into the idle buffer:
+      // unconditional, so no register copies across the loop)
+      load_item(it + 1 < it1 ? it + 1 : it);
+      Frag f[2];
+      ld(cur, 0, f[0]);
+#pragma unroll
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        if (s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) & 1]);
+        mm(f[s & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      write_item(nxt);
+      __syncthreads();
+    }
+    float *slab = p.slab + (int64_t)split * p.R * p.C * 9;
+    const int c = c0 + lo;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        if (r < p.R && c < p.C) slab[((int64_t)r * p.C + c) * 9 + q0 + t] = acc[t][i] + acl[t][i];
+      }
+  };
+  if (it0 < it1) {
+    load_item(it0);
+    write_item(lds);
+  }
+  __syncthreads();
+  if (tq == 0)
+    run(std::integral_constant<int, 3>{});
+  else
+    run(std::integral_constant<int, 2>{});
+}
+
+bool plan_wgrad_x3(WgradParams &w) {
+  if (w.V != 18 || w.s_in != 1 || w.NQ != 9 || w.off != -4 || w.C < 16) return false;
+  w.FT = WgX3Geo<18, 1>::FT;
+  w.n_mtiles = (w.M + w.FT - 1) / w.FT;
+  w.n_rtiles = (w.R + 63) / 64;
+  w.n_jtiles = (w.C + WgX3Geo<18, 1>::CB - 1) / WgX3Geo<18, 1>::CB;
+  const int tiles = w.n_rtiles * w.n_jtiles;
+  w.S = std::max(1, std::min((256 + tiles - 1) / tiles, w.N * w.n_mtiles));
+  w.bf16 = 3;
+  return true;
+}
+
+hipError_t launch_wgrad_x3(const WgradParams &p, hipStream_t s) {
+  if (p.bf16 != 3 || p.V != 18 || p.s_in != 1) return hipErrorInvalidValue;
+  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  constexpr int lds = WgX3Geo<18, 1>::LDS;
+  hipLaunchKernelGGL((k_wgrad_x3<18, 1>), dim3(nblk), dim3(512), lds, s, p);
+  return hipGetLastError();
 }
 
 }  // namespace stgcn

@@ -1,6 +1,7 @@
-"""GPU parity of the fp32 block with STGCN_F_F32X3: the stride-1 temporal conv
-forward / data-grad GEMMs as exact 3-way bf16 operand splits with six partial
-products on the bf16 matrix cores (st-gcn_amd/csrc/kernels_x3.hip).
+"""GPU parity of the fp32 block with STGCN_F_F32X3: the temporal conv forward /
+data-grad GEMMs (k_conv_x3) and the stride-1 V=18 weight gradient (k_wgrad_x3)
+as exact 3-way bf16 operand splits with six partial products on the bf16
+matrix cores (st-gcn_amd/csrc/kernels_x3.hip).
 
 The mode claims fp32-GEMM accuracy, so it is held to the SAME gate as the fp32
 MFMA path (test_gpu_block.py): rel-to-max error vs the fp64
@@ -58,6 +59,9 @@ def test_f32x3_block_random(pkg, case):
         key = "y" if stride == 1 else "grad.x"
         ref = _run_hip(pkg, arrays, x, g, gemm="fp32")
         assert not torch.equal(got[key], ref[key]), "split kernels did not run"
+        if V == 18 and stride == 1:  # k_wgrad_x3 (temporal weight gradient)
+            k = "grad.temporalConv.weight"
+            assert not torch.equal(got[k], ref[k]), "k_wgrad_x3 did not run"
 
 
 def test_f32x3_full_size_block(pkg):
