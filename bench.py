@@ -151,7 +151,8 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             elif x3 and V in (18, 25):
                 sym = {0: f"k_conv_x3<9,3,{V},{s}>",
                        1: f"k_conv_x3<9,3,{V},1>" if s == 1 else f"k_conv_x3<5|4,{V},1>",
-                       2: f"k_wgrad_taps<{V},{s}>", 3: f"k_tconv<1,8,{V},1>"}[which]
+                       2: f"k_wgrad_x3<{V},1>" if (V == 18 and s == 1) else f"k_wgrad_taps<{V},{s}>",
+                       3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
                        1: f"k_tconv<9,2,{V},1>" if s == 1 else f"k_tconv<5|4,2,{V},1>",
@@ -210,7 +211,7 @@ def main():
                     help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3"], default="mfma",
+    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3"], default="bf16x3",
                     help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma) or "
                          "as exact 3-way bf16 operand splits (bf16x3; fp32 accuracy)")
     ap.add_argument("--torch-ops", action="store_true",
@@ -279,6 +280,25 @@ def main():
     clips = cfg["N"] * world * args.steps / dt
     gf_clip = pkg.flops_per_clip(cfg["C"], cfg["T"], cfg["V"], cfg["K"], cfg["classes"]) / 1e9
 
+    # the exact fp32-MFMA path (every GEMM on v_mfma_f32_32x32x2_f32) timed
+    # beside the default bf16x3 path, same model and inputs (N=1 only)
+    alt = None
+    if world == 1 and not cfg["bf16"] and cfg["f32_gemm"] == "bf16x3":
+        for blk in model.conv:
+            blk.f32_gemm = "mfma"
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dta = time.perf_counter() - ta
+        alt = {"f32_gemm": "mfma", "value": round(cfg["N"] * args.steps / dta, 2),
+               "ms_per_step": round(dta / args.steps * 1e3, 3)}
+        for blk in model.conv:
+            blk.f32_gemm = "bf16x3"
+
     if rank == 0:
         out = {
             "metric": "skeleton clips/sec (fwd+bwd), synthetic (N,3,300,18); 1/2/4/8-GPU scaling",
@@ -291,13 +311,15 @@ def main():
                        "per_gpu_batch": cfg["N"], "global_batch": cfg["N"] * world,
                        "seq_len": cfg["T"], "parallelism": f"dp{world}",
                        "channel_gemm": ("bf16 operands, fp32 accumulate" if cfg["bf16"] else
-                                        "fp32: temporal conv fwd/data-grad as exact 3-way bf16 "
-                                        "splits (6 MFMAs, fp32-gated), weight-grad and spatial "
-                                        "GEMMs fp32 MFMA"
+                                        "fp32: temporal conv fwd/data-grad (and stride-1 "
+                                        "weight-grad) as exact 3-way bf16 splits (6 MFMAs, "
+                                        "fp32-gated parity); other GEMMs fp32 MFMA"
                                         if cfg["f32_gemm"] == "bf16x3" else "fp32 MFMA")},
             "model_tflops": round(clips * gf_clip / 1e3, 2),
             "loss": round(float(loss.item()), 5),
         }
+        if alt is not None:
+            out["fp32_mfma_path"] = alt
         if not args.no_roofline:
             out["per_block_clips_s"] = per_block_rates(model, cfg, device)
             kinds, symbols = kernel_roofline(pkg, device, cfg)

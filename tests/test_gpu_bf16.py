@@ -53,10 +53,10 @@ def _run(pkg, arrays, x, g, bf16, need_dx=True):
     if residual:
         y = pkg.fused.StgcnResBlockFn.apply(
             *common, cu.get("apply_residual.weight"), cu.get("apply_residual.bias"), *running,
-            stride, 4, 1e-5, 0.1, True, None, 0.0, bf16)
+            stride, 4, 1e-5, 0.1, True, None, 0.0, "bf16" if bf16 else "fp32")
     else:
         y = pkg.fused.StgcnBlockFn.apply(*common, *running, stride, 4, 1e-5, 0.1, True, None,
-                                         0.0, bf16)
+                                         0.0, "bf16" if bf16 else "fp32")
     # residual block: the inner ReLU's mask (Za = ReLU(BN2(Z)) > 0, saved by the
     # Function) so the oracle can take the same subgradient choices there too
     inner = (y.grad_fn.saved_tensors[2] > 0).cpu() if residual else None
