@@ -151,7 +151,7 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             elif x3 and V in (18, 25):
                 sym = {0: f"k_conv_x3<9,3,{V},{s}>",
                        1: f"k_conv_x3<9,3,{V},1>" if s == 1 else f"k_conv_x3<5|4,{V},1>",
-                       2: f"k_wgrad_x3<{V},1>" if (V == 18 and s == 1) else f"k_wgrad_taps<{V},{s}>",
+                       2: f"k_wgrad_x3<{V},{s}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
@@ -311,9 +311,9 @@ def main():
                        "per_gpu_batch": cfg["N"], "global_batch": cfg["N"] * world,
                        "seq_len": cfg["T"], "parallelism": f"dp{world}",
                        "channel_gemm": ("bf16 operands, fp32 accumulate" if cfg["bf16"] else
-                                        "fp32: temporal conv fwd/data-grad (and stride-1 "
-                                        "weight-grad) as exact 3-way bf16 splits (6 MFMAs, "
-                                        "fp32-gated parity); other GEMMs fp32 MFMA"
+                                        "fp32: temporal conv fwd/data-grad/weight-grad as exact "
+                                        "3-way bf16 splits (6 MFMAs, fp32-gated parity); "
+                                        "spatial GEMMs fp32 MFMA"
                                         if cfg["f32_gemm"] == "bf16x3" else "fp32 MFMA")},
             "model_tflops": round(clips * gf_clip / 1e3, 2),
             "loss": round(float(loss.item()), 5),

@@ -436,7 +436,7 @@ namespace stgcn {
 
 // ---------------------------------------------------------------------------
 // k_wgrad_x3<V, SIN>: the temporal-conv weight gradient (WgradParams, NQ = 9,
-// off = -4) in fp32 via the same exact 3-way bf16 splits, six products per
+// off = -4, stride SIN = 1 or 2) in fp32 via the same exact 3-way bf16 splits, six products per
 // fp32 product, h*h and cross terms in separate accumulators:
 //   slab[split][r][c*9 + q] = sum_{items of split} sum_{m,v} P[n,r,m,v] Q[n,c,SIN*m+q-4,v]
 // Output tile 64 rows x 32 channels x 9 taps; 8 waves = (row half) x (tap
@@ -448,7 +448,8 @@ namespace stgcn {
 // lane half h takes 4-groups 2s, 2s+1 of frame half h: A = one ds_read_b128 per
 // plane, B per tap = two ds_read_b64 per plane (row pitches 8 mod 16 / 4 mod 8
 // elements: conflict-free). Images: 3 planes each of P [64][KP] and Q
-// [32][QF*Vp], double-buffered (157.5 KiB at V = 18); the next item is loaded
+// [32][QF*Vp], double-buffered at stride 1 (157.5 KiB at V = 18; one buffer and
+// a second barrier at stride 2); the next item is loaded
 // into registers (4-joint groups, fp32 dwords) under this item's MFMAs, split
 // and written after them; one barrier per item.
 // ---------------------------------------------------------------------------
@@ -468,7 +469,10 @@ struct WgX3Geo {
   static constexpr int PPL = 64 * PPITCH * 2;  // bytes per P plane
   static constexpr int QPL = CB * QPITCH * 2;  // bytes per Q plane
   static constexpr int BUF = 3 * (PPL + QPL);
-  static constexpr int LDS = 2 * BUF;
+  // double-buffered where it fits (stride 1); else one buffer written between
+  // two barriers (stride 2: 15 Q frames per item)
+  static constexpr int NBUF = 2 * BUF <= 160 * 1024 ? 2 : 1;
+  static constexpr int LDS = NBUF * BUF;
   static constexpr int PG = FT * G4;  // 4-joint groups per P row
   static constexpr int QG = QF * G4;  // ... per Q row
   static constexpr int NGRP = 64 * PG + CB * QG;
@@ -605,8 +609,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[2], f.b[0][t], acl[t]);
     };
     for (int it = it0; it < it1; ++it) {
-      const char *cur = lds + ((it - it0) & 1) * G::BUF;
-      char *nxt = lds + ((it - it0 + 1) & 1) * G::BUF;
+      const char *cur = lds + (G::NBUF == 2 ? ((it - it0) & 1) * G::BUF : 0);
+      char *nxt = lds + (G::NBUF == 2 ? ((it - it0 + 1) & 1) * G::BUF : 0);
       // next item (the last iteration reloads its own item into the idle buffer:
       // unconditional, so no register copies across the loop)
       load_item(it + 1 < it1 ? it + 1 : it);
@@ -618,6 +622,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         mm(f[s & 1]);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (G::NBUF == 1) __syncthreads();  // every wave is done reading the buffer
       write_item(nxt);
       __syncthreads();
     }
@@ -643,7 +648,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 }
 
 bool plan_wgrad_x3(WgradParams &w) {
-  if (w.V != 18 || w.s_in != 1 || w.NQ != 9 || w.off != -4 || w.C < 16) return false;
+  if (w.V != 18 || (w.s_in != 1 && w.s_in != 2) || w.NQ != 9 || w.off != -4 || w.C < 16)
+    return false;
   w.FT = WgX3Geo<18, 1>::FT;
   w.n_mtiles = (w.M + w.FT - 1) / w.FT;
   w.n_rtiles = (w.R + 63) / 64;
@@ -655,10 +661,15 @@ bool plan_wgrad_x3(WgradParams &w) {
 }
 
 hipError_t launch_wgrad_x3(const WgradParams &p, hipStream_t s) {
-  if (p.bf16 != 3 || p.V != 18 || p.s_in != 1) return hipErrorInvalidValue;
+  if (p.bf16 != 3 || p.V != 18 || (p.s_in != 1 && p.s_in != 2)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
-  constexpr int lds = WgX3Geo<18, 1>::LDS;
-  hipLaunchKernelGGL((k_wgrad_x3<18, 1>), dim3(nblk), dim3(512), lds, s, p);
+  if (p.s_in == 1) {
+    constexpr int lds = WgX3Geo<18, 1>::LDS;
+    hipLaunchKernelGGL((k_wgrad_x3<18, 1>), dim3(nblk), dim3(512), lds, s, p);
+  } else {
+    constexpr int lds = WgX3Geo<18, 2>::LDS;
+    hipLaunchKernelGGL((k_wgrad_x3<18, 2>), dim3(nblk), dim3(512), lds, s, p);
+  }
   return hipGetLastError();
 }
 
