@@ -214,6 +214,8 @@ def main():
     ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3"], default="bf16x3",
                     help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma) or "
                          "as exact 3-way bf16 operand splits (bf16x3; fp32 accuracy)")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip timing the exact fp32-MFMA path beside the bf16x3 default")
     ap.add_argument("--torch-ops", action="store_true",
                     help="head + cross entropy + Adam from torch instead of the HIP library")
     args = ap.parse_args()
@@ -283,7 +285,7 @@ def main():
     # the exact fp32-MFMA path (every GEMM on v_mfma_f32_32x32x2_f32) timed
     # beside the default bf16x3 path, same model and inputs (N=1 only)
     alt = None
-    if world == 1 and not cfg["bf16"] and cfg["f32_gemm"] == "bf16x3":
+    if world == 1 and not cfg["bf16"] and cfg["f32_gemm"] == "bf16x3" and not args.no_alt:
         for blk in model.conv:
             blk.f32_gemm = "mfma"
         for _ in range(2):
