@@ -85,8 +85,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // wave (wave w: rows (w&1)*32..+31, column tiles (w>>1)*4..+3; the C/D layout
 // is the same for v_mfma_f32_32x32x2_f32 and v_mfma_f32_32x32x16_bf16).
 // Adds the biases, the residual, ReLU and dropout, stores, and accumulates the
-// per-row BN statistics (fp64). smem: >= 2 KiB of LDS no wave reads any more.
-template <int V, int NCOLS>
+// per-row BN statistics (fp64). smem: >= 2 KiB of LDS no wave reads any more
+// (BV_LDS: + 64*V floats; the tile's rows of the bias table bias_rv are staged
+// there by coalesced loads instead of one scattered load per element).
+template <int V, int NCOLS, bool BV_LDS = false>
 __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
                                                    int n, int r0, int m0, float *smem) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -101,6 +103,14 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
   const __amdgpu_buffer_rsrc_t rs_b = make_rsrc(p.bias_r ? p.bias_r : p.out, p.bias_r ? p.R : 0);
   const __amdgpu_buffer_rsrc_t rs_bv =
       make_rsrc(p.bias_rv ? p.bias_rv : p.out, p.bias_rv ? (int64_t)p.R * V : 0);
+  float *sbv = smem + 512;  // past the statistics partials (2 KiB)
+  if constexpr (BV_LDS) {
+    if (p.bias_rv) {  // uniform
+      const int nrow = min(64, p.R - r0);
+      for (int i = tid; i < nrow * V; i += blockDim.x) sbv[i] = p.bias_rv[r0 * V + i];
+      __syncthreads();
+    }
+  }
   const __amdgpu_buffer_rsrc_t rs_res = make_rsrc(
       p.res ? p.res + (int64_t)n * p.out_bstride : p.out, p.res ? p.out_bstride : 0);
   int ocol[4], cv[4];
@@ -134,8 +144,12 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
         for (int j = 0; j < 4; ++j) {
           const bool ok = rok && cok[j];
           float val = acc[j][i] + br;
-          val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                               rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
+          if constexpr (BV_LDS) {
+            if (p.bias_rv && ok) val += sbv[(row - r0) * V + cv[j]];
+          } else {
+            val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
+          }
           const int off = ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB;
           if (p.res)
             val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, off, 0, 0));

@@ -247,10 +247,10 @@ struct ConvGeo {
   static constexpr int IROWS_P = 4 * DPW - WROWS;       // input rows incl. padding
   static constexpr int WBUF = WROWS * 256, IBUF = IROWS_P * 64;
   static constexpr int BUF = WBUF + IBUF;               // floats per ring slot
-  // ring depth: 3 slots for the temporal taps (chunk compute ~ DMA latency),
-  // 2 for the short spatial chunks (measured)
+  // ring depth: 3 slots (the short spatial chunks too: 2 slots measured 4-5%
+  // slower at the cfg2 layer shapes once bias_rv moved to LDS)
 #ifndef STGCN_STAGES1
-#define STGCN_STAGES1 2
+#define STGCN_STAGES1 3
 #endif
   static constexpr int STAGES = NQ == 1 ? STGCN_STAGES1 : 3;
   static_assert((STAGES - 2) * DPW < 64, "vmcnt range");
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
   }
   asm volatile("s_barrier" ::: "memory");  // every wave done reading the ring (LDS reuse)
 
-  conv_tile_epilogue<V, G::NCOLS>(p, acc, n, r0, m0, smem);
+  conv_tile_epilogue<V, G::NCOLS, NQ == 1>(p, acc, n, r0, m0, smem);
 }
 
 

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_bf16(ConvGemmParams p) {
     if (more) write_img(nxt + G::WCH);
   }
   __syncthreads();  // every wave done with the buffers (the epilogue reuses LDS)
-  conv_tile_epilogue<V, G::NCOLS>(p, acc, n, r0, m0, smem);
+  conv_tile_epilogue<V, G::NCOLS, NQ == 1>(p, acc, n, r0, m0, smem);
 }
 
 // Packs w[r*w_sr + c*w_sc + q*w_sq] as bf16 into
