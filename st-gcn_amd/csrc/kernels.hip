@@ -2207,42 +2207,48 @@ static bool launch_bwd5(const float *H, const float *x, const float *mean, const
 // k_spatial_bwd6: k_spatial_bwd5 for joint counts above 32 (two 32-column
 // output tiles, V = 50: the two-person graph) with up to 3 partitions, where
 // bwd5's register-resident B operand (all column tiles) and LDS dA accumulator
-// do not fit. RB = 64 rows per block (2 row tiles x 2 column tiles of dx =
-// one MFMA tile per wave, so a wave keeps only its column tile of A_k as the B
-// operand: K * V/2 VGPRs), and the K x 2 x 2 dA tiles are dealt to the 4 waves
-// (K tiles each) and stay in registers for the whole persistent loop, flushed
-// once by global atomics. Staging, BN1 sums and the dx store as in bwd5.
+// do not fit. RB = 64 rows per block, 8 waves (two per SIMD, so one wave's LDS
+// reads and row pass run under the other's MFMAs): dx = 2 row tiles x 2 column
+// tiles x 2 halves of the joint reduction (wave = tile + 4 * half, each half
+// keeping only its k-steps of its column tile of A_k as the B operand:
+// K * 13 VGPRs; the halves meet in LDS, summed by the row pass); the K x 2 x 2
+// dA tiles x 2 row halves of the block are dealt to the 8 waves (K each) and
+// stay in registers for the whole persistent loop, flushed once by global
+// atomics. Staging, BN1 sums and the dx store as in bwd5.
 template <int V, int KMAX>
-__global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
+__global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
     int K, int64_t rows, int write_dx, int relu) {
-  constexpr int RB = 64;
+  constexpr int RB = 64, NW = 8;
   constexpr int VH = (V + 1) / 2;  // MFMA k-steps over v
+  constexpr int VQ = (VH + 1) / 2; // ... per reduction half
   static_assert(V > 32 && V <= 64, "two 32-column tiles");
   constexpr int MAXSEG = 32;
   constexpr int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
   const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
-  float *dxs = smem + 2 * BUF;   // [RB][V]
+  float *dxs = smem + 2 * BUF;   // [RB][V]: reduction half 0, then dx
+  float *dxs2 = dxs + PL;        // [RB][V]: reduction half 1
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 5, lo = lane & 31;
   const int CT = C * T;
   const int nblocks = (int)(rows / RB);
   const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
-  const int rt = wave & 1, ct = wave >> 1;  // this wave's dx tile
+  const int rt = wave & 1, ct = (wave >> 1) & 1, kh = wave >> 2;  // this wave's dx tile, half
 
-  // B operand of the dx GEMM for column tile ct: A_k[v = 2s + hi][w = 32ct + lo]
-  float Bm[KMAX][VH];
+  // B operand of the dx GEMM for column tile ct, k-steps kh*VQ..+VQ-1:
+  // A_k[v = 2s + hi][w = 32ct + lo]
+  float Bm[KMAX][VQ];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-    for (int s2 = 0; s2 < VH; ++s2) {
-      const int v = 2 * s2 + hi, w = 32 * ct + lo;
-      Bm[k][s2] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
+    for (int j = 0; j < VQ; ++j) {
+      const int v = 2 * (kh * VQ + j) + hi, w = 32 * ct + lo;
+      Bm[k][j] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
     }
 
   auto stage = [&](int blk, float *buf) {
@@ -2250,19 +2256,20 @@ __global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
     const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
     constexpr int ND = PL / 256;
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + (int64_t)r0 * V, (int64_t)RB * V);
-    for (int i = wave; i < ND; i += 4)
+    for (int i = wave; i < ND; i += NW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + K * PL + i * 256, 16,
                                                (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
     for (int k = 0; k < K; ++k) {
       const __amdgpu_buffer_rsrc_t rh =
           make_rsrc(H + ((int64_t)(n0 * K + k) * CT + rem0) * V, (int64_t)RB * V);
-      for (int i = wave; i < ND; i += 4)
+      for (int i = wave; i < ND; i += NW)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, buf + k * PL + i * 256, 16,
                                                  (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
     }
   };
 
-  // dA tiles of this wave: j = wave + 4i (i < KMAX) -> (k = j / 4, p2 = (j / 2) & 1, q2 = j & 1)
+  // dA tiles of this wave: j = (wave & 3) + 4i (i < KMAX) -> (k = i, p2 = (j / 2) & 1,
+  // q2 = j & 1), over rows kh*32..+31 of each block
   floatx16 dacc[KMAX];
 #pragma unroll
   for (int i = 0; i < KMAX; ++i)
@@ -2280,31 +2287,32 @@ __global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
     const int r0 = blk * RB;
     const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
     const int cfirst = n0 * C + rem0 / T;
-    {  // dx tile (rt, ct)
+    {  // dx tile (rt, ct), reduction half kh
       floatx16 acc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
         if (k < K) {
-          const float *hr = Hs + k * PL + (rt * 32 + lo) * V + hi;
+          const float *hr = Hs + k * PL + (rt * 32 + lo) * V + hi + 2 * kh * VQ;
 #pragma unroll
-          for (int s2 = 0; s2 < VH; ++s2) {
-            const float av = (2 * s2 + hi < V) ? hr[2 * s2] : 0.f;
-            acc = mfma32(av, Bm[k][s2], acc);
+          for (int j = 0; j < VQ; ++j) {
+            const float av = (2 * (kh * VQ + j) + hi < V) ? hr[2 * j] : 0.f;
+            acc = mfma32(av, Bm[k][j], acc);
           }
         }
       }
+      float *dst = kh ? dxs2 : dxs;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int row = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
         const int w = 32 * ct + lo;
-        if (w < V) dxs[row * V + w] = acc[i];
+        if (w < V) dst[row * V + w] = acc[i];
       }
     }
-    __syncthreads();  // dx tile complete
-    {  // per row (4 threads each): BN1 sums, BN1(x) in place (see bwd5)
-      constexpr int TPR = 256 / RB;
+    __syncthreads();  // dx tile halves complete
+    {  // per row (8 threads each): dx = sum of halves, BN1 sums, BN1(x) in place (see bwd5)
+      constexpr int TPR = NW * 64 / RB;
       const int rl = tid / TPR, part = tid % TPR;
       const int rem = rem0 + rl;
       const int ci = rem / T;
@@ -2317,12 +2325,10 @@ __global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
         const int w = part + j * TPR;
         if (w < V) {
           const float xv = xs[rl * V + w];
-          float d = dxs[rl * V + w];
+          float d = dxs[rl * V + w] + dxs2[rl * V + w];
           const float bn = (xv - mu) * a + be;
-          if (relu && bn <= 0.f) {
-            d = 0.f;
-            dxs[rl * V + w] = 0.f;
-          }
+          if (relu && bn <= 0.f) d = 0.f;
+          dxs[rl * V + w] = d;
           s += d;
           sn = fmaf(d, (xv - mu) * is, sn);
           xs[rl * V + w] = relu ? fmaxf(bn, 0.f) : bn;
@@ -2348,7 +2354,7 @@ __global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
         atomicAdd(sdn + ci, (double)sn);
       }
     }
-    __syncthreads();  // BN1(x) rows and segment sums complete
+    __syncthreads();  // BN1(x) rows, dx and segment sums complete
     if (seg_lds && tid < MAXSEG) {
       const int gc = cfirst + tid;
       const int rlast = r0 + RB - 1;
@@ -2362,13 +2368,13 @@ __global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
     // dA tiles: dA_k[v in p2][w in q2] += sum_rows H_k[row][v] BN1(x)[row][w]
 #pragma unroll
     for (int i = 0; i < KMAX; ++i) {
-      const int j = wave + 4 * i;
+      const int j = (wave & 3) + 4 * i;
       const int k = j >> 2, p2 = (j >> 1) & 1, q2 = j & 1;
       if (k < K) {
         const float *hk = Hs + k * PL;
         const int cv = p2 * 32 + lo, cw = q2 * 32 + lo;
 #pragma unroll 8
-        for (int s2 = 0; s2 < RB / 2; ++s2) {
+        for (int s2 = kh * (RB / 4); s2 < (kh + 1) * (RB / 4); ++s2) {
           const int rr = 2 * s2 + hi;
           const float av = cv < V ? hk[rr * V + cv] : 0.f;
           const float bw = cw < V ? xs[rr * V + cw] : 0.f;
@@ -2378,13 +2384,13 @@ __global__ __launch_bounds__(256, 1) void k_spatial_bwd6(
     }
     if (write_dx) {
       float *dst = dx + (int64_t)r0 * V;
-      for (int e = tid; e < RB * V / 4; e += 256)
+      for (int e = tid; e < RB * V / 4; e += NW * 64)
         *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(dxs + e * 4);
     }
   }
 #pragma unroll
   for (int i = 0; i < KMAX; ++i) {
-    const int j = wave + 4 * i;
+    const int j = (wave & 3) + 4 * i;
     const int k = j >> 2, p2 = (j >> 1) & 1, q2 = j & 1;
     if (k < K) {
 #pragma unroll
@@ -2404,11 +2410,12 @@ static bool launch_bwd6(const float *H, const float *x, const float *mean, const
                         int write_dx, int relu, hipStream_t s) {
   constexpr int RB = 64;
   constexpr int PL = (RB * V + 255) / 256 * 256;
-  const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 1) * PL);
-  if (K != KT || lds > 160 * 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31)
+  const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 2) * PL);
+  if (K != KT || lds > 160 * 1024 - 512 || ((int64_t)C * T) % RB != 0 ||
+      rows >= (int64_t)1 << 31)
     return false;
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256));
-  hipLaunchKernelGGL((k_spatial_bwd6<V, KT>), grid, dim3(256), lds, s, H, x, mean, invstd, g, b,
+  hipLaunchKernelGGL((k_spatial_bwd6<V, KT>), grid, dim3(512), lds, s, H, x, mean, invstd, g, b,
                      A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
   return true;
 }
