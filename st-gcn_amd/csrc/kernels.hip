@@ -2216,6 +2216,9 @@ static bool launch_bwd5(const float *H, const float *x, const float *mean, const
 // stay in registers for the whole persistent loop, flushed once by global
 // atomics. Staging, BN1 sums and the dx store as in bwd5.
 template <int V, int KMAX>
+#ifndef STGCN_BWD6_EXP  // timing experiments only (bits skip work; results wrong)
+#define STGCN_BWD6_EXP 0
+#endif
 __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
@@ -2297,6 +2300,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
           const float *hr = Hs + k * PL + (rt * 32 + lo) * V + hi + 2 * kh * VQ;
 #pragma unroll
           for (int j = 0; j < VQ; ++j) {
+            if (STGCN_BWD6_EXP & 2) continue;
             const float av = (2 * (kh * VQ + j) + hi < V) ? hr[2 * j] : 0.f;
             acc = mfma32(av, Bm[k][j], acc);
           }
@@ -2311,7 +2315,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       }
     }
     __syncthreads();  // dx tile halves complete
-    {  // per row (8 threads each): dx = sum of halves, BN1 sums, BN1(x) in place (see bwd5)
+    if (!(STGCN_BWD6_EXP & 4)) {  // per row (8 threads each): dx = sum of halves, BN1 sums, BN1(x) in place (see bwd5)
       constexpr int TPR = NW * 64 / RB;
       const int rl = tid / TPR, part = tid % TPR;
       const int rem = rem0 + rl;
@@ -2375,6 +2379,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
         const int cv = p2 * 32 + lo, cw = q2 * 32 + lo;
 #pragma unroll 8
         for (int s2 = kh * (RB / 4); s2 < (kh + 1) * (RB / 4); ++s2) {
+          if (STGCN_BWD6_EXP & 1) continue;
           const int rr = 2 * s2 + hi;
           const float av = cv < V ? hk[rr * V + cv] : 0.f;
           const float bw = cw < V ? xs[rr * V + cw] : 0.f;
