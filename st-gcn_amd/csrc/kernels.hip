@@ -2215,10 +2215,30 @@ static bool launch_bwd5(const float *H, const float *x, const float *mean, const
 // dA tiles x 2 row halves of the block are dealt to the 8 waves (K each) and
 // stay in registers for the whole persistent loop, flushed once by global
 // atomics. Staging, BN1 sums and the dx store as in bwd5.
-template <int V, int KMAX>
+// exact 3-way bf16 split (x == h + m + l, see kernels_x3.hip) for bwd6's dA
+typedef __bf16 bwd6_bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bwd6_bf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned bwd6_pk(float a, float b) {
+  const bwd6_bf2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ void bwd6_split2(float a, float b, unsigned &h, unsigned &m,
+                                            unsigned &l) {
+  h = bwd6_pk(a, b);
+  const float ra = a - __builtin_bit_cast(float, h << 16);
+  const float rb = b - __builtin_bit_cast(float, h & 0xffff0000u);
+  m = bwd6_pk(ra, rb);
+  l = bwd6_pk(ra - __builtin_bit_cast(float, m << 16), rb - __builtin_bit_cast(float, m & 0xffff0000u));
+}
+__device__ __forceinline__ floatx16 bwd6_mfma(uint4 a, uint4 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bwd6_bf8, a),
+                                                 __builtin_bit_cast(bwd6_bf8, b), c, 0, 0, 0);
+}
+
 #ifndef STGCN_BWD6_EXP  // timing experiments only (bits skip work; results wrong)
 #define STGCN_BWD6_EXP 0
 #endif
+template <int V, int KMAX>
 __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
@@ -2235,6 +2255,10 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
   const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
   float *dxs = smem + 2 * BUF;   // [RB][V]: reduction half 0, then dx
   float *dxs2 = dxs + PL;        // [RB][V]: reduction half 1
+  // f(BN1(x)) split into 3 bf16 planes, joint-major [w][row] (pitch XTP: 16-byte
+  // row groups at an odd 16-byte stride), the dA GEMM's B operand
+  constexpr int XTP = RB + 8, XTPL = V * XTP * 2;
+  char *XT = reinterpret_cast<char *>(dxs2 + PL);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 5, lo = lane & 31;
@@ -2273,11 +2297,11 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
 
   // dA tiles of this wave: j = (wave & 3) + 4i (i < KMAX) -> (k = i, p2 = (j / 2) & 1,
   // q2 = j & 1), over rows kh*32..+31 of each block
-  floatx16 dacc[KMAX];
+  floatx16 dacc[KMAX], dacl[KMAX];
 #pragma unroll
   for (int i = 0; i < KMAX; ++i)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) dacc[i][e] = 0.f;
+    for (int e = 0; e < 16; ++e) dacc[i][e] = dacl[i][e] = 0.f;
 
   int blk = blockIdx.x;
   if (blk < nblocks) stage(blk, smem);
@@ -2335,7 +2359,14 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
           dxs[rl * V + w] = d;
           s += d;
           sn = fmaf(d, (xv - mu) * is, sn);
-          xs[rl * V + w] = relu ? fmaxf(bn, 0.f) : bn;
+          const float f = relu ? fmaxf(bn, 0.f) : bn;
+          const __bf16 fh = (__bf16)f;
+          const float r1 = f - (float)fh;
+          const __bf16 fm = (__bf16)r1;
+          __bf16 *xt = reinterpret_cast<__bf16 *>(XT) + w * XTP + rl;
+          xt[0] = fh;
+          xt[XTPL / 2] = fm;
+          xt[XTPL] = (__bf16)(r1 - (float)fm);
         }
       }
       const int seg0 = __builtin_amdgcn_readfirstlane(seg);
@@ -2369,21 +2400,42 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
         atomicAdd(sdn + cc, seg_n[tid]);
       }
     }
-    // dA tiles: dA_k[v in p2][w in q2] += sum_rows H_k[row][v] BN1(x)[row][w]
+    // dA tiles: dA_k[v in p2][w in q2] += sum_rows H_k[row][v] f(BN1(x))[row][w],
+    // rows kh*32..+31 as two 16-row k-steps of v_mfma_f32_32x32x16_bf16 on the
+    // exact 3-way splits: six products, h*h apart from the five cross terms
+    {
+      const int p2 = (wave >> 1) & 1, q2 = wave & 1;
+      const int cv = p2 * 32 + lo, cw = q2 * 32 + lo;
 #pragma unroll
-    for (int i = 0; i < KMAX; ++i) {
-      const int j = (wave & 3) + 4 * i;
-      const int k = j >> 2, p2 = (j >> 1) & 1, q2 = j & 1;
-      if (k < K) {
-        const float *hk = Hs + k * PL;
-        const int cv = p2 * 32 + lo, cw = q2 * 32 + lo;
-#pragma unroll 8
-        for (int s2 = kh * (RB / 4); s2 < (kh + 1) * (RB / 4); ++s2) {
-          if (STGCN_BWD6_EXP & 1) continue;
-          const int rr = 2 * s2 + hi;
-          const float av = cv < V ? hk[rr * V + cv] : 0.f;
-          const float bw = cw < V ? xs[rr * V + cw] : 0.f;
-          dacc[i] = mfma32(av, bw, dacc[i]);
+      for (int ks = 0; ks < 2; ++ks) {
+        if (STGCN_BWD6_EXP & 1) continue;
+        const int rb = kh * 32 + ks * 16 + 8 * hi;  // this lane's 8 rows
+        uint4 bh = {0, 0, 0, 0}, bm = bh, bl = bh;
+        if (cw < V) {
+          const char *xt = XT + (cw * XTP + rb) * 2;
+          bh = *reinterpret_cast<const uint4 *>(xt);
+          bm = *reinterpret_cast<const uint4 *>(xt + XTPL);
+          bl = *reinterpret_cast<const uint4 *>(xt + 2 * XTPL);
+        }
+#pragma unroll
+        for (int i = 0; i < KMAX; ++i) {
+          if (i < K) {
+            const float *hk = Hs + i * PL + rb * V + cv;
+            float av[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) av[e] = cv < V ? hk[e * V] : 0.f;
+            uint4 ah, am, al;
+            bwd6_split2(av[0], av[1], ah.x, am.x, al.x);
+            bwd6_split2(av[2], av[3], ah.y, am.y, al.y);
+            bwd6_split2(av[4], av[5], ah.z, am.z, al.z);
+            bwd6_split2(av[6], av[7], ah.w, am.w, al.w);
+            dacc[i] = bwd6_mfma(ah, bh, dacc[i]);
+            dacl[i] = bwd6_mfma(ah, bm, dacl[i]);
+            dacl[i] = bwd6_mfma(am, bh, dacl[i]);
+            dacl[i] = bwd6_mfma(ah, bl, dacl[i]);
+            dacl[i] = bwd6_mfma(am, bm, dacl[i]);
+            dacl[i] = bwd6_mfma(al, bh, dacl[i]);
+          }
         }
       }
     }
@@ -2402,7 +2454,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       for (int e = 0; e < 16; ++e) {
         const int v = p2 * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
         const int w = q2 * 32 + lo;
-        if (v < V && w < V) atomicAdd(dA + (k * V + v) * V + w, dacc[i][e]);
+        if (v < V && w < V) atomicAdd(dA + (k * V + v) * V + w, dacc[i][e] + dacl[i][e]);
       }
     }
   }
@@ -2415,7 +2467,7 @@ static bool launch_bwd6(const float *H, const float *x, const float *mean, const
                         int write_dx, int relu, hipStream_t s) {
   constexpr int RB = 64;
   constexpr int PL = (RB * V + 255) / 256 * 256;
-  const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 2) * PL);
+  const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 2) * PL) + 3 * (size_t)V * (RB + 8) * 2;
   if (K != KT || lds > 160 * 1024 - 512 || ((int64_t)C * T) % RB != 0 ||
       rows >= (int64_t)1 << 31)
     return false;
