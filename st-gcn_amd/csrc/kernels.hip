@@ -1957,15 +1957,25 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
 //                                                    as the B operand (k = v)
 //   BN1 sums per row from the dx tile in LDS, BN1(x) in place (one thread/row)
 //   dA_k[v][w] += sum_rows H_k[row][v] BN1(x)[row][w]  MFMA, LDS accumulator
-// dx leaves through LDS as float4 stores. Requires K * ceil(V/2) * ceil(V/32)
-// <= 48 (B-operand registers) and the k_spatial_bwd4 host conditions.
+// dx leaves through LDS as float4 stores. With 3 partitions, 8 waves (two per
+// SIMD): wave w takes dx row tile w & 3 (if < RB/32) over half w >> 2 of the
+// joint reduction (the halves meet in LDS and are summed by the row pass), and
+// rows 2(w + 8j) + h of the dA partials; with 1 or 2 partitions 4 waves and
+// the whole reduction per wave (measured: 8 waves are slower at V = 18, K = 1,
+// 7% faster at V = 25, K = 3). Requires K * ceil(V/2) * ceil(V/32) <= 48 (B-operand
+// registers) and the k_spatial_bwd4 host conditions.
+constexpr int bwd5_nw(int kmax) { return kmax >= 3 ? 8 : 4; }
+
 template <int V, int RB, int KMAX>
-__global__ __launch_bounds__(256) void k_spatial_bwd5(
+__global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
     int K, int64_t rows, int write_dx, int relu) {
   constexpr int VH = (V + 1) / 2;           // MFMA k-steps over v
+  constexpr int NW = bwd5_nw(KMAX);         // waves
+  constexpr int NH = NW / 4;                // reduction halves of the dx GEMM
+  constexpr int VQ = (VH + NH - 1) / NH;    // MFMA k-steps per half
   constexpr int NT = (V + 31) / 32;         // 32-column output tiles over w
   constexpr int DW = NT * 32;
   constexpr int MAXSEG = 32;
@@ -1975,8 +1985,9 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
   const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
-  float *dxs = smem + 2 * BUF;   // [RB][V]
-  float *dred = dxs + PL;        // [K][DW][DW]
+  float *dxs = smem + 2 * BUF;   // [RB][V]: reduction half 0, then dx
+  float *dxs2 = dxs + PL;        // [RB][V]: reduction half 1 (NH == 2)
+  float *dred = dxs + NH * PL;   // [K][DW][DW]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 5, lo = lane & 31;
@@ -1984,15 +1995,17 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
   const int nblocks = (int)(rows / RB);
   const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
 
-  // B operand of the dx GEMM: Bm[k][s][t] = A_k[v = 2s + hi][w = 32t + lo] (0 outside)
-  float Bm[KMAX][VH][NT];
+  const int kh = wave >> 2, rtile = wave & 3;  // dx reduction half, row tile
+  // B operand of the dx GEMM, this wave's half: Bm[k][j][t] = A_k[v = 2(kh VQ + j) + hi]
+  // [w = 32t + lo] (0 outside)
+  float Bm[KMAX][VQ][NT];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-    for (int s2 = 0; s2 < VH; ++s2)
+    for (int s2 = 0; s2 < VQ; ++s2)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const int v = 2 * s2 + hi, w = 32 * t + lo;
+        const int v = 2 * (kh * VQ + s2) + hi, w = 32 * t + lo;
         Bm[k][s2][t] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
       }
 
@@ -2001,19 +2014,19 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
     const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
     constexpr int ND = PL / 256;  // DMA rounds per plane
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x + (int64_t)r0 * V, (int64_t)RB * V);
-    for (int i = wave; i < ND; i += 4)
+    for (int i = wave; i < ND; i += NW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, buf + K * PL + i * 256, 16,
                                                (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
     for (int k = 0; k < K; ++k) {
       const __amdgpu_buffer_rsrc_t rh =
           make_rsrc(H + ((int64_t)(n0 * K + k) * CT + rem0) * V, (int64_t)RB * V);
-      for (int i = wave; i < ND; i += 4)
+      for (int i = wave; i < ND; i += NW)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rh, buf + k * PL + i * 256, 16,
                                                  (unsigned)(i * 256 + lane * 4) * 4u, 0, 0, 0);
     }
   };
 
-  for (int i = tid; i < K * DW * DW; i += 256) dred[i] = 0.f;
+  for (int i = tid; i < K * DW * DW; i += NW * 64) dred[i] = 0.f;
   floatx16 dacc[DREG ? KMAX : 1][NT][NT];
   auto zero_dacc = [&](int kd) {
 #pragma unroll
@@ -2051,8 +2064,9 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
     const int r0 = blk * RB;
     const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
     const int cfirst = n0 * C + rem0 / T;  // global (n*C + ci) of row r0
-    // dx tile of this wave's 32 rows on MFMA (RB = 64: waves 2, 3 idle here)
-    if (wave < NRT) {
+    // dx tile rtile (32 rows), reduction half kh, on MFMA (RB = 64: waves 2, 3,
+    // 6, 7 idle here)
+    if (rtile < NRT) {
       floatx16 acc[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -2061,10 +2075,10 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
         if (k < K) {
-          const float *hr = Hs + k * PL + (wave * 32 + lo) * V + hi;
+          const float *hr = Hs + k * PL + (rtile * 32 + lo) * V + hi + 2 * kh * VQ;
 #pragma unroll
-          for (int s2 = 0; s2 < VH; ++s2) {
-            const float av = (2 * s2 + hi < V) ? hr[2 * s2] : 0.f;
+          for (int s2 = 0; s2 < VQ; ++s2) {
+            const float av = (2 * (kh * VQ + s2) + hi < V) ? hr[2 * s2] : 0.f;
 #pragma unroll
             for (int t = 0; t < NT; ++t) acc[t] = mfma32(av, Bm[k][s2][t], acc[t]);
           }
@@ -2074,9 +2088,9 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int row = wave * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int row = rtile * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
           const int w = 32 * t + lo;
-          if (w < V) dxs[row * V + w] = acc[t][i];
+          if (w < V) (kh ? dxs2 : dxs)[row * V + w] = acc[t][i];
         }
     }
     __syncthreads();  // dx tile complete
@@ -2084,7 +2098,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
     // place; per-channel-segment sums (a wave's rows usually share one
     // channel: then one wave reduction)
     {
-      constexpr int TPR = 256 / RB;
+      constexpr int TPR = NW * 64 / RB;
       const int rl = tid / TPR, part = tid % TPR;
       const int rem = rem0 + rl;
       const int ci = rem / T;
@@ -2097,12 +2111,10 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
         const int w = part + j * TPR;
         if (w < V) {
           const float xv = xs[rl * V + w];
-          float d = dxs[rl * V + w];
+          float d = NH == 2 ? dxs[rl * V + w] + dxs2[rl * V + w] : dxs[rl * V + w];
           const float bn = (xv - mu) * a + be;
-          if (relu && bn <= 0.f) {  // ReLU'(BN1(x))
-            d = 0.f;
-            dxs[rl * V + w] = 0.f;
-          }
+          if (relu && bn <= 0.f) d = 0.f;  // ReLU'(BN1(x))
+          dxs[rl * V + w] = d;
           s += d;
           sn = fmaf(d, (xv - mu) * is, sn);
           xs[rl * V + w] = relu ? fmaxf(bn, 0.f) : bn;
@@ -2139,7 +2151,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
         atomicAdd(sdn + cc, seg_n[tid]);
       }
     }
-    // dA partials on MFMA: wave takes row pairs kk = wave + 4j; accumulators
+    // dA partials on MFMA: wave takes row pairs kk = wave + 8j; accumulators
     // stay in registers across blocks (DREG) or are flushed per block
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -2147,8 +2159,8 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
         floatx16(&dk)[NT][NT] = dacc[DREG ? k : 0];
         const float *hk = Hs + k * PL;
 #pragma unroll
-        for (int j = 0; j < RB / 8; ++j) {
-          const int rr = 2 * (wave + 4 * j) + hi;
+        for (int j = 0; j < RB / (2 * NW); ++j) {
+          const int rr = 2 * (wave + NW * j) + hi;
           float av[NT], bw[NT];
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
@@ -2166,7 +2178,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
     }
     if (write_dx) {
       float *dst = dx + (int64_t)r0 * V;
-      for (int e = tid; e < RB * V / 4; e += 256)
+      for (int e = tid; e < RB * V / 4; e += NW * 64)
         *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(dxs + e * 4);
     }
   }
@@ -2176,7 +2188,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd5(
       if (k < K) flush_dacc(k);
   }
   __syncthreads();
-  for (int i = tid; i < K * V * V; i += 256) {
+  for (int i = tid; i < K * V * V; i += NW * 64) {
     const int k = i / (V * V), rm = i - k * V * V, v = rm / V, w = rm - v * V;
     atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
   }
@@ -2186,7 +2198,8 @@ template <int V, int RB>
 static size_t bwd5_lds(int K) {
   constexpr int PL = (RB * V + 255) / 256 * 256;
   constexpr int DW = (V + 31) / 32 * 32;
-  return sizeof(float) * ((size_t)(2 * (K + 1) + 1) * PL + (size_t)K * DW * DW);
+  const int nh = bwd5_nw(K) / 4;
+  return sizeof(float) * ((size_t)(2 * (K + 1) + nh) * PL + (size_t)K * DW * DW);
 }
 
 template <int V, int RB, int KT>
@@ -2195,11 +2208,11 @@ static bool launch_bwd5(const float *H, const float *x, const float *mean, const
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
                         int write_dx, int relu, hipStream_t s) {
   const size_t lds = bwd5_lds<V, RB>(K);
-  if (lds > 160 * 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
+  if (lds > 160 * 1024 - 512 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
   const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 512))));
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
   if (K != KT) return false;
-  hipLaunchKernelGGL((k_spatial_bwd5<V, RB, KT>), grid, dim3(256), lds, s, H, x, mean, invstd, g,
+  hipLaunchKernelGGL((k_spatial_bwd5<V, RB, KT>), grid, dim3(bwd5_nw(KT) * 64), lds, s, H, x, mean, invstd, g,
                      b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
   return true;
 }
@@ -2245,8 +2258,6 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
     int K, int64_t rows, int write_dx, int relu) {
   constexpr int RB = 64, NW = 8;
-  constexpr int VH = (V + 1) / 2;  // MFMA k-steps over v
-  constexpr int VQ = (VH + 1) / 2; // ... per reduction half
   static_assert(V > 32 && V <= 64, "two 32-column tiles");
   constexpr int MAXSEG = 32;
   constexpr int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
@@ -2267,15 +2278,23 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
   const bool seg_lds = (RB + T - 1) / T + 1 <= MAXSEG;
   const int rt = wave & 1, ct = (wave >> 1) & 1, kh = wave >> 2;  // this wave's dx tile, half
 
-  // B operand of the dx GEMM for column tile ct, k-steps kh*VQ..+VQ-1:
-  // A_k[v = 2s + hi][w = 32ct + lo]
-  float Bm[KMAX][VQ];
+  // B operand of the dx GEMM (v_mfma_f32_32x32x16_bf16 on exact 3-way splits):
+  // column tile ct, joints v = 32 kh + 16 ks + 8 hi + j (ks = 0, 1): this wave's
+  // half of the reduction, A_k[v][w = 32ct + lo] split into h / m / l planes
+  uint4 Bh[KMAX][2], Bmd[KMAX][2], Bl[KMAX][2];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-    for (int j = 0; j < VQ; ++j) {
-      const int v = 2 * (kh * VQ + j) + hi, w = 32 * ct + lo;
-      Bm[k][j] = (k < K && v < V && w < V) ? A[(k * V + v) * V + w] : 0.f;
+    for (int ks = 0; ks < 2; ++ks) {
+      const int v0 = 32 * kh + 16 * ks + 8 * hi, w = 32 * ct + lo;
+      float bv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        bv[j] = (k < K && v0 + j < V && w < V) ? A[(k * V + v0 + j) * V + w] : 0.f;
+      bwd6_split2(bv[0], bv[1], Bh[k][ks].x, Bmd[k][ks].x, Bl[k][ks].x);
+      bwd6_split2(bv[2], bv[3], Bh[k][ks].y, Bmd[k][ks].y, Bl[k][ks].y);
+      bwd6_split2(bv[4], bv[5], Bh[k][ks].z, Bmd[k][ks].z, Bl[k][ks].z);
+      bwd6_split2(bv[6], bv[7], Bh[k][ks].w, Bmd[k][ks].w, Bl[k][ks].w);
     }
 
   auto stage = [&](int blk, float *buf) {
@@ -2314,22 +2333,36 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const int r0 = blk * RB;
     const int n0 = r0 / CT, rem0 = r0 - n0 * CT;
     const int cfirst = n0 * C + rem0 / T;
-    {  // dx tile (rt, ct), reduction half kh
-      floatx16 acc;
+    {  // dx tile (rt, ct), reduction half kh: six bf16 products per fp32 product
+      floatx16 acc, acl;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+      for (int i = 0; i < 16; ++i) acc[i] = acl[i] = 0.f;
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
         if (k < K) {
-          const float *hr = Hs + k * PL + (rt * 32 + lo) * V + hi + 2 * kh * VQ;
 #pragma unroll
-          for (int j = 0; j < VQ; ++j) {
+          for (int ks = 0; ks < 2; ++ks) {
             if (STGCN_BWD6_EXP & 2) continue;
-            const float av = (2 * (kh * VQ + j) + hi < V) ? hr[2 * j] : 0.f;
-            acc = mfma32(av, Bm[k][j], acc);
+            const int v0 = 32 * kh + 16 * ks + 8 * hi;
+            const float *hr = Hs + k * PL + (rt * 32 + lo) * V + v0;
+            float av[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) av[j] = v0 + j < V ? hr[j] : 0.f;
+            uint4 ah, am, al;
+            bwd6_split2(av[0], av[1], ah.x, am.x, al.x);
+            bwd6_split2(av[2], av[3], ah.y, am.y, al.y);
+            bwd6_split2(av[4], av[5], ah.z, am.z, al.z);
+            bwd6_split2(av[6], av[7], ah.w, am.w, al.w);
+            acc = bwd6_mfma(ah, Bh[k][ks], acc);
+            acl = bwd6_mfma(ah, Bmd[k][ks], acl);
+            acl = bwd6_mfma(am, Bh[k][ks], acl);
+            acl = bwd6_mfma(ah, Bl[k][ks], acl);
+            acl = bwd6_mfma(am, Bmd[k][ks], acl);
+            acl = bwd6_mfma(al, Bh[k][ks], acl);
           }
         }
       }
+      acc += acl;
       float *dst = kh ? dxs2 : dxs;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
