@@ -75,8 +75,15 @@ struct ConvBf16Geo {
   static_assert(CK % 16 == 0 && (SLOTS & 1), "k-step = 16 channels; odd slot pitch");
 };
 
+#ifndef STGCN_CB1_CK  // chunk channels of the NQ = 1 (spatial / projection) GEMMs
+#define STGCN_CB1_CK 16
+#endif
+#ifndef STGCN_CB1_MINB  // ... and their minimum resident workgroups per CU
+#define STGCN_CB1_MINB 2
+#endif
+
 template <int NQ, int CK, int V, int SIN>
-__global__ __launch_bounds__(256, 2) void k_conv_bf16(ConvGemmParams p) {
+__global__ __launch_bounds__(256, NQ == 1 ? STGCN_CB1_MINB : 2) void k_conv_bf16(ConvGemmParams p) {
   using G = ConvBf16Geo<NQ, CK, V, SIN>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
@@ -211,7 +218,7 @@ __global__ void k_pack_conv_w_bf16(const float *w, __bf16 *wpk, int R, int C, in
   wpk[idx] = (__bf16)v;
 }
 
-static int conv_bf16_ck(int NQ) { return NQ == 1 ? 32 : 16; }
+static int conv_bf16_ck(int NQ) { return NQ == 1 ? STGCN_CB1_CK : 16; }
 
 bool conv_bf16_supported(const ConvGemmParams &p) {
   // a reduction over fewer than 16 channels (the first block's C_in = 3: the
@@ -235,7 +242,7 @@ size_t conv_bf16_lds_bytes(const ConvGemmParams &p) {
 template <int NQ, int V, int SIN>
 static bool launch_cb_if(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
   if (p.V != V || p.s_in != SIN) return false;
-  constexpr int CK = NQ == 1 ? 32 : 16;
+  constexpr int CK = NQ == 1 ? STGCN_CB1_CK : 16;
   hipLaunchKernelGGL((k_conv_bf16<NQ, CK, V, SIN>), dim3(nblk), dim3(256), lds, s, p);
   return true;
 }
