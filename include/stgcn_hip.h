@@ -12,7 +12,10 @@
  * stride (st_graphconv.py:24-28), i.e. SpatialTemporalConv.forward
  * (src/network/st_graphconv.py:85-109, residual_block :60-82) with
  * SpatialConv.forward (st_graphconv.py:139-152) and its autograd backward.
- * Dropout (p > 0) is applied by the caller on y.
+ * Dropout (p > 0, training) is fused into the block's output pass
+ * (stgcn_fwd_args_t.dropout_p / seed, ABI 2); training and eval mode are
+ * both differentiable (eval: BatchNorm with the running statistics as
+ * constants, ABI 4).
  * The reference has no FFI of its own (pure Python over PyTorch); the entry
  * points below are what its module boundary binds to (the ctypes binding in
  * st-gcn_amd/hip_lib.py, shown in INTEGRATION.md):
@@ -23,6 +26,8 @@
  *                    residual_block :60-82 with apply_residual :24-28)
  *   stgcn_block_bwd  replaces the autograd backward of the same ops
  *                    (driven by lightning_model.py:199-205 -> loss.backward())
+ *   stgcn_spatial_fwd / stgcn_spatial_bwd  replace SpatialConv.forward used on
+ *                    its own (st_graphconv.py:139-152) and its backward (ABI 4)
  *
  * Conventions
  *   - All tensors are caller-owned, contiguous, fp32, device memory, layout
@@ -46,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 3
+#define STGCN_ABI_VERSION 4
 
 /* stgcn_desc_t.flags */
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
@@ -140,6 +145,13 @@ typedef struct stgcn_bwd_args {
   double *prev_sums;
   float dropout_p;                      /* the forward's dropout (same seed)  */
   uint64_t seed;
+  /* ABI 4, optional with prev_sums: the previous block's saved pre-BN2 tensor
+   * U (N, C_in, T, V) and its stats (mean2[C_in], invstd2[C_in]). Channels
+   * where reconstructing uhat = (x - prev_b2) / prev_g2 from x is
+   * ill-conditioned (|prev_b2| > 4 |prev_g2|, including prev_g2 == 0) read
+   * uhat from U instead. Null: reconstruct everywhere. */
+  const float *prev_U;
+  const float *prev_stats;
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);
@@ -155,6 +167,29 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
                     void *workspace, size_t workspace_bytes, void *stream);
 int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a,
                     void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * ABI 4: SpatialConv on its own (st_graphconv.py:139-152):
+ *   out[n,c,t,v] = sum_k sum_w A[k,v,w] * (W_k x[n,:,t,w] + bW_k)[c]
+ * computed as out = sum_k W_k (x A_k^T) + sum_k bW_k rowsum(A_k) (the block's
+ * form (1), no BatchNorm). x (N, C_in, T, V), A (K, V, V), W (K*C_out, C_in),
+ * bW (K*C_out), out (N, C_out, T, V); flags: STGCN_F_BF16 runs the channel
+ * GEMMs on bf16 MFMA (fp32 otherwise). Backward: dout -> dx (may be null),
+ * dA, dW, dbW.
+ */
+typedef struct stgcn_spatial_desc {
+  int32_t N, C_in, C_out, T, V, K;
+  int32_t flags;       /* 0 or STGCN_F_BF16                                 */
+} stgcn_spatial_desc_t;
+
+size_t stgcn_spatial_workspace_bytes(const stgcn_spatial_desc_t *d, int backward);
+int stgcn_spatial_fwd(const stgcn_spatial_desc_t *d, const float *x, const float *A,
+                      const float *W, const float *bW, float *out, void *workspace,
+                      size_t workspace_bytes, void *stream);
+int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const float *x,
+                      const float *A, const float *W, const float *bW, float *dx, float *dA,
+                      float *dW, float *dbW, void *workspace, size_t workspace_bytes,
+                      void *stream);
 
 /* Measurement (bench.py roofline): time one of the block's GEMM kernels,
  * launched `iters` times with the exact parameters the block uses for this

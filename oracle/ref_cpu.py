@@ -125,10 +125,10 @@ def block_forward(x, p, b, stride, pad=4, residual=False, training=True,
     if residual:
         res = x.clone()
         f = _bn(x, p, b, "batch_n", training, momentum, eps)
-        f = F.relu(f.clone())
+        f = F.relu(f.clone(), inplace=True)
         f = spatial_conv(f, A, p["spatialConv.W.weight"], p["spatialConv.W.bias"], gemm_bf16)
         f = _bn(f, p, b, "batch_n_2", training, momentum, eps)
-        f = F.relu(f.clone()) if inner_mask is None else f * inner_mask.to(f.dtype)
+        f = F.relu(f.clone(), inplace=True) if inner_mask is None else f * inner_mask.to(f.dtype)
         f = _conv(f, p["temporalConv.weight"], p["temporalConv.bias"],
                   stride=(stride, 1), padding=(pad, 0), gemm_bf16=gemm_bf16)
         if "apply_residual.weight" in p:
@@ -146,7 +146,7 @@ def block_forward(x, p, b, stride, pad=4, residual=False, training=True,
         return f
     if relu_mask is not None:
         return f * relu_mask.to(f.dtype)
-    return F.relu(f.clone())
+    return F.relu(f.clone(), inplace=True)  # nn.ReLU(inplace=True) on a clone (:49, :105)
 
 
 def block_params_from_arrays(arrays, prefix="param.", dtype=torch.float32, requires_grad=True):
@@ -199,14 +199,26 @@ class Stack:
     def __init__(self, params, buffers, residual=False):
         self.p, self.b, self.residual = params, buffers, residual
 
-    def forward(self, x_ntvc, training=True, dtype=torch.float32, gemm_bf16=False):
+    def forward(self, x_ntvc, training=True, dtype=torch.float32, gemm_bf16=False,
+                relu_masks=None):
+        """relu_masks (optional, one 0/1 tensor per block): each block's final
+        ReLU uses that mask (block_forward's relu_mask: the parity tests
+        differentiate through the implementation's own subgradient choices at
+        ReLU ties); the blocks' pre-ReLU values are then kept in ``self.pre``."""
         x = x_ntvc.to(dtype).permute(0, 3, 1, 2)
+        self.pre = []
         for i, (_, s) in enumerate(LAYERS):
             pre = f"conv.{i}."
             p = {k[len(pre):]: v for k, v in self.p.items() if k.startswith(pre)}
             b = {k[len(pre):]: v for k, v in self.b.items() if k.startswith(pre)}
-            x = block_forward(x, p, b, s, residual=self.residual, training=training, dtype=dtype,
-                              gemm_bf16=gemm_bf16)
+            if relu_masks is None:
+                x = block_forward(x, p, b, s, residual=self.residual, training=training,
+                                  dtype=dtype, gemm_bf16=gemm_bf16)
+            else:
+                f = block_forward(x, p, b, s, residual=self.residual, training=training,
+                                  dtype=dtype, gemm_bf16=gemm_bf16, return_pre_relu=True)
+                self.pre.append(f.detach())
+                x = f * relu_masks[i].to(f.dtype)
             for k, v in b.items():
                 self.b[pre + k] = v
         V = x.shape[3]
@@ -215,14 +227,29 @@ class Stack:
         return F.linear(x, self.p["fc_layer.weight"], self.p["fc_layer.bias"])
 
 
-def init_stack_params(C_in, nr_classes, A, seed=0, residual=False):
+def init_stack_params(C_in, nr_classes, A, seed=0, residual=False, masks=None,
+                      max_mask_jitter=0.001):
     """Parameters with the reference's module init order under
     ``torch.manual_seed(seed)`` (lightning_model.py:65-88): for every block
     BN1, W, temporal conv, BN2 (st_graphconv.py:28-46), then the FC layer.
-    Returns (params, buffers) dicts in state_dict naming."""
+    Returns (params, buffers) dicts in state_dict naming.
+
+    masks: None (no edge importance), "jitter" (L_STGCN --use_edge_importance,
+    lightning_model.py:53-57: ten masks 1 + 2(randn_like(A) - 0.5)*jitter drawn
+    before the blocks) or "ones" (legacy STGCN, stgcn.py:33-35); the masks are
+    returned in params as ``Masks.{i}`` and block i starts from A * Masks[i]."""
     import torch.nn as nn
     torch.manual_seed(seed)
     p, b = {}, {}
+    mk = [None] * len(LAYERS)
+    if masks == "jitter":
+        jit = [2 * (torch.randn_like(A) - 0.5) * max_mask_jitter for _ in LAYERS]
+        mk = [jit[i] + torch.ones(A.shape) for i in range(len(LAYERS))]
+    elif masks == "ones":
+        mk = [torch.ones(A.shape) for _ in LAYERS]
+    for i, m in enumerate(mk):
+        if m is not None:
+            p[f"Masks.{i}"] = m
     c = C_in
     for i, (co, s) in enumerate(LAYERS):
         pre = f"conv.{i}."
@@ -241,7 +268,7 @@ def init_stack_params(C_in, nr_classes, A, seed=0, residual=False):
             b[pre + name + ".running_mean"] = m.running_mean.clone()
             b[pre + name + ".running_var"] = m.running_var.clone()
             b[pre + name + ".num_batches_tracked"] = m.num_batches_tracked.clone()
-        p[pre + "spatialConv.A"] = A.float().clone()
+        p[pre + "spatialConv.A"] = (A if mk[i] is None else A * mk[i]).float().clone()
         p[pre + "spatialConv.W.weight"] = w.weight.detach()
         p[pre + "spatialConv.W.bias"] = w.bias.detach()
         p[pre + "temporalConv.weight"] = t.weight.detach()

@@ -1,13 +1,18 @@
-"""Build libstgcn_hip.so in-tree with hipcc for gfx950 (no cmake, no JIT)."""
+"""Build libstgcn_hip.so in-tree with hipcc for gfx950 (no cmake, no JIT).
+
+Each source is compiled to its own object in parallel (no cross-TU device
+calls, so no -fgpu-rdc is needed) and the objects are linked into one shared
+library."""
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libstgcn_hip.so")
 SOURCES = ["kernels.hip", "kernels_bf16.hip", "kernels_x3.hip", "train_ops.hip", "capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wall"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall"]
 
 
 def build(verbose=False, variant=None, defines=()):
@@ -15,9 +20,24 @@ def build(verbose=False, variant=None, defines=()):
     kernel experiments, loaded with STGCN_LIB_VARIANT=<variant>)."""
     out = OUT if variant is None else os.path.join(os.path.dirname(OUT),
                                                    f"libstgcn_hip_{variant}.so")
+    objdir = os.path.join(HERE, "build", variant or "default")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines],
-           *[os.path.join(CSRC, s) for s in SOURCES], "-o", out + ".tmp"]
+    os.makedirs(objdir, exist_ok=True)
+    defs = [f"-D{d}" for d in defines]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, src + ".o")
+        cmd = [HIPCC, *FLAGS, *defs, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

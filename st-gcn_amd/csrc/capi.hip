@@ -511,7 +511,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   const Dropout drop = make_dropout(d, a->dropout_p, a->seed);
   if (drop.thresh && a->dy_sums)
     return fail(STGCN_E_INVALID, "dy_sums cannot be combined with dropout");
-  if (!d->training) return fail(STGCN_E_UNSUPPORTED, "backward in eval mode is not implemented");
+  if (!d->training && (a->dy_sums || a->prev_sums))
+    return fail(STGCN_E_INVALID, "stack chaining applies to training mode only");
   const BwdLayout L = bwd_layout(d, workspace);
   if (!workspace || workspace_bytes < L.total)
     return fail(STGCN_E_INVALID, "workspace too small");
@@ -533,7 +534,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                                         L.sg, L.sgu, drop, s));
     }
     HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
-                                     L.sdu, N, R, To * V, drop, s));
+                                     L.sdu, N, R, To * V, d->training, drop, s));
     HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
     // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
@@ -594,7 +595,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_bn_relu_bwd_reduce(L.dZ, a->Z, mean2, invstd2, a->g2, a->b2, N, R, T * V,
                                       L.sg, L.sgu, Dropout(), s));
     HIP_TRY(launch_bn_relu_bwd_apply(L.dZ, a->Z, mean2, invstd2, a->g2, a->b2, L.sg, L.sgu,
-                                     L.dZ, L.sdu, N, R, T * V, Dropout(), s));
+                                     L.dZ, L.sdu, N, R, T * V, d->training, Dropout(), s));
     HIP_TRY(launch_bn_grads_out(L.sg, L.sgu, nullptr, R, a->dg2, a->db2, nullptr, s));
   }
   // Spatial conv backward. Recompute G = f(BN1(x)) A^T (f = ReLU in the
@@ -684,12 +685,15 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     }
   }
   if (d->need_dx) {
-    const bool chain = a->prev_g2 && a->prev_b2 && a->prev_sums;
+    const bool chain = d->training && a->prev_g2 && a->prev_b2 && a->prev_sums;
+    const bool chain_u = chain && a->prev_U && a->prev_stats;
     if (chain) HIP_TRY(hipMemsetAsync(a->prev_sums, 0, sizeof(double) * 2 * C, s));
     HIP_TRY(launch_bn1_bwd_apply(a->dx, a->x, mean1, invstd1, a->g1, L.sd, L.sdn, add, N, C,
-                                 T * V, (int64_t)N * T * V, chain ? a->prev_g2 : nullptr,
-                                 chain ? a->prev_b2 : nullptr, chain ? a->prev_sums : nullptr,
-                                 s));
+                                 T * V, (int64_t)N * T * V, d->training,
+                                 chain ? a->prev_g2 : nullptr, chain ? a->prev_b2 : nullptr,
+                                 chain ? a->prev_sums : nullptr, chain_u ? a->prev_U : nullptr,
+                                 chain_u ? a->prev_stats : nullptr,
+                                 chain_u ? a->prev_stats + C : nullptr, s));
   }
   return STGCN_OK;
 }
@@ -862,6 +866,200 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
   (void)hipEventDestroy(e1);
   *avg_ms = ms / iters;
   *flops = P.flops;
+  return STGCN_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// SpatialConv on its own (st_graphconv.py:139-152), ABI 4: the block's
+// spatial kernels with BatchNorm replaced by the identity (mean 0, invstd 1,
+// gamma 1, beta 0: (x - 0) * 1 * 1 + 0 == x exactly in fp32).
+//   fwd: G = x A_k^T (joint contraction), out = W' G + sum_k bW_k rowsum(A_k)
+//   bwd: dW' = dout G^T, H = W'^T dout, dx = sum_k H_k A_k,
+//        dA = sum H_k^T x + bias part, dbW = sum dout rowsum(A_k)
+// ---------------------------------------------------------------------------
+namespace {
+
+// A block descriptor with the spatial shape (stride 1; the temporal fields
+// only satisfy the planner).
+stgcn_desc_t spatial_as_block(const stgcn_spatial_desc_t *sd) {
+  stgcn_desc_t d{};
+  d.N = sd->N;
+  d.C_in = sd->C_in;
+  d.C_out = sd->C_out;
+  d.T = sd->T;
+  d.T_out = sd->T;
+  d.V = sd->V;
+  d.K = sd->K;
+  d.gamma = 9;
+  d.stride = 1;
+  d.pad = 4;
+  d.eps = 1e-5f;
+  d.momentum = 0.1f;
+  d.training = 1;
+  d.need_dx = 1;
+  d.flags = sd->flags & STGCN_F_BF16;
+  return d;
+}
+
+struct SpatialLayout {
+  float *ident;  // [4][C_in]: mean 0 | invstd 1 | gamma 1 | beta 0
+  double *sd, *sdn, *SdZ;
+  float *G, *H, *Wpk, *biasZ, *wpk, *slab;
+  size_t total;
+};
+
+SpatialLayout spatial_layout(const stgcn_desc_t *d, void *ws, bool backward) {
+  Carve c(ws);
+  SpatialLayout L{};
+  const int R = d->C_out, C = d->C_in, K = d->K;
+  L.ident = c.take<float>((size_t)4 * C);
+  L.G = c.take<float>((size_t)d->N * K * C * nT(d));
+  L.Wpk = c.take<float>((size_t)R * K * C);
+  L.wpk = c.take<float>(wpk_floats(d));
+  if (!backward) {
+    L.biasZ = c.take<float>((size_t)R * d->V);
+  } else {
+    L.sd = c.take<double>(C);
+    L.sdn = c.take<double>(C);
+    L.SdZ = c.take<double>((size_t)R * d->V);
+    L.H = c.take<float>((size_t)d->N * K * C * nT(d));
+    WgradParams w = make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
+    L.slab = c.take<float>((size_t)w.S * R * K * C);
+  }
+  L.total = c.off;
+  return L;
+}
+
+int spatial_check(const stgcn_spatial_desc_t *sd, stgcn_desc_t *d) {
+  if (!sd) return fail(STGCN_E_INVALID, "null descriptor");
+  if (sd->flags & ~STGCN_F_BF16) return fail(STGCN_E_UNSUPPORTED, "unknown spatial flags");
+  *d = spatial_as_block(sd);
+  return stgcn_check_desc(d);
+}
+
+hipError_t fill_identity_bn(float *ident, int C, hipStream_t s) {
+  hipError_t e = hipMemsetD32Async((hipDeviceptr_t)ident, 0u, (size_t)C, s);  // mean 0
+  if (e == hipSuccess)  // invstd 1, gamma 1
+    e = hipMemsetD32Async((hipDeviceptr_t)(ident + C), 0x3f800000u, (size_t)2 * C, s);
+  if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(ident + 3 * C), 0u, (size_t)C, s);
+  return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t stgcn_spatial_workspace_bytes(const stgcn_spatial_desc_t *sd, int backward) {
+  stgcn_desc_t d;
+  if (spatial_check(sd, &d) != STGCN_OK) return 0;
+  return spatial_layout(&d, nullptr, backward != 0).total;
+}
+
+int stgcn_spatial_fwd(const stgcn_spatial_desc_t *sd, const float *x, const float *A,
+                      const float *W, const float *bW, float *out, void *workspace,
+                      size_t workspace_bytes, void *stream) {
+  stgcn_desc_t dd;
+  int rc = spatial_check(sd, &dd);
+  if (rc) return rc;
+  const stgcn_desc_t *d = &dd;
+  if (!x || !A || !W || !bW || !out) return fail(STGCN_E_INVALID, "null tensor argument");
+  const SpatialLayout L = spatial_layout(d, workspace, false);
+  if (!workspace || workspace_bytes < L.total) return fail(STGCN_E_INVALID, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, V = d->V, K = d->K;
+  HIP_TRY(fill_identity_bn(L.ident, C, s));
+  HIP_TRY(launch_bias_rv(A, bW, L.biasZ, K, R, V, s));
+  const float *Wz = W;
+  if (K > 1) {
+    HIP_TRY(launch_pack_w(W, L.Wpk, K, R, C, s));
+    Wz = L.Wpk;
+  }
+  HIP_TRY(launch_gather_fwd(x, L.ident, L.ident + C, L.ident + 2 * C, L.ident + 3 * C, A, L.G, N,
+                            C, T, V, K, 0, s));
+  ConvGemmParams p = conv_base(d, L.wpk);
+  p.in = L.G;
+  p.w = Wz;
+  p.out = out;
+  p.bias_rv = L.biasZ;
+  p.in_bstride = (int64_t)K * C * T * V;
+  p.out_bstride = (int64_t)R * T * V;
+  p.w_sr = (int64_t)K * C;
+  p.w_sc = 1;
+  p.w_sq = 0;
+  p.C = K * C;
+  p.R = R;
+  p.NQ = 1;
+  p.s_in = 1;
+  p.off = 0;
+  p.s_out = 1;
+  p.p_out = 0;
+  p.M = T;
+  p.T_src = T;
+  p.T_dst = T;
+  conv_tiles(p);
+  HIP_TRY(launch_conv_gemm(p, s));
+  return STGCN_OK;
+}
+
+int stgcn_spatial_bwd(const stgcn_spatial_desc_t *sd, const float *dout, const float *x,
+                      const float *A, const float *W, const float *bW, float *dx, float *dA,
+                      float *dW, float *dbW, void *workspace, size_t workspace_bytes,
+                      void *stream) {
+  stgcn_desc_t dd;
+  int rc = spatial_check(sd, &dd);
+  if (rc) return rc;
+  const stgcn_desc_t *d = &dd;
+  if (!dout || !x || !A || !W || !bW || !dA || !dW || !dbW)
+    return fail(STGCN_E_INVALID, "null tensor argument");
+  const SpatialLayout L = spatial_layout(d, workspace, true);
+  if (!workspace || workspace_bytes < L.total) return fail(STGCN_E_INVALID, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, V = d->V, K = d->K;
+  HIP_TRY(fill_identity_bn(L.ident, C, s));
+  HIP_TRY(hipMemsetAsync(L.sd, 0, sizeof(double) * C, s));
+  HIP_TRY(hipMemsetAsync(L.sdn, 0, sizeof(double) * C, s));
+  HIP_TRY(hipMemsetAsync(L.SdZ, 0, sizeof(double) * R * V, s));
+  const float *mean = L.ident, *invstd = L.ident + C, *g = L.ident + 2 * C, *b = L.ident + 3 * C;
+  HIP_TRY(launch_gather_fwd(x, mean, invstd, g, b, A, L.G, N, C, T, V, K, 0, s));
+  {
+    WgradParams w = make_wgrad(d, dout, (int64_t)R * T * V, R, T, L.G, (int64_t)K * C * T * V,
+                               K * C, T, 1, 1, 0, L.slab);
+    HIP_TRY(launch_wgrad(w, s));
+    HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, dW, 1, R, K, C, s));
+  }
+  HIP_TRY(launch_sum_nt(dout, N, R, T, V, L.SdZ, s));
+  HIP_TRY(launch_spatial_small(L.SdZ, A, bW, K, R, V, dbW, dA, s));
+  const float *Wz = W;
+  if (K > 1) {
+    HIP_TRY(launch_pack_w(W, L.Wpk, K, R, C, s));
+    Wz = L.Wpk;
+  }
+  ConvGemmParams p = conv_base(d, L.wpk);
+  p.in = dout;
+  p.w = Wz;
+  p.out = L.H;
+  p.in_bstride = (int64_t)R * T * V;
+  p.out_bstride = (int64_t)K * C * T * V;
+  p.w_sr = 1;
+  p.w_sc = (int64_t)K * C;
+  p.w_sq = 0;
+  p.C = R;
+  p.R = K * C;
+  p.NQ = 1;
+  p.s_in = 1;
+  p.off = 0;
+  p.s_out = 1;
+  p.p_out = 0;
+  p.M = T;
+  p.T_src = T;
+  p.T_dst = T;
+  conv_tiles(p);
+  HIP_TRY(launch_conv_gemm(p, s));
+  // dx = sum_k H_k A_k (BatchNorm identity: dx is dxhat; sd/sdn unused)
+  HIP_TRY(launch_spatial_dx(L.H, x, mean, invstd, g, b, A, dx, dA, L.sd, L.sdn, N, C, T, V, K,
+                            dx != nullptr, 0, s));
   return STGCN_OK;
 }
 

@@ -142,17 +142,21 @@ hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const floa
 hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU,
-                                    double *sdu, int N, int C, int L, Dropout drop,
-                                    hipStream_t s);
+                                    double *sdu, int N, int C, int L, int training,
+                                    Dropout drop, hipStream_t s);
 hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
                                float *dgamma, float *dbeta, float *dbias, hipStream_t s);
 // add (same layout as dx, or null) is added after the BN1 backward (residual path)
-// pg2/pb2/psum (or null): also the previous block's ReLU+BN2 backward sums
+// training = 0: eval-mode BatchNorm backward (running statistics are constants)
+// pg2/pb2/psum (or null): also the previous block's ReLU+BN2 backward sums;
+// pU/pmean/pinvstd (or null): that block's pre-BN2 tensor and statistics, read
+// for channels where uhat = (x - b2) / g2 is ill-conditioned
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean,
                                 const float *invstd, const float *g, const double *sd,
                                 const double *sdn, const float *add, int N, int C, int L,
-                                int64_t M, const float *pg2, const float *pb2, double *psum,
-                                hipStream_t s);
+                                int64_t M, int training, const float *pg2, const float *pb2,
+                                double *psum, const float *pU, const float *pmean,
+                                const float *pinvstd, hipStream_t s);
 // dout = dy * (y > 0) (the final ReLU of the residual block), sum[c] += sum dout
 // (with dropout: y is the dropped output; dout = dy * scale where y > 0)
 hipError_t launch_relu_bwd(const float *dy, const float *y, float *dout, double *sum, int N,

@@ -1481,8 +1481,10 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
 hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU, double *sdu,
-                                    int N, int C, int L, Dropout drop, hipStream_t s) {
-  const double invM = 1.0 / ((double)N * L);
+                                    int N, int C, int L, int training, Dropout drop,
+                                    hipStream_t s) {
+  // eval mode (constant running statistics): no batch-mean terms
+  const double invM = training ? 1.0 / ((double)N * L) : 0.0;
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_apply, slice_vec(L, {dy, U, dU}), dim3(C, N), dy, U, mean,
                    invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop);
   return hipGetLastError();
@@ -1504,11 +1506,17 @@ hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double
   return hipGetLastError();
 }
 
-// dx = g*invstd * (dxhat - sum(dxhat)/M - xnorm * sum(dxhat*xnorm)/M), in place.
+// dx = g*invstd * (dxhat - sum(dxhat)/M - xnorm * sum(dxhat*xnorm)/M), in place
+// (invM = 0: eval mode, constant running statistics -> dx = g*invstd*dxhat).
 // Optionally (pg2 != null) also the previous block's ReLU+BN2 backward sums:
 // x = ReLU(g2*uhat + b2) of that block, so its ReLU mask is x > 0 and
 // uhat = (x - b2) / g2 there; with dy_prev = dx:
 //   psum[c] += sum dx * [x > 0],  psum[C + c] += sum dx * [x > 0] * uhat.
+// The division loses precision when |b2| >> |g2| (and is undefined at g2 = 0):
+// for such channels (|b2| > 4|g2|, a channel-uniform branch) uhat is read from
+// the previous block's saved pre-BN2 tensor pU instead, exactly as that
+// block's own reduction computes it: uhat = (U - mean2) * invstd2, mask
+// (U - mean2) * invstd2*g2 + b2 > 0.
 template <int VEC>
 __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x,
                                                        const float *mean, const float *invstd,
@@ -1516,13 +1524,18 @@ __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x
                                                        const double *sdn, const float *add,
                                                        int C, int L, double invM,
                                                        const float *pg2, const float *pb2,
-                                                       double *psum) {
+                                                       double *psum, const float *pU,
+                                                       const float *pmean, const float *pinvstd) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c];
   const float md = (float)(sd[c] * invM), mdn = (float)(sdn[c] * invM);
   const float pg = pg2 ? pg2[c] : 1.f, pb = pg2 ? pb2[c] : 0.f;
+  // poorly conditioned reconstruction (or g2 == 0 / non-finite): use U
+  const bool from_u = pg2 && pU && !(fabsf(pb) <= 4.f * fabsf(pg));
+  const float pmu = from_u ? pmean[c] : 0.f, pis = from_u ? pinvstd[c] : 1.f;
+  const float pa = pis * pg;
   double s = 0.0, q = 0.0;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float xv[VEC], d[VEC];
@@ -1537,7 +1550,16 @@ __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x
       for (int j = 0; j < VEC; ++j) d[j] += r[j];
     }
     vst<VEC>(dx + base + i, d);
-    if (pg2) {
+    if (from_u) {
+      float u[VEC];
+      vld<VEC>(pU + base + i, u);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if ((u[j] - pmu) * pa + pb > 0.f) {
+          s += d[j];
+          q += (double)d[j] * (double)((u[j] - pmu) * pis);
+        }
+    } else if (pg2) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
         if (xv[j] > 0.f) {
@@ -1551,10 +1573,13 @@ __global__ __launch_bounds__(256) void k_bn1_bwd_apply(float *dx, const float *x
 
 hipError_t launch_bn1_bwd_apply(float *dx, const float *x, const float *mean, const float *invstd,
                                 const float *g, const double *sd, const double *sdn,
-                                const float *add, int N, int C, int L, int64_t M,
-                                const float *pg2, const float *pb2, double *psum, hipStream_t s) {
-  STGCN_VEC_LAUNCH(k_bn1_bwd_apply, slice_vec(L, {dx, x, add}), dim3(C, N), dx, x, mean, invstd,
-                   g, sd, sdn, add, C, L, 1.0 / (double)M, pg2, pb2, psum);
+                                const float *add, int N, int C, int L, int64_t M, int training,
+                                const float *pg2, const float *pb2, double *psum,
+                                const float *pU, const float *pmean, const float *pinvstd,
+                                hipStream_t s) {
+  STGCN_VEC_LAUNCH(k_bn1_bwd_apply, slice_vec(L, {dx, x, add, pU}), dim3(C, N), dx, x, mean,
+                   invstd, g, sd, sdn, add, C, L, training ? 1.0 / (double)M : 0.0, pg2, pb2,
+                   psum, pU, pmean, pinvstd);
   return hipGetLastError();
 }
 

@@ -4,11 +4,20 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm, over
 xGMI). Each rank runs the full stack on its own N/world clips; BatchNorm stays
 per replica (DDP semantics). Parameters are grouped into
 buckets in reverse registration order (= the order backward produces them,
-last block first); when every gradient of a bucket has been accumulated
-(``register_post_accumulate_grad_hook``), the bucket is flattened and an
-asynchronous all-reduce(SUM) is issued, so the reduction of the late blocks'
-gradients overlaps the backward of the earlier blocks. ``synchronize()``
-waits, divides by the world size and writes the averages back into ``.grad``.
+last block first). Every bucket owns one flat gradient buffer and each
+parameter's ``.grad`` is a view into it ("gradient as bucket view"): autograd
+accumulates straight into the bucket, so launching a bucket's all-reduce is
+one asynchronous collective on the flat buffer, with no gather copy before it
+and no scatter copy after it. When every gradient of a bucket has been
+accumulated (``register_post_accumulate_grad_hook``) its all-reduce(SUM) is
+issued, so the reduction of the late blocks' gradients overlaps the backward
+of the earlier blocks; ``synchronize()`` waits and divides each flat buffer
+by the world size in place.
+
+Use ``zero_grad()`` (zeroes the flat buffers, keeps the views) instead of
+``optimizer.zero_grad(set_to_none=True)``. If a gradient arrives that is not
+the bucket view (the caller set ``.grad`` to None or replaced it), the hook
+copies it into the view and re-installs the view.
 
 The reference has no distributed code of its own (only
 PyTorch-Lightning's inherited Trainer flags could enable DDP); this is the
@@ -27,6 +36,9 @@ class GradAllReduce:
         self.buckets = []
         cur, size = [], 0
         for p in reversed(params):
+            if cur and (p.dtype != cur[0].dtype or p.device != cur[0].device):
+                self.buckets.append(cur)
+                cur, size = [], 0
             cur.append(p)
             size += p.numel() * p.element_size()
             if size >= bucket_bytes:
@@ -34,51 +46,62 @@ class GradAllReduce:
                 cur, size = [], 0
         if cur:
             self.buckets.append(cur)
-        self._bucket_of = {}
+        self._bucket_of, self._view = {}, {}
+        self._flat = []
         for bi, ps in enumerate(self.buckets):
+            flat = torch.zeros(sum(p.numel() for p in ps), dtype=ps[0].dtype,
+                               device=ps[0].device)
+            off = 0
             for p in ps:
                 self._bucket_of[p] = bi
-        self._pending = [0] * len(self.buckets)
-        self._flat = [None] * len(self.buckets)
-        self._work = [None] * len(self.buckets)
+                self._view[p] = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            self._flat.append(flat)
+        self._install_views()
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._reset()
+
+    def _install_views(self):
+        for p, v in self._view.items():
+            if p.grad is not v:
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                p.grad = v
 
     def _reset(self):
         self._pending = [len(ps) for ps in self.buckets]
         self._work = [None] * len(self.buckets)
 
+    def zero_grad(self):
+        """Zero every bucket (one fill per flat buffer) and keep the views."""
+        for flat in self._flat:
+            flat.zero_()
+        self._install_views()
+
     def _hook(self, p):
+        v = self._view[p]
+        if p.grad is not v:  # not accumulated into the bucket: move it there
+            v.copy_(p.grad)
+            p.grad = v
         bi = self._bucket_of[p]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:
             self._launch(bi)
 
     def _launch(self, bi):
-        ps = self.buckets[bi]
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in ps]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        self._flat[bi] = flat
-        self._work[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group,
-                                         async_op=True)
+        self._work[bi] = dist.all_reduce(self._flat[bi], op=dist.ReduceOp.SUM,
+                                         group=self.group, async_op=True)
 
     def synchronize(self):
-        """Wait for every bucket's all-reduce and install the averaged grads."""
-        for bi, ps in enumerate(self.buckets):
+        """Wait for every bucket's all-reduce; the grads (bucket views) then
+        hold the average over ranks."""
+        for bi in range(len(self.buckets)):
             if self._work[bi] is None:  # some grads never arrived (unused params)
+                self._install_views()
                 self._launch(bi)
             self._work[bi].wait()
-            flat = self._flat[bi]
-            flat.div_(self.world)
-            off = 0
-            for p in ps:
-                n = p.numel()
-                g = flat[off:off + n].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
-                off += n
+            self._flat[bi].div_(self.world)
+        self._install_views()
         self._reset()
 
     def remove(self):

@@ -63,22 +63,27 @@ class ChainCtx:
     and to the next one (``out_link``)."""
 
     def __init__(self, x_stats=None, y_stats=None, in_link=None, out_link=None, prev_g2=None,
-                 prev_b2=None):
+                 prev_b2=None, prev_U=None, prev_stats=None):
         self.x_stats, self.y_stats = x_stats, y_stats
         self.in_link, self.out_link = in_link, out_link
         self.prev_g2, self.prev_b2 = prev_g2, prev_b2
+        # the previous block's pre-BN2 tensor and [mean2 | invstd2] (ABI 4): read
+        # by the link for channels where uhat = (x - b2) / g2 is ill-conditioned
+        self.prev_U, self.prev_stats = prev_U, prev_stats
+        # this block's (U, [mean2 | invstd2]) for the next block's link
+        self.U, self.stats2 = None, None
 
 
 def _chain_bwd_args(cc, dy, need_dx, C_in, dev):
-    """(dy_sums, prev_g2, prev_b2, prev_sums) for stgcn_block_bwd."""
+    """(dy_sums, prev_g2, prev_b2, prev_sums, prev_U, prev_stats) for stgcn_block_bwd."""
     if cc is None:
-        return None, None, None, None
+        return None, None, None, None, None, None
     dy_sums = cc.out_link.sums if (cc.out_link is not None and cc.out_link.valid_for(dy)) \
         else None
     if cc.in_link is not None and need_dx:
         prev_sums = torch.empty(2 * C_in, device=dev, dtype=torch.float64)
-        return dy_sums, cc.prev_g2, cc.prev_b2, prev_sums
-    return dy_sums, None, None, None
+        return dy_sums, cc.prev_g2, cc.prev_b2, prev_sums, cc.prev_U, cc.prev_stats
+    return dy_sums, None, None, None, None, None
 
 
 def _chain_publish(cc, prev_sums, dx):
@@ -96,10 +101,12 @@ def _dropout_seed(drop, training):
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
-def _args(cls, ptrs, drop, seed):
+def _args(cls, ptrs, drop, seed, **extra):
     a = cls(*ptrs)
     a.dropout_p = float(drop)
     a.seed = seed
+    for k, v in extra.items():
+        setattr(a, k, v)
     return a
 
 
@@ -152,6 +159,8 @@ class StgcnBlockFn(torch.autograd.Function):
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
+        if cc is not None:
+            cc.U, cc.stats2 = U, stats[2 * C_in:]
         ctx.cfg = (stride, pad, eps, momentum, training)
         ctx.gemm = gemm
         ctx.cc = cc
@@ -168,7 +177,8 @@ class StgcnBlockFn(torch.autograd.Function):
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
                          need_dx=need_dx, **_gemm_flags(ctx.gemm))
-        dy_sums, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], x.device)
+        dy_sums, pg2, pb2, psums, pU, pst = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1],
+                                                            x.device)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
         dbWt = torch.empty(C_out, device=x.device, dtype=torch.float32)
@@ -178,7 +188,8 @@ class StgcnBlockFn(torch.autograd.Function):
         args = _args(hip_lib.BwdArgs, [hip_lib.ptr(t) for t in (
             dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
-            None, None, None, None, None, G, dy_sums, pg2, pb2, psums)], *ctx.drop)
+            None, None, None, None, None, G, dy_sums, pg2, pb2, psums)], *ctx.drop,
+            prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst))
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))
@@ -258,15 +269,58 @@ class StgcnResBlockFn(torch.autograd.Function):
         dg1, db1, dg2, db2 = (torch.empty_like(t) for t in (g1, b1, g2, b2))
         dWr = torch.empty_like(Wr) if Wr is not None else None
         dbr = torch.empty(C_out, device=dev, dtype=torch.float32) if Wr is not None else None
-        _, pg2, pb2, psums = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], dev)
+        _, pg2, pb2, psums, pU, pst = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], dev)
         nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = _args(hip_lib.BwdArgs, [hip_lib.ptr(t) for t in (
             dy, x, Z, None, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
-            Wr, Za, y, dWr, dbr, G, None, pg2, pb2, psums)], *ctx.drop)
+            Wr, Za, y, dWr, dbr, G, None, pg2, pb2, psums)], *ctx.drop,
+            prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst))
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         _chain_publish(ctx.cc, psums, dx)
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2, dWr, dbr,
                 None, None, None, None, None, None, None, None, None, None, None, None)
+
+
+class SpatialConvFn(torch.autograd.Function):
+    """``SpatialConv.forward`` on its own (st_graphconv.py:139-152) through
+    stgcn_spatial_fwd / stgcn_spatial_bwd (ABI 4):
+    forward(x, A, W, bW, bf16) -> out (N, C_out, T, V); backward returns
+    dx, dA, dW, dbW (W is the (K*C_out, C_in, 1, 1) Conv2d weight)."""
+
+    @staticmethod
+    def forward(ctx, x, A, W, bW, bf16=False):
+        lib = hip_lib.lib()
+        x = x.contiguous()
+        for t, n in ((x, "x"), (A, "A"), (W, "W"), (bW, "bW")):
+            _f32c(t, n)
+        N, C_in, T, V = x.shape
+        K = A.shape[0]
+        C_out = W.shape[0] // K
+        desc = hip_lib.SpatialDesc(N, C_in, C_out, T, V, K, hip_lib.F_BF16 if bf16 else 0)
+        nbytes = lib.stgcn_spatial_workspace_bytes(ctypes.byref(desc), 0)
+        if nbytes == 0:
+            hip_lib.check(-2)
+        out = torch.empty((N, C_out, T, V), device=x.device, dtype=torch.float32)
+        ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+        hip_lib.check(lib.stgcn_spatial_fwd(ctypes.byref(desc), *[hip_lib.ptr(t) for t in (
+            x, A, W, bW, out, ws)], nbytes, hip_lib.stream_handle(x.device)))
+        ctx.save_for_backward(x, A, W, bW)
+        ctx.desc = desc
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = hip_lib.lib()
+        x, A, W, bW = ctx.saved_tensors
+        dout = dout.contiguous()
+        desc = ctx.desc
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dA, dW, dbW = (torch.empty_like(t) for t in (A, W, bW))
+        nbytes = lib.stgcn_spatial_workspace_bytes(ctypes.byref(desc), 1)
+        ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
+        hip_lib.check(lib.stgcn_spatial_bwd(ctypes.byref(desc), *[hip_lib.ptr(t) for t in (
+            dout, x, A, W, bW, dx, dA, dW, dbW, ws)], nbytes, hip_lib.stream_handle(x.device)))
+        return dx, dA, dW, dbW, None

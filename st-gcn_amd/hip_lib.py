@@ -18,7 +18,7 @@ LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libstgcn_hip.so")
 if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in-tree only
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -53,7 +53,13 @@ class BwdArgs(ctypes.Structure):
         "Wr", "Za", "y", "dWr", "dbr",         # ABI 2: residual block
         "G",                                   # ABI 2: optional kept joint contraction
         "dy_sums", "prev_g2", "prev_b2", "prev_sums")  # ABI 2: optional stack chaining
-    ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)]  # ABI 2: fused dropout
+    ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)  # ABI 2: fused dropout
+         ] + [("prev_U", _vp), ("prev_stats", _vp)]  # ABI 4: chain conditioning fallback
+
+
+class SpatialDesc(ctypes.Structure):  # ABI 4: SpatialConv on its own
+    _fields_ = [("N", _c_int), ("C_in", _c_int), ("C_out", _c_int), ("T", _c_int),
+                ("V", _c_int), ("K", _c_int), ("flags", _c_int)]
 
 
 class HeadDesc(ctypes.Structure):  # ABI 3
@@ -70,7 +76,8 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_fwd_workspace_bytes", "stgcn_bwd_workspace_bytes",
             "stgcn_block_fwd", "stgcn_block_bwd", "stgcn_time_kernel_bytes",
             "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
-            "stgcn_adam_build_table", "stgcn_adam_step")
+            "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
+            "stgcn_spatial_fwd", "stgcn_spatial_bwd")
 
 _LIB = None
 
@@ -113,6 +120,14 @@ def load_library(path=LIB_PATH):
     lib.stgcn_adam_step.argtypes = [_vp, ctypes.c_int, ctypes.c_int64] + \
         [ctypes.c_double] * 5 + [ctypes.c_int64, _vp]
     lib.stgcn_adam_step.restype = ctypes.c_int
+    lib.stgcn_spatial_workspace_bytes.argtypes = [ctypes.POINTER(SpatialDesc), ctypes.c_int]
+    lib.stgcn_spatial_workspace_bytes.restype = ctypes.c_size_t
+    lib.stgcn_spatial_fwd.argtypes = [ctypes.POINTER(SpatialDesc)] + [_vp] * 6 + \
+        [ctypes.c_size_t, _vp]
+    lib.stgcn_spatial_fwd.restype = ctypes.c_int
+    lib.stgcn_spatial_bwd.argtypes = [ctypes.POINTER(SpatialDesc)] + [_vp] * 10 + \
+        [ctypes.c_size_t, _vp]
+    lib.stgcn_spatial_bwd.restype = ctypes.c_int
     if lib.stgcn_abi_version() != ABI_VERSION:
         raise RuntimeError("libstgcn_hip.so ABI version mismatch; rebuild it")
     return lib

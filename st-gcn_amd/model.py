@@ -7,6 +7,7 @@ NTVC -> permute -> 10 blocks -> avg_pool2d over (T, V) -> Linear.
 import torch
 import torch.nn as nn
 
+from .graph import Strategy, get_normalized_adjacency_matrices
 from .network import SpatialTemporalConv, StackChain
 from .train_ops import StgcnHeadFn
 
@@ -16,15 +17,30 @@ LAYERS = [(64, 1), (64, 1), (64, 1), (64, 1), (128, 2), (128, 1), (128, 1),
 
 
 class STGCNStack(nn.Module):
+    """use_edge_importance / max_mask_jitter: the reference's edge-importance
+    masks (lightning_model.py:53-59): ten masks 1 + 2(randn - 0.5)*jitter drawn
+    before the blocks (same RNG consumption), registered as ``Masks.{i}``
+    (state_dict interchange), each block built on A * Masks[i]. As in the
+    reference the masks only scale the blocks' initial A (each block's
+    ``spatialConv.A`` is its own leaf parameter), so they receive no gradient."""
+
     def __init__(self, C_in, nr_classes, A, gamma=9, dropout_rate=0, residual=False,
-                 gemm_dtype=torch.float32, f32_gemm="mfma"):
+                 gemm_dtype=torch.float32, f32_gemm="mfma", use_edge_importance=False,
+                 max_mask_jitter=0.001):
         super().__init__()
         pad = (gamma - 1) // 2
         self.K, self.V = A.shape[0], A.shape[1]
         self.nr_classes = nr_classes
+        n_layers = len(LAYERS)
+        if use_edge_importance:
+            jitters = [2 * (torch.randn_like(A) - 0.5) * max_mask_jitter for _ in range(n_layers)]
+            self.Masks = nn.ParameterList([nn.Parameter(jitters[i] + torch.ones(A.shape))
+                                           for i in range(n_layers)])
+        else:
+            self.Masks = [torch.ones(A.shape) for _ in range(n_layers)]  # not trainable
         blocks, c = [], C_in
-        for co, s in LAYERS:
-            blocks.append(SpatialTemporalConv(c, co, A, gamma, s, pad,
+        for i, (co, s) in enumerate(LAYERS):
+            blocks.append(SpatialTemporalConv(c, co, A * self.Masks[i], gamma, s, pad,
                                               dropout_rate=dropout_rate, residual=residual,
                                               gemm_dtype=gemm_dtype, f32_gemm=f32_gemm))
             c = co
@@ -55,6 +71,47 @@ class STGCNStack(nn.Module):
         for blk in self.conv:
             x = blk(x, chain=chain)
         return StgcnHeadFn.apply(x, self.fc_layer.weight, self.fc_layer.bias, labels)
+
+
+class STGCN(nn.Module):
+    """The legacy network class of the reference (src/network/stgcn.py:8-80),
+    on the drop-in blocks: same constructor (C_in, gamma, nr_classes, strat, d,
+    edge_importance), same child names / state_dict keys (``Masks.{i}`` when
+    edge_importance, ``conv.{i}.*``, ``fc_layer.*``), the blocks' default
+    dropout 0.5 (stgcn.py:40-51), and a softmax over the classes at the end of
+    forward (stgcn.py:77). ``graph`` (not in the reference) selects the
+    skeleton; the reference builds on its default body25 graph (V = 25)."""
+
+    def __init__(self, C_in, gamma, nr_classes, strat=Strategy.UNI_LABELING, d=1,
+                 edge_importance=True, graph=None, gemm_dtype=torch.float32, f32_gemm="mfma"):
+        super().__init__()
+        self.nr_classes = nr_classes
+        temporal_padding = (gamma - 1) // 2
+        A = get_normalized_adjacency_matrices(strat, d, graph=graph)
+        self.K = A.shape[0]
+        self.V = A.shape[1]
+        self.C_in = C_in
+        self.C_out = 256
+        if edge_importance:
+            self.Masks = nn.ParameterList([nn.Parameter(torch.ones(A.shape)) for _ in range(10)])
+        else:
+            self.Masks = [torch.ones(A.shape) for _ in range(10)]  # not trainable
+        blocks, c = [], C_in
+        for i, (co, s) in enumerate(LAYERS):
+            blocks.append(SpatialTemporalConv(c, co, A * self.Masks[i], gamma, s,
+                                              temporal_padding, gemm_dtype=gemm_dtype,
+                                              f32_gemm=f32_gemm))
+            c = co
+        self.conv = nn.Sequential(*blocks).float()
+        self.fc_layer = nn.Linear(256, self.nr_classes).float()
+        self.softmax = nn.Softmax(dim=1)
+
+    def forward(self, x):
+        """x: (N, T, V, C_in) -> class probabilities (N, nr_classes)."""
+        x = x.permute(0, 3, 1, 2)
+        x = self.conv(x)
+        x = x.flatten(2).mean(dim=2)  # avg_pool2d over (T, V) (stgcn.py:72-73)
+        return self.softmax(self.fc_layer(x))
 
 
 def flops_per_clip(C_in, T, V, K, nr_classes, gamma=9):

@@ -12,7 +12,7 @@ forward raises.
 import torch
 import torch.nn as nn
 
-from .fused import ChainCtx, Link, StgcnBlockFn, StgcnResBlockFn
+from .fused import ChainCtx, Link, SpatialConvFn, StgcnBlockFn, StgcnResBlockFn
 
 
 class StackChain:
@@ -30,15 +30,18 @@ class StackChain:
 
     def reset(self):
         self.y, self.y_version, self.y_stats, self.link, self.g2b2 = None, None, None, None, None
+        self.u_stats = None
 
 
 class SpatialConv(nn.Module):
     """Reference: st_graphconv.py:111-152. Holds the trainable adjacency A
-    (K, V, V) and the 1x1 conv W (C_in -> K*C_out). In this build the layer's
-    arithmetic runs inside the fused block (``SpatialTemporalConv``); a
-    standalone ``forward`` is not part of the accelerated path."""
+    (K, V, V) and the 1x1 conv W (C_in -> K*C_out). Inside
+    ``SpatialTemporalConv`` the layer's arithmetic runs in the fused block;
+    called on its own, ``forward`` runs the HIP spatial kernels
+    (``fused.SpatialConvFn``: stgcn_spatial_fwd / _bwd) with the reference's
+    semantics: out[n,c,t,v] = sum_k sum_w A[k,v,w] (W x + b)[n,k,c,t,w]."""
 
-    def __init__(self, C_in, C_out, A):
+    def __init__(self, C_in, C_out, A, gemm_dtype=torch.float32):
         super().__init__()
         self.C_in = C_in
         self.C_out = C_out
@@ -46,11 +49,13 @@ class SpatialConv(nn.Module):
         self.K = self.A.shape[0]
         self.V = self.A.shape[1]
         self.W = nn.Conv2d(C_in, self.K * C_out, (1, 1))
+        # (not in the reference) bf16 channel GEMMs for the standalone call
+        self.gemm_dtype = gemm_dtype
 
     def forward(self, f_in):
-        raise NotImplementedError(
-            "SpatialConv.forward on its own is not on the accelerated path; "
-            "use it through SpatialTemporalConv (the fused HIP block)")
+        """f_in (N, C_in, T, V) -> (N, C_out, T, V) (st_graphconv.py:139-152)."""
+        return SpatialConvFn.apply(f_in.float(), self.A, self.W.weight, self.W.bias,
+                                   self.gemm_dtype == torch.bfloat16)
 
 
 class SpatialTemporalConv(nn.Module):
@@ -131,6 +136,7 @@ class SpatialTemporalConv(nn.Module):
                 if chain.link is not None:
                     cc.in_link = chain.link
                     cc.prev_g2, cc.prev_b2 = chain.g2b2
+                    cc.prev_U, cc.prev_stats = chain.u_stats
         if self.residual:
             proj = self.apply_residual if isinstance(self.apply_residual, nn.Conv2d) else None
             y = StgcnResBlockFn.apply(
@@ -153,4 +159,5 @@ class SpatialTemporalConv(nn.Module):
                 chain.y, chain.y_version, chain.y_stats = y, y._version, cc.y_stats
                 chain.link = cc.out_link
                 chain.g2b2 = None if self.residual else (bn2.weight, bn2.bias)
+                chain.u_stats = None if self.residual else (cc.U, cc.stats2)
         return y  # dropout (p > 0, training) is fused into the block's output pass

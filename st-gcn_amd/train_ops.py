@@ -80,16 +80,14 @@ class FusedAdam(torch.optim.Optimizer):
     table (pointers of param / grad / exp_avg / exp_avg_sq) is rebuilt on the
     host only when a pointer changed (e.g. grads re-allocated after
     zero_grad(set_to_none=True)) and copied to the device asynchronously from
-    pinned memory."""
+    pinned memory; one table per parameter group (keyed by the group's index)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
                  amsgrad=False):
         if amsgrad:
             raise NotImplementedError("FusedAdam: amsgrad")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        self._key = None
-        self._dev_table = None
-        self._chunks = 0
+        self._tables = {}  # group index -> (key, device table, chunks, ntensors)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -98,7 +96,7 @@ class FusedAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = hip_lib.lib()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             plist = [p for p in group["params"] if p.grad is not None]
             if not plist:
                 continue
@@ -121,7 +119,8 @@ class FusedAdam(torch.optim.Optimizer):
                     for p in plist]
             key = tuple((t.param, t.grad, t.exp_avg, t.exp_avg_sq, t.numel) for t in tabs)
             dev = plist[0].device
-            if key != self._key:
+            cached = self._tables.get(gi)
+            if cached is None or cached[0] != key:
                 n = len(tabs)
                 nbytes = lib.stgcn_adam_table_bytes(n)
                 host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -129,11 +128,13 @@ class FusedAdam(torch.optim.Optimizer):
                 arr = (hip_lib.AdamTensor * n)(*tabs)
                 hip_lib.check(lib.stgcn_adam_build_table(arr, n, ctypes.c_void_p(host.data_ptr()),
                                                          nbytes, ctypes.byref(chunks)))
-                self._dev_table = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-                self._dev_table.copy_(host, non_blocking=True)
-                self._key, self._chunks, self._n = key, chunks.value, n
+                dev_table = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+                dev_table.copy_(host, non_blocking=True)
+                cached = (key, dev_table, chunks.value, n)
+                self._tables[gi] = cached
+            _, dev_table, nchunks, n = cached
             b1, b2 = group["betas"]
             hip_lib.check(lib.stgcn_adam_step(
-                hip_lib.ptr(self._dev_table), self._n, self._chunks, group["lr"], b1, b2,
+                hip_lib.ptr(dev_table), n, nchunks, group["lr"], b1, b2,
                 group["eps"], group["weight_decay"], step, hip_lib.stream_handle(dev)))
         return loss

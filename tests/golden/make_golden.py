@@ -18,6 +18,9 @@ Outputs (small .npz files next to this script):
                   running stats after the step.
   stack_cfg1.npz  full L_STGCN (src/lightning_model.py) cfg1 plumbing case:
                   logits, loss, param checksums and sampled grads.
+  spatialconv_*.npz  SpatialConv on its own (st_graphconv.py:139-152).
+  stack_cfg1_edge.npz  the cfg1 case with --use_edge_importance (masks).
+  legacy_stgcn.npz  src/network/stgcn.py STGCN in eval mode (probs + grads).
   data_pipeline.npz  host input pipeline:
                   src/data/util.py loopy_pad_collate_fn on a ragged batch,
                   src/data/augmentation.py augment_data under fixed
@@ -25,6 +28,8 @@ Outputs (small .npz files next to this script):
                   synthetic (T, 25, 3) .npy clips written to a temp dir.
 
   --only data     regenerate data_pipeline.npz only.
+  --only extra    regenerate the round-2 fixtures only (spatialconv_*,
+                  stack_cfg1_edge, legacy_stgcn).
 """
 import argparse
 import os
@@ -202,6 +207,106 @@ def make_stack_cfg1(lightning_model, adjacency):
     np.savez_compressed(os.path.join(HERE, "stack_cfg1.npz"), **rec)
 
 
+SPATIAL_CASES = [
+    # name, C_in, C_out, V, strategy, N, T
+    ("s3x64_v18", 3, 64, 18, 0, 2, 20),
+    ("s64x64_v25k3", 64, 64, 25, 2, 2, 16),
+    ("s64x128_v50k3", 64, 128, 50, 2, 2, 9),
+]
+
+
+def make_spatialconv(st_graphconv, adj_mats, name, C_in, C_out, V, strat, N, T):
+    """SpatialConv used on its own (st_graphconv.py:139-152), fwd + bwd."""
+    A = torch.from_numpy(adj_mats[f"V{V}_s{strat}_d1"])
+    torch.manual_seed(0)
+    sc = st_graphconv.SpatialConv(C_in, C_out, A)
+    params0 = {k: v.detach().clone() for k, v in sc.state_dict().items()}
+    x = torch.randn(N, C_in, T, V, generator=torch.Generator().manual_seed(1))
+    x.requires_grad_(True)
+    y = sc(x)
+    g = torch.randn(y.shape, generator=torch.Generator().manual_seed(2))
+    (y * g).sum().backward()
+    rec = {"x": x.detach().numpy(), "g": g.numpy(), "y": y.detach().numpy(),
+           "grad.x": x.grad.numpy(), "meta": np.array([C_in, C_out, V, strat, N, T])}
+    for k, v in params0.items():
+        rec["param." + k] = v.numpy()
+    for k, p in sc.named_parameters():
+        rec["grad." + k] = p.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, f"spatialconv_{name}.npz"), **rec)
+
+
+def _sampled(model, rec, gen, grads=True):
+    for k, p in model.named_parameters():
+        flat_p = p.detach().reshape(-1)
+        idx = torch.randint(0, flat_p.numel(), (min(256, flat_p.numel()),), generator=gen)
+        rec["pidx." + k] = idx.numpy()
+        rec["pval." + k] = flat_p[idx].numpy()
+        rec["psum." + k] = np.array(flat_p.double().sum().item())
+        if grads and p.grad is not None:
+            flat_g = p.grad.reshape(-1)
+            rec["gval." + k] = flat_g[idx].numpy()
+            rec["gsum." + k] = np.array(flat_g.double().sum().item())
+            rec["gnorm." + k] = np.array(flat_g.double().norm().item())
+    rec["state_keys"] = np.array(list(model.state_dict().keys()))
+
+
+def make_stack_cfg1_edge(lightning_model, adjacency):
+    """L_STGCN --use_edge_importance (lightning_model.py:53-57), cfg1 shape."""
+    parser = lightning_model.build_argument_parser()
+    hp = parser.parse_args(["--C_in", "3", "--nr_classes", "2", "--use_edge_importance", "True",
+                            "--max_mask_jitter", "0.05"])
+    with _patched_adjacency(adjacency, 18):
+        torch.manual_seed(0)
+        model = lightning_model.L_STGCN(hp)
+    model.train()
+    N, T, V, C = 4, 50, 18, 3
+    x = torch.randn(N, T, V, C, generator=torch.Generator().manual_seed(1))
+    y = torch.randint(0, 2, (N,), generator=torch.Generator().manual_seed(2))
+    logits = model(x)
+    loss = torch.nn.functional.cross_entropy(logits, y)
+    loss.backward()
+    rec = {"x": x.numpy(), "labels": y.numpy(), "logits": logits.detach().numpy(),
+           "loss": np.array(loss.item())}
+    _sampled(model, rec, torch.Generator().manual_seed(4))
+    np.savez_compressed(os.path.join(HERE, "stack_cfg1_edge.npz"), **rec)
+
+
+def make_legacy_stgcn(stgcn):
+    """The legacy STGCN class (src/network/stgcn.py:8-80: edge-importance masks
+    of ones, blocks with the default dropout 0.5, softmax output) in eval mode
+    (dropout off, BatchNorm on running statistics): probabilities and the
+    gradients of sum(probs * g). The running statistics are calibrated first
+    (one no-grad training-mode pass over the same clips with momentum 1 and
+    the dropouts at p = 0, so they equal that batch's statistics): with the
+    reference's un-normalised A (entries ~1e4) arbitrary running statistics
+    overflow fp32 within a few blocks. They are stored in the fixture."""
+    torch.manual_seed(0)
+    model = stgcn.STGCN(3, 9, 5)
+    N, T, V, C = 3, 30, 25, 3
+    x = torch.randn(N, T, V, C, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        for blk in model.conv:
+            blk.batch_n.momentum = blk.batch_n_2.momentum = 1.0
+            blk.dropout.p = 0.0
+        model.train()
+        model(x)
+        for blk in model.conv:
+            blk.batch_n.momentum = blk.batch_n_2.momentum = 0.1
+            blk.dropout.p = 0.5
+    model.eval()
+    x.requires_grad_(True)
+    probs = model(x)
+    g = torch.randn(probs.shape, generator=torch.Generator().manual_seed(2))
+    (probs * g).sum().backward()
+    rec = {"x": x.detach().numpy(), "g": g.numpy(), "probs": probs.detach().numpy(),
+           "grad.x": x.grad.numpy()}
+    for name, buf in model.named_buffers():
+        if "running" in name:
+            rec["run." + name] = buf.numpy()
+    _sampled(model, rec, torch.Generator().manual_seed(4))
+    np.savez_compressed(os.path.join(HERE, "legacy_stgcn.npz"), **rec)
+
+
 def make_data_pipeline(util, augmentation, calc):
     rec = {}
     rng = np.random.default_rng(7)
@@ -240,7 +345,7 @@ def make_data_pipeline(util, augmentation, calc):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("reference", nargs="?", default="/root/reference")
-    ap.add_argument("--only", choices=["data"], default=None)
+    ap.add_argument("--only", choices=["data", "extra"], default=None)
     args = ap.parse_args()
     _install_stubs()
     sys.path.insert(0, os.path.join(args.reference, "src"))
@@ -257,13 +362,23 @@ def main():
         from data import adjacency  # noqa: E402
         from network import st_graphconv  # noqa: E402
         import lightning_model  # noqa: E402
+        from network import stgcn  # noqa: E402
     torch.set_num_threads(8)
-    with tempfile.TemporaryDirectory() as tmp:
-        mats = make_adjacency(adjacency, tmp)
+    if args.only == "extra":  # round-2 fixtures (round-1 files untouched)
+        with np.load(os.path.join(HERE, "adjacency.npz")) as f:
+            mats = {k: f[k] for k in f.files}
+    else:
+        with tempfile.TemporaryDirectory() as tmp:
+            mats = make_adjacency(adjacency, tmp)
     with contextlib.redirect_stdout(io.StringIO()):
-        for case in BLOCK_CASES:
-            make_block(st_graphconv, mats, *case)
-        make_stack_cfg1(lightning_model, adjacency)
+        if args.only != "extra":
+            for case in BLOCK_CASES:
+                make_block(st_graphconv, mats, *case)
+            make_stack_cfg1(lightning_model, adjacency)
+        for case in SPATIAL_CASES:
+            make_spatialconv(st_graphconv, mats, *case)
+        make_stack_cfg1_edge(lightning_model, adjacency)
+        make_legacy_stgcn(stgcn)
     print("wrote fixtures to", HERE)
 
 

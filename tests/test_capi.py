@@ -29,7 +29,7 @@ def test_header_declares_entry_points(pkg):
 def test_library_exports_every_header_symbol(pkg, lib):
     for name in _header_functions():
         assert hasattr(lib, name), name
-    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 3
+    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 4
 
 
 def _desc(pkg, **kw):
@@ -87,3 +87,24 @@ def test_cpu_tensors_fail_loudly(pkg):
     blk = pkg.SpatialTemporalConv(3, 64, A, 9, 1, 4, dropout_rate=0)
     with pytest.raises(RuntimeError):
         blk(torch.randn(2, 3, 20, 18))
+
+
+def test_spatial_desc_workspace_and_rejects(pkg, lib):
+    """ABI 4 SpatialConv entry points: workspace queries for the reference's
+    graphs; unknown flags / bad shapes rejected without touching the GPU."""
+    SD = pkg.hip_lib.SpatialDesc
+    for kw in (dict(V=18, K=1, C_in=3), dict(V=25, K=3), dict(V=50, K=3, flags=2)):
+        base = dict(N=8, C_in=64, C_out=64, T=300, V=18, K=1, flags=0)
+        base.update(kw)
+        d = SD(**base)
+        assert lib.stgcn_spatial_workspace_bytes(ctypes.byref(d), 0) > 0, kw
+        assert lib.stgcn_spatial_workspace_bytes(ctypes.byref(d), 1) > 0, kw
+    for kw in (dict(flags=1), dict(flags=4), dict(N=0), dict(V=300)):
+        base = dict(N=8, C_in=64, C_out=64, T=300, V=18, K=1, flags=0)
+        base.update(kw)
+        d = SD(**base)
+        assert lib.stgcn_spatial_workspace_bytes(ctypes.byref(d), 0) == 0, kw
+    d = SD(N=8, C_in=64, C_out=64, T=30, V=18, K=1, flags=0)
+    assert lib.stgcn_spatial_fwd(ctypes.byref(d), None, None, None, None, None, None, 0,
+                                 None) == -1
+    assert b"null" in lib.stgcn_last_error()

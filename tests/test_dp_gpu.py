@@ -1,0 +1,42 @@
+"""GPU: the multi-rank HIP data-parallel path (dp.GradAllReduce bucket views +
+STGCNStack on the HIP library + FusedAdam) executed with world size 2 on the
+box's one GPU, over gloo (tests/dp_gpu_worker.py documents the checks).
+
+The ranks are started as child processes by torch.distributed.run before this
+process touches the GPU (the file sorts before every other GPU test module and
+this test makes no HIP call itself)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_dp_two_ranks_on_hip(tmp_path, world):
+    out = tmp_path / "dp.json"
+    env = dict(os.environ, DP_OUT=str(out), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.join(ROOT, "tests", "dp_gpu_worker.py")]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    print(res)
+    assert res["bucket_views"] and res["buckets"] >= 2
+    assert res["ranks_identical"]
+    assert res["grad_err"] < 1e-6, res
+    assert res["grad_err_A"] < 1e-3, res
+    assert res["step_err"] < 1e-6, res

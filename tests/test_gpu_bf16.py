@@ -171,3 +171,11 @@ def test_bf16_full_size_block(pkg):
     """cfg3 layer-1 shape (V=25, K=3, T=300) at N=16."""
     errs = _check_bf16(pkg, (64, 64, 1, 25, 3, 16, 300), seed=7)
     print({k: float(np.format_float_scientific(v, 2)) for k, v in errs.items()})
+
+
+def test_bf16_cfg5_full_size_block(pkg):
+    """cfg5 layer shape (V = 50 two-person graph, K = 3) at the full T = 300,
+    N = 8: k_spatial_bwd6's persistent grid and its resident dA accumulators at
+    a realistic grid size."""
+    errs = _check_bf16(pkg, (64, 64, 1, 50, 3, 8, 300), seed=11)
+    print({k: float(np.format_float_scientific(v, 2)) for k, v in errs.items()})

@@ -372,3 +372,17 @@ def test_block_dropout_seed_reproducible(pkg):
     assert sa == sb and torch.equal(a["y"], b["y"])
     assert not torch.equal(_keep_mask(sa, (2, 64, 30, 18), 0.5),
                            _keep_mask(sa + 1, (2, 64, 30, 18), 0.5))
+
+
+@pytest.mark.parametrize("gemm", ["fp32", "f32x3"])
+def test_bench_size_block(pkg, gemm):
+    """The cfg2 layer-1 block at the bench's exact per-GPU size (N = 128,
+    T = 300, V = 18), fp32 MFMA and the benched bf16x3 split path, against the
+    fp64 oracle at the fp32 gate (bias-type gradients: 2x the fp32
+    reference's own error, as everywhere)."""
+    arrays, x, g = _random_case(pkg, 64, 64, 1, 18, 1, 128, 300, seed=9)
+    got = _run_hip(pkg, arrays, x, g, gemm=gemm)
+    for k, v in got.items():
+        assert torch.isfinite(v).all(), k
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, floor=floor)

@@ -121,3 +121,36 @@ def test_fused_adam_state_dict_interchanges_with_torch_adam(pkg):
     torch.cuda.synchronize()
     assert np.allclose(dut[0].detach().cpu().numpy(), ref[0].detach().numpy(), rtol=2e-6,
                        atol=1e-8)
+
+
+def test_fused_adam_param_groups_keep_their_tables(pkg):
+    """Two parameter groups (different lr / weight decay) with gradients that
+    stay in place across steps (as with dp.GradAllReduce bucket views): each
+    group keeps its own device table, and the result matches torch's Adam."""
+    g = torch.Generator().manual_seed(5)
+    shapes = [(64, 3, 1, 1), (64,), (1, 18, 18), (400, 256)]
+    p0 = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(4)]
+    ref = [p.clone().requires_grad_(True) for p in p0]
+    dut = [p.clone().to(DEV).requires_grad_(True) for p in p0]
+    groups = lambda ps: [dict(params=ps[:2], lr=1e-2), dict(params=ps[2:], lr=3e-3,  # noqa
+                                                                weight_decay=0.1)]
+    opt_ref = torch.optim.Adam(groups(ref), foreach=False)
+    opt = pkg.FusedAdam(groups(dut))
+    for p in dut:
+        p.grad = torch.zeros_like(p)
+    for k in range(4):
+        for p, gr in zip(ref, grads[k]):
+            p.grad = gr.clone()
+        for p, gr in zip(dut, grads[k]):
+            p.grad.copy_(gr.to(DEV))     # same grad tensors every step
+        opt_ref.step()
+        opt.step()
+        if k == 0:
+            tables = {gi: t[1].data_ptr() for gi, t in opt._tables.items()}
+    torch.cuda.synchronize()
+    assert sorted(opt._tables) == [0, 1]
+    assert {gi: t[1].data_ptr() for gi, t in opt._tables.items()} == tables  # not rebuilt
+    for a, b in zip(dut, ref):
+        d = (a.detach().cpu() - b.detach()).abs()
+        assert (d <= 2e-6 * b.detach().abs() + 1e-7).all(), float(d.max())
