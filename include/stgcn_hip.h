@@ -106,8 +106,10 @@ typedef struct stgcn_fwd_args {
   /* ABI 2 (residual block; null otherwise) */
   const float *Wr, *br;                 /* apply_residual Conv2d (projection) */
   float *Za;                            /* saved: ReLU(BN2(Z)) N,C_out,T,V    */
-  /* ABI 2, optional: keep the joint contraction G = f(BN1(x)) A^T
-   * (N, K*C_in, T, V) for the backward instead of recomputing it */
+  /* ABI 2, optional: keep the joint contraction G = f(BN1(x)) A^T for the
+   * backward instead of recomputing it: stgcn_keep_g_bytes(d) bytes; fp32
+   * (N, K*C_in, T, V), or, where the bf16 path's fused spatial kernel runs
+   * (STGCN_F_BF16, C_in >= 16), bf16 in frame tiles (ABI 4: opaque to the caller) */
   float *G;
   /* ABI 2, optional stack chaining (training): x_stats = [sum(C_in), sumsq(C_in)]
    * of x over (n,t,v) in fp64 (produced by the previous block's y_stats: the
@@ -161,6 +163,8 @@ const char *stgcn_last_error(void);
 int stgcn_check_desc(const stgcn_desc_t *d);
 
 size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d);
+/* ABI 4: bytes of the optional kept-G buffer (stgcn_fwd_args_t.G / bwd G) */
+size_t stgcn_keep_g_bytes(const stgcn_desc_t *d);
 size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d);
 
 int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -79,6 +80,12 @@ Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
   dr.thresh = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
   dr.scale = p < 1.f ? (float)(1.0 / (1.0 - (double)p)) : 0.f;
   return dr;
+}
+// the fused spatial forward (kernels_fused.hip) of the bf16 path applies
+// (STGCN_UNFUSED_SP: the unfused gather + GEMM kernels, A/B measurement only)
+bool fused_sp(const stgcn_desc_t *d) {
+  static const bool off = getenv("STGCN_UNFUSED_SP") != nullptr;
+  return !off && bf16(d) && sp_fwd_bf16_supported(d->C_in, d->V, d->K);
 }
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {
@@ -191,6 +198,15 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   WgradParams w2 =
       make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
   size_t slab = std::max((size_t)w1.S * R * R * 9, (size_t)w2.S * R * K * C);
+  if (fused_sp(d)) {  // dW' from the kept bf16 G (k_wgrad_gemm_gk)
+    WgradParams wg{};
+    wg.R = R;
+    wg.C = K * C;
+    wg.V = d->V;
+    wg.N = d->N;
+    plan_wgrad_gk(wg, d->T);
+    slab = std::max(slab, (size_t)wg.S * R * K * C);
+  }
   if (projection(d)) {
     WgradParams w3 = make_wgrad(d, nullptr, 0, R, d->T_out, nullptr, 0, C, d->T, 1, d->stride, 0,
                                 nullptr);
@@ -379,6 +395,12 @@ size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d) {
   return fwd_layout(d, nullptr).total;
 }
 
+size_t stgcn_keep_g_bytes(const stgcn_desc_t *d) {
+  if (stgcn_check_desc(d) != STGCN_OK) return 0;
+  if (fused_sp(d)) return sp_keep_g_bytes(d->N, d->C_in, d->T, d->V, d->K);
+  return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V;
+}
+
 size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d) {
   if (stgcn_check_desc(d) != STGCN_OK) return 0;
   return bwd_layout(d, nullptr).total;
@@ -424,6 +446,14 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     Wz = L.Wpk;
   }
   // (residual block: SpatialConv sees ReLU(BN1(x)), st_graphconv.py:72-74)
+  if (fused_sp(d)) {
+    // bf16 path: BN1 + joint contraction + W' GEMM in one kernel; G kept in bf16
+    // for the backward when the caller asks (stgcn_keep_g_bytes)
+    HIP_TRY(launch_sp_fwd_bf16(a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.biasZ, L.wpk,
+                               a->Z, reinterpret_cast<__bf16 *>(a->G),
+                               (res && d->training) ? L.s2 : nullptr,
+                               (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s));
+  } else {
   float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
   HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s));
   {
@@ -453,6 +483,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.T_dst = T;
     conv_tiles(p);
     HIP_TRY(launch_conv_gemm(p, s));
+  }
   }
   if (res) return residual_fwd_tail(d, a, L, s);
   // Temporal (9,1) conv, stride (s,1), pad (4,0), bias (st_graphconv.py:41-43,99),
@@ -602,13 +633,31 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   // residual block), then
   //   dW' = dZ G^T (split-K), H_k = W_k^T dZ, dxhat = sum_k H_k A_k,
   //   dA = sum H_k^T f(BN1(x)) + bias part, dbW = sum dZ rowsum(A_k).
-  const float *G = a->G;  // kept by the forward, else recomputed
-  if (!G) {
-    HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K, res,
-                              s));
-    G = L.G;
-  }
-  {
+  if (fused_sp(d) && a->G) {
+    // the bf16 G kept by the fused forward (k_sp_fwd_bf16) -> k_wgrad_gemm_gk
+    WgradParams w{};
+    w.P = L.dZ;
+    w.Q = a->G;
+    w.slab = L.slab;
+    w.p_bstride = (int64_t)R * T * V;
+    w.R = R;
+    w.C = K * C;
+    w.NQ = 1;
+    w.s_in = 1;
+    w.M = T;
+    w.T_src = T;
+    w.V = V;
+    w.N = N;
+    plan_wgrad_gk(w, T);
+    HIP_TRY(launch_wgrad_gk(w, s));
+    HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));
+  } else {
+    const float *G = fused_sp(d) ? nullptr : a->G;  // kept fp32 G, else recomputed
+    if (!G) {
+      HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K,
+                                res, s));
+      G = L.G;
+    }
     WgradParams w = make_wgrad(d, L.dZ, (int64_t)R * T * V, R, T, G, (int64_t)K * C * T * V,
                                K * C, T, 1, 1, 0, L.slab);
     HIP_TRY(launch_wgrad(w, s));

@@ -180,4 +180,20 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              int N, int C, int T, int V, int K, int write_dx, int relu,
                              hipStream_t s);
 
+// Fused spatial graph convolution of the bf16 path (kernels_fused.hip):
+// Z = W' (f(BN1(x)) A^T) + biasZ in one kernel (BN1 + joint contraction on MFMA
+// with A in LDS + W' GEMM; G never materialised in fp32). Optionally keeps G in
+// bf16 (Gk, layout [n][k*C + ci][frame tile][256]) for the weight gradient.
+bool sp_fwd_bf16_supported(int C, int V, int K);
+size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K);
+size_t sp_keep_g_bytes(int N, int C, int T, int V, int K);
+hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,
+                              const float *g, const float *b, const float *A, const float *W,
+                              const float *biasZ, void *wpk, float *Z, __bf16 *Gk, double *ssum,
+                              double *ssq, int N, int C, int R, int T, int V, int K, int relu,
+                              hipStream_t s);
+// dW' = dZ Gk^T from the kept bf16 G (P = dZ fp32, Q = Gk, C = K*C_in).
+void plan_wgrad_gk(WgradParams &w, int T);
+hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s);
+
 }  // namespace stgcn

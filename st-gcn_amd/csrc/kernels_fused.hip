@@ -1,0 +1,607 @@
+// Fused spatial graph convolution, bf16 path (STGCN_F_BF16) — gfx950 only.
+//
+// k_sp_fwd_bf16<V, K>: the whole SpatialConv of the block in one kernel,
+//   Z[n, co, t, v] = sum_k sum_ci W_k[co, ci] * G_k[n, ci, t, v] + biasZ[co, v],
+//   G_k[n, ci, t, v] = sum_w A_k[v, w] * f(BN1(x))[n, ci, t, w]
+// (st_graphconv.py:98 BN1, :139-152 SpatialConv in the form (1) of capi.hip;
+// f = ReLU for the residual block, :72-74). The joint contraction runs on the
+// matrix cores with A pinned in LDS, so the K*C_in-channel G is never written to
+// and read back from HBM in fp32 (the unfused path: k_gather_mfma writes G,
+// k_conv_bf16<1,...> reads it):
+//   per workgroup: clip n, FT = 256/V frames, 64 output channels (row tile);
+//   per chunk of 16 input channels:
+//     X  = bf16(f(BN1(x)))  [row = t*16 + ch][w]            (staged from HBM)
+//     G  = X * (Ah + Am)^T  on v_mfma_f32_32x32x16_bf16, A as two exact bf16
+//          planes (A = Ah + Am to 2^-16): rows (t, ch) x cols (k, v), k-dim w
+//     G  -> bf16 image [position t*V + v][k*16 + ch] (16-byte octet slots,
+//          2K+1 slots per position: odd, ds_read_b128 conflict-free)
+//     Z += W'(chunk) * G    on v_mfma_f32_32x32x16_bf16 (the W' GEMM; packed
+//          bf16 weights [chunk][k][octet][64 rows][8] by LDS-DMA)
+//   epilogue: conv_tile_epilogue (bias table, BN2 statistics of the residual
+//   block), Z in fp32.
+// Numerics: the same roundings as the reference run with bf16 conv operands
+// (BN1(x) and W rounded to bf16, fp32 accumulation) plus G rounded to bf16 as
+// the W' GEMM operand (as in the unfused bf16 path); A enters exactly to 2^-16.
+// Optionally (Gk != null, row-tile 0 only) the bf16 G image is also written to
+// HBM for the backward weight gradient dW' = dZ G^T, in the layout
+//   Gk[n][k*C_in + ci][mtile][256 positions]   (positions >= NCOLS are zero)
+// i.e. half the bytes of the fp32 G and already the operand precision the
+// bf16 weight gradient uses (k_wgrad_gemm_bf16 rounds G to bf16 at read).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+#include "internal.h"
+
+namespace stgcn {
+
+typedef __bf16 bf16x8f __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2f __attribute__((ext_vector_type(2)));
+typedef int int4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ floatx16 mfma_bf(bf16x8f a, bf16x8f b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ unsigned pkbf(float a, float b) {
+  const bf16x2f v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+
+template <int V, int K>
+struct SpFwdGeo {
+  static constexpr int FT = kTileCols / V;
+  static constexpr int NCOLS = FT * V;
+  static constexpr int CK = 16;                    // input channels per chunk
+  static constexpr int XROWS = CK * FT;            // gather rows (t, ch)
+  static constexpr int RT = (XROWS + 31) / 32;     // gather row tiles
+  static constexpr int KW = (V + 15) & ~15;        // gather reduction (joints w), padded
+  static constexpr int KS = KW / 16;               // gather k-steps
+  static constexpr int XP = KW + 8;                // X / A image pitch (bf16): conflict-free b128
+  static constexpr int NGC = K * V;                // gather columns (k, v)
+  static constexpr int GC = (NGC + 31) / 32;       // gather column tiles
+  static constexpr int GT = RT * GC;               // gather tiles
+  static constexpr int SLOTS = 2 * K + 1;          // G image 16-byte slots per position
+  static constexpr int X_BYTES = RT * 32 * XP * 2;
+  static constexpr int A_BYTES = GC * 32 * XP * 2;  // one plane
+  static constexpr int G_BYTES = NCOLS * SLOTS * 16;
+  static constexpr int W_BYTES = K * 2 * 1024;     // packed W' chunk
+  static constexpr int NIT = CK * NCOLS;           // x staging items (ch, pos)
+  static constexpr int IPT = (NIT + 255) / 256;
+  // layout: [A h][A m][X][G][W0][W1][BN tables 2 x 3 x 16 floats]
+  static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = 2 * A_BYTES;
+  static constexpr int OFF_G = OFF_X + X_BYTES, OFF_W = OFF_G + G_BYTES;
+  static constexpr int OFF_BN = OFF_W + 2 * W_BYTES;
+  static constexpr int LDS = OFF_BN + 2 * 3 * 16 * 4;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(LDS >= 2048 + 64 * V * 4, "epilogue scratch fits");
+  static_assert(IPT <= 16, "staging registers");
+};
+
+struct SpFwdParams {
+  const float *x, *mean, *invstd, *g, *b, *A;
+  const __bf16 *wpk;  // [rt][chunk][k][octet][64][8]
+  __bf16 *Gk;         // optional kept G (bf16 tile layout), or null
+  int C, T, relu, nchunks;
+  ConvGemmParams ep;  // epilogue: out = Z, bias_rv, stats, R, V, M, T_dst, tiles
+};
+
+#define SPF_ST16(k)                                                                        \
+  "+v"(st[k + 0]), "+v"(st[k + 1]), "+v"(st[k + 2]), "+v"(st[k + 3]), "+v"(st[k + 4]),   \
+      "+v"(st[k + 5]), "+v"(st[k + 6]), "+v"(st[k + 7])
+__device__ __forceinline__ void spf_wait_all(float (&st)[16]) {
+  asm volatile("s_waitcnt vmcnt(0)" : SPF_ST16(0), SPF_ST16(8)::"memory");
+}
+#undef SPF_ST16
+
+template <int V, int K>
+__global__ __launch_bounds__(256, 2) void k_sp_fwd_bf16(SpFwdParams P) {
+  using G = SpFwdGeo<V, K>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const ConvGemmParams &p = P.ep;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rt = bid % p.n_rtiles;
+  bid /= p.n_rtiles;
+  const int mt = bid % p.n_mtiles;
+  const int n = bid / p.n_mtiles;
+  const int r0 = rt * kTileRows, m0 = mt * G::FT;
+  const int TV = P.T * V;
+  const int nch = P.nchunks;
+
+  // ---- prologue: A planes (h, m) and zeroed X pads --------------------------
+  {
+    __bf16 *ah = reinterpret_cast<__bf16 *>(lds + G::OFF_AH);
+    __bf16 *am = reinterpret_cast<__bf16 *>(lds + G::OFF_AM);
+    for (int e = tid; e < G::GC * 32 * G::XP; e += 256) {
+      const int c = e / G::XP, w = e - c * G::XP;
+      const int k = c / V, v = c - k * V;
+      float a = 0.f;
+      if (c < G::NGC && w < V) a = P.A[(k * V + v) * V + w];
+      const __bf16 h = (__bf16)a;
+      ah[e] = h;
+      am[e] = (__bf16)(a - (float)h);
+    }
+    unsigned *xz = reinterpret_cast<unsigned *>(lds + G::OFF_X);
+    for (int e = tid; e < G::X_BYTES / 4; e += 256) xz[e] = 0u;
+  }
+  // ---- x staging: items (ch, pos), consecutive threads = consecutive positions
+  const uint64_t xsrc = reinterpret_cast<uint64_t>(P.x + (int64_t)n * P.C * TV);
+  int loff[G::IPT];     // X image element offset (-1: no item)
+  unsigned goff[G::IPT];  // byte offset within the chunk's first channel (kOOB: zero)
+  int ich[G::IPT];
+#pragma unroll
+  for (int k = 0; k < G::IPT; ++k) {
+    const int e = k * 256 + tid;
+    const int ch = e / G::NCOLS, pos = e - ch * G::NCOLS;
+    const int t = pos / V, w = pos - t * V;
+    const bool live = e < G::NIT;
+    loff[k] = live ? (t * 16 + ch) * G::XP + w : -1;
+    ich[k] = live ? ch : 0;
+    goff[k] = (live && m0 * V + pos < TV) ? (unsigned)((ch * TV + m0 * V + pos) * 4) : kOOB;
+  }
+  float st[16];
+  auto load_x = [&](int chunk) {
+    const int64_t rem = (int64_t)(P.C - chunk * G::CK) * TV * 4;
+    const uint64_t src = xsrc + (uint64_t)chunk * G::CK * TV * 4;
+    const int4f rs = {(int)(uint32_t)src, (int)((src >> 32) & 0xffff),
+                      (int)(rem > 0x7fffffff ? 0x7fffffff : (rem > 0 ? rem : 0)), 0x00020000};
+    asm volatile("s_nop 4" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                   : "=v"(st[k])
+                   : "v"(goff[k]), "s"(rs)
+                   : "memory");
+  };
+  float *bnt = reinterpret_cast<float *>(lds + G::OFF_BN);  // [2][3][16]: mean, a, beta
+  auto bn_table = [&](int chunk, int slot) {
+    if (tid < 16) {
+      const int c = chunk * G::CK + tid;
+      float mu = 0.f, a = 0.f, be = 0.f;
+      if (c < P.C) {
+        mu = P.mean[c];
+        a = P.invstd[c] * P.g[c];
+        be = P.b[c];
+      }
+      bnt[slot * 48 + tid] = mu;
+      bnt[slot * 48 + 16 + tid] = a;
+      bnt[slot * 48 + 32 + tid] = be;
+    }
+  };
+  auto write_x = [&](int chunk, int slot) {
+    __bf16 *xi = reinterpret_cast<__bf16 *>(lds + G::OFF_X);
+    const float *tb = bnt + slot * 48;
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+      if (loff[k] >= 0) {
+        const int ch = ich[k];
+        float v = 0.f;
+        if (chunk * G::CK + ch < P.C && goff[k] != kOOB) {
+          v = (st[k] - tb[ch]) * tb[16 + ch] + tb[32 + ch];
+          if (P.relu) v = fmaxf(v, 0.f);
+        }
+        xi[loff[k]] = (__bf16)v;
+      }
+  };
+  // packed W' chunk by LDS-DMA (inline asm: the compiler must not wait for it
+  // before unrelated LDS reads); completion by the s_waitcnt before write_x
+  const uint64_t wsrc =
+      reinterpret_cast<uint64_t>(P.wpk) + (uint64_t)rt * nch * G::W_BYTES;
+  const int4f rsw = {(int)(uint32_t)wsrc, (int)((wsrc >> 32) & 0xffff), nch * G::W_BYTES,
+                     0x00020000};
+  const unsigned ldsw = (unsigned)reinterpret_cast<uintptr_t>(lds + G::OFF_W);
+  auto dma_w = [&](int chunk, int buf) {
+#pragma unroll
+    for (int d = wave; d < 2 * K; d += 4) {
+      const unsigned voffw = (unsigned)(chunk * G::W_BYTES + d * 1024 + lane * 16);
+      const unsigned m0v = ldsw + (unsigned)(buf * G::W_BYTES + d * 1024);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "s"(m0v), "v"(voffw), "s"(rsw)
+          : "memory");
+    }
+  };
+
+  // W' GEMM fragments: wave w -> rows (w&1)*32.., column tiles (w>>1)*4..+3
+  const int mi = wave & 1, nj0 = (wave >> 1) * 4;
+  const int ao = (hi * 64 + mi * 32 + lo) * 16;  // + k * 2 KiB
+  int bo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (nj0 + j) * 32 + lo;
+    bo[j] = ((col < G::NCOLS ? col : 0) * G::SLOTS + hi) * 16;  // + k * 32
+  }
+  floatx16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+
+  bn_table(0, 0);
+  dma_w(0, 0);
+  load_x(0);
+  spf_wait_all(st);
+  __syncthreads();  // BN table, A planes, X pads
+  write_x(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // A: X(c) and W'(c) are in LDS; every wave is done with G(c-1)
+    const bool more = c + 1 < nch;
+    if (more) {
+      bn_table(c + 1, (c + 1) & 1);
+      dma_w(c + 1, (c + 1) & 1);
+      load_x(c + 1);
+    }
+    // -- joint contraction on MFMA: G tiles -> bf16 G image
+    {
+      const char *xi = lds + G::OFF_X;
+      const char *ah = lds + G::OFF_AH, *am = lds + G::OFF_AM;
+      char *gi = lds + G::OFF_G;
+      for (int tt = wave; tt < G::GT; tt += 4) {
+        const int grt = tt / G::GC, gct = tt - grt * G::GC;
+        floatx16 ga;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ga[i] = 0.f;
+        const int xo = ((grt * 32 + lo) * G::XP + 8 * hi) * 2;
+        const int bo2 = ((gct * 32 + lo) * G::XP + 8 * hi) * 2;
+#pragma unroll
+        for (int s = 0; s < G::KS; ++s) {
+          const bf16x8f a = *reinterpret_cast<const bf16x8f *>(xi + xo + s * 32);
+          const bf16x8f bh = *reinterpret_cast<const bf16x8f *>(ah + bo2 + s * 32);
+          const bf16x8f bm = *reinterpret_cast<const bf16x8f *>(am + bo2 + s * 32);
+          ga = mfma_bf(a, bh, ga);
+          ga = mfma_bf(a, bm, ga);
+        }
+        const int col = gct * 32 + lo;
+        const int kk = col / V, v = col - kk * V;
+        if (col < G::NGC) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // register group: 4 consecutive channels
+            const int row = grt * 32 + 8 * q + 4 * hi;
+            const int t = row >> 4, ch0 = row & 15;
+            if (t < G::FT) {
+              uint2 d;
+              d.x = pkbf(ga[4 * q], ga[4 * q + 1]);
+              d.y = pkbf(ga[4 * q + 2], ga[4 * q + 3]);
+              *reinterpret_cast<uint2 *>(gi + ((t * V + v) * G::SLOTS) * 16 +
+                                         (kk * 16 + ch0) * 2) = d;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // B: G(c) complete; X(c) no longer read
+    if (P.Gk && rt == 0) {
+      // kept G for the backward: item (octet o of the 16K channels, 8-position
+      // block b): 8 x ds_read_b128, 8x8 bf16 transpose, 8 x 16-byte stores
+      const char *gi = lds + G::OFF_G;
+      const int o = tid >> 5, b = tid & 31;
+      if (o < 2 * K) {
+        unsigned short vv[8][8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int pos = b * 8 + u;
+          uint4 r = make_uint4(0u, 0u, 0u, 0u);
+          if (pos < G::NCOLS) r = *reinterpret_cast<const uint4 *>(gi + (pos * G::SLOTS + o) * 16);
+          const unsigned w4[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vv[e][u] = (unsigned short)(w4[e >> 1] >> (16 * (e & 1)));
+        }
+        const int kk = o >> 1;  // partition
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int ch = (o & 1) * 8 + e;
+          const int ci = c * G::CK + ch;
+          if (ci < P.C) {
+            uint4 w;
+            w.x = vv[e][0] | ((unsigned)vv[e][1] << 16);
+            w.y = vv[e][2] | ((unsigned)vv[e][3] << 16);
+            w.z = vv[e][4] | ((unsigned)vv[e][5] << 16);
+            w.w = vv[e][6] | ((unsigned)vv[e][7] << 16);
+            const int64_t row = (int64_t)n * K * P.C + (int64_t)kk * P.C + ci;
+            *reinterpret_cast<uint4 *>(P.Gk + (row * p.n_mtiles + mt) * 256 + b * 8) = w;
+          }
+        }
+      }
+    }
+    // -- the W' GEMM: K k-steps (one per partition) of 16 channels
+    {
+      const char *wa = lds + G::OFF_W + (c & 1) * G::W_BYTES + ao;
+      const char *gi = lds + G::OFF_G;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const bf16x8f a = *reinterpret_cast<const bf16x8f *>(wa + k * 2048);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x8f b = *reinterpret_cast<const bf16x8f *>(gi + bo[j] + k * 32);
+          acc[j] = mfma_bf(a, b, acc[j]);
+        }
+      }
+    }
+    if (more) {
+      spf_wait_all(st);  // x(c+1) and W'(c+1) landed
+      write_x(c + 1, (c + 1) & 1);
+    }
+  }
+  __syncthreads();  // every wave is done with the images (the epilogue reuses LDS)
+  conv_tile_epilogue<V, G::NCOLS, true>(p, acc, n, r0, m0, smem);
+}
+
+// W (K*C_out, C_in) -> wpk[rt][chunk][k][octet][64 rows][8] bf16 (zero padded)
+__global__ void k_pack_sp_w_bf16(const float *W, __bf16 *wpk, int K, int R, int C, int nch,
+                                 int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int j = (int)(idx & 7);
+  int64_t t = idx >> 3;
+  const int rl = (int)(t & 63);
+  t >>= 6;
+  const int o = (int)(t & 1);
+  t >>= 1;
+  const int k = (int)(t % K);
+  t /= K;
+  const int chunk = (int)(t % nch);
+  const int rt = (int)(t / nch);
+  const int r = rt * 64 + rl, c = chunk * 16 + o * 8 + j;
+  float v = 0.f;
+  if (r < R && c < C) v = W[((int64_t)k * R + r) * C + c];
+  wpk[idx] = (__bf16)v;
+}
+
+bool sp_fwd_bf16_supported(int C, int V, int K) {
+  if (C < 16) return false;  // the first block's 3-channel input stays on the fp32 path
+  // V = 50 is compiled but not selected: its gather (3 x 5 tiles x 4 k-steps x
+  // 2 A planes per 16 channels, recomputed by every 64-row tile) and 100 KB of
+  // LDS (one workgroup per CU) made cfg5 10% slower than the unfused kernels
+  // (1606 vs 1779 clips/s in one A/B call); DESIGN.md §8 has the planned
+  // W-first ordering for it
+  if (V != 18 && V != 25) return false;
+  return K >= 1 && K <= 3;
+}
+
+size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K) {
+  return (size_t)((R + 63) / 64) * ((C + 15) / 16) * K * 2 * 64 * 8 * 2;
+}
+
+size_t sp_keep_g_bytes(int N, int C, int T, int V, int K) {
+  const int FT = kTileCols / V;
+  return (size_t)N * K * C * ((T + FT - 1) / FT) * 256 * 2;
+}
+
+template <int V, int K>
+static void launch_spf(const SpFwdParams &P, int nblk, hipStream_t s) {
+  constexpr int lds = SpFwdGeo<V, K>::LDS;
+  hipLaunchKernelGGL((k_sp_fwd_bf16<V, K>), dim3(nblk), dim3(256), lds, s, P);
+}
+
+hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,
+                              const float *g, const float *b, const float *A, const float *W,
+                              const float *biasZ, void *wpk, float *Z, __bf16 *Gk, double *ssum,
+                              double *ssq, int N, int C, int R, int T, int V, int K, int relu,
+                              hipStream_t s) {
+  if (!sp_fwd_bf16_supported(C, V, K)) return hipErrorInvalidValue;
+  const int nch = (C + 15) / 16;
+  const int nrt = (R + 63) / 64;
+  {
+    const int64_t total = (int64_t)nrt * nch * K * 2 * 64 * 8;
+    hipLaunchKernelGGL(k_pack_sp_w_bf16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W,
+                       reinterpret_cast<__bf16 *>(wpk), K, R, C, nch, total);
+  }
+  SpFwdParams P{};
+  P.x = x;
+  P.mean = mean;
+  P.invstd = invstd;
+  P.g = g;
+  P.b = b;
+  P.A = A;
+  P.wpk = reinterpret_cast<const __bf16 *>(wpk);
+  P.Gk = Gk;
+  P.C = C;
+  P.T = T;
+  P.relu = relu;
+  P.nchunks = nch;
+  ConvGemmParams &p = P.ep;
+  p.out = Z;
+  p.bias_rv = biasZ;
+  p.stat_sum = ssum;
+  p.stat_sq = ssq;
+  p.out_bstride = (int64_t)R * T * V;
+  p.R = R;
+  p.V = V;
+  p.FT = kTileCols / V;
+  p.M = T;
+  p.T_dst = T;
+  p.s_out = 1;
+  p.p_out = 0;
+  p.N = N;
+  p.n_mtiles = (T + p.FT - 1) / p.FT;
+  p.n_rtiles = nrt;
+  const int nblk = N * p.n_mtiles * nrt;
+#define SPF_K(VV)                            \
+  if (K == 1) launch_spf<VV, 1>(P, nblk, s); \
+  else if (K == 2) launch_spf<VV, 2>(P, nblk, s); \
+  else launch_spf<VV, 3>(P, nblk, s);
+  if (V == 18) {
+    SPF_K(18)
+  } else if (V == 25) {
+    SPF_K(25)
+  } else {
+    SPF_K(50)
+  }
+#undef SPF_K
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// k_wgrad_gemm_gk<TR>: the spatial weight gradient dW' = dZ G^T of the bf16
+// path reading the G kept by k_sp_fwd_bf16 (bf16, Gk[n][c][mtile][256]):
+//   slab[split][r][c] = sum_{items} sum_{i < 32} dZ[n][r][m0*V + kc*32 + i]
+//                                               * Gk[n][c][mt][kc*32 + i]
+// item = (clip n, frame tile mt, 32-position piece kc < 8). Tiles TR x 256
+// (8 or 4 waves of 64 x 64) as k_wgrad_gemm_bf16; dZ staged in fp32 by 4-byte
+// LDS-DMA and rounded at fragment read, G staged in bf16 by 16-byte LDS-DMA
+// into rows of 5 slots (the fifth an OOB zero pad: 80-byte pitch, conflict-free
+// ds_read_b128 straight into the MFMA B fragment, no conversion).
+// ---------------------------------------------------------------------------
+template <int TR>
+struct WgGkGeo {
+  static constexpr int TC = 256, KC = 32, PITCH = KC + 4;  // P pitch (floats)
+  static constexpr int PSZ = TR * PITCH;                    // floats
+  static constexpr int QSLOTS = TC * 5;                     // 16-byte slots of the G image
+  static constexpr int QBYTES = QSLOTS * 16;
+  static constexpr int BUF = PSZ * 4 + QBYTES;              // bytes per buffer
+  static constexpr int NWR = TR / 64, NW = NWR * 4, NTH = NW * 64;
+  static constexpr int PROUNDS = (PSZ + NTH - 1) / NTH;
+  static constexpr int QROUNDS = (QSLOTS + NTH - 1) / NTH;
+};
+
+template <int TR>
+__global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
+  using G = WgGkGeo<TR>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = p.n_rtiles * p.n_jtiles;
+  const int tile = bid % ntiles;
+  const int split = bid / ntiles;
+  const int ct = tile % p.n_jtiles, rt = tile / p.n_jtiles;
+  const int V = p.V, L = p.M * V, FTV = (kTileCols / V) * V;
+  const int nmt = p.n_mtiles / 8;  // frame tiles per clip
+  const int r0 = rt * TR, c0 = ct * G::TC;
+  const int prow_lim = min(TR, p.R - r0), qrow_lim = min(G::TC, p.C - c0);
+  const int total = p.N * p.n_mtiles;
+  const int per = (total + p.S - 1) / p.S;
+  const int it0 = split * per, it1 = min(total, it0 + per);
+  // P: round i of this wave fills floats [(i*NW + wave)*64 + lane]
+  int prow[G::PROUNDS], pcol[G::PROUNDS];
+#pragma unroll
+  for (int i = 0; i < G::PROUNDS; ++i) {
+    const int pos = (i * G::NW + wave) * 64 + lane;
+    prow[i] = pos < G::PSZ ? pos / G::PITCH : -1;
+    pcol[i] = pos < G::PSZ ? pos - prow[i] * G::PITCH : 0;
+  }
+  // Q: round i fills slots [(i*NW + wave)*64 + lane]: row = slot / 5, piece = slot % 5
+  int qrow[G::QROUNDS], qpc[G::QROUNDS];
+#pragma unroll
+  for (int i = 0; i < G::QROUNDS; ++i) {
+    const int sl = (i * G::NW + wave) * 64 + lane;
+    qrow[i] = sl < G::QSLOTS ? sl / 5 : -1;
+    qpc[i] = sl < G::QSLOTS ? sl - (sl / 5) * 5 : 4;
+  }
+  const __bf16 *Gk = reinterpret_cast<const __bf16 *>(p.Q);
+  auto stage = [&](int it, char *buf) {
+    const int n = it / p.n_mtiles, rem = it - n * p.n_mtiles;
+    const int mt = rem >> 3, kc = rem & 7;
+    const int l0 = mt * FTV + kc * G::KC;
+    const int lim = min(min(G::KC, FTV - kc * G::KC), L - l0);  // valid positions of the piece
+    const __amdgpu_buffer_rsrc_t rs_p =
+        make_rsrc(p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * L, (int64_t)prow_lim * L);
+    float *pb = reinterpret_cast<float *>(buf);
+#pragma unroll
+    for (int i = 0; i < G::PROUNDS; ++i) {
+      const int base = (i * G::NW + wave) * 64;  // wave-uniform
+      if (base < G::PSZ) {
+        const bool ok = prow[i] >= 0 && prow[i] < prow_lim && pcol[i] < lim;
+        const unsigned voff = ok ? (unsigned)(prow[i] * L + l0 + pcol[i]) * 4u : kOOB;
+        blds_f32(rs_p, voff, pb + base);
+      }
+    }
+    // Gk rows of this clip / column tile: (c0 + row) * nmt * 256 + mt * 256 + kc * 32
+    const __amdgpu_buffer_rsrc_t rs_q = make_rsrc(
+        reinterpret_cast<const float *>(Gk + ((int64_t)n * p.C + c0) * nmt * 256),
+        (int64_t)qrow_lim * nmt * 256 / 2);
+#pragma unroll
+    for (int i = 0; i < G::QROUNDS; ++i) {
+      const int base = (i * G::NW + wave) * 64;
+      if (base < G::QSLOTS) {
+        const bool ok = qrow[i] >= 0 && qrow[i] < qrow_lim && qpc[i] < 4;
+        const unsigned voff =
+            ok ? (unsigned)((qrow[i] * nmt + mt) * 256 + kc * G::KC + qpc[i] * 8) * 2u : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs_q, reinterpret_cast<float *>(buf + G::PSZ * 4 + base * 16), 16, voff, 0, 0, 0);
+      }
+    }
+  };
+  const int wr = wave / 4, wc = wave % 4;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  char *buf0 = lds, *buf1 = lds + G::BUF;
+  if (it0 < it1) stage(it0, buf0);
+  __syncthreads();
+  for (int it = it0; it < it1; ++it) {
+    const bool odd = (it - it0) & 1;
+    const char *cur = odd ? buf1 : buf0;
+    if (it + 1 < it1) stage(it + 1, odd ? buf0 : buf1);
+    const float *pa = reinterpret_cast<const float *>(cur) + (wr * 64 + lo) * G::PITCH + 8 * hi;
+    const char *qb = cur + G::PSZ * 4 + ((wc * 64 + lo) * 5 + hi) * 16;
+#pragma unroll
+    for (int s = 0; s < G::KC / 16; ++s) {
+      bf16x8f a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float *src = pa + i * 32 * G::PITCH + 16 * s;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[i][u] = (__bf16)src[u];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        b[j] = *reinterpret_cast<const bf16x8f *>(qb + j * 32 * 5 * 16 + s * 32);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
+  }
+  float *slab = p.slab + (int64_t)split * p.R * p.C;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c0 + wc * 64 + j * 32 + lo;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int r = r0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
+        if (r < p.R && c < p.C) slab[(int64_t)r * p.C + c] = acc[i][j][e];
+      }
+    }
+}
+
+void plan_wgrad_gk(WgradParams &w, int T) {
+  const int FT = kTileCols / w.V;
+  w.FT = 0;
+  w.CT = w.R > 64 ? 128 : 64;
+  w.n_mtiles = (T + FT - 1) / FT * 8;
+  w.n_rtiles = (w.R + w.CT - 1) / w.CT;
+  w.n_jtiles = (w.C + 255) / 256;
+  const int tiles = w.n_rtiles * w.n_jtiles;
+  w.S = std::max(1, std::min((256 + tiles - 1) / tiles, w.N * w.n_mtiles));
+  w.bf16 = 1;
+}
+
+hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s) {
+  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  if (p.CT == 128)
+    hipLaunchKernelGGL((k_wgrad_gemm_gk<128>), dim3(nblk), dim3(WgGkGeo<128>::NTH),
+                       2 * WgGkGeo<128>::BUF, s, p);
+  else
+    hipLaunchKernelGGL((k_wgrad_gemm_gk<64>), dim3(nblk), dim3(WgGkGeo<64>::NTH),
+                       2 * WgGkGeo<64>::BUF, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace stgcn

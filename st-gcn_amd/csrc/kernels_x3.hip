@@ -302,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
         if (qq + 1 < TG) {
           // tap qq+1's 9 fragment reads among tap qq's 12 MFMAs
           ld(wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) & 1]);
-          mm(f[qq & 1]);
+          if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
 #pragma unroll
           for (int i = 0; i < 9; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
           }
           __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
         } else {
-          mm(f[qq & 1]);
+          if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }

@@ -110,14 +110,16 @@ def _args(cls, ptrs, drop, seed, **extra):
     return a
 
 
-def _keep_g(ctx, x, K):
-    """Buffer for the joint contraction G (N, K*C_in, T, V) when a backward
-    will run (the forward writes it once; the backward then skips recomputing
-    it), else None (eval / no-grad: the library uses its workspace)."""
+def _keep_g(ctx, x, desc):
+    """Buffer for the joint contraction G when a backward will run (the
+    forward writes it once; the backward then skips recomputing it), else None
+    (eval / no-grad: the library uses its workspace). Size and format from
+    stgcn_keep_g_bytes: fp32 (N, K*C_in, T, V), or bf16 frame tiles where the
+    bf16 path's fused spatial kernel runs."""
     if not (torch.is_grad_enabled() or any(ctx.needs_input_grad)):
         return None
-    N, C, T, V = x.shape
-    return torch.empty((N, K * C, T, V), device=x.device, dtype=torch.float32)
+    nbytes = hip_lib.lib().stgcn_keep_g_bytes(ctypes.byref(desc))
+    return torch.empty(nbytes, device=x.device, dtype=torch.uint8)
 
 
 class StgcnBlockFn(torch.autograd.Function):
@@ -150,7 +152,7 @@ class StgcnBlockFn(torch.autograd.Function):
         Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
         U = torch.empty_like(y)
         stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
-        G = _keep_g(ctx, x, K)
+        G = _keep_g(ctx, x, desc)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (
@@ -236,7 +238,7 @@ class StgcnResBlockFn(torch.autograd.Function):
         Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
         Za = torch.empty_like(Z)
         stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
-        G = _keep_g(ctx, x, K)
+        G = _keep_g(ctx, x, desc)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (

@@ -77,7 +77,7 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_block_fwd", "stgcn_block_bwd", "stgcn_time_kernel_bytes",
             "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
             "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
-            "stgcn_spatial_fwd", "stgcn_spatial_bwd")
+            "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes")
 
 _LIB = None
 
@@ -93,7 +93,8 @@ def load_library(path=LIB_PATH):
     lib.stgcn_last_error.restype = ctypes.c_char_p
     lib.stgcn_check_desc.argtypes = [ctypes.POINTER(Desc)]
     lib.stgcn_check_desc.restype = ctypes.c_int
-    for f in (lib.stgcn_fwd_workspace_bytes, lib.stgcn_bwd_workspace_bytes):
+    for f in (lib.stgcn_fwd_workspace_bytes, lib.stgcn_bwd_workspace_bytes,
+              lib.stgcn_keep_g_bytes):
         f.argtypes = [ctypes.POINTER(Desc)]
         f.restype = ctypes.c_size_t
     lib.stgcn_block_fwd.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(FwdArgs), _vp,
