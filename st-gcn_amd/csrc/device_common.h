@@ -137,8 +137,12 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
         const int i = g * 4 + ii;
         const int row = rowb + (i & 3) + 8 * (i >> 2);
         const bool rok = row < p.R;
-        const float br = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(rs_b, rok ? row * 4 : (int)kOOB, 0, 0));
+        // (null bias pointers: uniform branches, so no load is issued for them --
+        // an OOB load still costs a trip through the memory pipeline and a wait)
+        float br = 0.f;
+        if (p.bias_r)
+          br = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rs_b, rok ? row * 4 : (int)kOOB, 0, 0));
         double s = 0.0, sq = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -147,8 +151,9 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
           if constexpr (BV_LDS) {
             if (p.bias_rv && ok) val += sbv[(row - r0) * V + cv[j]];
           } else {
-            val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                 rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
+            if (p.bias_rv)
+              val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
           }
           const int off = ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB;
           if (p.res)
@@ -204,6 +209,115 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
     epilogue(std::true_type{});
   else
     epilogue(std::false_type{});
+}
+
+// ---------------------------------------------------------------------------
+// Row-major epilogue for tiles staged in LDS (k_conv_x3): the workgroup's
+// 64 x NCOLS tile is first written as fp32 into an LDS image [64][kEpiPitch]
+// (acc_to_img, one ds_write_b32 per accumulator register: lanes 0-31 and 32-63
+// each write 32 consecutive words), then every thread takes whole 16-byte
+// pieces of rows (TPR = NT / 64 threads per row, piece q, q + TPR, ...) and
+// applies bias / bias table / residual / ReLU / dropout / BN statistics in
+// registers and stores with 16-byte stores (8- or 4-byte where the output
+// rows are not so aligned). Per-row statistics reduce over the TPR adjacent
+// lanes of the row by shuffles. Versus conv_tile_epilogue: all waves store,
+// NT/64 x fewer store instructions per byte, no register hand-over between
+// waves. Output stride s_out == 1 only (the caller keeps conv_tile_epilogue
+// for the stride-2 data-gradient phases).
+// ---------------------------------------------------------------------------
+constexpr int kEpiPitch = 260;  // floats: rows 4 words apart modulo 64 banks
+
+__device__ __forceinline__ void acc_to_img(float *img, const floatx16 &a, int row0, int col0) {
+  const int lane = threadIdx.x & 63, hi = lane >> 5, lo = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    img[(row0 + (i & 3) + 8 * (i >> 2) + 4 * hi) * kEpiPitch + col0 + lo] = a[i];
+}
+
+template <int V, int NCOLS, int NT>
+__device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, const float *img,
+                                                     float *sbv, int n, int r0, int m0) {
+  constexpr int TPR = NT / 64;
+  constexpr int NP = (NCOLS + 3) / 4;  // 16-byte pieces per row
+  constexpr int PPT = (NP + TPR - 1) / TPR;
+  const int tid = threadIdx.x;
+  const int r = tid / TPR, q = tid - r * TPR;
+  const int row = r0 + r;
+  const bool rok = row < p.R;
+  const int ostride = p.T_dst * V;
+  const int ncv = min(NCOLS, (p.M - m0) * V);  // valid columns of the tile
+  if (p.bias_rv) {  // the tile's rows of the bias table, coalesced (uniform branch)
+    const int nrow = min(64, p.R - r0);
+    for (int i = tid; i < nrow * V; i += NT) sbv[i] = p.bias_rv[r0 * V + i];
+    __syncthreads();
+  }
+  const float br = (p.bias_r && rok) ? p.bias_r[row] : 0.f;
+  const int64_t obase = (int64_t)n * p.out_bstride + (int64_t)row * ostride + (int64_t)m0 * V;
+  float *out = p.out + obase;
+  const float *res = p.res ? p.res + obase : nullptr;
+  const int vec = ((obase & 3) == 0 && (ostride & 3) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(p.out) & 15) == 0) &&
+                   (!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0))
+                      ? 4
+                      : (((obase & 1) == 0 && (ostride & 1) == 0) ? 2 : 1);
+  double s = 0.0, sq = 0.0;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int pc = q + k * TPR;
+    if (pc >= NP) break;
+    const int c0 = pc * 4;
+    const float4 a = *reinterpret_cast<const float4 *>(img + r * kEpiPitch + c0);
+    float v[4] = {a.x, a.y, a.z, a.w};
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool full = rok && c0 + 3 < ncv;
+    if (res && rok) {
+      if (full && vec == 4) {
+        const float4 t = *reinterpret_cast<const float4 *>(res + c0);
+        rv[0] = t.x; rv[1] = t.y; rv[2] = t.z; rv[3] = t.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c0 + e < ncv) rv[e] = res[c0 + e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = c0 + e;
+      const bool ok = rok && col < ncv;
+      float val = v[e] + br;
+      if (p.bias_rv && ok) val += sbv[r * V + col % V];
+      val += rv[e];
+      if (p.relu_out) val = fmaxf(val, 0.f);
+      if (p.drop.thresh && ok)
+        val = dropout_keep(p.drop, (uint64_t)(obase + col)) ? val * p.drop.scale : 0.f;
+      v[e] = val;
+      if (p.stat_sum && ok) {
+        s += (double)val;
+        sq += (double)val * (double)val;
+      }
+    }
+    if (full && vec == 4) {
+      *reinterpret_cast<float4 *>(out + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else if (full && vec == 2) {
+      *reinterpret_cast<float2 *>(out + c0) = make_float2(v[0], v[1]);
+      *reinterpret_cast<float2 *>(out + c0 + 2) = make_float2(v[2], v[3]);
+    } else if (rok) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c0 + e < ncv) out[c0 + e] = v[e];
+    }
+  }
+  if (p.stat_sum) {  // per-row sums over the TPR adjacent lanes of the row
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) {
+      s += __shfl_xor(s, o, 64);
+      sq += __shfl_xor(sq, o, 64);
+    }
+    if (q == 0 && rok) {
+      atomicAdd(p.stat_sum + row, s);
+      atomicAdd(p.stat_sq + row, sq);
+    }
+  }
 }
 
 }  // namespace stgcn

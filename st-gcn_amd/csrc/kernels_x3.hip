@@ -125,6 +125,7 @@ struct ConvX3Geo {
   static_assert(NQ % TG == 0, "whole tap groups");
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(4096 + 4 * 2 * 64 * 16 * 4 <= LDS, "epilogue hand-over fits");
+  static_assert((64 * kEpiPitch + 64 * V) * 4 <= LDS, "row-major epilogue image fits");
 };
 
 template <int NQ, int TG, int V, int SIN>
@@ -325,6 +326,20 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[j] += acl[j];
+  if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
+    if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
+    return;
+  }
+  if (p.s_out == 1) {
+    // row-major epilogue through LDS: every wave writes its two tiles, then all
+    // 512 threads store whole 16-byte row pieces (device_common.h)
+    __syncthreads();  // every wave is done with the buffers
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc_to_img(smem, acc[j], mi * 32, (nj0 + j) * 32);
+    __syncthreads();
+    conv_tile_store_rows<V, G::NCOLS, 512>(p, smem, smem + 64 * kEpiPitch, n, r0, m0);
+    return;
+  }
   // hand-over: waves 4-7 give their two column tiles to waves 0-3 (same rows,
   // next two tiles), which run the shared 4-wave epilogue
   float *ho = smem + 1024 + (wave & 3) * 2 * 64 * 16;
