@@ -213,10 +213,10 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
 
 // ---------------------------------------------------------------------------
 // Row-major epilogue for tiles staged in LDS (k_conv_x3): the workgroup's
-// 64 x NCOLS tile is first written as fp32 into an LDS image [64][kEpiPitch]
+// ROWS (64 or 128) x NCOLS tile is first written as fp32 into an LDS image [ROWS][kEpiPitch]
 // (acc_to_img, one ds_write_b32 per accumulator register: lanes 0-31 and 32-63
 // each write 32 consecutive words), then every thread takes whole 16-byte
-// pieces of rows (TPR = NT / 64 threads per row, piece q, q + TPR, ...) and
+// pieces of rows (TPR = NT / ROWS threads per row, piece q, q + TPR, ...) and
 // applies bias / bias table / residual / ReLU / dropout / BN statistics in
 // registers and stores with 16-byte stores (8- or 4-byte where the output
 // rows are not so aligned). Per-row statistics reduce over the TPR adjacent
@@ -234,10 +234,11 @@ __device__ __forceinline__ void acc_to_img(float *img, const floatx16 &a, int ro
     img[(row0 + (i & 3) + 8 * (i >> 2) + 4 * hi) * kEpiPitch + col0 + lo] = a[i];
 }
 
-template <int V, int NCOLS, int NT>
+template <int V, int NCOLS, int NT, int ROWS = 64>
 __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, const float *img,
                                                      float *sbv, int n, int r0, int m0) {
-  constexpr int TPR = NT / 64;
+  constexpr int TPR = NT / ROWS;
+  static_assert(TPR >= 1 && NT % ROWS == 0, "whole threads per row");
   constexpr int NP = (NCOLS + 3) / 4;  // 16-byte pieces per row
   constexpr int PPT = (NP + TPR - 1) / TPR;
   const int tid = threadIdx.x;
@@ -247,7 +248,7 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
   const int ostride = p.T_dst * V;
   const int ncv = min(NCOLS, (p.M - m0) * V);  // valid columns of the tile
   if (p.bias_rv) {  // the tile's rows of the bias table, coalesced (uniform branch)
-    const int nrow = min(64, p.R - r0);
+    const int nrow = min(ROWS, p.R - r0);
     for (int i = tid; i < nrow * V; i += NT) sbv[i] = p.bias_rv[r0 * V + i];
     __syncthreads();
   }

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 #include "internal.h"
@@ -90,8 +91,9 @@ __device__ __forceinline__ void wait_img(float (&st)[3][8]) {
 }
 #undef X3_ST8
 
-template <int NQ, int TG, int V, int SIN>
+template <int NQ, int TG, int V, int SIN, int MR>
 struct ConvX3Geo {
+  static constexpr int ROWS = 64 * MR;            // output rows per workgroup
   static constexpr int CK = 16;                   // channels per chunk (one k-step)
   static constexpr int FT = kTileCols / V;
   static constexpr int NCOLS = FT * V;
@@ -99,12 +101,18 @@ struct ConvX3Geo {
   static constexpr int SLOTS = 7;                 // 6 (plane, octet) slots + 1 pad
   static constexpr int IMG = SPAN * SLOTS * 16;   // window bytes
   static constexpr int NG = NQ / TG;              // steps per chunk
-  static constexpr int WST = 3 * TG * 2 * 1024;   // packed weight bytes per step
+  static constexpr int WST = 3 * TG * 2 * 1024 * MR;  // packed weight bytes per step
   static constexpr int WDMA = WST / 1024;         // 1 KiB DMA pieces per step
-  // weight ring: 3 step buffers (prefetch distance 2) where LDS allows
-  // window double-buffered where LDS allows (else written between two barriers)
-  static constexpr int NWIN = 3 * WST + 2 * IMG <= 160 * 1024 ? 2 : 1;
-  static constexpr int NWB = 3 * WST + NWIN * IMG <= 160 * 1024 ? 3 : 2;
+  // LDS plan, first that fits: window double-buffered with a 3-step weight ring
+  // (prefetch distance 2), double-buffered with a 2-step ring, or a single
+  // window (written between two barriers) with a 3- or 2-step ring
+  static constexpr int BUDGET = 160 * 1024;
+  static constexpr int PLAN = 3 * WST + 2 * IMG <= BUDGET   ? 0
+                              : 2 * WST + 2 * IMG <= BUDGET ? 1
+                              : 3 * WST + IMG <= BUDGET     ? 2
+                                                            : 3;
+  static constexpr int NWIN = PLAN <= 1 ? 2 : 1;
+  static constexpr int NWB = (PLAN == 0 || PLAN == 2) ? 3 : 2;
   static constexpr int PD = NWB - 1;
   static constexpr int LDS = NWB * WST + NWIN * IMG;
   static constexpr int NIT = SPAN * 2;            // (position, octet) staging items
@@ -115,7 +123,9 @@ struct ConvX3Geo {
   // vmcnt allowance at step g's barrier (DMA(s) must have landed): the VMEM
   // operations every wave issued after DMA(s) in steady state — the pieces of
   // the PD-1 later weight steps and the window loads of the chunk-start steps
-  // among the PD steps before s (fewer before that: the wait is conservative)
+  // among the PD steps before s (fewer before that: the wait is conservative).
+  // In a tile's last PD-1 steps fewer weight steps follow: the kernel waits
+  // for everything there (vmcnt(0)).
   static constexpr int wait_n(int g) {
     int n = (PD - 1) * DPWMIN;
     for (int k = 1; k <= PD; ++k)
@@ -123,14 +133,14 @@ struct ConvX3Geo {
     return n;
   }
   static_assert(NQ % TG == 0, "whole tap groups");
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  static_assert(4096 + 4 * 2 * 64 * 16 * 4 <= LDS, "epilogue hand-over fits");
-  static_assert((64 * kEpiPitch + 64 * V) * 4 <= LDS, "row-major epilogue image fits");
+  static_assert(LDS <= BUDGET, "LDS budget");
+  static_assert(MR == 2 || 4096 + 4 * 2 * 64 * 16 * 4 <= LDS, "epilogue hand-over fits");
+  static_assert((ROWS * kEpiPitch + ROWS * V) * 4 <= LDS, "row-major epilogue image fits");
 };
 
-template <int NQ, int TG, int V, int SIN>
+template <int NQ, int TG, int V, int SIN, int MR>
 __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
-  using G = ConvX3Geo<NQ, TG, V, SIN>;
+  using G = ConvX3Geo<NQ, TG, V, SIN, MR>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   char *const wbuf0 = lds, *const win0 = lds + G::NWB * G::WST;
@@ -143,7 +153,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   bid /= p.n_rtiles;
   const int mt = bid % p.n_mtiles;
   const int n = bid / p.n_mtiles;
-  const int r0 = rt * kTileRows, m0 = mt * G::FT;
+  const int r0 = rt * G::ROWS, m0 = mt * G::FT;
   const int cstride = p.T_src * V;
   const int g0 = (SIN * m0 + p.off) * V;
   const float *inN = p.in + (int64_t)n * p.in_bstride;
@@ -152,8 +162,9 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   const char *wblk = reinterpret_cast<const char *>(p.wpk) + (int64_t)rt * nsteps * G::WST;
   const int mi = wave & 1, nj0 = ((wave >> 1) & 1) * 4 + half * 2;
 
-  // A fragment (plane 0, tap 0, octet hi) and B fragments (tap 0, plane 0, octet hi)
-  const int ao = (hi * 64 + mi * 32 + lo) * 16;
+  // A fragment (plane 0, tap 0, octet hi, row block 0) and B fragments (tap 0,
+  // plane 0, octet hi); wave rows mi*32*MR .. +32*MR-1 (MR 32-row blocks)
+  const int ao = (hi * G::ROWS + mi * 32 * MR + lo) * 16;
   int bo[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -236,20 +247,29 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   };
 
   // acc: the h*h products; acl: the five small cross terms (<= 2^-8 of acc),
-  // accumulated apart so their roundings stay 2^-8 smaller; summed at the end
-  floatx16 acc[4], acl[2];
+  // accumulated apart so their roundings stay 2^-8 smaller; summed at the end.
+  // Tile (row block rb, column tile j) -> acc[rb*2 + j] (MR = 1: acc[2..3] are
+  // the hand-over registers of the stride-2 epilogue)
+  floatx16 acc[4], acl[2 * MR];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[j][i] = acl[j][i] = 0.f;
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2 * MR; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acl[j][i] = 0.f;
 
   struct Frag {
-    bf16x8_t a[3], b[3][2];
+    bf16x8_t a[3][MR], b[3][2];
   };
   auto ld = [&](const char *wa, const char *win, int qq, int q, Frag &f) {
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
-      f.a[pl] = *reinterpret_cast<const bf16x8_t *>(wa + ((pl * TG + qq) * 2) * 1024);
+#pragma unroll
+      for (int rb = 0; rb < MR; ++rb)
+        f.a[pl][rb] = *reinterpret_cast<const bf16x8_t *>(
+            wa + ((pl * TG + qq) * 2 * MR) * 1024 + rb * 32 * 16);
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
@@ -257,19 +277,20 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
         f.b[pl][j] =
             *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * V * G::SLOTS + 2 * pl) * 16);
   };
+  // the six products (plane of A, plane of B) of one tap over the MR x 2 tiles
   auto mm = [&](const Frag &f) {
+    constexpr int PA[6] = {0, 0, 1, 0, 1, 2}, PB[6] = {0, 1, 0, 2, 1, 0};
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[j] = mfma_x(f.a[0], f.b[0][j], acc[j]);
+    for (int t = 0; t < 6; ++t)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[0], f.b[1][j], acl[j]);
+      for (int rb = 0; rb < MR; ++rb)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[1], f.b[0][j], acl[j]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[0], f.b[2][j], acl[j]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[1], f.b[1][j], acl[j]);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acl[j] = mfma_x(f.a[2], f.b[0][j], acl[j]);
+        for (int j = 0; j < 2; ++j) {
+          if (t == 0)
+            acc[rb * 2 + j] = mfma_x(f.a[0][rb], f.b[0][j], acc[rb * 2 + j]);
+          else
+            acl[rb * 2 + j] = mfma_x(f.a[PA[t]][rb], f.b[PB[t]][j], acl[rb * 2 + j]);
+        }
   };
 
 #pragma unroll
@@ -287,7 +308,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
       // steps earlier; later pieces and window loads stay in flight), then the
       // barrier publishes them and chunk c's window (written in the previous
       // chunk's last step)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::wait_n(g)) : "memory");
+      if (s + G::PD - 1 < nsteps)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::wait_n(g)) : "memory");
+      else  // a tile's last steps: fewer weight steps were issued after DMA(s)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!(STGCN_X3_EXP & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       const char *wa = wbuf0 + (s % G::NWB) * G::WST + ao;
       Frag f[2];
@@ -298,22 +322,78 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
       // unconditional: chunk == nchunks loads zeros and is never read.
       if (!(STGCN_X3_EXP & 2) && s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
       if (!(STGCN_X3_EXP & 4) && g == 0) load_img(c + 1);
+      if constexpr (MR == 1) {
 #pragma unroll
-      for (int qq = 0; qq < TG; ++qq) {
-        if (qq + 1 < TG) {
-          // tap qq+1's 9 fragment reads among tap qq's 12 MFMAs
-          ld(wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) & 1]);
-          if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
+        for (int qq = 0; qq < TG; ++qq) {
+          if (qq + 1 < TG) {
+            // tap qq+1's 9 fragment reads among tap qq's 12 MFMAs
+            ld(wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) & 1]);
+            if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
 #pragma unroll
-          for (int i = 0; i < 9; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            for (int i = 0; i < 9; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+          } else {
+            if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
           }
-          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-        } else {
-          if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
+          __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        // MR = 2: one fragment set, refilled in place for the next tap as its
+        // planes retire (48 instead of 96 fragment registers live). Product
+        // order per tap: mm, lh, hl, mh, hm, hh -- the first (a1 x b1) uses
+        // neither plane-0 fragment, which are the last ones refilled
+        Frag &fr = f[0];
+        auto grp = [&](int pa, int pb) {
+#pragma unroll
+          for (int rb = 0; rb < MR; ++rb)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              if (pa == 0 && pb == 0)
+                acc[rb * 2 + j] = mfma_x(fr.a[0][rb], fr.b[0][j], acc[rb * 2 + j]);
+              else
+                acl[rb * 2 + j] = mfma_x(fr.a[pa][rb], fr.b[pb][j], acl[rb * 2 + j]);
+            }
+        };
+        auto lda = [&](int qq, int pl) {
+#pragma unroll
+          for (int rb = 0; rb < MR; ++rb)
+            fr.a[pl][rb] = *reinterpret_cast<const bf16x8_t *>(
+                wa + ((pl * TG + qq) * 2 * MR) * 1024 + rb * 32 * 16);
+        };
+        auto ldb = [&](int q, int pl) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            fr.b[pl][j] =
+                *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * V * G::SLOTS + 2 * pl) * 16);
+        };
+#pragma unroll
+        for (int qq = 0; qq < TG; ++qq) {
+          const bool nx = qq + 1 < TG;
+          const int q1 = g * TG + qq + 1;
+          grp(1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          grp(2, 0);
+          if (nx) lda(qq + 1, 2);
+          __builtin_amdgcn_sched_barrier(0);
+          grp(0, 2);
+          if (nx) ldb(q1, 2);
+          __builtin_amdgcn_sched_barrier(0);
+          grp(1, 0);
+          if (nx) lda(qq + 1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          grp(0, 1);
+          if (nx) ldb(q1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          grp(0, 0);
+          if (nx) {
+            lda(qq + 1, 0);
+            ldb(q1, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if (!(STGCN_X3_EXP & 1) && g == G::NG - 1) {
         // issued after the loads (step g = 0): the weight pieces of steps 1..NG-1
@@ -325,7 +405,7 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
     }
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) acc[j] += acl[j];
+  for (int j = 0; j < 2 * MR; ++j) acc[j] += acl[j];
   if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
     if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
     return;
@@ -335,11 +415,16 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
     // 512 threads store whole 16-byte row pieces (device_common.h)
     __syncthreads();  // every wave is done with the buffers
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc_to_img(smem, acc[j], mi * 32, (nj0 + j) * 32);
+    for (int rb = 0; rb < MR; ++rb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc_to_img(smem, acc[rb * 2 + j], mi * 32 * MR + rb * 32, (nj0 + j) * 32);
     __syncthreads();
-    conv_tile_store_rows<V, G::NCOLS, 512>(p, smem, smem + 64 * kEpiPitch, n, r0, m0);
+    conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS>(p, smem, smem + G::ROWS * kEpiPitch, n, r0,
+                                                      m0);
     return;
   }
+  if constexpr (MR == 2) return;  // (never: 128-row tiles are launched for s_out == 1 only)
   // hand-over: waves 4-7 give their two column tiles to waves 0-3 (same rows,
   // next two tiles), which run the shared 4-wave epilogue
   float *ho = smem + 1024 + (wave & 3) * 2 * 64 * 16;
@@ -363,17 +448,18 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
 }
 
 // Packs w[r*w_sr + c*w_sc + q*w_sq] split into three bf16 planes:
-// wpk[rt][chunk][tap group][plane][tap in group][octet][64 rows][8] (zero
-// padded rows and channels), so one step's weights are one contiguous run.
+// wpk[rt][chunk][tap group][plane][tap in group][octet][ROWS][8] (ROWS = 64 or
+// 128 rows per tile; zero padded rows and channels), so one step's weights are
+// one contiguous run.
 __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int NQ, int TG,
-                                 int nch, int64_t w_sr, int64_t w_sc, int64_t w_sq,
+                                 int nch, int rows, int64_t w_sr, int64_t w_sc, int64_t w_sq,
                                  int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int jj = (int)(idx & 7);
   int64_t t = idx >> 3;
-  const int rl = (int)(t & 63);
-  t >>= 6;
+  const int rl = (int)(t % rows);
+  t /= rows;
   const int o = (int)(t & 1);
   t >>= 1;
   const int qq = (int)(t % TG);
@@ -385,7 +471,7 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
   t /= NG;
   const int ch = (int)(t % nch);
   const int rt = (int)(t / nch);
-  const int r = rt * 64 + rl, c = ch * 16 + o * 8 + jj, q = g * TG + qq;
+  const int r = rt * rows + rl, c = ch * 16 + o * 8 + jj, q = g * TG + qq;
   float v = 0.f;
   if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
   const __bf16 h = (__bf16)v;
@@ -409,38 +495,56 @@ size_t conv_x3_wpk_bytes(const ConvGemmParams &p) {
   return (size_t)p.n_rtiles * ((p.C + 15) / 16) * 3 * p.NQ * 16 * 64 * 2;
 }
 
-template <int NQ, int V, int SIN>
+// 128-row tiles (two 32-row blocks per wave: half the weight and window
+// staging per MFMA, half the window re-reads over the row tiles) for the
+// 9-tap launches with a whole number of them and unit output stride
+// (STGCN_X3_MR1: 64-row tiles everywhere, A/B measurement only)
+static bool x3_wide_rows(const ConvGemmParams &p) {
+  static const bool off = getenv("STGCN_X3_MR1") != nullptr;
+  return !off && p.NQ == 9 && p.s_out == 1 && p.R % 128 == 0;
+}
+
+template <int NQ, int V, int SIN, int MR>
 static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
   if (p.V != V || p.s_in != SIN) return false;
   constexpr int TG = NQ == 9 ? 3 : NQ;
-  constexpr int lds = ConvX3Geo<NQ, TG, V, SIN>::LDS;
-  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN>), dim3(nblk), dim3(512), lds, s, p);
+  constexpr int lds = ConvX3Geo<NQ, TG, V, SIN, MR>::LDS;
+  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR>), dim3(nblk), dim3(512), lds, s, p);
   return true;
 }
 
-template <int NQ>
+template <int NQ, int MR>
 static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
-  if (launch_cx_if<NQ, 18, 1>(p, nblk, s) || launch_cx_if<NQ, 25, 1>(p, nblk, s)) return true;
+  if (launch_cx_if<NQ, 18, 1, MR>(p, nblk, s) || launch_cx_if<NQ, 25, 1, MR>(p, nblk, s))
+    return true;
   if constexpr (NQ == 9)
-    return launch_cx_if<NQ, 18, 2>(p, nblk, s) || launch_cx_if<NQ, 25, 2>(p, nblk, s);
+    return launch_cx_if<NQ, 18, 2, MR>(p, nblk, s) || launch_cx_if<NQ, 25, 2, MR>(p, nblk, s);
   return false;
 }
 
-hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
-  if (!conv_x3_supported(p) || !p.wpk) return hipErrorInvalidValue;
+hipError_t launch_conv_x3(const ConvGemmParams &p0, hipStream_t s) {
+  if (!conv_x3_supported(p0) || !p0.wpk) return hipErrorInvalidValue;
+  const bool wide = x3_wide_rows(p0);
+  ConvGemmParams p = p0;
+  const int rows = wide ? 128 : 64;
+  p.n_rtiles = (p.R + rows - 1) / rows;
   const int nch = (p.C + 15) / 16;
   {
-    const int64_t total = (int64_t)p.n_rtiles * nch * 3 * p.NQ * 2 * 64 * 8;
+    const int64_t total = (int64_t)p.n_rtiles * nch * 3 * p.NQ * 2 * rows * 8;
     hipLaunchKernelGGL(k_pack_conv_w_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, x3_tg(p.NQ), nch,
-                       p.w_sr, p.w_sc, p.w_sq, total);
+                       rows, p.w_sr, p.w_sc, p.w_sq, total);
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   bool done = false;
-  switch (p.NQ) {
-    case 4: done = launch_cx_v<4>(p, nblk, s); break;
-    case 5: done = launch_cx_v<5>(p, nblk, s); break;
-    case 9: done = launch_cx_v<9>(p, nblk, s); break;
+  if (wide) {
+    done = launch_cx_v<9, 2>(p, nblk, s);
+  } else {
+    switch (p.NQ) {
+      case 4: done = launch_cx_v<4, 1>(p, nblk, s); break;
+      case 5: done = launch_cx_v<5, 1>(p, nblk, s); break;
+      case 9: done = launch_cx_v<9, 1>(p, nblk, s); break;
+    }
   }
   return done ? hipGetLastError() : hipErrorInvalidValue;
 }
@@ -562,9 +666,11 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       }
     }
   };
-  auto write_item = [&](char *buf) {
+  // splits and writes staging groups [K0, K1) of the loaded item
+  auto write_part = [&](char *buf, auto k0_c, auto k1_c) {
+    constexpr int K0 = decltype(k0_c)::value, K1 = decltype(k1_c)::value;
 #pragma unroll
-    for (int k = 0; k < G::GPT; ++k)
+    for (int k = K0; k < K1; ++k)
       if (gl[k] >= 0) {
         uint2 h, m, l;
         split2(st[k][0], st[k][1], h.x, m.x, l.x);
@@ -575,6 +681,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         *reinterpret_cast<uint2 *>(dst + pl) = m;
         *reinterpret_cast<uint2 *>(dst + 2 * pl) = l;
       }
+  };
+  auto write_item = [&](char *buf) {
+    write_part(buf, std::integral_constant<int, 0>{}, std::integral_constant<int, G::GPT>{});
   };
 
   // lane bases (elements) of the A (P) and B (Q) fragments in plane 0
@@ -635,10 +744,27 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       for (int s = 0; s < G::KSTEPS; ++s) {
         if (s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) & 1]);
         mm(f[s & 1]);
+        if constexpr (G::NBUF == 2) {
+          // double buffer: the next item's split + LDS writes ride in the MFMA
+          // shadow of k-steps 1.. (part s-1 of KSTEPS-1), not after the loop
+          static_assert(G::KSTEPS == 5, "four write parts");
+          using std::integral_constant;
+          constexpr int Q = G::GPT;
+          if (s == 1)
+            write_part(nxt, integral_constant<int, 0>{}, integral_constant<int, Q / 4>{});
+          else if (s == 2)
+            write_part(nxt, integral_constant<int, Q / 4>{}, integral_constant<int, Q / 2>{});
+          else if (s == 3)
+            write_part(nxt, integral_constant<int, Q / 2>{}, integral_constant<int, 3 * Q / 4>{});
+          else if (s == 4)
+            write_part(nxt, integral_constant<int, 3 * Q / 4>{}, integral_constant<int, Q>{});
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (G::NBUF == 1) __syncthreads();  // every wave is done reading the buffer
-      write_item(nxt);
+      if constexpr (G::NBUF == 1) {
+        __syncthreads();  // every wave is done reading the buffer
+        write_item(nxt);
+      }
       __syncthreads();
     }
     float *slab = p.slab + (int64_t)split * p.R * p.C * 9;
