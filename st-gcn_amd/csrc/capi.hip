@@ -85,7 +85,7 @@ Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
 // (STGCN_UNFUSED_SP: the unfused gather + GEMM kernels, A/B measurement only)
 bool fused_sp(const stgcn_desc_t *d) {
   static const bool off = getenv("STGCN_UNFUSED_SP") != nullptr;
-  return !off && bf16(d) && sp_fwd_bf16_supported(d->C_in, d->V, d->K);
+  return !off && bf16(d) && sp_fwd_bf16_supported(d->C_in, d->V, d->K, d->C_out, residual(d));
 }
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {

@@ -184,7 +184,7 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
 // Z = W' (f(BN1(x)) A^T) + biasZ in one kernel (BN1 + joint contraction on MFMA
 // with A in LDS + W' GEMM; G never materialised in fp32). Optionally keeps G in
 // bf16 (Gk, layout [n][k*C + ci][frame tile][256]) for the weight gradient.
-bool sp_fwd_bf16_supported(int C, int V, int K);
+bool sp_fwd_bf16_supported(int C, int V, int K, int R, bool residual);
 size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K);
 size_t sp_keep_g_bytes(int N, int C, int T, int V, int K);
 hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,

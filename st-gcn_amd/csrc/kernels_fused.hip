@@ -333,36 +333,358 @@ __global__ __launch_bounds__(256, 2) void k_sp_fwd_bf16(SpFwdParams P) {
   conv_tile_epilogue<V, G::NCOLS, true>(p, acc, n, r0, m0, smem);
 }
 
-// W (K*C_out, C_in) -> wpk[rt][chunk][k][octet][64 rows][8] bf16 (zero padded)
+// ---------------------------------------------------------------------------
+// k_sp_fwd_wide<V, K, ROWS>: the same fused SpatialConv forward for the wide
+// two-person graph (V = 50, K = 3; BASELINE cfg5) with ALL output channels in
+// one workgroup (ROWS = C_out rounded to 64, <= 256), so the joint contraction
+// of a 16-channel chunk -- 3 x 5 tiles x 4 k-steps x 2 A planes, 2.5x the W'
+// GEMM's MFMAs at C_out = 64 -- runs once per (clip, frame tile) instead of
+// once per 64-row tile. 8 waves (two per SIMD), one workgroup per CU:
+//   joint contraction: tile tt of the chunk's RT x GC G tiles -> wave tt % 8;
+//   W' GEMM: wave w -> rows (w & 1) * ROWS/2 .. (ROWS/64 32-row blocks) x
+//            column tiles 2 (w >> 1), +1; packed bf16 W' [chunk][k][octet]
+//            [ROWS][8] by 16-byte LDS-DMA, double-buffered;
+//   epilogue: the row-major LDS image epilogue (conv_tile_store_rows) for
+//            ROWS <= 128; per-wave register stores at 256 (no BN statistics:
+//            residual blocks stay at ROWS <= 128).
+// The x chunk of the next step is loaded under this chunk's MFMAs.
+// ---------------------------------------------------------------------------
+template <int V, int K, int ROWS>
+struct SpWideGeo {
+  static constexpr int NT = 512;
+  static constexpr int FT = kTileCols / V;
+  static constexpr int NCOLS = FT * V;
+  static constexpr int CK = 16;
+  static constexpr int XROWS = CK * FT;
+  static constexpr int RT = (XROWS + 31) / 32;
+  static constexpr int KW = (V + 15) & ~15;
+  static constexpr int KS = KW / 16;
+  static constexpr int XP = KW + 8;
+  static constexpr int NGC = K * V;
+  static constexpr int GC = (NGC + 31) / 32;
+  static constexpr int GT = RT * GC;
+  static constexpr int SLOTS = 2 * K + 1;
+  static constexpr int MB = ROWS / 64;            // 32-row blocks per wave
+  static constexpr int X_BYTES = RT * 32 * XP * 2;
+  static constexpr int A_BYTES = GC * 32 * XP * 2;
+  static constexpr int G_BYTES = NCOLS * SLOTS * 16;
+  static constexpr int W_BYTES = K * 2 * ROWS * 16;  // packed W' chunk
+  static constexpr int NIT = CK * NCOLS;
+  static constexpr int IPT = (NIT + NT - 1) / NT;
+  static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = 2 * A_BYTES;
+  static constexpr int OFF_G = OFF_X + X_BYTES, OFF_W = OFF_G + G_BYTES;
+  static constexpr int OFF_BN = OFF_W + 2 * W_BYTES;
+  static constexpr int MAIN = OFF_BN + 2 * 3 * 16 * 4;
+  static constexpr int EROWS = ROWS < 128 ? ROWS : 128;  // LDS-image epilogue rows
+  static constexpr int EPI = ROWS == 256 ? 0 : (EROWS * kEpiPitch + EROWS * V) * 4;
+  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(IPT == 8, "staging register count");
+  static_assert(ROWS == 64 || ROWS == 128 || ROWS == 256, "row tiles");
+};
+
+template <int V, int K, int ROWS>
+__global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
+  using G = SpWideGeo<V, K, ROWS>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const ConvGemmParams &p = P.ep;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid % p.n_mtiles;
+  const int n = bid / p.n_mtiles;
+  const int m0 = mt * G::FT;
+  const int TV = P.T * V;
+  const int nch = P.nchunks;
+
+  // ---- prologue: A planes (h, m) and zeroed X pads --------------------------
+  {
+    __bf16 *ah = reinterpret_cast<__bf16 *>(lds + G::OFF_AH);
+    __bf16 *am = reinterpret_cast<__bf16 *>(lds + G::OFF_AM);
+    for (int e = tid; e < G::GC * 32 * G::XP; e += G::NT) {
+      const int c = e / G::XP, w = e - c * G::XP;
+      const int k = c / V, v = c - k * V;
+      float a = 0.f;
+      if (c < G::NGC && w < V) a = P.A[(k * V + v) * V + w];
+      const __bf16 h = (__bf16)a;
+      ah[e] = h;
+      am[e] = (__bf16)(a - (float)h);
+    }
+    unsigned *xz = reinterpret_cast<unsigned *>(lds + G::OFF_X);
+    for (int e = tid; e < G::X_BYTES / 4; e += G::NT) xz[e] = 0u;
+  }
+  // ---- x staging: items (ch, pos), consecutive threads = consecutive positions
+  // (item indices recomputed at use: constant divisions, no index registers)
+  const uint64_t xsrc = reinterpret_cast<uint64_t>(P.x + (int64_t)n * P.C * TV);
+  const int pos_lim = min(G::NCOLS, TV - m0 * V);  // valid positions of the tile
+  float st[G::IPT];
+  auto load_x = [&](int chunk) {
+    const int64_t rem = (int64_t)(P.C - chunk * G::CK) * TV * 4;
+    const uint64_t src = xsrc + (uint64_t)chunk * G::CK * TV * 4;
+    const int4f rs = {(int)(uint32_t)src, (int)((src >> 32) & 0xffff),
+                      (int)(rem > 0x7fffffff ? 0x7fffffff : (rem > 0 ? rem : 0)), 0x00020000};
+    unsigned goff[G::IPT];
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k) {
+      const int e = k * G::NT + tid;
+      const int ch = e / G::NCOLS, pos = e - ch * G::NCOLS;
+      goff[k] = (e < G::NIT && pos < pos_lim) ? (unsigned)((ch * TV + m0 * V + pos) * 4) : kOOB;
+    }
+    asm volatile("s_nop 4" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k)
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                   : "=v"(st[k])
+                   : "v"(goff[k]), "s"(rs)
+                   : "memory");
+  };
+  auto wait_x = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4]), "+v"(st[5]),
+                   "+v"(st[6]), "+v"(st[7])::"memory");
+  };
+  float *bnt = reinterpret_cast<float *>(lds + G::OFF_BN);  // [2][3][16]: mean, a, beta
+  auto bn_table = [&](int chunk, int slot) {
+    if (tid < 16) {
+      const int c = chunk * G::CK + tid;
+      float mu = 0.f, a = 0.f, be = 0.f;
+      if (c < P.C) {
+        mu = P.mean[c];
+        a = P.invstd[c] * P.g[c];
+        be = P.b[c];
+      }
+      bnt[slot * 48 + tid] = mu;
+      bnt[slot * 48 + 16 + tid] = a;
+      bnt[slot * 48 + 32 + tid] = be;
+    }
+  };
+  auto write_x = [&](int chunk, int slot) {
+    __bf16 *xi = reinterpret_cast<__bf16 *>(lds + G::OFF_X);
+    const float *tb = bnt + slot * 48;
+#pragma unroll
+    for (int k = 0; k < G::IPT; ++k) {
+      const int e = k * G::NT + tid;
+      const int ch = e / G::NCOLS, pos = e - ch * G::NCOLS;
+      const int t = pos / V, w = pos - t * V;
+      if (e < G::NIT) {
+        float v = 0.f;
+        if (chunk * G::CK + ch < P.C && pos < pos_lim) {
+          v = (st[k] - tb[ch]) * tb[16 + ch] + tb[32 + ch];
+          if (P.relu) v = fmaxf(v, 0.f);
+        }
+        xi[(t * 16 + ch) * G::XP + w] = (__bf16)v;
+      }
+    }
+  };
+  const uint64_t wsrc = reinterpret_cast<uint64_t>(P.wpk);
+  const int4f rsw = {(int)(uint32_t)wsrc, (int)((wsrc >> 32) & 0xffff), nch * G::W_BYTES,
+                     0x00020000};
+  const unsigned ldsw = (unsigned)reinterpret_cast<uintptr_t>(lds + G::OFF_W);
+  auto dma_w = [&](int chunk, int buf) {
+#pragma unroll
+    for (int d = wave; d < G::W_BYTES / 1024; d += 8) {
+      const unsigned voffw = (unsigned)(chunk * G::W_BYTES + d * 1024 + lane * 16);
+      const unsigned m0v = ldsw + (unsigned)(buf * G::W_BYTES + d * 1024);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "s"(m0v), "v"(voffw), "s"(rsw)
+          : "memory");
+    }
+  };
+
+  // W' GEMM: wave w -> rows mi*ROWS/2 + rb*32 (rb < MB), column tiles cj*2 + j
+  const int mi = wave & 1, cj = wave >> 1;
+  int ao[G::MB];
+#pragma unroll
+  for (int rb = 0; rb < G::MB; ++rb) ao[rb] = (hi * ROWS + mi * (ROWS / 2) + rb * 32 + lo) * 16;
+  int bo[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (cj * 2 + j) * 32 + lo;
+    bo[j] = ((col < G::NCOLS ? col : 0) * G::SLOTS + hi) * 16;
+  }
+  floatx16 acc[G::MB][2];
+#pragma unroll
+  for (int rb = 0; rb < G::MB; ++rb)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[rb][j][i] = 0.f;
+
+  bn_table(0, 0);
+  dma_w(0, 0);
+  load_x(0);
+  wait_x();
+  __syncthreads();  // BN table, A planes, X pads
+  write_x(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // A: X(c) and W'(c) are in LDS; every wave is done with G(c-1)
+    const bool more = c + 1 < nch;
+    if (more) {
+      bn_table(c + 1, (c + 1) & 1);
+      dma_w(c + 1, (c + 1) & 1);
+      load_x(c + 1);
+    }
+    // -- joint contraction on MFMA: G tiles -> bf16 G image
+    {
+      const char *xi = lds + G::OFF_X;
+      const char *ah = lds + G::OFF_AH, *am = lds + G::OFF_AM;
+      char *gi = lds + G::OFF_G;
+      for (int tt = wave; tt < G::GT; tt += 8) {
+        const int grt = tt / G::GC, gct = tt - grt * G::GC;
+        floatx16 ga;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ga[i] = 0.f;
+        const int xo = ((grt * 32 + lo) * G::XP + 8 * hi) * 2;
+        const int bo2 = ((gct * 32 + lo) * G::XP + 8 * hi) * 2;
+#pragma unroll
+        for (int s = 0; s < G::KS; ++s) {
+          const bf16x8f xa = *reinterpret_cast<const bf16x8f *>(xi + xo + s * 32);
+          const bf16x8f bh = *reinterpret_cast<const bf16x8f *>(ah + bo2 + s * 32);
+          const bf16x8f bm = *reinterpret_cast<const bf16x8f *>(am + bo2 + s * 32);
+          ga = mfma_bf(xa, bh, ga);
+          ga = mfma_bf(xa, bm, ga);
+        }
+        const int col = gct * 32 + lo;
+        const int kk = col / V, v = col - kk * V;
+        if (col < G::NGC) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // register group: 4 consecutive channels
+            const int row = grt * 32 + 8 * q + 4 * hi;
+            const int t = row >> 4, ch0 = row & 15;
+            if (t < G::FT) {
+              uint2 d;
+              d.x = pkbf(ga[4 * q], ga[4 * q + 1]);
+              d.y = pkbf(ga[4 * q + 2], ga[4 * q + 3]);
+              *reinterpret_cast<uint2 *>(gi + ((t * V + v) * G::SLOTS) * 16 + (kk * 16 + ch0) * 2) =
+                  d;
+              if (P.Gk) {
+                // kept G for the backward dW' (k_wgrad_gemm_gk layout
+                // Gk[n][k*C_in + ci][mtile][256]): lanes = consecutive positions
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int ci = c * G::CK + ch0 + r;
+                  if (ci < P.C) {
+                    const int64_t grow = ((int64_t)n * K + kk) * P.C + ci;
+                    P.Gk[(grow * p.n_mtiles + mt) * 256 + t * V + v] = (__bf16)ga[4 * q + r];
+                  }
+                }
+              }
+            }
+          }
+        }
+      }
+      // the 256 - NCOLS pad positions of the chunk's kept G rows stay zero
+      // (k_wgrad_gemm_gk reads whole 32-position pieces)
+      if (P.Gk && tid < G::CK * K) {
+        const int kk = tid / G::CK, ci = c * G::CK + (tid - kk * G::CK);
+        if (ci < P.C) {
+          const int64_t grow = ((int64_t)n * K + kk) * P.C + ci;
+          __bf16 *dst = P.Gk + (grow * p.n_mtiles + mt) * 256;
+          for (int q2 = G::NCOLS; q2 < 256; ++q2) dst[q2] = (__bf16)0.f;
+        }
+      }
+    }
+    __syncthreads();  // B: G(c) complete; X(c) no longer read
+    // -- the W' GEMM: K k-steps (one per partition) of 16 channels
+    {
+      const char *wa = lds + G::OFF_W + (c & 1) * G::W_BYTES;
+      const char *gi = lds + G::OFF_G;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        bf16x8f a[G::MB], b[2];
+#pragma unroll
+        for (int rb = 0; rb < G::MB; ++rb)
+          a[rb] = *reinterpret_cast<const bf16x8f *>(wa + k * 2 * ROWS * 16 + ao[rb]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const bf16x8f *>(gi + bo[j] + k * 32);
+#pragma unroll
+        for (int rb = 0; rb < G::MB; ++rb)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[rb][j] = mfma_bf(a[rb], b[j], acc[rb][j]);
+      }
+    }
+    if (more) {
+      wait_x();  // x(c+1) and W'(c+1) landed
+      write_x(c + 1, (c + 1) & 1);
+    }
+  }
+  if constexpr (ROWS == 256) {
+    // ---- epilogue, 256 rows: each wave stores its own tiles from registers
+    // (an LDS image of all rows does not fit; bias table, no statistics: the
+    // launcher keeps residual blocks, whose BN2 statistics come from here, at
+    // ROWS <= 128). Lanes = consecutive positions: 128-byte row pieces.
+    const __amdgpu_buffer_rsrc_t rs_o =
+        make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
+    const __amdgpu_buffer_rsrc_t rs_bv = make_rsrc(p.bias_rv, (int64_t)p.R * V);
+    const int ostride = p.T_dst * V;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = (cj * 2 + j) * 32 + lo;
+      const bool cok = col < pos_lim;
+      const int v = col % V;
+#pragma unroll
+      for (int rb = 0; rb < G::MB; ++rb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = mi * (ROWS / 2) + rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const bool ok = cok && row < p.R;
+          const float bv = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(rs_bv, ok ? (row * V + v) * 4 : (int)kOOB,
+                                                          0, 0));
+          __builtin_amdgcn_raw_buffer_store_b32(
+              __builtin_bit_cast(unsigned, acc[rb][j][i] + bv), rs_o,
+              ok ? (row * ostride + m0 * V + col) * 4 : (int)kOOB, 0, 0);
+        }
+    }
+    return;
+  } else {
+    // ---- epilogue: row-major LDS image (conv_tile_store_rows), one pass
+    __syncthreads();  // every wave is done with the images
+#pragma unroll
+    for (int rb = 0; rb < G::MB; ++rb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc_to_img(smem, acc[rb][j], mi * (ROWS / 2) + rb * 32, (cj * 2 + j) * 32);
+    __syncthreads();
+    conv_tile_store_rows<V, G::NCOLS, G::NT, ROWS>(p, smem, smem + ROWS * kEpiPitch, n, 0, m0);
+  }
+}
+
+// W (K*C_out, C_in) -> wpk[rt][chunk][k][octet][rows][8] bf16 (zero padded;
+// rows = 64 per row tile, or all ROWS of k_sp_fwd_wide)
 __global__ void k_pack_sp_w_bf16(const float *W, __bf16 *wpk, int K, int R, int C, int nch,
-                                 int64_t total) {
+                                 int rows, int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int j = (int)(idx & 7);
   int64_t t = idx >> 3;
-  const int rl = (int)(t & 63);
-  t >>= 6;
+  const int rl = (int)(t % rows);
+  t /= rows;
   const int o = (int)(t & 1);
   t >>= 1;
   const int k = (int)(t % K);
   t /= K;
   const int chunk = (int)(t % nch);
   const int rt = (int)(t / nch);
-  const int r = rt * 64 + rl, c = chunk * 16 + o * 8 + j;
+  const int r = rt * rows + rl, c = chunk * 16 + o * 8 + j;
   float v = 0.f;
   if (r < R && c < C) v = W[((int64_t)k * R + r) * C + c];
   wpk[idx] = (__bf16)v;
 }
 
-bool sp_fwd_bf16_supported(int C, int V, int K) {
+bool sp_fwd_bf16_supported(int C, int V, int K, int R, bool residual) {
   if (C < 16) return false;  // the first block's 3-channel input stays on the fp32 path
-  // V = 50 is compiled but not selected: its gather (3 x 5 tiles x 4 k-steps x
-  // 2 A planes per 16 channels, recomputed by every 64-row tile) and 100 KB of
-  // LDS (one workgroup per CU) made cfg5 10% slower than the unfused kernels
-  // (1606 vs 1779 clips/s in one A/B call); DESIGN.md §8 has the planned
-  // W-first ordering for it
-  if (V != 18 && V != 25) return false;
-  return K >= 1 && K <= 3;
+  if (K < 1 || K > 3) return false;
+  if (V == 18 || V == 25) return true;
+  // the two-person graph: all output channels in one workgroup (k_sp_fwd_wide;
+  // its 256-row epilogue computes no BN2 statistics for the residual block)
+  return V == 50 && K == 3 && (R <= 128 || (R <= 256 && !residual));
 }
 
 size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K) {
@@ -380,18 +702,26 @@ static void launch_spf(const SpFwdParams &P, int nblk, hipStream_t s) {
   hipLaunchKernelGGL((k_sp_fwd_bf16<V, K>), dim3(nblk), dim3(256), lds, s, P);
 }
 
+template <int V, int K, int ROWS>
+static void launch_spw(const SpFwdParams &P, int nblk, hipStream_t s) {
+  constexpr int lds = SpWideGeo<V, K, ROWS>::LDS;
+  hipLaunchKernelGGL((k_sp_fwd_wide<V, K, ROWS>), dim3(nblk), dim3(512), lds, s, P);
+}
+
 hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,
                               const float *g, const float *b, const float *A, const float *W,
                               const float *biasZ, void *wpk, float *Z, __bf16 *Gk, double *ssum,
                               double *ssq, int N, int C, int R, int T, int V, int K, int relu,
                               hipStream_t s) {
-  if (!sp_fwd_bf16_supported(C, V, K)) return hipErrorInvalidValue;
+  if (!sp_fwd_bf16_supported(C, V, K, R, relu != 0)) return hipErrorInvalidValue;
+  const bool wide = V == 50;
   const int nch = (C + 15) / 16;
-  const int nrt = (R + 63) / 64;
+  const int rows = !wide ? 64 : (R <= 64 ? 64 : (R <= 128 ? 128 : 256));
+  const int nrt = (R + rows - 1) / rows;
   {
-    const int64_t total = (int64_t)nrt * nch * K * 2 * 64 * 8;
+    const int64_t total = (int64_t)nrt * nch * K * 2 * rows * 8;
     hipLaunchKernelGGL(k_pack_sp_w_bf16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W,
-                       reinterpret_cast<__bf16 *>(wpk), K, R, C, nch, total);
+                       reinterpret_cast<__bf16 *>(wpk), K, R, C, nch, rows, total);
   }
   SpFwdParams P{};
   P.x = x;
@@ -423,16 +753,20 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
   p.n_mtiles = (T + p.FT - 1) / p.FT;
   p.n_rtiles = nrt;
   const int nblk = N * p.n_mtiles * nrt;
+  if (wide) {
+    if (rows == 64) launch_spw<50, 3, 64>(P, nblk, s);
+    else if (rows == 128) launch_spw<50, 3, 128>(P, nblk, s);
+    else launch_spw<50, 3, 256>(P, nblk, s);
+    return hipGetLastError();
+  }
 #define SPF_K(VV)                            \
   if (K == 1) launch_spf<VV, 1>(P, nblk, s); \
   else if (K == 2) launch_spf<VV, 2>(P, nblk, s); \
   else launch_spf<VV, 3>(P, nblk, s);
   if (V == 18) {
     SPF_K(18)
-  } else if (V == 25) {
-    SPF_K(25)
   } else {
-    SPF_K(50)
+    SPF_K(25)
   }
 #undef SPF_K
   return hipGetLastError();

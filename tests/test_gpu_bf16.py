@@ -143,7 +143,10 @@ def _check_bf16(pkg, case, residual=False, need_dx=True, seed=0):
     (128, 256, 2, 25, 3, 2, 21),
     (3, 64, 1, 50, 3, 2, 20),       # cfg5 (two-person V=50)
     (64, 64, 1, 50, 3, 2, 17),
-    (64, 128, 2, 50, 3, 2, 23),
+    (64, 128, 2, 50, 3, 2, 23),     # k_sp_fwd_wide, 128 rows
+    (128, 256, 2, 50, 3, 2, 13),    # k_sp_fwd_wide, 256 rows (per-wave epilogue)
+    (256, 256, 1, 50, 3, 2, 7),     # 16 channel chunks, ragged last frame tile
+    (24, 40, 1, 50, 3, 2, 11),      # partial chunk (24 = 16 + 8) and rows (40 of 64)
     (5, 21, 1, 18, 1, 2, 9),        # odd channel counts: partial tiles and chunks (5: fp32 W)
     (64, 64, 2, 25, 3, 8, 1),       # T = 1 (single frame: all taps but one in the halo)
 ])
@@ -157,6 +160,8 @@ def test_bf16_block_matches_oracle(pkg, case):
     (64, 128, 2, 18, 1, 2, 37),     # projection, stride 2 (bf16 projection GEMMs)
     (64, 128, 2, 25, 3, 2, 33),
     (3, 64, 1, 50, 3, 2, 20),       # projection, stride 1
+    (64, 64, 1, 50, 3, 2, 16),      # identity: k_sp_fwd_wide with ReLU input + BN2 statistics
+    (64, 128, 2, 50, 3, 2, 19),     # projection: 128-row k_sp_fwd_wide
 ])
 def test_bf16_residual_block_matches_oracle(pkg, case):
     errs = _check_bf16(pkg, case, residual=True)
