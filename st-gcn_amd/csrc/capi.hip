@@ -61,9 +61,13 @@ size_t wpk_floats(const stgcn_desc_t *d) {
   const int rows = std::max(d->C_out, d->K * d->C_in);  // (stacked H GEMM: K*C_in rows)
   const int red = std::max(d->C_out, d->K * d->C_in);
   // reduction padded to a whole number of chunks for any chunk size <= 32
-  const size_t n = (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32 + 32) * 9;
+  size_t n = (size_t)((rows + 63) / 64 * 64) * ((red + 31) / 32 * 32 + 32) * 9;
   // STGCN_F_F32X3: three bf16 planes of the weights (1.5x the fp32 floats)
-  return (d->flags & STGCN_F_F32X3) ? 2 * n : n;
+  if (d->flags & STGCN_F_F32X3) n *= 2;
+  // the fused bf16 spatial forward: packed W' + the A image
+  if (d->flags & STGCN_F_BF16)
+    n = std::max(n, (sp_fwd_bf16_wpk_bytes(d->C_in, d->C_out, d->K, d->V) + 3) / 4);
+  return n;
 }
 
 int64_t nT(const stgcn_desc_t *d) { return (int64_t)d->T * d->V; }

@@ -89,6 +89,9 @@ hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s);
 bool conv_x3_supported(const ConvGemmParams &p);
 size_t conv_x3_wpk_bytes(const ConvGemmParams &p);
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s);
+// bf16 temporal-conv GEMMs on the one-plane k_conv_x3 pipeline (kernels_x3.hip)
+bool conv_b1_supported(const ConvGemmParams &p);
+hipError_t launch_conv_b1(const ConvGemmParams &p, hipStream_t s);
 // Re-plans the temporal weight gradient (NQ = 9, stride 1, V = 18) for
 // k_wgrad_x3 (sets FT, tiles, S, bf16 = 3); false (w unchanged) otherwise.
 // launch_wgrad_taps dispatches to launch_wgrad_x3 when w.bf16 == 3.
@@ -185,7 +188,7 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
 // with A in LDS + W' GEMM; G never materialised in fp32). Optionally keeps G in
 // bf16 (Gk, layout [n][k*C + ci][frame tile][256]) for the weight gradient.
 bool sp_fwd_bf16_supported(int C, int V, int K, int R, bool residual);
-size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K);
+size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K, int V);  // packed W' + A image
 size_t sp_keep_g_bytes(int N, int C, int T, int V, int K);
 hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,
                               const float *g, const float *b, const float *A, const float *W,

@@ -492,6 +492,7 @@ static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t ld
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
   if (p0.bf16 == 3 && conv_x3_supported(p0)) return launch_conv_x3(p0, s);
+  if (p0.bf16 == 1 && conv_b1_supported(p0)) return launch_conv_b1(p0, s);
   if (p0.bf16 == 1 && conv_bf16_supported(p0)) return launch_conv_bf16(p0, s);
   ConvGemmParams p = p0;
   if (!conv_gemm_supported(p) || !p.wpk) return hipErrorInvalidValue;

@@ -69,7 +69,8 @@ struct SpFwdGeo {
   static constexpr int NIT = CK * NCOLS;           // x staging items (ch, pos)
   static constexpr int IPT = (NIT + 255) / 256;
   // layout: [A h][A m][X][G][W0][W1][BN tables 2 x 3 x 16 floats]
-  static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = 2 * A_BYTES;
+  static constexpr int A_IMG = (2 * A_BYTES + 1023) & ~1023;  // both planes, whole KiB
+  static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = A_IMG;
   static constexpr int OFF_G = OFF_X + X_BYTES, OFF_W = OFF_G + G_BYTES;
   static constexpr int OFF_BN = OFF_W + 2 * W_BYTES;
   static constexpr int LDS = OFF_BN + 2 * 3 * 16 * 4;
@@ -80,6 +81,7 @@ struct SpFwdGeo {
 
 struct SpFwdParams {
   const float *x, *mean, *invstd, *g, *b, *A;
+  const __bf16 *aimg;  // the LDS image of the A planes (k_pack_sp_a), DMA'd per workgroup
   const __bf16 *wpk;  // [rt][chunk][k][octet][64][8]
   __bf16 *Gk;         // optional kept G (bf16 tile layout), or null
   int C, T, relu, nchunks;
@@ -112,19 +114,14 @@ __global__ __launch_bounds__(256, 2) void k_sp_fwd_bf16(SpFwdParams P) {
   const int TV = P.T * V;
   const int nch = P.nchunks;
 
-  // ---- prologue: A planes (h, m) and zeroed X pads --------------------------
+  // ---- prologue: A planes (h, m) by 16-byte LDS-DMA of the prebuilt image
+  // (k_pack_sp_a), zeroed X pads; landed by the vmcnt(0) before the first barrier
   {
-    __bf16 *ah = reinterpret_cast<__bf16 *>(lds + G::OFF_AH);
-    __bf16 *am = reinterpret_cast<__bf16 *>(lds + G::OFF_AM);
-    for (int e = tid; e < G::GC * 32 * G::XP; e += 256) {
-      const int c = e / G::XP, w = e - c * G::XP;
-      const int k = c / V, v = c - k * V;
-      float a = 0.f;
-      if (c < G::NGC && w < V) a = P.A[(k * V + v) * V + w];
-      const __bf16 h = (__bf16)a;
-      ah[e] = h;
-      am[e] = (__bf16)(a - (float)h);
-    }
+    const __amdgpu_buffer_rsrc_t ra =
+        make_rsrc(reinterpret_cast<const float *>(P.aimg), G::A_IMG / 4);
+    for (int i = wave; i < G::A_IMG / 1024; i += 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, smem + i * 256, 16,
+                                               (unsigned)(i * 1024 + lane * 16), 0, 0, 0);
     unsigned *xz = reinterpret_cast<unsigned *>(lds + G::OFF_X);
     for (int e = tid; e < G::X_BYTES / 4; e += 256) xz[e] = 0u;
   }
@@ -371,7 +368,8 @@ struct SpWideGeo {
   static constexpr int W_BYTES = K * 2 * ROWS * 16;  // packed W' chunk
   static constexpr int NIT = CK * NCOLS;
   static constexpr int IPT = (NIT + NT - 1) / NT;
-  static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = 2 * A_BYTES;
+  static constexpr int A_IMG = (2 * A_BYTES + 1023) & ~1023;  // both planes, whole KiB
+  static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = A_IMG;
   static constexpr int OFF_G = OFF_X + X_BYTES, OFF_W = OFF_G + G_BYTES;
   static constexpr int OFF_BN = OFF_W + 2 * W_BYTES;
   static constexpr int MAIN = OFF_BN + 2 * 3 * 16 * 4;
@@ -399,19 +397,14 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
   const int TV = P.T * V;
   const int nch = P.nchunks;
 
-  // ---- prologue: A planes (h, m) and zeroed X pads --------------------------
+  // ---- prologue: A planes (h, m) by 16-byte LDS-DMA of the prebuilt image
+  // (k_pack_sp_a), zeroed X pads; landed by the vmcnt(0) before the first barrier
   {
-    __bf16 *ah = reinterpret_cast<__bf16 *>(lds + G::OFF_AH);
-    __bf16 *am = reinterpret_cast<__bf16 *>(lds + G::OFF_AM);
-    for (int e = tid; e < G::GC * 32 * G::XP; e += G::NT) {
-      const int c = e / G::XP, w = e - c * G::XP;
-      const int k = c / V, v = c - k * V;
-      float a = 0.f;
-      if (c < G::NGC && w < V) a = P.A[(k * V + v) * V + w];
-      const __bf16 h = (__bf16)a;
-      ah[e] = h;
-      am[e] = (__bf16)(a - (float)h);
-    }
+    const __amdgpu_buffer_rsrc_t ra =
+        make_rsrc(reinterpret_cast<const float *>(P.aimg), G::A_IMG / 4);
+    for (int i = wave; i < G::A_IMG / 1024; i += 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, smem + i * 256, 16,
+                                               (unsigned)(i * 1024 + lane * 16), 0, 0, 0);
     unsigned *xz = reinterpret_cast<unsigned *>(lds + G::OFF_X);
     for (int e = tid; e < G::X_BYTES / 4; e += G::NT) xz[e] = 0u;
   }
@@ -678,6 +671,22 @@ __global__ void k_pack_sp_w_bf16(const float *W, __bf16 *wpk, int K, int R, int 
   wpk[idx] = (__bf16)v;
 }
 
+// A (K, V, V) -> the LDS image of both kernels: planes h, m of the gather's B
+// operand [c = k*V + v][w] (pitch XP bf16, zero padded), whole KiB
+__global__ void k_pack_sp_a(const float *A, __bf16 *img, int K, int V, int GC, int XP,
+                            int plane, int total) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int pl = e / plane, r = e - pl * plane;
+  float a = 0.f;
+  if (pl < 2) {
+    const int c = r / XP, w = r - c * XP;
+    if (c < K * V && w < V) a = A[c * V + w];
+  }
+  const __bf16 h = (__bf16)a;
+  img[e] = pl == 0 ? h : (pl == 1 ? (__bf16)(a - (float)h) : (__bf16)0.f);
+}
+
 bool sp_fwd_bf16_supported(int C, int V, int K, int R, bool residual) {
   if (C < 16) return false;  // the first block's 3-channel input stays on the fp32 path
   if (K < 1 || K > 3) return false;
@@ -687,8 +696,11 @@ bool sp_fwd_bf16_supported(int C, int V, int K, int R, bool residual) {
   return V == 50 && K == 3 && (R <= 128 || (R <= 256 && !residual));
 }
 
-size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K) {
-  return (size_t)((R + 63) / 64) * ((C + 15) / 16) * K * 2 * 64 * 8 * 2;
+size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K, int V) {
+  const int KW = (V + 15) & ~15, XP = KW + 8, GC = (K * V + 31) / 32;
+  const size_t a = ((size_t)2 * GC * 32 * XP * 2 + 1023) & ~(size_t)1023;
+  const size_t w = (size_t)((R + 255) / 64) * ((C + 15) / 16) * K * 2 * 64 * 8 * 2;  // rows <= 256
+  return ((w + 1023) & ~(size_t)1023) + a;
 }
 
 size_t sp_keep_g_bytes(int N, int C, int T, int V, int K) {
@@ -723,7 +735,18 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
     hipLaunchKernelGGL(k_pack_sp_w_bf16, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W,
                        reinterpret_cast<__bf16 *>(wpk), K, R, C, nch, rows, total);
   }
+  // the A image after the packed W' in the scratch
+  const size_t wbytes = ((size_t)nrt * nch * K * 2 * rows * 8 * 2 + 1023) & ~(size_t)1023;
+  __bf16 *aimg = reinterpret_cast<__bf16 *>(reinterpret_cast<char *>(wpk) + wbytes);
+  {
+    const int KW = (V + 15) & ~15, XP = KW + 8, GC = (K * V + 31) / 32;
+    const int plane = GC * 32 * XP;
+    const int total = (2 * plane * 2 + 1023) / 1024 * 1024 / 2;  // bf16 elements, whole KiB
+    hipLaunchKernelGGL(k_pack_sp_a, dim3((total + 255) / 256), dim3(256), 0, s, A, aimg, K, V, GC,
+                       XP, plane, total);
+  }
   SpFwdParams P{};
+  P.aimg = aimg;
   P.x = x;
   P.mean = mean;
   P.invstd = invstd;

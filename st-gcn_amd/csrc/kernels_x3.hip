@@ -89,24 +89,32 @@ template <int NA>
 __device__ __forceinline__ void wait_img(float (&st)[3][8]) {
   asm volatile("s_waitcnt vmcnt(%24)" : X3_ST8(0), X3_ST8(1), X3_ST8(2) : "n"(NA) : "memory");
 }
+template <int NA>
+__device__ __forceinline__ void wait_img(float (&st)[4][8]) {
+  asm volatile("s_waitcnt vmcnt(%32)"
+               : X3_ST8(0), X3_ST8(1), X3_ST8(2), X3_ST8(3)
+               : "n"(NA)
+               : "memory");
+}
 #undef X3_ST8
 
-template <int NQ, int TG, int V, int SIN, int MR>
+template <int NQ, int TG, int V, int SIN, int MR, int NPL>
 struct ConvX3Geo {
   static constexpr int ROWS = 64 * MR;            // output rows per workgroup
   static constexpr int CK = 16;                   // channels per chunk (one k-step)
   static constexpr int FT = kTileCols / V;
   static constexpr int NCOLS = FT * V;
   static constexpr int SPAN = (SIN * (FT - 1) + NQ) * V;  // window positions
-  static constexpr int SLOTS = 7;                 // 6 (plane, octet) slots + 1 pad
+  static constexpr int SLOTS = 2 * NPL + 1;       // (plane, octet) slots + 1 pad (odd)
   static constexpr int IMG = SPAN * SLOTS * 16;   // window bytes
   static constexpr int NG = NQ / TG;              // steps per chunk
-  static constexpr int WST = 3 * TG * 2 * 1024 * MR;  // packed weight bytes per step
+  static constexpr int WST = NPL * TG * 2 * 1024 * MR;  // packed weight bytes per step
   static constexpr int WDMA = WST / 1024;         // 1 KiB DMA pieces per step
   // LDS plan, first that fits: window double-buffered with a 3-step weight ring
   // (prefetch distance 2), double-buffered with a 2-step ring, or a single
   // window (written between two barriers) with a 3- or 2-step ring
-  static constexpr int BUDGET = 160 * 1024;
+  // (NPL = 1: two workgroups per CU)
+  static constexpr int BUDGET = NPL == 1 ? 80 * 1024 : 160 * 1024;
   static constexpr int PLAN = 3 * WST + 2 * IMG <= BUDGET   ? 0
                               : 2 * WST + 2 * IMG <= BUDGET ? 1
                               : 3 * WST + IMG <= BUDGET     ? 2
@@ -114,10 +122,12 @@ struct ConvX3Geo {
   static constexpr int NWIN = PLAN <= 1 ? 2 : 1;
   static constexpr int NWB = (PLAN == 0 || PLAN == 2) ? 3 : 2;
   static constexpr int PD = NWB - 1;
-  static constexpr int LDS = NWB * WST + NWIN * IMG;
+  static constexpr int EPI = MR == 1 ? (64 * kEpiPitch + 64 * V) * 4 : (ROWS * kEpiPitch + ROWS * V) * 4;
+  static constexpr int MAIN = NWB * WST + NWIN * IMG;
+  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   static constexpr int NIT = SPAN * 2;            // (position, octet) staging items
   static constexpr int IPT = (NIT + 511) / 512;   // staging items per thread
-  static_assert(IPT == 2 || IPT == 3, "wait_img overloads");
+  static_assert(IPT >= 2 && IPT <= 4, "wait_img overloads");
   static constexpr int DPW = (WDMA + 7) / 8;      // DMA pieces per wave and step (max)
   static constexpr int DPWMIN = WDMA / 8;         // ... issued by every wave
   // vmcnt allowance at step g's barrier (DMA(s) must have landed): the VMEM
@@ -138,9 +148,9 @@ struct ConvX3Geo {
   static_assert((ROWS * kEpiPitch + ROWS * V) * 4 <= LDS, "row-major epilogue image fits");
 };
 
-template <int NQ, int TG, int V, int SIN, int MR>
-__global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
-  using G = ConvX3Geo<NQ, TG, V, SIN, MR>;
+template <int NQ, int TG, int V, int SIN, int MR, int NPL>
+__global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
+  using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   char *const wbuf0 = lds, *const win0 = lds + G::NWB * G::WST;
@@ -209,7 +219,14 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   auto write_img = [&](char *win) {
 #pragma unroll
     for (int k = 0; k < G::IPT; ++k)
-      if (loff[k] >= 0) {
+      if (NPL == 1 && loff[k] >= 0) {  // bf16 operands: one rounded plane
+        uint4 h;
+        h.x = pk2(st[k][0], st[k][1]);
+        h.y = pk2(st[k][2], st[k][3]);
+        h.z = pk2(st[k][4], st[k][5]);
+        h.w = pk2(st[k][6], st[k][7]);
+        *reinterpret_cast<uint4 *>(win + loff[k]) = h;
+      } else if (loff[k] >= 0) {
         uint4 h, m, l;
         split2(st[k][0], st[k][1], h.x, m.x, l.x);
         split2(st[k][2], st[k][3], h.y, m.y, l.y);
@@ -250,38 +267,41 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
   // accumulated apart so their roundings stay 2^-8 smaller; summed at the end.
   // Tile (row block rb, column tile j) -> acc[rb*2 + j] (MR = 1: acc[2..3] are
   // the hand-over registers of the stride-2 epilogue)
-  floatx16 acc[4], acl[2 * MR];
+  // (NPL = 1: plain bf16 operands, acc only)
+  constexpr int NACL = NPL == 3 ? 2 * MR : 1;
+  floatx16 acc[4], acl[NACL];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
 #pragma unroll
-  for (int j = 0; j < 2 * MR; ++j)
+  for (int j = 0; j < NACL; ++j)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acl[j][i] = 0.f;
 
   struct Frag {
-    bf16x8_t a[3][MR], b[3][2];
+    bf16x8_t a[NPL][MR], b[NPL][2];
   };
   auto ld = [&](const char *wa, const char *win, int qq, int q, Frag &f) {
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NPL; ++pl)
 #pragma unroll
       for (int rb = 0; rb < MR; ++rb)
         f.a[pl][rb] = *reinterpret_cast<const bf16x8_t *>(
             wa + ((pl * TG + qq) * 2 * MR) * 1024 + rb * 32 * 16);
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+    for (int pl = 0; pl < NPL; ++pl)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         f.b[pl][j] =
             *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * V * G::SLOTS + 2 * pl) * 16);
   };
   // the six products (plane of A, plane of B) of one tap over the MR x 2 tiles
+  // (NPL = 1: the one product)
   auto mm = [&](const Frag &f) {
     constexpr int PA[6] = {0, 0, 1, 0, 1, 2}, PB[6] = {0, 1, 0, 2, 1, 0};
 #pragma unroll
-    for (int t = 0; t < 6; ++t)
+    for (int t = 0; t < (NPL == 3 ? 6 : 1); ++t)
 #pragma unroll
       for (int rb = 0; rb < MR; ++rb)
 #pragma unroll
@@ -289,7 +309,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
           if (t == 0)
             acc[rb * 2 + j] = mfma_x(f.a[0][rb], f.b[0][j], acc[rb * 2 + j]);
           else
-            acl[rb * 2 + j] = mfma_x(f.a[PA[t]][rb], f.b[PB[t]][j], acl[rb * 2 + j]);
+            acl[(rb * 2 + j) % NACL] =
+                mfma_x(f.a[PA[t] % NPL][rb], f.b[PB[t] % NPL][j], acl[(rb * 2 + j) % NACL]);
         }
   };
 
@@ -323,18 +344,22 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
       if (!(STGCN_X3_EXP & 2) && s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
       if (!(STGCN_X3_EXP & 4) && g == 0) load_img(c + 1);
       if constexpr (MR == 1) {
+        // per tap: NR fragment reads, NM MFMAs
+        constexpr int NR = NPL * (MR + 2), NM = (NPL == 3 ? 6 : 1) * 2 * MR;
+        constexpr int NI = NR < NM ? NR : NM;
 #pragma unroll
         for (int qq = 0; qq < TG; ++qq) {
           if (qq + 1 < TG) {
-            // tap qq+1's 9 fragment reads among tap qq's 12 MFMAs
+            // tap qq+1's fragment reads among tap qq's MFMAs
             ld(wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) & 1]);
             if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
 #pragma unroll
-            for (int i = 0; i < 9; ++i) {
+            for (int i = 0; i < NI; ++i) {
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
               __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            if constexpr (NM > NI) __builtin_amdgcn_sched_group_barrier(0x008, NM - NI, 0);
+            if constexpr (NR > NI) __builtin_amdgcn_sched_group_barrier(0x100, NR - NI, 0);
           } else {
             if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
           }
@@ -404,8 +429,10 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
       }
     }
   }
+  if constexpr (NPL == 3) {
 #pragma unroll
-  for (int j = 0; j < 2 * MR; ++j) acc[j] += acl[j];
+    for (int j = 0; j < 2 * MR; ++j) acc[j] += acl[j];
+  }
   if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
     if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
     return;
@@ -452,8 +479,8 @@ __global__ __launch_bounds__(512, 1) void k_conv_x3(ConvGemmParams p) {
 // 128 rows per tile; zero padded rows and channels), so one step's weights are
 // one contiguous run.
 __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int NQ, int TG,
-                                 int nch, int rows, int64_t w_sr, int64_t w_sc, int64_t w_sq,
-                                 int64_t total) {
+                                 int nch, int rows, int npl, int64_t w_sr, int64_t w_sc,
+                                 int64_t w_sq, int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int jj = (int)(idx & 7);
@@ -464,8 +491,8 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
   t >>= 1;
   const int qq = (int)(t % TG);
   t /= TG;
-  const int pl = (int)(t % 3);
-  t /= 3;
+  const int pl = (int)(t % npl);
+  t /= npl;
   const int NG = NQ / TG;
   const int g = (int)(t % NG);
   t /= NG;
@@ -504,49 +531,82 @@ static bool x3_wide_rows(const ConvGemmParams &p) {
   return !off && p.NQ == 9 && p.s_out == 1 && p.R % 128 == 0;
 }
 
-template <int NQ, int V, int SIN, int MR>
+template <int NQ, int V, int SIN, int MR, int NPL>
 static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
   if (p.V != V || p.s_in != SIN) return false;
   constexpr int TG = NQ == 9 ? 3 : NQ;
-  constexpr int lds = ConvX3Geo<NQ, TG, V, SIN, MR>::LDS;
-  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR>), dim3(nblk), dim3(512), lds, s, p);
+  constexpr int lds = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>::LDS;
+  hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL>), dim3(nblk), dim3(512), lds, s, p);
   return true;
 }
 
-template <int NQ, int MR>
+template <int NQ, int MR, int NPL>
 static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
-  if (launch_cx_if<NQ, 18, 1, MR>(p, nblk, s) || launch_cx_if<NQ, 25, 1, MR>(p, nblk, s))
+  if (launch_cx_if<NQ, 18, 1, MR, NPL>(p, nblk, s) || launch_cx_if<NQ, 25, 1, MR, NPL>(p, nblk, s))
     return true;
-  if constexpr (NQ == 9)
-    return launch_cx_if<NQ, 18, 2, MR>(p, nblk, s) || launch_cx_if<NQ, 25, 2, MR>(p, nblk, s);
+  if constexpr (NPL == 1)
+    if (launch_cx_if<NQ, 50, 1, MR, NPL>(p, nblk, s)) return true;
+  if constexpr (NQ == 9) {
+    if (launch_cx_if<NQ, 18, 2, MR, NPL>(p, nblk, s) || launch_cx_if<NQ, 25, 2, MR, NPL>(p, nblk, s))
+      return true;
+    if constexpr (NPL == 1) return launch_cx_if<NQ, 50, 2, MR, NPL>(p, nblk, s);
+  }
   return false;
 }
 
-hipError_t launch_conv_x3(const ConvGemmParams &p0, hipStream_t s) {
-  if (!conv_x3_supported(p0) || !p0.wpk) return hipErrorInvalidValue;
-  const bool wide = x3_wide_rows(p0);
+// npl = 3: fp32 as exact 3-way splits (STGCN_F_F32X3); npl = 1: bf16 operands
+// (STGCN_F_BF16), the same pipeline with one plane and two workgroups per CU
+static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStream_t s) {
+  const bool wide = npl == 3 && x3_wide_rows(p0);
   ConvGemmParams p = p0;
   const int rows = wide ? 128 : 64;
   p.n_rtiles = (p.R + rows - 1) / rows;
   const int nch = (p.C + 15) / 16;
   {
-    const int64_t total = (int64_t)p.n_rtiles * nch * 3 * p.NQ * 2 * rows * 8;
+    const int64_t total = (int64_t)p.n_rtiles * nch * npl * p.NQ * 2 * rows * 8;
     hipLaunchKernelGGL(k_pack_conv_w_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, x3_tg(p.NQ), nch,
-                       rows, p.w_sr, p.w_sc, p.w_sq, total);
+                       rows, npl, p.w_sr, p.w_sc, p.w_sq, total);
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   bool done = false;
   if (wide) {
-    done = launch_cx_v<9, 2>(p, nblk, s);
+    done = launch_cx_v<9, 2, 3>(p, nblk, s);
+  } else if (npl == 3) {
+    switch (p.NQ) {
+      case 4: done = launch_cx_v<4, 1, 3>(p, nblk, s); break;
+      case 5: done = launch_cx_v<5, 1, 3>(p, nblk, s); break;
+      case 9: done = launch_cx_v<9, 1, 3>(p, nblk, s); break;
+    }
   } else {
     switch (p.NQ) {
-      case 4: done = launch_cx_v<4, 1>(p, nblk, s); break;
-      case 5: done = launch_cx_v<5, 1>(p, nblk, s); break;
-      case 9: done = launch_cx_v<9, 1>(p, nblk, s); break;
+      case 4: done = launch_cx_v<4, 1, 1>(p, nblk, s); break;
+      case 5: done = launch_cx_v<5, 1, 1>(p, nblk, s); break;
+      case 9: done = launch_cx_v<9, 1, 1>(p, nblk, s); break;
     }
   }
   return done ? hipGetLastError() : hipErrorInvalidValue;
+}
+
+hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
+  if (!conv_x3_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  return launch_conv_planes(p, 3, s);
+}
+
+// The bf16 temporal-conv GEMMs (9 taps; stride-2 data-gradient phases 5 / 4) on
+// the one-plane k_conv_x3 (STGCN_OLD_BF16CONV: k_conv_bf16, A/B only)
+bool conv_b1_supported(const ConvGemmParams &p) {
+  static const bool off = getenv("STGCN_OLD_BF16CONV") != nullptr;
+  if (off || p.C < 16) return false;
+  if (p.V != 18 && p.V != 25 && p.V != 50) return false;
+  if (p.FT != kTileCols / p.V) return false;
+  if (p.s_in == 2) return p.NQ == 9;
+  return p.s_in == 1 && (p.NQ == 9 || p.NQ == 5 || p.NQ == 4);
+}
+
+hipError_t launch_conv_b1(const ConvGemmParams &p, hipStream_t s) {
+  if (!conv_b1_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  return launch_conv_planes(p, 1, s);
 }
 
 }  // namespace stgcn
