@@ -47,6 +47,7 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense (no sparsity)
 # fp32 work on the bf16 matrix cores by exact 3-way operand splits: six bf16
 # MFMAs per fp32 product (kernels_x3.hip), so the fp32-work ceiling is 1/6 of BF16
 X3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
 HBM_PEAK_GBS = 8000.0
 
 
@@ -126,10 +127,11 @@ def kernel_roofline(pkg, device, cfg, iters=10):
     lib = hl.lib()
     kinds, symbols = {}, {}
 
-    def add(d, key, ms, fl, n):
-        t = d.get(key, (0.0, 0.0, 0))
-        d[key] = (t[0] + ms, t[1] + fl, t[2] + n)
+    def add(d, key, ms, fl, n, nb=0.0):
+        t = d.get(key, (0.0, 0.0, 0, 0.0))
+        d[key] = (t[0] + ms, t[1] + fl, t[2] + n, t[3] + nb)
 
+    V4 = cfg["V"] * 4
     for ci, co, t, s in stack_layers(cfg):
         x3 = cfg.get("f32_gemm") == "bf16x3" and not cfg["bf16"]
         d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
@@ -142,22 +144,37 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                                            hl.stream_handle(device), ctypes.byref(ms),
                                            ctypes.byref(fl)))
             del scratch
-            add(kinds, kind, ms.value, fl.value, 1)
-            V = cfg["V"]
+            # algorithmic HBM bytes of the timed launch(es): fp32 activations in
+            # and out (the kept G of the fused spatial forward in bf16)
+            N, to = cfg["N"], (t - 1) // s + 1
+            act = {0: N * (co * t + co * to) * V4, 1: N * (co * to + co * t) * V4,
+                   2: N * (co * to + co * t) * V4,
+                   3: N * (ci * t + co * t) * V4 + (N * cfg["K"] * ci * t * cfg["V"] * 2
+                                                 if cfg["bf16"] and ci >= 16 else
+                                                 N * cfg["K"] * ci * t * V4)}[which]
+            add(kinds, kind, ms.value, fl.value, 1, act)
+            V, K = cfg["V"], cfg["K"]
+            # rocprof short names of the kernel each timing runs
             if cfg["bf16"]:
-                sym = {0: f"k_conv_bf16<9,16,{V},{s}>",
-                       1: f"k_conv_bf16<9,16,{V},1>" if s == 1 else f"k_conv_bf16<5|4,16,{V},1>",
-                       2: f"k_wgrad_bf16<9,{V},{s}>", 3: f"k_conv_bf16<1,32,{V},1>"}[which]
+                # temporal GEMMs: k_conv_x3 with one operand plane (NPL = 1)
+                sym = {0: f"k_conv_x3<9,3,{V},{s},1,1>",
+                       1: f"k_conv_x3<9,3,{V},1,1,1>" if s == 1 else f"k_conv_x3<5|4,{V},1,1,1>",
+                       2: f"k_wgrad_bf16<9,{V},{s}>",
+                       3: (f"k_conv_bf16<1,16,{V},1>" if ci < 16 else
+                           f"k_sp_fwd_bf16<{V},{K}>" if not (V == 50 or (V == 25 and K == 3)) else
+                           f"k_sp_fwd_wide<{V},3,{64 if co <= 64 else 128 if co <= 128 else 256}>")
+                       }[which]
             elif x3 and V in (18, 25):
-                sym = {0: f"k_conv_x3<9,3,{V},{s}>",
-                       1: f"k_conv_x3<9,3,{V},1>" if s == 1 else f"k_conv_x3<5|4,{V},1>",
+                mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
+                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},3>",
+                       1: f"k_conv_x3<9,3,{V},1,{mr},3>" if s == 1 else f"k_conv_x3<5|4,{V},1,1,3>",
                        2: f"k_wgrad_x3<{V},{s}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
                        1: f"k_tconv<9,2,{V},1>" if s == 1 else f"k_tconv<5|4,2,{V},1>",
                        2: f"k_wgrad_taps<{V},{s}>", 3: f"k_tconv<1,8,{V},1>"}[which]
-            add(symbols, sym, ms.value, fl.value, 1 if (which != 1 or s == 1) else 2)
+            add(symbols, sym, ms.value, fl.value, 1 if (which != 1 or s == 1) else 2, act)
     return kinds, symbols
 
 
@@ -354,18 +371,30 @@ def main():
             out["per_block_clips_s"] = per_block_rates(model, cfg, device)
             kinds, symbols = kernel_roofline(pkg, device, cfg)
             sym = max(symbols, key=lambda k: symbols[k][0])
-            ms_tot, fl_tot, nl = symbols[sym]
-            ach = fl_tot / (ms_tot * 1e-3) / 1e12
+            ms_tot, fl_tot, nl, nb_tot = symbols[sym]
             traffic = traffic_from_profiles(sym)
-            peak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
-                    X3_PEAK_TFLOPS if sym.startswith("k_conv_x3") else MFMA_F32_PEAK_TFLOPS)
+            fpeak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
+                     X3_PEAK_TFLOPS if sym.startswith("k_conv_x3") else MFMA_F32_PEAK_TFLOPS)
+            # the roof that bounds the kernel's algorithmic work: MFMA or HBM
+            # (the bf16 GEMMs over fp32 activations at 64-128 channels sit
+            # below the bf16 ridge of 2500 / 8 = 312 FLOP/B)
+            hbm = nb_tot / (HBM_PEAK_GBS * 1e9) > fl_tot / (fpeak * 1e12)
+            if hbm:
+                ach, peak, unit = nb_tot / (ms_tot * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s"
+            else:
+                ach, peak, unit = fl_tot / (ms_tot * 1e-3) / 1e12, fpeak, "TFLOP/s"
             out["roofline"] = {
-                "kernel": sym, "bound": "mfma", "achieved": round(ach, 2),
-                "peak": peak, "unit": "TFLOP/s",
+                "kernel": sym, "bound": "hbm" if hbm else "mfma", "achieved": round(ach, 2),
+                "peak": peak, "unit": unit,
                 "frac": round(ach / peak, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": round(nb_tot / nl),
+                "algorithmic_flops_per_launch": round(fl_tot / nl),
+                "tflops": round(fl_tot / (ms_tot * 1e-3) / 1e12, 2),
+                "gbs": round(nb_tot / (ms_tot * 1e-3) / 1e9, 1),
                 "avg_launch_ms": round(ms_tot / nl, 4), "launches_per_step": nl,
                 "per_kind_tflops": {k: round(v[1] / (v[0] * 1e-3) / 1e12, 1)
                                     for k, v in kinds.items()},
+                "per_kind_gbs": {k: round(v[3] / (v[0] * 1e-3) / 1e9, 1) for k, v in kinds.items()},
                 "per_kind_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()}}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)

@@ -760,7 +760,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 //   which 0: temporal (9,1) conv forward      (k_conv_gemm<9>)
 //         1: temporal conv data-gradient      (k_conv_gemm<9> or <5>+<4>)
 //         2: temporal conv weight-gradient    (k_wgrad<9>, slab reduce excluded)
-//         3: spatial channel GEMM Z = W' G    (k_conv_gemm<1>)
+//         3: spatial channel GEMM Z = W' G    (k_conv_gemm<1>; with the fused bf16
+//            spatial forward: that kernel, joint contraction FLOPs included)
 // flops = the algorithmic FLOPs of one launch (SURVEY.md §8d terms).
 // ---------------------------------------------------------------------------
 namespace {
@@ -769,6 +770,12 @@ struct TimedPlan {
   int ncp = 0;
   WgradParams wp{};
   bool wgrad = false;
+  // which 3 on the fused bf16 spatial forward (k_sp_fwd_bf16 / k_sp_fwd_wide)
+  bool spf = false;
+  const float *x = nullptr, *st = nullptr, *A = nullptr, *W = nullptr, *biasZ = nullptr;
+  void *wpk = nullptr;
+  float *Z = nullptr;
+  __bf16 *Gk = nullptr;
   size_t bytes = 0;
   double flops = 0;
 };
@@ -851,6 +858,18 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.wp = w;
     P.wgrad = true;
     P.flops = tflops;
+  } else if (fused_sp(d)) {
+    // the forward's fused spatial kernel (G kept in bf16 as in the stack)
+    P.spf = true;
+    P.wpk = wpk;
+    P.x = c.take<float>((size_t)N * C * T * V);
+    P.st = c.take<float>((size_t)4 * C);
+    P.A = c.take<float>((size_t)K * V * V);
+    P.W = c.take<float>((size_t)K * R * C);
+    P.biasZ = c.take<float>((size_t)R * V);
+    P.Z = c.take<float>((size_t)N * R * T * V);
+    P.Gk = reinterpret_cast<__bf16 *>(c.take<char>(sp_keep_g_bytes(N, C, T, V, K)));
+    P.flops = 2.0 * K * C * (double)R * T * V * N + 2.0 * K * C * (double)T * V * V * N;
   } else {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * K * C * T * V);
@@ -899,6 +918,12 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
   hipStream_t s = (hipStream_t)stream;
   auto launch = [&]() -> hipError_t {
     if (P.wgrad) return launch_wgrad_taps(P.wp, s);
+    if (P.spf) {
+      const int C = d->C_in;
+      return launch_sp_fwd_bf16(P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A, P.W,
+                                P.biasZ, P.wpk, P.Z, P.Gk, nullptr, nullptr, d->N, C, d->C_out,
+                                d->T, d->V, d->K, residual(d) ? 1 : 0, s);
+    }
     for (int i = 0; i < P.ncp; ++i) {
       hipError_t e = launch_conv_gemm(P.cp[i], s);
       if (e != hipSuccess) return e;

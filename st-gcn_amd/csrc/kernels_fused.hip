@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 #include "internal.h"
@@ -726,7 +727,10 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
                               double *ssq, int N, int C, int R, int T, int V, int K, int relu,
                               hipStream_t s) {
   if (!sp_fwd_bf16_supported(C, V, K, R, relu != 0)) return hipErrorInvalidValue;
-  const bool wide = V == 50;
+  // all output channels per workgroup: the two-person graph, and V = 25 with
+  // K = 3 (STGCN_SPF_NARROW25: the 64-row k_sp_fwd_bf16 there, A/B only)
+  static const bool narrow25 = getenv("STGCN_SPF_NARROW25") != nullptr;
+  const bool wide = V == 50 || (V == 25 && K == 3 && !narrow25 && (R <= 128 || !relu));
   const int nch = (C + 15) / 16;
   const int rows = !wide ? 64 : (R <= 64 ? 64 : (R <= 128 ? 128 : 256));
   const int nrt = (R + rows - 1) / rows;
@@ -776,10 +780,16 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
   p.n_mtiles = (T + p.FT - 1) / p.FT;
   p.n_rtiles = nrt;
   const int nblk = N * p.n_mtiles * nrt;
-  if (wide) {
+  if (wide && V == 50) {
     if (rows == 64) launch_spw<50, 3, 64>(P, nblk, s);
     else if (rows == 128) launch_spw<50, 3, 128>(P, nblk, s);
     else launch_spw<50, 3, 256>(P, nblk, s);
+    return hipGetLastError();
+  }
+  if (wide) {
+    if (rows == 64) launch_spw<25, 3, 64>(P, nblk, s);
+    else if (rows == 128) launch_spw<25, 3, 128>(P, nblk, s);
+    else launch_spw<25, 3, 256>(P, nblk, s);
     return hipGetLastError();
   }
 #define SPF_K(VV)                            \
