@@ -557,30 +557,8 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
               d.y = pkbf(ga[4 * q + 2], ga[4 * q + 3]);
               *reinterpret_cast<uint2 *>(gi + ((t * V + v) * G::SLOTS) * 16 + (kk * 16 + ch0) * 2) =
                   d;
-              if (P.Gk) {
-                // kept G for the backward dW' (k_wgrad_gemm_gk layout
-                // Gk[n][k*C_in + ci][mtile][256]): lanes = consecutive positions
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const int ci = c * G::CK + ch0 + r;
-                  if (ci < P.C) {
-                    const int64_t grow = ((int64_t)n * K + kk) * P.C + ci;
-                    P.Gk[(grow * p.n_mtiles + mt) * 256 + t * V + v] = (__bf16)ga[4 * q + r];
-                  }
-                }
-              }
             }
           }
-        }
-      }
-      // the 256 - NCOLS pad positions of the chunk's kept G rows stay zero
-      // (k_wgrad_gemm_gk reads whole 32-position pieces)
-      if (P.Gk && tid < G::CK * K) {
-        const int kk = tid / G::CK, ci = c * G::CK + (tid - kk * G::CK);
-        if (ci < P.C) {
-          const int64_t grow = ((int64_t)n * K + kk) * P.C + ci;
-          __bf16 *dst = P.Gk + (grow * p.n_mtiles + mt) * 256;
-          for (int q2 = G::NCOLS; q2 < 256; ++q2) dst[q2] = (__bf16)0.f;
         }
       }
     }
@@ -606,6 +584,30 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
     if (more) {
       wait_x();  // x(c+1) and W'(c+1) landed
       write_x(c + 1, (c + 1) & 1);
+    }
+    if (P.Gk) {
+      // kept G for the backward dW' (k_wgrad_gemm_gk layout Gk[n][k*C_in + ci]
+      // [mtile][256]), from the LDS image after the x wait, so the stores drain
+      // under the next chunk: item (position, octet) = 8 channels of one
+      // position; lanes = consecutive positions (128-byte pieces per store);
+      // the 256 - NCOLS pad positions are written as zeros
+      const char *gi = lds + G::OFF_G;
+      for (int e = tid; e < 256 * 2 * K; e += G::NT) {
+        const int o = e >> 8, pos = e & 255;
+        uint4 r = make_uint4(0u, 0u, 0u, 0u);
+        if (pos < G::NCOLS) r = *reinterpret_cast<const uint4 *>(gi + (pos * G::SLOTS + o) * 16);
+        const unsigned w4[4] = {r.x, r.y, r.z, r.w};
+        const int kk = o >> 1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int ci = c * G::CK + (o & 1) * 8 + q;
+          if (ci < P.C) {
+            const int64_t grow = ((int64_t)n * K + kk) * P.C + ci;
+            P.Gk[(grow * p.n_mtiles + mt) * 256 + pos] =
+                __builtin_bit_cast(__bf16, (unsigned short)(w4[q >> 1] >> (16 * (q & 1))));
+          }
+        }
+      }
     }
   }
   if constexpr (ROWS == 256) {
