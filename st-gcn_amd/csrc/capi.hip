@@ -700,7 +700,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_conv_gemm(p, s));
   }
   HIP_TRY(launch_spatial_dx(L.H, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
-                            L.sdn, N, C, T, V, K, d->need_dx, res, s));
+                            L.sdn, N, C, T, V, K, d->need_dx, res, bf16(d) ? 1 : 0, s));
   HIP_TRY(launch_bn_grads_out(L.sd, L.sdn, nullptr, C, a->dg1, a->db1, nullptr, s));
   // residual path gradient (added to dx after the BN1 backward)
   const float *add = nullptr;
@@ -1137,7 +1137,7 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *sd, const float *dout, const f
   HIP_TRY(launch_conv_gemm(p, s));
   // dx = sum_k H_k A_k (BatchNorm identity: dx is dxhat; sd/sdn unused)
   HIP_TRY(launch_spatial_dx(L.H, x, mean, invstd, g, b, A, dx, dA, L.sd, L.sdn, N, C, T, V, K,
-                            dx != nullptr, 0, s));
+                            dx != nullptr, 0, bf16(d) ? 1 : 0, s));
   return STGCN_OK;
 }
 

@@ -181,7 +181,7 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b,
                              const float *A, float *dx, float *dA, double *sd, double *sdn,
                              int N, int C, int T, int V, int K, int write_dx, int relu,
-                             hipStream_t s);
+                             int bf16ops, hipStream_t s);
 
 // Fused spatial graph convolution of the bf16 path (kernels_fused.hip):
 // Z = W' (f(BN1(x)) A^T) + biasZ in one kernel (BN1 + joint contraction on MFMA

@@ -2277,7 +2277,12 @@ __device__ __forceinline__ floatx16 bwd6_mfma(uint4 a, uint4 b, floatx16 c) {
 #ifndef STGCN_BWD6_EXP  // timing experiments only (bits skip work; results wrong)
 #define STGCN_BWD6_EXP 0
 #endif
-template <int V, int KMAX>
+// BF (STGCN_F_BF16 blocks): H and A to 2^-16 (h + m planes; the dropped terms
+// are below 2^-16 of each product), f(BN1(x)) of the dA GEMM to bf16: three
+// products for dx and two for dA instead of six each. (H to bf16 alone moved
+// the residual V = 50 block's BN1 bias gradient to 4.5x the bf16 reference's
+// own error, past the 3x gate.)
+template <int V, int KMAX, bool BF>
 __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
@@ -2382,9 +2387,11 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
             acc = bwd6_mfma(ah, Bh[k][ks], acc);
             acl = bwd6_mfma(ah, Bmd[k][ks], acl);
             acl = bwd6_mfma(am, Bh[k][ks], acl);
-            acl = bwd6_mfma(ah, Bl[k][ks], acl);
-            acl = bwd6_mfma(am, Bmd[k][ks], acl);
-            acl = bwd6_mfma(al, Bh[k][ks], acl);
+            if constexpr (!BF) {
+              acl = bwd6_mfma(ah, Bl[k][ks], acl);
+              acl = bwd6_mfma(am, Bmd[k][ks], acl);
+              acl = bwd6_mfma(al, Bh[k][ks], acl);
+            }
           }
         }
       }
@@ -2420,12 +2427,14 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
           sn = fmaf(d, (xv - mu) * is, sn);
           const float f = relu ? fmaxf(bn, 0.f) : bn;
           const __bf16 fh = (__bf16)f;
-          const float r1 = f - (float)fh;
-          const __bf16 fm = (__bf16)r1;
           __bf16 *xt = reinterpret_cast<__bf16 *>(XT) + w * XTP + rl;
           xt[0] = fh;
-          xt[XTPL / 2] = fm;
-          xt[XTPL] = (__bf16)(r1 - (float)fm);
+          if constexpr (!BF) {
+            const float r1 = f - (float)fh;
+            const __bf16 fm = (__bf16)r1;
+            xt[XTPL / 2] = fm;
+            xt[XTPL] = (__bf16)(r1 - (float)fm);
+          }
         }
       }
       const int seg0 = __builtin_amdgcn_readfirstlane(seg);
@@ -2473,8 +2482,10 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
         if (cw < V) {
           const char *xt = XT + (cw * XTP + rb) * 2;
           bh = *reinterpret_cast<const uint4 *>(xt);
-          bm = *reinterpret_cast<const uint4 *>(xt + XTPL);
-          bl = *reinterpret_cast<const uint4 *>(xt + 2 * XTPL);
+          if constexpr (!BF) {
+            bm = *reinterpret_cast<const uint4 *>(xt + XTPL);
+            bl = *reinterpret_cast<const uint4 *>(xt + 2 * XTPL);
+          }
         }
 #pragma unroll
         for (int i = 0; i < KMAX; ++i) {
@@ -2489,11 +2500,13 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
             bwd6_split2(av[4], av[5], ah.z, am.z, al.z);
             bwd6_split2(av[6], av[7], ah.w, am.w, al.w);
             dacc[i] = bwd6_mfma(ah, bh, dacc[i]);
-            dacl[i] = bwd6_mfma(ah, bm, dacl[i]);
             dacl[i] = bwd6_mfma(am, bh, dacl[i]);
-            dacl[i] = bwd6_mfma(ah, bl, dacl[i]);
-            dacl[i] = bwd6_mfma(am, bm, dacl[i]);
-            dacl[i] = bwd6_mfma(al, bh, dacl[i]);
+            if constexpr (!BF) {
+              dacl[i] = bwd6_mfma(ah, bm, dacl[i]);
+              dacl[i] = bwd6_mfma(ah, bl, dacl[i]);
+              dacl[i] = bwd6_mfma(am, bm, dacl[i]);
+              dacl[i] = bwd6_mfma(al, bh, dacl[i]);
+            }
           }
         }
       }
@@ -2519,7 +2532,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
   }
 }
 
-template <int V, int KT>
+template <int V, int KT, bool BF>
 static bool launch_bwd6(const float *H, const float *x, const float *mean, const float *invstd,
                         const float *g, const float *b, const float *A, float *dx, float *dA,
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
@@ -2531,7 +2544,7 @@ static bool launch_bwd6(const float *H, const float *x, const float *mean, const
       rows >= (int64_t)1 << 31)
     return false;
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256));
-  hipLaunchKernelGGL((k_spatial_bwd6<V, KT>), grid, dim3(512), lds, s, H, x, mean, invstd, g, b,
+  hipLaunchKernelGGL((k_spatial_bwd6<V, KT, BF>), grid, dim3(512), lds, s, H, x, mean, invstd, g, b,
                      A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
   return true;
 }
@@ -2875,8 +2888,11 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
 hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b, const float *A,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
-                             int V, int K, int write_dx, int relu, hipStream_t s) {
+                             int V, int K, int write_dx, int relu, int bf16ops, hipStream_t s) {
   static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
+  // (STGCN_BWD6_EXACT: the exact-split k_spatial_bwd6 for bf16 blocks too, A/B only)
+  static const bool exact6 = env_flag("STGCN_BWD6_EXACT");
+  const bool bf6 = bf16ops && !exact6;
   const bool aligned = ((int64_t)N * C * T * V) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
                        ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0;
   if (!joint3 && aligned && K <= 3 && K * ((V + 1) / 2) * ((V + 31) / 32) <= 48) {
@@ -2900,9 +2916,13 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
   if (!joint3 && aligned && V == 50 && K <= 3) {  // two-person graph, 2 or 3 partitions
     const int64_t rows = (int64_t)N * C * T;
     bool done = false;
-#define STGCN_BWD6(KK) \
-  launch_bwd6<50, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, s)
-    done = STGCN_BWD6(1) || STGCN_BWD6(2) || STGCN_BWD6(3);
+#define STGCN_BWD6(KK, BF)                                                                     \
+  launch_bwd6<50, KK, BF>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, \
+                          relu, s)
+    if (bf6)
+      done = STGCN_BWD6(1, true) || STGCN_BWD6(2, true) || STGCN_BWD6(3, true);
+    else
+      done = STGCN_BWD6(1, false) || STGCN_BWD6(2, false) || STGCN_BWD6(3, false);
 #undef STGCN_BWD6
     if (done) return hipGetLastError();
   }
