@@ -203,17 +203,18 @@ def per_block_rates(model, cfg, device, iters=5):
     return out
 
 
-def traffic_from_profiles(symbol):
+def traffic_from_profiles(symbol, key="hbm_bytes_per_launch"):
     """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC pass
     (profiles/pmc_*.json: FETCH_SIZE doubled per the gfx950 correction +
-    WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+    WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None. key="mfma_busy":
+    the kernel's MFMA-busy fraction of SIMD cycles from the same file."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
         return None
     try:
         data = json.load(open(files[-1]))
-        return data.get("hbm_bytes_per_launch", {}).get(symbol)
+        return data.get(key, {}).get(symbol)
     except (OSError, ValueError):
         return None
 
@@ -387,6 +388,7 @@ def main():
                 "kernel": sym, "bound": "hbm" if hbm else "mfma", "achieved": round(ach, 2),
                 "peak": peak, "unit": unit,
                 "frac": round(ach / peak, 4), "traffic": traffic,
+                "mfma_busy": traffic_from_profiles(sym, "mfma_busy"),
                 "algorithmic_bytes_per_launch": round(nb_tot / nl),
                 "algorithmic_flops_per_launch": round(fl_tot / nl),
                 "tflops": round(fl_tot / (ms_tot * 1e-3) / 1e12, 2),

@@ -21,10 +21,15 @@ echo "benches done"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv \
   -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/stats_bench.log 2>&1
 rc=$?; echo "stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
-i=0
-for ctr in FETCH_SIZE WRITE_SIZE; do
-  i=$((i+1))
-  timeout -k 10 -s KILL 300 rocprofv3 --pmc $ctr -d $OUT/pmc/p$i -o run --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-roofline > $OUT/pmc_p$i.log 2>&1
-  rc=$?; echo "pmc $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
+# HBM traffic (FETCH_SIZE / WRITE_SIZE, separate passes) per config, then
+# MFMA-busy cycles + the clock (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE) on cfg2
+for c in cfg2 cfg3 cfg5; do
+  i=0
+  for ctr in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    [ $i -eq 3 ] && [ $c != cfg2 ] && continue
+    timeout -k 10 -s KILL 300 rocprofv3 --pmc $ctr -d $OUT/pmc_$c/p$i -o run --output-format csv \
+      -- python3 bench.py --config $c --steps 2 --warmup 1 --no-cpu-baseline --no-roofline --no-alt --no-repeats > $OUT/pmc_${c}_p$i.log 2>&1
+    rc=$?; echo "pmc $c $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
 done

@@ -9,7 +9,12 @@ kernels also read with 4-byte lanes, so the file carries a calibration row:
 k_bn_stats reads each layer input exactly once (known byte count) with
 4-byte loads.
 
-Usage: python scripts/pmc_traffic.py gpurun_out/pmcb_<tag> profiles/pmc_<tag>.json
+Several pass directories (one per config) may be given: a kernel symbol
+keeps the value of the first directory that has it (cfg2 first). A pass with
+SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE adds `mfma_busy` per kernel: MFMA
+busy cycles over the 1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs).
+
+Usage: python scripts/pmc_traffic.py profiles/pmc_<tag>.json <pass dir> [<pass dir> ...]
 """
 import csv
 import glob
@@ -30,17 +35,23 @@ def short(name):
     return m.group(1) + (m.group(2) or "").replace(" ", "")
 
 
-def main(src, dst):
+def main(dst, *srcs):
     vals = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(src + "/*/run_counter_collection.csv"):
-        for r in csv.DictReader(open(f)):
-            k = short(r.get("Kernel_Name", r.get("Kernel-Name", "")))
-            if k:
-                vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for src in srcs:
+        seen = defaultdict(lambda: defaultdict(list))
+        for f in glob.glob(src + "/*/run_counter_collection.csv"):
+            for r in csv.DictReader(open(f)):
+                k = short(r.get("Kernel_Name", r.get("Kernel-Name", "")))
+                if k:
+                    seen[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, cs in seen.items():
+            for c, v in cs.items():
+                if c not in vals[k]:
+                    vals[k][c] = v
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
                      "bench.py --steps 2 --warmup 1 --no-roofline",
            "formula": "2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (bytes per launch)",
-           "hbm_bytes_per_launch": {}, "raw_kib": {}}
+           "hbm_bytes_per_launch": {}, "raw_kib": {}, "mfma_busy": {}}
     for k, cs in sorted(vals.items()):
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
@@ -49,6 +60,12 @@ def main(src, dst):
         out["hbm_bytes_per_launch"][k] = round(2 * fs * 1024 + ws * 1024)
         out["raw_kib"][k] = {"FETCH_SIZE": round(fs, 1), "WRITE_SIZE": round(ws, 1),
                              "launches": len(cs["FETCH_SIZE"])}
+    for k, cs in sorted(vals.items()):
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs:
+            mb = sum(cs["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(cs["SQ_VALU_MFMA_BUSY_CYCLES"])
+            gg = sum(cs["GRBM_GUI_ACTIVE"]) / len(cs["GRBM_GUI_ACTIVE"]) / 8
+            if gg > 0:
+                out["mfma_busy"][k] = round(mb / (gg * 1024), 4)
     stats = [k for k in out["raw_kib"] if k.startswith("k_bn_stats")]
     if stats:
         # with stack chaining only block 0 runs its own BN1 statistics pass
@@ -68,4 +85,4 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], *sys.argv[2:])
