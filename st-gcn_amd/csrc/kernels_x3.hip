@@ -44,6 +44,12 @@
 #include "device_common.h"
 #include "internal.h"
 
+#ifndef STGCN_WG_WSTART  // k_wgrad_x3: first k-step carrying the next item's writes
+#define STGCN_WG_WSTART 1  // (>= KSTEPS: after the k-steps)
+#endif
+#ifndef STGCN_WG_EXP  // k_wgrad_x3 timing experiments only (results wrong): bit 1 no
+#define STGCN_WG_EXP 0  // staging, 2 no MFMAs, 4 no fragment reads, 8 no item barrier
+#endif
 #ifndef STGCN_X3_EXP  // timing experiments only (bits skip work; results wrong)
 #define STGCN_X3_EXP 0
 #endif
@@ -718,14 +724,22 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         const bool ok = gl[k] >= 0 && r < p.R && m < p.M;
         base = ok ? (unsigned)(r * MV + m * V + gv0[k]) * 4u : kOOB;
       }
+      // P / Q split of the staging groups falls on wave boundaries (64 * PG is a
+      // multiple of 64): a wave-uniform descriptor choice (no waterfall loop)
+      const bool q_k = __builtin_amdgcn_readfirstlane((int)isq[k]) != 0;
+      const __amdgpu_buffer_rsrc_t rs = q_k ? rq : rp;
+      // two 8-byte loads per 4-joint group (V even: pairs never straddle a
+      // frame; pad pairs read 0 through an OOB offset)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const unsigned off = gv0[k] + j < V ? base + 4u * j : kOOB;  // pad joints: 0
-        st[k][j] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(isq[k] ? rq : rp, off, 0, 0));
+      for (int j = 0; j < 2; ++j) {
+        const unsigned off = gv0[k] + 2 * j < V ? base + 8u * j : kOOB;
+        const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        st[k][2 * j] = __builtin_bit_cast(float, (unsigned)v2[0]);
+        st[k][2 * j + 1] = __builtin_bit_cast(float, (unsigned)v2[1]);
       }
     }
   };
+  static_assert(V % 2 == 0 && (64 * G::PG) % 64 == 0, "pair loads, uniform P/Q waves");
   // splits and writes staging groups [K0, K1) of the loaded item
   auto write_part = [&](char *buf, auto k0_c, auto k1_c) {
     constexpr int K0 = decltype(k0_c)::value, K1 = decltype(k1_c)::value;
@@ -797,34 +811,38 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       char *nxt = lds + (G::NBUF == 2 ? ((it - it0 + 1) & 1) * G::BUF : 0);
       // next item (the last iteration reloads its own item into the idle buffer:
       // unconditional, so no register copies across the loop)
-      load_item(it + 1 < it1 ? it + 1 : it);
+      if (!(STGCN_WG_EXP & 1)) load_item(it + 1 < it1 ? it + 1 : it);
       Frag f[2];
       ld(cur, 0, f[0]);
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
-        if (s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) & 1]);
-        mm(f[s & 1]);
-        if constexpr (G::NBUF == 2) {
+        if (!(STGCN_WG_EXP & 4) && s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) & 1]);
+        if (!(STGCN_WG_EXP & 2)) mm(f[s & 1]);
+        if constexpr (G::NBUF == 2 && STGCN_WG_WSTART < G::KSTEPS && !(STGCN_WG_EXP & 1)) {
           // double buffer: the next item's split + LDS writes ride in the MFMA
-          // shadow of k-steps 1.. (part s-1 of KSTEPS-1), not after the loop
-          static_assert(G::KSTEPS == 5, "four write parts");
+          // shadow of k-steps WSTART.. (the loads were issued at the item start)
           using std::integral_constant;
-          constexpr int Q = G::GPT;
-          if (s == 1)
-            write_part(nxt, integral_constant<int, 0>{}, integral_constant<int, Q / 4>{});
-          else if (s == 2)
-            write_part(nxt, integral_constant<int, Q / 4>{}, integral_constant<int, Q / 2>{});
-          else if (s == 3)
-            write_part(nxt, integral_constant<int, Q / 2>{}, integral_constant<int, 3 * Q / 4>{});
-          else if (s == 4)
-            write_part(nxt, integral_constant<int, 3 * Q / 4>{}, integral_constant<int, Q>{});
+          constexpr int W0 = STGCN_WG_WSTART, NP = G::KSTEPS - W0, Q = G::GPT;
+          static_assert(W0 >= 1 && NP >= 1 && NP <= 4, "write parts");
+          if (s == W0)
+            write_part(nxt, integral_constant<int, 0>{}, integral_constant<int, Q / NP>{});
+          else if (NP >= 2 && s == W0 + 1)
+            write_part(nxt, integral_constant<int, Q / NP>{}, integral_constant<int, 2 * Q / NP>{});
+          else if (NP >= 3 && s == W0 + 2)
+            write_part(nxt, integral_constant<int, 2 * Q / NP>{},
+                       integral_constant<int, 3 * Q / NP>{});
+          else if (NP >= 4 && s == W0 + 3)
+            write_part(nxt, integral_constant<int, 3 * Q / NP>{}, integral_constant<int, Q>{});
         }
         __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (G::NBUF == 1) {
         __syncthreads();  // every wave is done reading the buffer
         write_item(nxt);
+      } else if constexpr (STGCN_WG_WSTART >= G::KSTEPS && !(STGCN_WG_EXP & 1)) {
+        write_item(nxt);
       }
+      if (STGCN_WG_EXP & 8) continue;  // (no barrier: timing experiment only)
       __syncthreads();
     }
     float *slab = p.slab + (int64_t)split * p.R * p.C * 9;
