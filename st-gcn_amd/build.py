@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "lib", "libstgcn_hip.so")
 SOURCES = ["kernels.hip", "kernels_bf16.hip", "kernels_x3.hip", "kernels_fused.hip",
-           "train_ops.hip", "capi.hip"]
+           "kernels_spbwd.hip", "train_ops.hip", "capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wall"]
 

@@ -65,8 +65,11 @@ size_t wpk_floats(const stgcn_desc_t *d) {
   // STGCN_F_F32X3: three bf16 planes of the weights (1.5x the fp32 floats)
   if (d->flags & STGCN_F_F32X3) n *= 2;
   // the fused bf16 spatial forward: packed W' + the A image
-  if (d->flags & STGCN_F_BF16)
+  if (d->flags & STGCN_F_BF16) {
     n = std::max(n, (sp_fwd_bf16_wpk_bytes(d->C_in, d->C_out, d->K, d->V) + 3) / 4);
+    // the fused bf16 spatial backward: packed W' + its A image
+    n = std::max(n, (sp_bwd_fused_wpk_bytes(d->C_in, d->C_out, d->K, d->V) + 3) / 4);
+  }
   return n;
 }
 
@@ -90,6 +93,12 @@ Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
 bool fused_sp(const stgcn_desc_t *d) {
   static const bool off = getenv("STGCN_UNFUSED_SP") != nullptr;
   return !off && bf16(d) && sp_fwd_bf16_supported(d->C_in, d->V, d->K, d->C_out, residual(d));
+}
+// the fused spatial backward (kernels_spbwd.hip) of the bf16 path applies
+// (STGCN_UNFUSED_SPB: the H GEMM + k_spatial_bwd5/6 pair, A/B measurement only)
+bool fused_spb(const stgcn_desc_t *d) {
+  static const bool off = getenv("STGCN_UNFUSED_SPB") != nullptr;
+  return !off && bf16(d) && sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out);
 }
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {
@@ -669,6 +678,11 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s));
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
+  if (fused_spb(d)) {
+    // H = W'^T dZ, dx = sum_k H_k A_k, dA, BN1 sums in one kernel (H stays on chip)
+    HIP_TRY(launch_sp_bwd_fused(L.dZ, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.wpk,
+                                a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res, s));
+  } else {
   {
     // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
     // the channels of H_k): dZ is read once instead of K times
@@ -701,6 +715,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   HIP_TRY(launch_spatial_dx(L.H, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
                             L.sdn, N, C, T, V, K, d->need_dx, res, bf16(d) ? 1 : 0, s));
+  }
   HIP_TRY(launch_bn_grads_out(L.sd, L.sdn, nullptr, C, a->dg1, a->db1, nullptr, s));
   // residual path gradient (added to dx after the BN1 backward)
   const float *add = nullptr;

@@ -199,4 +199,16 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
 void plan_wgrad_gk(WgradParams &w, int T);
 hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s);
 
+// Fused SpatialConv backward of the bf16 path (kernels_spbwd.hip): from dZ to
+// dx (BN1 input side, before the BN1 backward apply), dA += sum H_k^T f(BN1(x))
+// and the BN1 backward sums, H = W'^T dZ never in HBM. wpk: scratch of
+// sp_bwd_fused_wpk_bytes (packed W' + the A image).
+bool sp_bwd_fused_supported(int C, int V, int K, int R);
+size_t sp_bwd_fused_wpk_bytes(int C, int R, int K, int V);
+hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mean,
+                               const float *invstd, const float *g, const float *b,
+                               const float *A, const float *W, void *wpk, float *dx, float *dA,
+                               double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
+                               int write_dx, int relu, hipStream_t s);
+
 }  // namespace stgcn
