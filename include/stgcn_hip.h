@@ -199,7 +199,7 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
  * launched `iters` times with the exact parameters the block uses for this
  * descriptor, between two hipEvents on `stream`. which: 0 temporal conv fwd,
  * 1 temporal conv data-grad, 2 temporal conv weight-grad, 3 spatial channel
- * GEMM. scratch (>= stgcn_time_kernel_bytes) supplies operand memory.
+ * GEMM, 4 spatial backward (dZ -> dx, dA, BN1 sums). scratch (>= stgcn_time_kernel_bytes) supplies operand memory.
  * *flops receives the algorithmic FLOPs of one launch. */
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which);
 int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t scratch_bytes,

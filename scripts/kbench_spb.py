@@ -1,0 +1,30 @@
+"""Time the spatial backward (stgcn_time_kernel which=4: k_sp_bwd_fused, or the
+H GEMM + joint kernel with STGCN_UNFUSED_SPB) at the cfg3 / cfg5 layer shapes
+(bf16 path, K = 3). Usage: KB_V=25 python scripts/kbench_spb.py [iters]"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+from stgcn_loader import load  # noqa: E402
+
+pkg = load()
+hl = pkg.hip_lib
+lib = hl.lib()
+dev = torch.device("cuda", 0)
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+V = int(os.environ.get("KB_V", "25"))
+shapes = [("L1 64->64 T300", 64, 64, 300), ("L4 64->128 T300", 64, 128, 300),
+          ("L5 128->128 T150", 128, 128, 150), ("L8 256->256 T75", 256, 256, 75)]
+for label, ci, co, T in shapes:
+    d = pkg.fused.make_desc((128, ci, T, V), co, 3, 1, 4, 1e-5, 0.1, True, bf16=True)
+    nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), 4)
+    scratch = torch.randn(nbytes // 4 + 1, device=dev) * 0.1
+    ms, fl = ctypes.c_float(0), ctypes.c_double(0)
+    hl.check(lib.stgcn_time_kernel(ctypes.byref(d), 4, hl.ptr(scratch), nbytes, iters,
+                                   hl.stream_handle(dev), ctypes.byref(ms), ctypes.byref(fl)))
+    mb = 4 * 128 * T * V * (co + 2 * ci) / 1e6
+    print(f"{label:18s} {ms.value * 1e3:8.1f} us  {fl.value / ms.value / 1e9:6.1f} TF/s  "
+          f"{mb / ms.value / 1e3:6.2f} TB/s (dZ + x + dx)", flush=True)
+    del scratch

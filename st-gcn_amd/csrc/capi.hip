@@ -98,7 +98,7 @@ bool fused_sp(const stgcn_desc_t *d) {
 // (STGCN_UNFUSED_SPB: the H GEMM + k_spatial_bwd5/6 pair, A/B measurement only)
 bool fused_spb(const stgcn_desc_t *d) {
   static const bool off = getenv("STGCN_UNFUSED_SPB") != nullptr;
-  return !off && bf16(d) && sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out);
+  return !off && bf16(d) && sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T);
 }
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {
@@ -777,6 +777,9 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 //         2: temporal conv weight-gradient    (k_wgrad<9>, slab reduce excluded)
 //         3: spatial channel GEMM Z = W' G    (k_conv_gemm<1>; with the fused bf16
 //            spatial forward: that kernel, joint contraction FLOPs included)
+//         4: spatial backward dZ -> dx, dA, BN1 sums (k_sp_bwd_fused where it
+//            applies, else the stacked H GEMM + the joint kernel; H GEMM and
+//            joint contraction FLOPs)
 // flops = the algorithmic FLOPs of one launch (SURVEY.md §8d terms).
 // ---------------------------------------------------------------------------
 namespace {
@@ -791,6 +794,11 @@ struct TimedPlan {
   void *wpk = nullptr;
   float *Z = nullptr;
   __bf16 *Gk = nullptr;
+  // which 4: the spatial backward
+  bool spb = false;
+  const float *dZ = nullptr;
+  float *H = nullptr, *dx = nullptr, *dA = nullptr;
+  double *sd = nullptr;
   size_t bytes = 0;
   double flops = 0;
 };
@@ -873,6 +881,42 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.wp = w;
     P.wgrad = true;
     P.flops = tflops;
+  } else if (which == 4) {
+    P.spb = true;
+    P.wpk = wpk;
+    P.x = c.take<float>((size_t)N * C * T * V);
+    P.st = c.take<float>((size_t)4 * C);
+    P.A = c.take<float>((size_t)K * V * V);
+    P.W = c.take<float>((size_t)K * R * C);
+    P.dZ = c.take<float>((size_t)N * R * T * V);
+    P.dx = c.take<float>((size_t)N * C * T * V);
+    P.dA = c.take<float>((size_t)K * V * V);
+    P.sd = c.take<double>((size_t)2 * C);
+    if (!fused_spb(d)) {
+      P.H = c.take<float>((size_t)N * K * C * T * V);
+      ConvGemmParams p = conv_base(d, wpk);
+      p.in = P.dZ;
+      p.w = c.take<float>((size_t)R * K * C);  // (the packed W' of the block)
+      p.out = P.H;
+      p.in_bstride = (int64_t)R * T * V;
+      p.out_bstride = (int64_t)K * C * T * V;
+      p.w_sr = 1;
+      p.w_sc = (int64_t)K * C;
+      p.w_sq = 0;
+      p.C = R;
+      p.R = K * C;
+      p.NQ = 1;
+      p.s_in = 1;
+      p.off = 0;
+      p.s_out = 1;
+      p.p_out = 0;
+      p.M = T;
+      p.T_src = T;
+      p.T_dst = T;
+      conv_tiles(p);
+      P.cp[P.ncp++] = p;
+    }
+    P.flops = 2.0 * K * C * (double)R * T * V * N + 4.0 * K * C * (double)T * V * V * N;
   } else if (fused_sp(d)) {
     // the forward's fused spatial kernel (G kept in bf16 as in the stack)
     P.spf = true;
@@ -918,7 +962,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
 extern "C" {
 
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which) {
-  if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 3) return 0;
+  if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 4) return 0;
   return plan_timed(d, which, nullptr).bytes;
 }
 
@@ -926,13 +970,25 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
                       int iters, void *stream, float *avg_ms, double *flops) {
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
-  if (which < 0 || which > 3 || iters <= 0 || !avg_ms || !flops)
+  if (which < 0 || which > 4 || iters <= 0 || !avg_ms || !flops)
     return fail(STGCN_E_INVALID, "bad timing request");
   TimedPlan P = plan_timed(d, which, scratch);
   if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
   hipStream_t s = (hipStream_t)stream;
   auto launch = [&]() -> hipError_t {
     if (P.wgrad) return launch_wgrad_taps(P.wp, s);
+    if (P.spb) {
+      const int C = d->C_in;
+      if (fused_spb(d))
+        return launch_sp_bwd_fused(P.dZ, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A,
+                                   P.W, P.wpk, P.dx, P.dA, P.sd, P.sd + C, d->N, C, d->C_out,
+                                   d->T, d->V, d->K, 1, residual(d) ? 1 : 0, s);
+      hipError_t e = launch_conv_gemm(P.cp[0], s);
+      if (e != hipSuccess) return e;
+      return launch_spatial_dx(P.H, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A, P.dx,
+                               P.dA, P.sd, P.sd + C, d->N, C, d->T, d->V, d->K, 1,
+                               residual(d) ? 1 : 0, bf16(d) ? 1 : 0, s);
+    }
     if (P.spf) {
       const int C = d->C_in;
       return launch_sp_fwd_bf16(P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A, P.W,

@@ -203,7 +203,7 @@ hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s);
 // dx (BN1 input side, before the BN1 backward apply), dA += sum H_k^T f(BN1(x))
 // and the BN1 backward sums, H = W'^T dZ never in HBM. wpk: scratch of
 // sp_bwd_fused_wpk_bytes (packed W' + the A image).
-bool sp_bwd_fused_supported(int C, int V, int K, int R);
+bool sp_bwd_fused_supported(int C, int V, int K, int R, int T);
 size_t sp_bwd_fused_wpk_bytes(int C, int R, int K, int V);
 hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mean,
                                const float *invstd, const float *g, const float *b,
