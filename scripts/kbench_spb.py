@@ -1,6 +1,7 @@
 """Time the spatial backward (stgcn_time_kernel which=4: k_sp_bwd_fused, or the
 H GEMM + joint kernel with STGCN_UNFUSED_SPB) at the cfg3 / cfg5 layer shapes
-(bf16 path, K = 3). Usage: KB_V=25 python scripts/kbench_spb.py [iters]"""
+(bf16 path, K = 3) or the cfg2 shapes (KB_V=18: fp32 split path, K = 1).
+Usage: KB_V=25 python scripts/kbench_spb.py [iters]"""
 import ctypes
 import os
 import sys
@@ -15,10 +16,12 @@ lib = hl.lib()
 dev = torch.device("cuda", 0)
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 V = int(os.environ.get("KB_V", "25"))
+K = 1 if V == 18 else 3
+x3 = V == 18  # cfg2: the fp32 split path; cfg3 / cfg5: bf16
 shapes = [("L1 64->64 T300", 64, 64, 300), ("L4 64->128 T300", 64, 128, 300),
           ("L5 128->128 T150", 128, 128, 150), ("L8 256->256 T75", 256, 256, 75)]
 for label, ci, co, T in shapes:
-    d = pkg.fused.make_desc((128, ci, T, V), co, 3, 1, 4, 1e-5, 0.1, True, bf16=True)
+    d = pkg.fused.make_desc((128, ci, T, V), co, K, 1, 4, 1e-5, 0.1, True, bf16=not x3, f32x3=x3)
     nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), 4)
     scratch = torch.randn(nbytes // 4 + 1, device=dev) * 0.1
     ms, fl = ctypes.c_float(0), ctypes.c_double(0)

@@ -65,11 +65,11 @@ size_t wpk_floats(const stgcn_desc_t *d) {
   // STGCN_F_F32X3: three bf16 planes of the weights (1.5x the fp32 floats)
   if (d->flags & STGCN_F_F32X3) n *= 2;
   // the fused bf16 spatial forward: packed W' + the A image
-  if (d->flags & STGCN_F_BF16) {
+  if (d->flags & STGCN_F_BF16)
     n = std::max(n, (sp_fwd_bf16_wpk_bytes(d->C_in, d->C_out, d->K, d->V) + 3) / 4);
-    // the fused bf16 spatial backward: packed W' + its A image
+  // the fused spatial backward: packed W' planes + its A image
+  if (d->flags & (STGCN_F_BF16 | STGCN_F_F32X3))
     n = std::max(n, (sp_bwd_fused_wpk_bytes(d->C_in, d->C_out, d->K, d->V) + 3) / 4);
-  }
   return n;
 }
 
@@ -94,11 +94,12 @@ bool fused_sp(const stgcn_desc_t *d) {
   static const bool off = getenv("STGCN_UNFUSED_SP") != nullptr;
   return !off && bf16(d) && sp_fwd_bf16_supported(d->C_in, d->V, d->K, d->C_out, residual(d));
 }
-// the fused spatial backward (kernels_spbwd.hip) of the bf16 path applies
-// (STGCN_UNFUSED_SPB: the H GEMM + k_spatial_bwd5/6 pair, A/B measurement only)
+// the fused spatial backward (kernels_spbwd.hip) applies: bf16 path, or the fp32
+// split path (STGCN_UNFUSED_SPB: the H GEMM + k_spatial_bwd5/6 pair, A/B only)
 bool fused_spb(const stgcn_desc_t *d) {
   static const bool off = getenv("STGCN_UNFUSED_SPB") != nullptr;
-  return !off && bf16(d) && sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T);
+  return !off && (bf16(d) || f32x3(d)) &&
+         sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T, f32x3(d));
 }
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {
@@ -681,7 +682,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   if (fused_spb(d)) {
     // H = W'^T dZ, dx = sum_k H_k A_k, dA, BN1 sums in one kernel (H stays on chip)
     HIP_TRY(launch_sp_bwd_fused(L.dZ, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.wpk,
-                                a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res, s));
+                                a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res,
+                                f32x3(d), s));
   } else {
   {
     // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
@@ -982,7 +984,7 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
       if (fused_spb(d))
         return launch_sp_bwd_fused(P.dZ, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A,
                                    P.W, P.wpk, P.dx, P.dA, P.sd, P.sd + C, d->N, C, d->C_out,
-                                   d->T, d->V, d->K, 1, residual(d) ? 1 : 0, s);
+                                   d->T, d->V, d->K, 1, residual(d) ? 1 : 0, f32x3(d), s);
       hipError_t e = launch_conv_gemm(P.cp[0], s);
       if (e != hipSuccess) return e;
       return launch_spatial_dx(P.H, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A, P.dx,

@@ -203,12 +203,13 @@ hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s);
 // dx (BN1 input side, before the BN1 backward apply), dA += sum H_k^T f(BN1(x))
 // and the BN1 backward sums, H = W'^T dZ never in HBM. wpk: scratch of
 // sp_bwd_fused_wpk_bytes (packed W' + the A image).
-bool sp_bwd_fused_supported(int C, int V, int K, int R, int T);
+// x3: the fp32 path of STGCN_F_F32X3 (exact bf16 splits) instead of the bf16 path
+bool sp_bwd_fused_supported(int C, int V, int K, int R, int T, bool x3);
 size_t sp_bwd_fused_wpk_bytes(int C, int R, int K, int V);
 hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mean,
                                const float *invstd, const float *g, const float *b,
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
-                               int write_dx, int relu, hipStream_t s);
+                               int write_dx, int relu, bool x3, hipStream_t s);
 
 }  // namespace stgcn

@@ -102,9 +102,53 @@ __device__ __forceinline__ void spb_barrier() {
 #define STGCN_SPB_EXP 0
 #endif
 
-template <int V, int K>
+// (a, b) -> packed bf16 planes h, m, l (a == h + m + l exactly; kernels_x3.hip)
+__device__ __forceinline__ void spb_split3(float a, float b, unsigned &h, unsigned &m,
+                                           unsigned &l) {
+  h = spb_pk(a, b);
+  const float ra = a - __builtin_bit_cast(float, h << 16);
+  const float rb = b - __builtin_bit_cast(float, h & 0xffff0000u);
+  m = spb_pk(ra, rb);
+  l = spb_pk(ra - __builtin_bit_cast(float, m << 16), rb - __builtin_bit_cast(float, m & 0xffff0000u));
+}
+// 8 floats -> operand planes (2: h, m; 3: h, m, l)
+template <int NP>
+__device__ __forceinline__ void spb_planes(const float (&v)[8], uint4 (&o)[NP]) {
+  static_assert(NP == 2 || NP == 3, "planes");
+  if constexpr (NP == 2) {
+    spb_split(v[0], v[1], o[0].x, o[1].x);
+    spb_split(v[2], v[3], o[0].y, o[1].y);
+    spb_split(v[4], v[5], o[0].z, o[1].z);
+    spb_split(v[6], v[7], o[0].w, o[1].w);
+  } else {
+    spb_split3(v[0], v[1], o[0].x, o[1].x, o[2].x);
+    spb_split3(v[2], v[3], o[0].y, o[1].y, o[2].y);
+    spb_split3(v[4], v[5], o[0].z, o[1].z, o[2].z);
+    spb_split3(v[6], v[7], o[0].w, o[1].w, o[2].w);
+  }
+}
+// sum over the split products of weight >= 2^-16 of two 3-plane operands:
+// h*h into acc[0], h*m + m*h + h*l + m*m + l*h into acc[1] (kernels_x3.hip)
+__device__ __forceinline__ void spb_mfma6(const uint4 (&a)[3], const uint4 (&b)[3],
+                                          floatx16 (&acc)[2]) {
+  acc[0] = spb_mfma(a[0], b[0], acc[0]);
+  acc[1] = spb_mfma(a[0], b[1], acc[1]);
+  acc[1] = spb_mfma(a[1], b[0], acc[1]);
+  acc[1] = spb_mfma(a[0], b[2], acc[1]);
+  acc[1] = spb_mfma(a[1], b[1], acc[1]);
+  acc[1] = spb_mfma(a[2], b[0], acc[1]);
+}
+
+// X3 = false: the bf16 path (bf16 W', dZ rounded to bf16; H, A to 2^-16).
+// X3 = true : the fp32 path of STGCN_F_F32X3 (every operand as its exact 3-way
+//             bf16 split, six products per fp32 product, h*h accumulated apart).
+template <int V, int K, bool X3>
 struct SpBwdGeo {
   static_assert(V <= 32, "one 32-joint tile");
+  static constexpr int NPLW = X3 ? 3 : 1;           // W' planes
+  static constexpr int NPLA = X3 ? 3 : 2;           // A planes (dx A operand)
+  static constexpr int NPLX = X3 ? 3 : 1;           // f(BN1(x)) planes (dA B operand)
+  static constexpr int NACC = X3 ? 2 : 1;           // accumulators per tile (h*h apart)
   static constexpr int FT = 8;                      // frames per item (wave = frame)
   static constexpr int NPOS = FT * V;               // positions per item
   // 16-byte pieces per row: NPOS positions from a 16-byte aligned start up to 3
@@ -117,11 +161,12 @@ struct SpBwdGeo {
   static constexpr int RP = (NPC * 4) % 8 == 0 ? NPC * 4 + 4 : NPC * 4;
   static_assert(NPOS % 4 == 0, "item starts p0 16-byte aligned within a row");
   static constexpr int RING_SLOT = CR * RP * 4;     // fp32 [r][RP]
-  static constexpr int W_BYTES = K * CR * 64;       // W' chunk [k][octet 2][ci 32][8] bf16
+  static constexpr int W_BYTES = K * NPLW * CR * 64;  // W' chunk [k][plane][octet 2][ci 32][8]
   static constexpr int WPW = W_BYTES / 16 / 8;      // W' pieces per wave
   static constexpr int XBP = 80;                    // f(BN1(x)) image row pitch, bytes
-  static constexpr int XB_BYTES = FT * 32 * XBP;
-  static constexpr int AIMG_BYTES = K * 2 * 2 * 1024;  // [k][ks][plane] 1 KiB fragments
+  static constexpr int XB_ROWS = NPOS + 1;          // rows (frame, w) + one zero row
+  static constexpr int XB_PLANE = XB_ROWS * XBP;
+  static constexpr int AIMG_BYTES = K * 2 * NPLA * 1024;  // [k][ks][plane] 1 KiB fragments
   static constexpr int SP = NPOS + 1;               // dx row image pitch (floats, odd)
   static constexpr int CMAX = 256;                  // channels of the BN tables / sums
   static constexpr int OFF_A = 0, OFF_RING = AIMG_BYTES;
@@ -129,7 +174,7 @@ struct SpBwdGeo {
   static constexpr int OFF_X = OFF_W + D * W_BYTES;                        // fp32 [ci][RP]
   static constexpr int OFF_ST = OFF_X + CB * RP * 4;                        // fp32 [ci][SP]
   static constexpr int OFF_XB = (OFF_ST + CB * SP * 4 + 15) & ~15;          // bf16 image
-  static constexpr int OFF_TAB = OFF_XB + XB_BYTES;  // [mean | invstd | a | beta][CMAX] fp32
+  static constexpr int OFF_TAB = (OFF_XB + NPLX * XB_PLANE + 15) & ~15;  // [mean|invstd|a|beta][CMAX]
   static constexpr int OFF_SUM = OFF_TAB + 4 * CMAX * 4;  // [s | sn][CMAX] fp64
   static constexpr int LDS = OFF_SUM + 2 * CMAX * 8;
   static_assert(LDS <= 160 * 1024, "LDS budget");
@@ -140,17 +185,17 @@ struct SpBwdGeo {
 
 struct SpBwdParams {
   const float *dZ, *x, *mean, *invstd, *g, *b;
-  const __bf16 *wpk;   // [cb][chunk][k][octet][ci 32][8]
+  const __bf16 *wpk;   // [cb][chunk][k][plane][octet][ci 32][8]
   const __bf16 *aimg;  // [k][ks][plane][lane][8]
   float *dx, *dA;
   double *sd, *sdn;
   int C, R, T, ncb, nft, nitems, write_dx, relu;
 };
 
-template <int V, int K>
+template <int V, int K, bool X3>
 __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
-  using G = SpBwdGeo<V, K>;
-  constexpr int D = G::D;
+  using G = SpBwdGeo<V, K, X3>;
+  constexpr int D = G::D, NACC = G::NACC;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -162,7 +207,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
   const int NG = gridDim.x;
   const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(lds);
 
-  // ---- prologue: BN tables of all channels, zeroed sums, A image by LDS-DMA
+  // ---- prologue: BN tables of all channels, zeroed sums and zero row, A image
   float *tab = reinterpret_cast<float *>(lds + G::OFF_TAB);
   double *sums = reinterpret_cast<double *>(lds + G::OFF_SUM);
   for (int c = tid; c < P.C; c += 512) {
@@ -173,6 +218,10 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     tab[3 * G::CMAX + c] = P.b[c];
     sums[c] = 0.0;
     sums[G::CMAX + c] = 0.0;
+  }
+  for (int e = tid; e < G::NPLX * (G::XBP / 4); e += 512) {
+    const int p = e / (G::XBP / 4), q = e - p * (G::XBP / 4);
+    reinterpret_cast<unsigned *>(lds + G::OFF_XB + p * G::XB_PLANE + G::NPOS * G::XBP)[q] = 0u;
   }
   __syncthreads();  // (full drain: the table loads are ordinary loads)
   {
@@ -228,11 +277,13 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     }
   };
 
-  floatx16 T[K], S[K], dacc[K];
+  floatx16 T[K][NACC], S[K][NACC], dacc[K][NACC];
 #pragma unroll
   for (int k = 0; k < K; ++k)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dacc[k][i] = 0.f;
+    for (int a = 0; a < NACC; ++a)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dacc[k][a][i] = 0.f;
   float *st = reinterpret_cast<float *>(lds + G::OFF_ST);
   const float *xs = reinterpret_cast<const float *>(lds + G::OFF_X);
 
@@ -248,7 +299,9 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
 #pragma unroll
     for (int kk = 0; kk < K; ++kk)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) T[kk][i] = S[kk][i] = 0.f;
+      for (int a = 0; a < NACC; ++a)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) T[kk][a][i] = S[kk][a][i] = 0.f;
 
     // ---- H_k = W_k^T dZ in both orientations, 16 channels of dZ per chunk
     for (int c = 0; c < NCH; ++c, ++gch) {
@@ -261,9 +314,9 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       if (gch + D - 1 < nchunks) issue_chunk(gch + D - 1);
       const int slot = gch % D;
       if (STGCN_SPB_EXP & 1) continue;
-      // A operand: dZ[r = 8 hi + j][frame f, joint lo] rounded to bf16 (0 past V:
-      // read at a clamped joint, then selected, so the 8 reads issue back to back)
-      // (row 8 hi + j starts (8 hi + j) * TV mod 4 = j * TV mod 4 floats into its LDS row)
+      // A operand: dZ[r = 8 hi + j][frame f, joint lo] (0 past V: read at a
+      // clamped joint, then selected, so the 8 reads issue back to back); row
+      // 8 hi + j starts (8 hi + j) * TV mod 4 = j * TV mod 4 floats into its LDS row
       const float *rz = reinterpret_cast<const float *>(lds + G::OFF_RING + slot * G::RING_SLOT) +
                         8 * hi * G::RP + f * V + (lo < V ? lo : V - 1);
       float dv[8];
@@ -271,47 +324,72 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       for (int j = 0; j < 8; ++j) dv[j] = rz[j * G::RP + ((j * TV) & 3)];
 #pragma unroll
       for (int j = 0; j < 8; ++j) dv[j] = lo < V ? dv[j] : 0.f;
-      uint4 a;
-      a.x = spb_pk(dv[0], dv[1]);
-      a.y = spb_pk(dv[2], dv[3]);
-      a.z = spb_pk(dv[4], dv[5]);
-      a.w = spb_pk(dv[6], dv[7]);
       const char *wb = lds + G::OFF_W + slot * G::W_BYTES + hi * 512 + lo * 16;
+      if constexpr (!X3) {
+        uint4 a;  // dZ rounded to bf16
+        a.x = spb_pk(dv[0], dv[1]);
+        a.y = spb_pk(dv[2], dv[3]);
+        a.z = spb_pk(dv[4], dv[5]);
+        a.w = spb_pk(dv[6], dv[7]);
 #pragma unroll
-      for (int kk = 0; kk < K; ++kk) {
-        const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
-        T[kk] = spb_mfma(a, w, T[kk]);  // [v][ci] = sum_r dZ[r][v] W_k[r][ci]
-        S[kk] = spb_mfma(w, a, S[kk]);  // [ci][v]
+        for (int kk = 0; kk < K; ++kk) {
+          const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
+          T[kk][0] = spb_mfma(a, w, T[kk][0]);  // [v][ci] = sum_r dZ[r][v] W_k[r][ci]
+          S[kk][0] = spb_mfma(w, a, S[kk][0]);  // [ci][v]
+        }
+      } else {
+        uint4 a[3];
+        spb_planes<3>(dv, a);
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) {
+          uint4 w[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            w[p] = *reinterpret_cast<const uint4 *>(wb + (kk * 3 + p) * 1024);
+          spb_mfma6(a, w, T[kk]);
+          spb_mfma6(w, a, S[kk]);
+        }
       }
     }
 
     // ---- dx^T[w][ci] = sum_k sum_v A_k[v][w] H_k^T[v][ci] -> dx row image [ci][f*V + w]
     if (!(STGCN_SPB_EXP & 2)) {
-      floatx16 dxp[K];  // one chain per partition, summed at the end
+      floatx16 dxp[K][NACC];  // one chain per partition, summed at the end
 #pragma unroll
       for (int kk = 0; kk < K; ++kk)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dxp[kk][i] = 0.f;
+        for (int a = 0; a < NACC; ++a)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dxp[kk][a][i] = 0.f;
       const char *aim = lds + G::OFF_A + lane * 16;
 #pragma unroll
       for (int kk = 0; kk < K; ++kk)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          uint4 bh, bm;
-          spb_split(T[kk][8 * ks + 0], T[kk][8 * ks + 1], bh.x, bm.x);
-          spb_split(T[kk][8 * ks + 2], T[kk][8 * ks + 3], bh.y, bm.y);
-          spb_split(T[kk][8 * ks + 4], T[kk][8 * ks + 5], bh.z, bm.z);
-          spb_split(T[kk][8 * ks + 6], T[kk][8 * ks + 7], bh.w, bm.w);
-          const char *ab = aim + (kk * 2 + ks) * 2048;
-          const uint4 ah = *reinterpret_cast<const uint4 *>(ab);
-          const uint4 am = *reinterpret_cast<const uint4 *>(ab + 1024);
-          dxp[kk] = spb_mfma(ah, bh, dxp[kk]);
-          dxp[kk] = spb_mfma(am, bh, dxp[kk]);
-          dxp[kk] = spb_mfma(ah, bm, dxp[kk]);
-        }
-      floatx16 dxa = dxp[0];
+          float tv[8];
 #pragma unroll
-      for (int kk = 1; kk < K; ++kk) dxa += dxp[kk];
+          for (int j = 0; j < 8; ++j)
+            tv[j] = NACC == 2 ? T[kk][0][8 * ks + j] + T[kk][NACC - 1][8 * ks + j]
+                              : T[kk][0][8 * ks + j];
+          uint4 b[G::NPLA], am[G::NPLA];
+          spb_planes<G::NPLA>(tv, b);
+#pragma unroll
+          for (int p = 0; p < G::NPLA; ++p)
+            am[p] = *reinterpret_cast<const uint4 *>(aim + ((kk * 2 + ks) * G::NPLA + p) * 1024);
+          if constexpr (!X3) {
+            dxp[kk][0] = spb_mfma(am[0], b[0], dxp[kk][0]);
+            dxp[kk][0] = spb_mfma(am[1], b[0], dxp[kk][0]);
+            dxp[kk][0] = spb_mfma(am[0], b[1], dxp[kk][0]);
+          } else {
+            spb_mfma6(am, b, dxp[kk]);
+          }
+        }
+      floatx16 dxa = dxp[0][0];
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk)
+#pragma unroll
+        for (int a = 0; a < NACC; ++a)
+          if (kk || a) dxa += dxp[kk][a];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int w = (i & 3) + 8 * (i >> 2) + 4 * hi;
@@ -321,7 +399,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     spb_barrier();  // dx row image complete (the x slice landed with the item's chunk waits)
 
     // ---- row pass, 16 threads per channel: ReLU mask, BN1 sums, dx store, and
-    // f(BN1(x)) in bf16 into the dA operand image (row (frame, w), slot of ci)
+    // f(BN1(x)) into the dA operand image (row (frame, w), slot of ci; bf16 planes)
     if (!(STGCN_SPB_EXP & 4)) {
       const int ci = tid >> 4, part = tid & 15;
       const int c = cb * G::CB + ci;
@@ -354,9 +432,16 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
         sn = fmaf(d, (xq[q] - mu) * is, sn);
         if (P.write_dx && live) dst[pos] = d;
         if (pos < G::NPOS) {
-          const int fr = pos / V, w = pos - fr * V;
-          xbi[(fr * 32 + w) * (G::XBP / 2)] =
-              (__bf16)(live ? (P.relu ? fmaxf(bn, 0.f) : bn) : 0.f);
+          const float fx = live ? (P.relu ? fmaxf(bn, 0.f) : bn) : 0.f;
+          __bf16 *xr = xbi + pos * (G::XBP / 2);  // row (frame, w) = pos
+          const __bf16 h = (__bf16)fx;
+          xr[0] = h;
+          if constexpr (X3) {
+            const float r1 = fx - (float)h;
+            const __bf16 m = (__bf16)r1;
+            xr[G::XB_PLANE / 2] = m;
+            xr[G::XB_PLANE] = (__bf16)(r1 - (float)m);
+          }
         }
       }
       double ds = s, dn = sn;
@@ -375,21 +460,31 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
 
     // ---- dA_k[v][w] += sum_ci H_k[ci][v] f(BN1(x))[ci][w] (this frame's 32 channels)
     if (!(STGCN_SPB_EXP & 8)) {
-      const char *xb = lds + G::OFF_XB + (f * 32 + lo) * G::XBP + hi * 16;
-      const uint4 x0 = *reinterpret_cast<const uint4 *>(xb);
-      const uint4 x1 = *reinterpret_cast<const uint4 *>(xb + 32);
+      const int row = lo < V ? f * V + lo : G::NPOS;  // joints past V: the zero row
+      const char *xb = lds + G::OFF_XB + row * G::XBP + hi * 16;
 #pragma unroll
-      for (int kk = 0; kk < K; ++kk) {
+      for (int ks = 0; ks < 2; ++ks) {
+        uint4 xv[G::NPLX];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          uint4 sh, sm;
-          spb_split(S[kk][8 * ks + 0], S[kk][8 * ks + 1], sh.x, sm.x);
-          spb_split(S[kk][8 * ks + 2], S[kk][8 * ks + 3], sh.y, sm.y);
-          spb_split(S[kk][8 * ks + 4], S[kk][8 * ks + 5], sh.z, sm.z);
-          spb_split(S[kk][8 * ks + 6], S[kk][8 * ks + 7], sh.w, sm.w);
-          const uint4 xv = ks ? x1 : x0;
-          dacc[kk] = spb_mfma(sh, xv, dacc[kk]);
-          dacc[kk] = spb_mfma(sm, xv, dacc[kk]);
+        for (int p = 0; p < G::NPLX; ++p)
+          xv[p] = *reinterpret_cast<const uint4 *>(xb + p * G::XB_PLANE + ks * 32);
+#pragma unroll
+        for (int kk = 0; kk < K; ++kk) {
+          float sv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            sv[j] = NACC == 2 ? S[kk][0][8 * ks + j] + S[kk][NACC - 1][8 * ks + j]
+                              : S[kk][0][8 * ks + j];
+          if constexpr (!X3) {
+            uint4 sp[2];
+            spb_planes<2>(sv, sp);
+            dacc[kk][0] = spb_mfma(sp[0], xv[0], dacc[kk][0]);
+            dacc[kk][0] = spb_mfma(sp[1], xv[0], dacc[kk][0]);
+          } else {
+            uint4 sp[3];
+            spb_planes<3>(sv, sp);
+            spb_mfma6(sp, xv, dacc[kk]);
+          }
         }
       }
     }
@@ -407,7 +502,8 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int v = (i & 3) + 8 * (i >> 2) + 4 * hi;
-      if (v < V && lo < V) atomicAdd(dred + (kk * V + v) * V + lo, dacc[kk][i]);
+      const float val = NACC == 2 ? dacc[kk][0][i] + dacc[kk][NACC - 1][i] : dacc[kk][0][i];
+      if (v < V && lo < V) atomicAdd(dred + (kk * V + v) * V + lo, val);
     }
   __syncthreads();
   if (myitems > 0) {
@@ -419,9 +515,10 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
   }
 }
 
-// W (K*R, C) -> [cb][chunk][k][octet][ci 32][8] bf16 (16 channels of R per chunk)
-__global__ void k_pack_spb_w(const float *W, __bf16 *wpk, int K, int R, int C) {
-  const int64_t total = (int64_t)K * R * C;
+// W (K*R, C) -> [cb][chunk][k][plane][octet][ci 32][8] bf16 (16 channels of R per
+// chunk; planes: bf16 rounding (NP = 1) or the exact h, m, l split (NP = 3))
+__global__ void k_pack_spb_w(const float *W, __bf16 *wpk, int K, int R, int C, int NP) {
+  const int64_t total = (int64_t)K * R * C * NP;
   const int nch = R / 16;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -432,64 +529,94 @@ __global__ void k_pack_spb_w(const float *W, __bf16 *wpk, int K, int R, int C) {
     r /= 32;
     const int o = (int)(r % 2);
     r /= 2;
+    const int p = (int)(r % NP);
+    r /= NP;
     const int k = (int)(r % K);
     r /= K;
     const int c = (int)(r % nch);
     const int cb = (int)(r / nch);
     const int rr = c * 16 + 8 * o + jj;
-    wpk[e] = (__bf16)W[((int64_t)k * R + rr) * C + cb * 32 + ci];
+    const float w = W[((int64_t)k * R + rr) * C + cb * 32 + ci];
+    const __bf16 h = (__bf16)w;
+    const float r1 = w - (float)h;
+    const __bf16 m = (__bf16)r1;
+    wpk[e] = p == 0 ? h : (p == 1 ? m : (__bf16)(r1 - (float)m));
   }
 }
 
-// A (K, V, V) -> the dx A-operand image [k][ks][plane h, m][lane][8]:
+// A (K, V, V) -> the dx A-operand image [k][ks][plane h, m(, l)][lane][8]:
 // lane (lo, hi), j -> A_k[v = 16 ks + (j & 3) + 8 (j >> 2) + 4 hi][w = lo]
-__global__ void k_pack_spb_a(const float *A, __bf16 *img, int K, int V) {
-  const int total = K * 2 * 2 * 512;
+__global__ void k_pack_spb_a(const float *A, __bf16 *img, int K, int V, int NP) {
+  const int total = K * 2 * NP * 512;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     int r = e;
     const int j = r % 8;
     r /= 8;
     const int lane = r % 64;
     r /= 64;
-    const int plane = r % 2;
-    r /= 2;
+    const int plane = r % NP;
+    r /= NP;
     const int ks = r % 2;
     const int k = r / 2;
     const int lo = lane & 31, hi = lane >> 5;
     const int v = 16 * ks + (j & 3) + 8 * (j >> 2) + 4 * hi, w = lo;
     const float a = (v < V && w < V) ? A[((int64_t)k * V + v) * V + w] : 0.f;
     const __bf16 h = (__bf16)a;
-    img[e] = plane == 0 ? h : (__bf16)(a - (float)h);
+    const float r1 = a - (float)h;
+    const __bf16 m = (__bf16)r1;
+    img[e] = plane == 0 ? h : (plane == 1 ? m : (__bf16)(r1 - (float)m));
   }
 }
 
-bool sp_bwd_fused_supported(int C, int V, int K, int R, int T) {
-  using G = SpBwdGeo<25, 3>;
-  return V == 25 && K == 3 && C > 0 && C % 32 == 0 && C <= G::CMAX && R % 16 == 0 &&
-         R / 16 >= G::D &&
+// instantiated shapes: the NTU graph with spatial partitioning on the bf16 path
+// (BASELINE cfg3) and the Kinetics graph, uniform partition, on the fp32 split
+// path (cfg2)
+// The fp32 split variant is compiled but not selected: at K = 1 the H tensor is
+// only C_in channels and the unfused pair (fp32-MFMA H GEMM at 3.5 TB/s +
+// k_spatial_bwd5) is faster (cfg2 L1 281 vs 351 us, L8 421 vs 781 us; the
+// twelve split MFMAs per 16-channel chunk serialise behind each chunk's wait);
+// STGCN_SPB_X3 selects it (A/B only).
+bool sp_bwd_fused_supported(int C, int V, int K, int R, int T, bool x3) {
+  constexpr int D = SpBwdGeo<25, 3, false>::D, CMAX = SpBwdGeo<25, 3, false>::CMAX;
+  static const bool x3_on = getenv("STGCN_SPB_X3") != nullptr;
+  const bool shape = x3 ? (x3_on && V == 18 && K == 1) : (V == 25 && K == 3);
+  return shape && C > 0 && C % 32 == 0 && C <= CMAX && R % 16 == 0 && R / 16 >= D &&
          (int64_t)std::max(R, C) * T * V * 4 < ((int64_t)1 << 31);
 }
 
-static constexpr size_t kSpbAimgBytes = 3 * 2 * 2 * 1024;
+static constexpr size_t kSpbAimgBytes = 3 * 2 * 3 * 1024;
 
 size_t sp_bwd_fused_wpk_bytes(int C, int R, int K, int V) {
   (void)V;
-  return kSpbAimgBytes + (size_t)K * R * C * 2 + 256;
+  return kSpbAimgBytes + (size_t)K * R * C * 2 * 3 + 256;
+}
+
+template <int V, int K, bool X3>
+static hipError_t launch_spb(const SpBwdParams &P0, hipStream_t s) {
+  using G = SpBwdGeo<V, K, X3>;
+  SpBwdParams P = P0;
+  P.nft = (P.T + G::FT - 1) / G::FT;
+  const int64_t items = (int64_t)P.ncb * P.nft * P.nitems;  // (nitems: N on entry)
+  if (items >= (int64_t)1 << 31) return hipErrorInvalidValue;
+  P.nitems = (int)items;
+  const int grid = (int)std::min<int64_t>(items, 256);
+  hipLaunchKernelGGL((k_sp_bwd_fused<V, K, X3>), dim3(grid), dim3(512), G::LDS, s, P);
+  return hipGetLastError();
 }
 
 hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mean,
                                const float *invstd, const float *g, const float *b,
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
-                               int write_dx, int relu, hipStream_t s) {
-  if (!sp_bwd_fused_supported(C, V, K, R, T)) return hipErrorInvalidValue;
-  using G = SpBwdGeo<25, 3>;
+                               int write_dx, int relu, bool x3, hipStream_t s) {
+  if (!sp_bwd_fused_supported(C, V, K, R, T, x3)) return hipErrorInvalidValue;
+  const int npw = x3 ? 3 : 1, npa = x3 ? 3 : 2;
   __bf16 *aimg = reinterpret_cast<__bf16 *>(wpk);
   __bf16 *wp = aimg + kSpbAimgBytes / 2;
-  hipLaunchKernelGGL(k_pack_spb_a, dim3(24), dim3(256), 0, s, A, aimg, K, V);
-  const int64_t nw = (int64_t)K * R * C;
+  hipLaunchKernelGGL(k_pack_spb_a, dim3(24), dim3(256), 0, s, A, aimg, K, V, npa);
+  const int64_t nw = (int64_t)K * R * C * npw;
   hipLaunchKernelGGL(k_pack_spb_w, dim3((unsigned)std::min<int64_t>((nw + 255) / 256, 1024)),
-                     dim3(256), 0, s, W, wp, K, R, C);
+                     dim3(256), 0, s, W, wp, K, R, C, npw);
   SpBwdParams P{};
   P.dZ = dZ;
   P.x = x;
@@ -507,15 +634,11 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
   P.R = R;
   P.T = T;
   P.ncb = C / 32;
-  P.nft = (T + G::FT - 1) / G::FT;
-  const int64_t items = (int64_t)N * P.nft * P.ncb;
-  if (items >= (int64_t)1 << 31) return hipErrorInvalidValue;
-  P.nitems = (int)items;
+  P.nitems = N;
   P.write_dx = write_dx;
   P.relu = relu;
-  const int grid = (int)std::min<int64_t>(items, 256);
-  hipLaunchKernelGGL((k_sp_bwd_fused<25, 3>), dim3(grid), dim3(512), G::LDS, s, P);
-  return hipGetLastError();
+  if (x3) return launch_spb<18, 1, true>(P, s);
+  return launch_spb<25, 3, false>(P, s);
 }
 
 }  // namespace stgcn
