@@ -113,7 +113,8 @@ def stack_layers(cfg):
     return out
 
 
-KERNEL_KINDS = {0: "tconv_fwd", 1: "tconv_dgrad", 2: "tconv_wgrad", 3: "spatial_gemm"}
+KERNEL_KINDS = {0: "tconv_fwd", 1: "tconv_dgrad", 2: "tconv_wgrad", 3: "spatial_gemm",
+                4: "spatial_bwd"}
 
 
 def kernel_roofline(pkg, device, cfg, iters=10):
@@ -151,10 +152,18 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                    2: N * (co * to + co * t) * V4,
                    3: N * (ci * t + co * t) * V4 + (N * cfg["K"] * ci * t * cfg["V"] * 2
                                                  if cfg["bf16"] and ci >= 16 else
-                                                 N * cfg["K"] * ci * t * V4)}[which]
+                                                 N * cfg["K"] * ci * t * V4),
+                   4: N * (co * t + 2 * ci * t) * V4}[which]  # dZ, x in; dx out
             add(kinds, kind, ms.value, fl.value, 1, act)
             V, K = cfg["V"], cfg["K"]
             # rocprof short names of the kernel each timing runs
+            if which == 4:
+                # the fused spatial backward (bf16, V = 25, K = 3); the unfused
+                # H GEMM + joint kernel pair is two kernels: kind only
+                if cfg["bf16"] and V == 25 and K == 3 and ci % 32 == 0 and co % 16 == 0 \
+                        and co >= 64:
+                    add(symbols, "k_sp_bwd_fused<25,3,false>", ms.value, fl.value, 1, act)
+                continue
             if cfg["bf16"]:
                 # temporal GEMMs: k_conv_x3 with one operand plane (NPL = 1)
                 sym = {0: f"k_conv_x3<9,3,{V},{s},1,1>",

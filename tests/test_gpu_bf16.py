@@ -172,6 +172,12 @@ def test_bf16_first_block_without_dx(pkg):
     _check_bf16(pkg, (3, 64, 1, 25, 3, 2, 30), need_dx=False)
 
 
+def test_bf16_fused_spatial_backward_without_dx(pkg):
+    """k_sp_bwd_fused (V = 25, K = 3, C_in % 32 == 0) with write_dx = 0: dA and
+    the BN1 sums only, odd T * V (per-row DMA shifts) and a ragged frame tile."""
+    _check_bf16(pkg, (64, 64, 1, 25, 3, 2, 29), need_dx=False)
+
+
 def test_bf16_full_size_block(pkg):
     """cfg3 layer-1 shape (V=25, K=3, T=300) at N=16."""
     errs = _check_bf16(pkg, (64, 64, 1, 25, 3, 16, 300), seed=7)
