@@ -274,6 +274,35 @@ void conv_tiles(ConvGemmParams &p) {
   p.n_rtiles = (p.R + kTileRows - 1) / kTileRows;
 }
 
+// Activations stored in bf16 on the bf16 path's non-residual blocks: Z (the
+// SpatialConv output) and dU (the gradient at the temporal conv output). Every
+// reader of them rounds them to bf16 anyway -- Z: the temporal conv forward
+// (k_conv_x3 one-plane) and the weight gradient's Q (k_wgrad_bf16); dU: the
+// data gradient (k_conv_x3 one-plane, stride-2 phases included) and the weight
+// gradient's P -- so the results are bit-identical to fp32 storage and half
+// the bytes move; the bias / BN gradients use the fp32 sums of the producing
+// passes. The tensors keep their fp32-sized buffers (the first half holds the
+// bf16 data). Producers: the fused spatial forward's epilogues (so C_in >= 16)
+// and the BN2 + ReLU backward pass. (STGCN_ACT_FP32: fp32 storage, A/B only)
+bool act_bf16(const stgcn_desc_t *d) {
+  static const bool off =
+      getenv("STGCN_ACT_FP32") != nullptr || getenv("STGCN_GENERIC_CONV") != nullptr;
+  // Stride-2 blocks keep fp32: their weight gradient (k_wgrad_bf16<9,V,2>) staged
+  // bf16 pairs slower than fp32 (cfg5 2.19 -> 2.66 ms per step), more than the
+  // strided forward and data-gradient phases gained.
+  if (off || !fused_sp(d) || residual(d) || d->stride != 1) return false;
+  ConvGemmParams p = conv_base(d, nullptr);  // the temporal conv forward and data gradient
+  p.C = d->C_out;
+  p.R = d->C_out;
+  p.NQ = 9;
+  p.s_in = 1;
+  if (!conv_b1_supported(p)) return false;
+  WgradParams w = make_wgrad_taps(d, nullptr, nullptr, nullptr);
+  return w.bf16 == 1;
+}
+bool z_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
+bool du_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
+
 }  // namespace
 
 // Every GEMM launch of the block fits its LDS budget.
@@ -464,7 +493,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     // bf16 path: BN1 + joint contraction + W' GEMM in one kernel; G kept in bf16
     // for the backward when the caller asks (stgcn_keep_g_bytes)
     HIP_TRY(launch_sp_fwd_bf16(a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.biasZ, L.wpk,
-                               a->Z, reinterpret_cast<__bf16 *>(a->G),
+                               a->Z, z_bf16(d) ? 1 : 0, reinterpret_cast<__bf16 *>(a->G),
                                (res && d->training) ? L.s2 : nullptr,
                                (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s));
   } else {
@@ -505,6 +534,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = a->Z;
+    p.in_bf16 = z_bf16(d) ? 1 : 0;
     p.w = a->Wt;
     p.out = a->U;
     p.bias_r = a->bWt;
@@ -579,7 +609,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                                         L.sg, L.sgu, drop, s));
     }
     HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
-                                     L.sdu, N, R, To * V, d->training, drop, s));
+                                     L.sdu, N, R, To * V, d->training, drop, s,
+                                     du_bf16(d) ? 1 : 0));
     HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
     // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
@@ -594,6 +625,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.dU;
+    p.in_bf16 = du_bf16(d) ? 1 : 0;
     p.out = L.dZ;
     p.in_bstride = (int64_t)R * To * V;
     p.out_bstride = (int64_t)R * T * V;
@@ -632,6 +664,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   // Temporal conv weight-gradient: dWt[co][ci][q] = sum dU[co] * Z[ci](shifted)
   {
     WgradParams w = make_wgrad_taps(d, L.dU, res ? a->Za : a->Z, L.slab);
+    w.q_bf16 = z_bf16(d) ? 1 : 0;
+    w.p_bf16 = du_bf16(d) ? 1 : 0;
     HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * R * 9, a->dWt, 0, R, 1, R, s));
   }
@@ -834,12 +868,14 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     p.M = To;
     p.T_src = T;
     p.T_dst = To;
+    p.in_bf16 = z_bf16(d) ? 1 : 0;
     conv_tiles(p);
     P.cp[P.ncp++] = p;
     P.flops = tflops;
   } else if (which == 1) {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * R * To * V);
+    p.in_bf16 = du_bf16(d) ? 1 : 0;
     const float *w = c.take<float>((size_t)R * R * 9);
     p.out = c.take<float>((size_t)N * R * T * V);
     p.in_bstride = (int64_t)R * To * V;
@@ -879,6 +915,8 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     const float *dU = c.take<float>((size_t)N * R * To * V);
     const float *Z = c.take<float>((size_t)N * R * T * V);
     WgradParams w = make_wgrad_taps(d, dU, Z, nullptr);
+    w.q_bf16 = z_bf16(d) ? 1 : 0;
+    w.p_bf16 = du_bf16(d) ? 1 : 0;
     w.slab = c.take<float>((size_t)w.S * R * R * 9);
     P.wp = w;
     P.wgrad = true;
@@ -994,7 +1032,7 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
     if (P.spf) {
       const int C = d->C_in;
       return launch_sp_fwd_bf16(P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A, P.W,
-                                P.biasZ, P.wpk, P.Z, P.Gk, nullptr, nullptr, d->N, C, d->C_out,
+                                P.biasZ, P.wpk, P.Z, z_bf16(d) ? 1 : 0, P.Gk, nullptr, nullptr, d->N, C, d->C_out,
                                 d->T, d->V, d->K, residual(d) ? 1 : 0, s);
     }
     for (int i = 0; i < P.ncp; ++i) {

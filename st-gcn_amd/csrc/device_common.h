@@ -88,7 +88,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // per-row BN statistics (fp64). smem: >= 2 KiB of LDS no wave reads any more
 // (BV_LDS: + 64*V floats; the tile's rows of the bias table bias_rv are staged
 // there by coalesced loads instead of one scattered load per element).
-template <int V, int NCOLS, bool BV_LDS = false>
+// OB: the kernel may write a bf16 output (p.out_bf16 read at run time; kept a
+// template switch so the fp32-only kernels' epilogue code is unchanged)
+template <int V, int NCOLS, bool BV_LDS = false, bool OB = false>
 __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
                                                    int n, int r0, int m0, float *smem) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -99,7 +101,13 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
   // loads/stores with 32-bit offsets; masked elements get offset kOOB (loads
   // return 0, stores are dropped), so there is no per-element branch.
   const int ostride = p.T_dst * V;
-  const __amdgpu_buffer_rsrc_t rs_o = make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
+  // (out_bf16: a resource over the bf16 tensor, byte offsets halved at the store)
+  const bool ob = OB && p.out_bf16;
+  const __amdgpu_buffer_rsrc_t rs_o =
+      ob ? make_rsrc(reinterpret_cast<const float *>(reinterpret_cast<const __bf16 *>(p.out) +
+                                                     (int64_t)n * p.out_bstride),
+                     (p.out_bstride + 1) / 2)
+         : make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
   const __amdgpu_buffer_rsrc_t rs_b = make_rsrc(p.bias_r ? p.bias_r : p.out, p.bias_r ? p.R : 0);
   const __amdgpu_buffer_rsrc_t rs_bv =
       make_rsrc(p.bias_rv ? p.bias_rv : p.out, p.bias_rv ? (int64_t)p.R * V : 0);
@@ -163,7 +171,12 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
             val = dropout_keep(p.drop, (uint64_t)n * p.out_bstride + row * ostride + ocol[j])
                       ? val * p.drop.scale
                       : 0.f;
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o, off, 0, 0);
+          if (ob)
+            __builtin_amdgcn_raw_buffer_store_b16(
+                __builtin_bit_cast(unsigned short, (__bf16)val), rs_o,
+                ok ? (row * ostride + ocol[j]) * 2 : (int)kOOB, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o, off, 0, 0);
           if constexpr (STATS) {
             const double dv = ok ? (double)val : 0.0;
             s += dv;
@@ -234,7 +247,7 @@ __device__ __forceinline__ void acc_to_img(float *img, const floatx16 &a, int ro
     img[(row0 + (i & 3) + 8 * (i >> 2) + 4 * hi) * kEpiPitch + col0 + lo] = a[i];
 }
 
-template <int V, int NCOLS, int NT, int ROWS = 64>
+template <int V, int NCOLS, int NT, int ROWS = 64, bool OB = false>
 __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, const float *img,
                                                      float *sbv, int n, int r0, int m0) {
   constexpr int TPR = NT / ROWS;
@@ -297,7 +310,23 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
         sq += (double)val * (double)val;
       }
     }
-    if (full && vec == 4) {
+    if (OB && p.out_bf16) {  // bf16 output: 8-byte pieces where the row allows
+      __bf16 *ob = reinterpret_cast<__bf16 *>(p.out) + obase;
+      const unsigned w0 = __builtin_bit_cast(unsigned short, (__bf16)v[0]) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[1]) << 16);
+      const unsigned w1 = __builtin_bit_cast(unsigned short, (__bf16)v[2]) |
+                          ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[3]) << 16);
+      if (full && vec == 4) {
+        *reinterpret_cast<uint2 *>(ob + c0) = make_uint2(w0, w1);
+      } else if (full && vec == 2) {
+        *reinterpret_cast<unsigned *>(ob + c0) = w0;
+        *reinterpret_cast<unsigned *>(ob + c0 + 2) = w1;
+      } else if (rok) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c0 + e < ncv) ob[c0 + e] = (__bf16)v[e];
+      }
+    } else if (full && vec == 4) {
       *reinterpret_cast<float4 *>(out + c0) = make_float4(v[0], v[1], v[2], v[3]);
     } else if (full && vec == 2) {
       *reinterpret_cast<float2 *>(out + c0) = make_float2(v[0], v[1]);

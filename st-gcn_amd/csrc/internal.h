@@ -57,6 +57,9 @@ struct ConvGemmParams {
   int bf16;          // 1: operands rounded to bf16 on v_mfma_f32_32x32x16_bf16 (fp32
                      // accumulate, fp32 in/out), where k_conv_bf16 covers the shape;
                      // 3: fp32 GEMM as exact 3-way bf16 splits (k_conv_x3) where covered
+  int in_bf16;       // in[] holds bf16 (same element strides; k_conv_x3 one-plane only)
+  int out_bf16;      // out[] is written as bf16 (same element strides; the shared
+                     // epilogues; no residual input)
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -74,6 +77,7 @@ struct WgradParams {
   int CT;  // k_wgrad_sp (NQ = 1): output columns per workgroup (64 or 128)
   int bf16;  // set by plan_wgrad_bf16: run k_wgrad_bf16 (bf16 operands, fp32 accumulate);
              // 3: set by plan_wgrad_x3 (fp32 via exact bf16 splits, k_wgrad_x3)
+  int p_bf16, q_bf16;  // P / Q hold bf16 (same element strides; k_wgrad_bf16 only)
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
@@ -146,7 +150,7 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU,
                                     double *sdu, int N, int C, int L, int training,
-                                    Dropout drop, hipStream_t s);
+                                    Dropout drop, hipStream_t s, int du_bf16 = 0);
 hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
                                float *dgamma, float *dbeta, float *dbias, hipStream_t s);
 // add (same layout as dx, or null) is added after the BN1 backward (residual path)
@@ -192,7 +196,8 @@ size_t sp_fwd_bf16_wpk_bytes(int C, int R, int K, int V);  // packed W' + A imag
 size_t sp_keep_g_bytes(int N, int C, int T, int V, int K);
 hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,
                               const float *g, const float *b, const float *A, const float *W,
-                              const float *biasZ, void *wpk, float *Z, __bf16 *Gk, double *ssum,
+                              const float *biasZ, void *wpk, float *Z, int z_bf16, __bf16 *Gk,
+                              double *ssum,
                               double *ssq, int N, int C, int R, int T, int V, int K, int relu,
                               hipStream_t s);
 // dW' = dZ Gk^T from the kept bf16 G (P = dZ fp32, Q = Gk, C = K*C_in).

@@ -1451,7 +1451,7 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
     const float *dy, const float *U, const float *mean, const float *invstd, const float *g,
     const float *b, const double *sg, const double *sgu, float *dU, double *sdu, int C, int L,
-    double invM, Dropout drop) {
+    double invM, Dropout drop, int du_bf16) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
@@ -1474,7 +1474,21 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
       o[j] = a * (gg - mg - uh * mgu);
       s += o[j];
     }
-    vst<VEC>(dU + base + i, o);
+    if (du_bf16) {  // dU stored in bf16 (its readers round it to bf16 anyway)
+      __bf16 *ob = reinterpret_cast<__bf16 *>(dU) + base + i;
+      unsigned short h[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) h[j] = __builtin_bit_cast(unsigned short, (__bf16)o[j]);
+      if constexpr (VEC == 4)
+        *reinterpret_cast<uint2 *>(ob) = make_uint2(h[0] | ((unsigned)h[1] << 16),
+                                                    h[2] | ((unsigned)h[3] << 16));
+      else if constexpr (VEC == 2)
+        *reinterpret_cast<unsigned *>(ob) = h[0] | ((unsigned)h[1] << 16);
+      else
+        *reinterpret_cast<unsigned short *>(ob) = h[0];
+    } else {
+      vst<VEC>(dU + base + i, o);
+    }
   }
   block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
 }
@@ -1483,11 +1497,11 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU, double *sdu,
                                     int N, int C, int L, int training, Dropout drop,
-                                    hipStream_t s) {
+                                    hipStream_t s, int du_bf16) {
   // eval mode (constant running statistics): no batch-mean terms
   const double invM = training ? 1.0 / ((double)N * L) : 0.0;
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_apply, slice_vec(L, {dy, U, dU}), dim3(C, N), dy, U, mean,
-                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop);
+                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop, du_bf16);
   return hipGetLastError();
 }
 

@@ -40,6 +40,25 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {
   return __builtin_bit_cast(unsigned, v);
 }
 
+// 4 consecutive bf16 elements starting at element e (stored as bf16; byte offset
+// base = 2 e, or kOOB) as two packed dwords: dword loads from the even element at
+// or below e, shifted by 16 bits when e is odd (odd V only: then a third dword)
+template <bool ODD_POSSIBLE>
+__device__ __forceinline__ void ld_b16x4(__amdgpu_buffer_rsrc_t rs, unsigned base, unsigned &x,
+                                         unsigned &y) {
+  const unsigned b = base == kOOB ? kOOB : (base & ~3u);
+  const unsigned d0 = __builtin_amdgcn_raw_buffer_load_b32(rs, b, 0, 0);
+  const unsigned d1 = __builtin_amdgcn_raw_buffer_load_b32(rs, b == kOOB ? kOOB : b + 4u, 0, 0);
+  if constexpr (ODD_POSSIBLE) {
+    const unsigned d2 = __builtin_amdgcn_raw_buffer_load_b32(rs, b == kOOB ? kOOB : b + 8u, 0, 0);
+    const bool odd = base != kOOB && (base & 2u);
+    x = odd ? __builtin_amdgcn_alignbit(d1, d0, 16) : d0;
+    y = odd ? __builtin_amdgcn_alignbit(d2, d1, 16) : d1;
+  } else {
+    x = d0;
+    y = d1;
+  }
+}
 __device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t rs, unsigned voff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, 0, 0));
 }
@@ -331,7 +350,9 @@ struct WgBf16Geo {
   static_assert(RSP >= 1 && RSQ >= 1, "a row of position groups fits the workgroup");
 };
 
-template <int NQ, int V, int SIN, int FT, int CB>
+// BI: P and Q are stored in bf16 (p.p_bf16 == p.q_bf16 == 1; a template switch so
+// the staging stays branch-free)
+template <int NQ, int V, int SIN, int FT, int CB, bool BI = false>
 __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgrad_bf16(WgradParams p) {
   using G = WgBf16Geo<NQ, V, SIN, FT, CB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -374,8 +395,15 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
   auto item_ref = [&](int item) {
     ItemRef ir;
     const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * FT;
-    ir.rp = make_rsrc(p.P + (int64_t)n * p.p_bstride, p.p_bstride);
-    ir.rq = make_rsrc(p.Q + (int64_t)n * p.q_bstride, p.q_bstride);
+    // (p_bf16 / q_bf16: the operand is stored in bf16; resources over its bytes)
+    ir.rp = BI ? make_rsrc(reinterpret_cast<const float *>(
+                                     reinterpret_cast<const __bf16 *>(p.P) + (int64_t)n * p.p_bstride),
+                                 (p.p_bstride + 1) / 2)
+                     : make_rsrc(p.P + (int64_t)n * p.p_bstride, p.p_bstride);
+    ir.rq = BI ? make_rsrc(reinterpret_cast<const float *>(
+                                     reinterpret_cast<const __bf16 *>(p.Q) + (int64_t)n * p.q_bstride),
+                                 (p.q_bstride + 1) / 2)
+                     : make_rsrc(p.Q + (int64_t)n * p.q_bstride, p.q_bstride);
     ir.fok = prow < G::RSP && m0 + pf < p.M;
     const int t = SIN * m0 + p.off + qf;
     ir.tok = qrow < G::RSQ && t >= 0 && t < p.T_src;
@@ -392,17 +420,34 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
       if (k < G::NPP) {
         const int r = r0 + prow + k * G::RSP;
         const bool ok = ir.fok && prow + k * G::RSP < 64 && r < p.R;
-        const unsigned base = ok ? (unsigned)(r * MV + ir.pbase) * 4u : kOOB;
+        const unsigned base = ok ? (unsigned)(r * MV + ir.pbase) * (BI ? 2u : 4u) : kOOB;
+        if constexpr (BI) {  // packed pairs in st[i][0..1]; pad joints (>= V) zeroed
+          unsigned x, y;
+          ld_b16x4<V % 2 == 1>(ir.rp, base, x, y);
+          if (pv + 1 >= V) x &= 0xffffu;
+          if (pv + 2 >= V) y = 0u;
+          else if (pv + 3 >= V) y &= 0xffffu;
+          st[i][0] = __builtin_bit_cast(float, x);
+          st[i][1] = __builtin_bit_cast(float, y);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          st[i][j] = (pv + j < V) ? ld_f32(ir.rp, base + 4u * j) : 0.f;  // pad joints: 0
+          for (int j = 0; j < 4; ++j)
+            st[i][j] = (pv + j < V) ? ld_f32(ir.rp, base + 4u * j) : 0.f;  // pad joints: 0
+        }
       } else if (k < G::NPP + G::NPQ) {
         const int kq = k - G::NPP;
         const int c = c0 + qrow + kq * G::RSQ;
         const bool ok = ir.tok && qrow + kq * G::RSQ < CB && c < p.C;
-        const unsigned base = ok ? (unsigned)(c * TV + ir.qbase) * 4u : kOOB;
+        const unsigned base = ok ? (unsigned)(c * TV + ir.qbase) * (BI ? 2u : 4u) : kOOB;
+        if constexpr (BI) {
+          unsigned x, y;
+          ld_b16x4<V % 2 == 1>(ir.rq, base, x, y);
+          st[i][0] = __builtin_bit_cast(float, x);
+          st[i][1] = __builtin_bit_cast(float, y);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) st[i][j] = ld_f32(ir.rq, base + 4u * j);
+          for (int j = 0; j < 4; ++j) st[i][j] = ld_f32(ir.rq, base + 4u * j);
+        }
       }
     }
   };
@@ -412,8 +457,13 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
     for (int i = 0; i < G::PPART; ++i) {
       const int k = PART * G::PPART + i;
       uint2 v;
-      v.x = pk_bf16(st[i][0], st[i][1]);
-      v.y = pk_bf16(st[i][2], st[i][3]);
+      if constexpr (BI) {  // already packed bf16 pairs
+        v.x = __builtin_bit_cast(unsigned, st[i][0]);
+        v.y = __builtin_bit_cast(unsigned, st[i][1]);
+      } else {
+        v.x = pk_bf16(st[i][0], st[i][1]);
+        v.y = pk_bf16(st[i][2], st[i][3]);
+      }
       if (k < G::NPP) {
         if (prow < G::RSP && prow + k * G::RSP < 64)
           *reinterpret_cast<uint2 *>(buf + ((prow + k * G::RSP) * G::PPITCH + pf * G::Vp + pv) * 2) = v;
@@ -706,6 +756,14 @@ static bool launch_wb_if(const WgradParams &p, hipStream_t s) {
   if (p.V != V || p.s_in != SIN || p.FT != FT) return false;
   using G = WgBf16Geo<NQ, V, SIN, FT, CB>;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+  if constexpr (NQ == 9) {  // (bf16 P and Q: the temporal weight gradient only)
+    if (p.p_bf16 && p.q_bf16) {
+      hipLaunchKernelGGL((k_wgrad_bf16<NQ, V, SIN, FT, CB, true>), dim3(nblk), dim3(G::NTH),
+                         2 * G::BUF, s, p);
+      return true;
+    }
+  }
+  if (p.p_bf16 || p.q_bf16) return false;
   hipLaunchKernelGGL((k_wgrad_bf16<NQ, V, SIN, FT, CB>), dim3(nblk), dim3(G::NTH), 2 * G::BUF, s,
                      p);
   return true;

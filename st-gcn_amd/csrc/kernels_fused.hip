@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void k_sp_fwd_bf16(SpFwdParams P) {
     }
   }
   __syncthreads();  // every wave is done with the images (the epilogue reuses LDS)
-  conv_tile_epilogue<V, G::NCOLS, true>(p, acc, n, r0, m0, smem);
+  conv_tile_epilogue<V, G::NCOLS, true, true>(p, acc, n, r0, m0, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -616,7 +616,10 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
     // launcher keeps residual blocks, whose BN2 statistics come from here, at
     // ROWS <= 128). Lanes = consecutive positions: 128-byte row pieces.
     const __amdgpu_buffer_rsrc_t rs_o =
-        make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
+        p.out_bf16 ? make_rsrc(reinterpret_cast<const float *>(reinterpret_cast<const __bf16 *>(p.out) +
+                                                               (int64_t)n * p.out_bstride),
+                               (p.out_bstride + 1) / 2)
+                   : make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
     const __amdgpu_buffer_rsrc_t rs_bv = make_rsrc(p.bias_rv, (int64_t)p.R * V);
     const int ostride = p.T_dst * V;
 #pragma unroll
@@ -633,9 +636,14 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
           const float bv = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(rs_bv, ok ? (row * V + v) * 4 : (int)kOOB,
                                                           0, 0));
-          __builtin_amdgcn_raw_buffer_store_b32(
-              __builtin_bit_cast(unsigned, acc[rb][j][i] + bv), rs_o,
-              ok ? (row * ostride + m0 * V + col) * 4 : (int)kOOB, 0, 0);
+          const int e = row * ostride + m0 * V + col;
+          if (p.out_bf16)
+            __builtin_amdgcn_raw_buffer_store_b16(
+                __builtin_bit_cast(unsigned short, (__bf16)(acc[rb][j][i] + bv)), rs_o,
+                ok ? e * 2 : (int)kOOB, 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[rb][j][i] + bv),
+                                                  rs_o, ok ? e * 4 : (int)kOOB, 0, 0);
         }
     }
     return;
@@ -648,7 +656,8 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
       for (int j = 0; j < 2; ++j)
         acc_to_img(smem, acc[rb][j], mi * (ROWS / 2) + rb * 32, (cj * 2 + j) * 32);
     __syncthreads();
-    conv_tile_store_rows<V, G::NCOLS, G::NT, ROWS>(p, smem, smem + ROWS * kEpiPitch, n, 0, m0);
+    conv_tile_store_rows<V, G::NCOLS, G::NT, ROWS, true>(p, smem, smem + ROWS * kEpiPitch, n, 0,
+                                                         m0);
   }
 }
 
@@ -725,7 +734,8 @@ static void launch_spw(const SpFwdParams &P, int nblk, hipStream_t s) {
 
 hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *invstd,
                               const float *g, const float *b, const float *A, const float *W,
-                              const float *biasZ, void *wpk, float *Z, __bf16 *Gk, double *ssum,
+                              const float *biasZ, void *wpk, float *Z, int z_bf16, __bf16 *Gk,
+                              double *ssum,
                               double *ssq, int N, int C, int R, int T, int V, int K, int relu,
                               hipStream_t s) {
   if (!sp_fwd_bf16_supported(C, V, K, R, relu != 0)) return hipErrorInvalidValue;
@@ -767,6 +777,7 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
   P.nchunks = nch;
   ConvGemmParams &p = P.ep;
   p.out = Z;
+  p.out_bf16 = z_bf16;
   p.bias_rv = biasZ;
   p.stat_sum = ssum;
   p.stat_sq = ssq;

@@ -154,7 +154,9 @@ struct ConvX3Geo {
   static_assert((ROWS * kEpiPitch + ROWS * V) * 4 <= LDS, "row-major epilogue image fits");
 };
 
-template <int NQ, int TG, int V, int SIN, int MR, int NPL>
+// IB (NPL = 1 only): the input is stored in bf16 (p.in_bf16; a template switch so
+// the staging code of the fp32-input kernels is unchanged)
+template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false>
 __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
   using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -172,7 +174,6 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   const int r0 = rt * G::ROWS, m0 = mt * G::FT;
   const int cstride = p.T_src * V;
   const int g0 = (SIN * m0 + p.off) * V;
-  const float *inN = p.in + (int64_t)n * p.in_bstride;
   const int nchunks = (p.C + G::CK - 1) / G::CK;
   const int nsteps = nchunks * G::NG;
   const char *wblk = reinterpret_cast<const char *>(p.wpk) + (int64_t)rt * nsteps * G::WST;
@@ -206,31 +207,57 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // counts them; a compiler-counted load here would make hipcc wait vmcnt(0)
   // -- including the weight DMA issued after it -- before the write). Their
   // completion is waited for by wait_img, which names every destination.
+  // (NPL = 1 with p.in_bf16: the input is bf16 -- e.g. the spatial conv output Z
+  // kept in bf16 -- loaded as zero-extended shorts at half the byte offsets)
+  static_assert(!IB || NPL == 1, "bf16 input: one-plane kernels");
+  constexpr bool inb = IB;
   auto load_img = [&](int chunk) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
-    const int64_t rem = (int64_t)(p.C - chunk * G::CK) * cstride * 4;
-    const uint64_t src = reinterpret_cast<uint64_t>(inN + (int64_t)chunk * G::CK * cstride);
+    const int esz = inb ? 2 : 4;
+    const int64_t rem = (int64_t)(p.C - chunk * G::CK) * cstride * esz;
+    const uint64_t src = reinterpret_cast<uint64_t>(p.in) +
+                         (uint64_t)(((int64_t)n * p.in_bstride + (int64_t)chunk * G::CK * cstride) * esz);
     const int4v rs = {(int)(uint32_t)src, (int)((src >> 32) & 0xffff),
                       (int)(rem > 0x7fffffff ? 0x7fffffff : (rem > 0 ? rem : 0)), 0x00020000};
     asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
+    if constexpr (inb) {
 #pragma unroll
-    for (int k = 0; k < G::IPT; ++k)
+      for (int k = 0; k < G::IPT; ++k)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
-                     : "=v"(st[k][j])
-                     : "v"(voff[k] + (unsigned)(j * cstride * 4)), "s"(rs)
-                     : "memory");
+        for (int j = 0; j < 8; ++j)
+          asm volatile("buffer_load_ushort %0, %1, %2, 0 offen"
+                       : "=v"(st[k][j])
+                       : "v"(voff[k] == kOOB ? kOOB : (voff[k] >> 1) + (unsigned)(j * cstride * 2)),
+                         "s"(rs)
+                       : "memory");
+    } else {
+#pragma unroll
+      for (int k = 0; k < G::IPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                       : "=v"(st[k][j])
+                       : "v"(voff[k] + (unsigned)(j * cstride * 4)), "s"(rs)
+                       : "memory");
+    }
   };
   auto write_img = [&](char *win) {
 #pragma unroll
     for (int k = 0; k < G::IPT; ++k)
       if (NPL == 1 && loff[k] >= 0) {  // bf16 operands: one rounded plane
         uint4 h;
-        h.x = pk2(st[k][0], st[k][1]);
-        h.y = pk2(st[k][2], st[k][3]);
-        h.z = pk2(st[k][4], st[k][5]);
-        h.w = pk2(st[k][6], st[k][7]);
+        if constexpr (inb) {  // already bf16 (zero-extended shorts)
+          const auto u = [&](int j) { return __builtin_bit_cast(unsigned, st[k][j]); };
+          h.x = u(0) | (u(1) << 16);
+          h.y = u(2) | (u(3) << 16);
+          h.z = u(4) | (u(5) << 16);
+          h.w = u(6) | (u(7) << 16);
+        } else {
+          h.x = pk2(st[k][0], st[k][1]);
+          h.y = pk2(st[k][2], st[k][3]);
+          h.z = pk2(st[k][4], st[k][5]);
+          h.w = pk2(st[k][6], st[k][7]);
+        }
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
       } else if (loff[k] >= 0) {
         uint4 h, m, l;
@@ -542,6 +569,13 @@ static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
   if (p.V != V || p.s_in != SIN) return false;
   constexpr int TG = NQ == 9 ? 3 : NQ;
   constexpr int lds = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>::LDS;
+  if constexpr (NPL == 1) {
+    if (p.in_bf16) {
+      hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL, true>), dim3(nblk), dim3(512), lds, s,
+                         p);
+      return true;
+    }
+  }
   hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL>), dim3(nblk), dim3(512), lds, s, p);
   return true;
 }
