@@ -148,11 +148,16 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # algorithmic HBM bytes of the timed launch(es): fp32 activations in
             # and out (the kept G of the fused spatial forward in bf16)
             N, to = cfg["N"], (t - 1) // s + 1
-            act = {0: N * (co * t + co * to) * V4, 1: N * (co * to + co * t) * V4,
-                   2: N * (co * to + co * t) * V4,
-                   3: N * (ci * t + co * t) * V4 + (N * cfg["K"] * ci * t * cfg["V"] * 2
-                                                 if cfg["bf16"] and ci >= 16 else
-                                                 N * cfg["K"] * ci * t * V4),
+            # bf16 storage of Z and dU (capi.hip act_bf16: bf16 path, stride-1
+            # non-residual blocks whose spatial forward is fused, C_in >= 16):
+            # those operands move 2 bytes per element
+            ab = cfg["bf16"] and s == 1 and ci >= 16
+            V2 = cfg["V"] * 2 if ab else V4
+            act = {0: N * (co * t * V2 + co * to * V4), 1: N * (co * to * V2 + co * t * V4),
+                   2: N * (co * to + co * t) * V2,
+                   3: N * (ci * t * V4 + co * t * V2) + (N * cfg["K"] * ci * t * cfg["V"] * 2
+                                                       if cfg["bf16"] and ci >= 16 else
+                                                       N * cfg["K"] * ci * t * V4),
                    4: N * (co * t + 2 * ci * t) * V4}[which]  # dZ, x in; dx out
             add(kinds, kind, ms.value, fl.value, 1, act)
             V, K = cfg["V"], cfg["K"]
@@ -166,17 +171,21 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 continue
             if cfg["bf16"]:
                 # temporal GEMMs: k_conv_x3 with one operand plane (NPL = 1)
-                sym = {0: f"k_conv_x3<9,3,{V},{s},1,1>",
-                       1: f"k_conv_x3<9,3,{V},1,1,1>" if s == 1 else f"k_conv_x3<5|4,{V},1,1,1>",
-                       2: f"k_wgrad_bf16<9,{V},{s}>",
+                ib = "true" if ab else "false"  # bf16 input instance
+                ft, cb = {18: (8, 64), 25: (4, 64), 50: (4, 32)}.get(V, (0, 0))
+                sym = {0: f"k_conv_x3<9,3,{V},{s},1,1,{ib}>",
+                       1: (f"k_conv_x3<9,3,{V},1,1,1,{ib}>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,1,false>"),
+                       2: f"k_wgrad_bf16<9,{V},{s},{ft},{cb},{ib}>",
                        3: (f"k_conv_bf16<1,16,{V},1>" if ci < 16 else
                            f"k_sp_fwd_bf16<{V},{K}>" if not (V == 50 or (V == 25 and K == 3)) else
                            f"k_sp_fwd_wide<{V},3,{64 if co <= 64 else 128 if co <= 128 else 256}>")
                        }[which]
             elif x3 and V in (18, 25):
                 mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
-                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},3>",
-                       1: f"k_conv_x3<9,3,{V},1,{mr},3>" if s == 1 else f"k_conv_x3<5|4,{V},1,1,3>",
+                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},3,false>",
+                       1: (f"k_conv_x3<9,3,{V},1,{mr},3,false>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,3,false>"),
                        2: f"k_wgrad_x3<{V},{s}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
