@@ -2745,8 +2745,12 @@ __global__ __launch_bounds__(256) void k_sum_nt(const float *X, int C, int T, in
 
 // k_sum_nt with float4 loads: 4*A consecutive floats per pass, A = the
 // largest multiple of the float4 period of V (V / gcd(4, V)) <= 256, so each
-// thread's 4 lanes keep fixed joints v = (4*tid + u) % V across passes; the
-// per-thread fp64 partials are then folded per joint through LDS.
+// thread's 4 lanes keep fixed joints across passes; the per-thread fp64
+// partials are then folded per joint through LDS. A row (n, c) that does not
+// start on a 16-byte boundary (T * V odd or 2 mod 4) is read from the aligned
+// address below its start: its elements sit `shift` floats into the float4
+// stream, lanes outside [0, T*V) are masked, and the fold maps stream position
+// q to joint (q - shift) mod V.
 __global__ __launch_bounds__(256) void k_sum_nt4(const float *X, int C, int T, int V,
                                                  double *out) {
   __shared__ double part[1024];
@@ -2754,15 +2758,26 @@ __global__ __launch_bounds__(256) void k_sum_nt4(const float *X, int C, int T, i
   const int L = T * V;
   const int per = V / (V % 4 == 0 ? 4 : (V % 2 == 0 ? 2 : 1));  // float4 period
   const int A = 256 / per * per;                                 // active threads
-  const float4 *src = reinterpret_cast<const float4 *>(X + ((int64_t)n * C + c) * L);
+  const int64_t start = ((int64_t)n * C + c) * L;
+  const int shift = (int)(start & 3);
+  const float4 *src = reinterpret_cast<const float4 *>(X + (start - shift));
+  const int nf = (L + shift + 3) / 4;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (tid < A) {
-    for (int f = tid; f < L / 4; f += A) {
+    for (int f = tid; f < nf; f += A) {
       const float4 q = src[f];
-      a0 += q.x;
-      a1 += q.y;
-      a2 += q.z;
-      a3 += q.w;
+      const int p0 = 4 * f - shift;  // row position of lane 0
+      if (p0 >= 0 && p0 + 3 < L) {
+        a0 += q.x;
+        a1 += q.y;
+        a2 += q.z;
+        a3 += q.w;
+      } else {
+        if (p0 >= 0 && p0 < L) a0 += q.x;
+        if (p0 + 1 >= 0 && p0 + 1 < L) a1 += q.y;
+        if (p0 + 2 >= 0 && p0 + 2 < L) a2 += q.z;
+        if (p0 + 3 >= 0 && p0 + 3 < L) a3 += q.w;
+      }
     }
   }
   part[4 * tid] = a0;
@@ -2772,13 +2787,17 @@ __global__ __launch_bounds__(256) void k_sum_nt4(const float *X, int C, int T, i
   __syncthreads();
   if (tid < V) {
     double acc = 0.0;
-    for (int p = tid; p < 4 * A; p += V) acc += part[p];  // 4*A is a multiple of V
+    // stream position q holds joint (q - shift) mod V; 4*A is a multiple of V
+    for (int q = (tid + shift) % V; q < 4 * A; q += V) acc += part[q];
     atomicAdd(out + c * V + tid, acc);
   }
 }
 
 hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out, hipStream_t s) {
-  if (((int64_t)T * V) % 4 == 0 && ((uintptr_t)X & 15) == 0 && V <= 256) {
+  // (rows of any alignment: the float4 kernel reads from the 16-byte boundary
+  // below a row's start; X 16-byte aligned and a whole number of float4 in
+  // total, so no read passes the tensor's end)
+  if (((uintptr_t)X & 15) == 0 && ((int64_t)N * C * T * V) % 4 == 0 && V <= 256) {
     hipLaunchKernelGGL(k_sum_nt4, dim3(C, N), dim3(256), 0, s, X, C, T, V, out);
     return hipGetLastError();
   }
