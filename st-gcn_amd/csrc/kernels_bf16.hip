@@ -659,11 +659,14 @@ __global__ __launch_bounds__((WgGemmGeo<TR, TC>::NTH), 1) void k_wgrad_gemm_bf16
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  auto frag = [&](const float *src) {  // 8 consecutive fp32 -> bf16x8
-    bf16x8 f;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) f[u] = (__bf16)src[u];
-    return f;
+  // 8 consecutive fp32 -> bf16x8, as two 16-byte LDS reads (fragment rows are
+  // 16-byte aligned; element-wise reads compiled to b96 + b32 pieces)
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  auto frag = [&](const float *src) {
+    const f32x4v *v = reinterpret_cast<const f32x4v *>(__builtin_assume_aligned(src, 16));
+    const f32x4v l4 = v[0], h4 = v[1];
+    return bf16x8{(__bf16)l4.x, (__bf16)l4.y, (__bf16)l4.z, (__bf16)l4.w,
+                  (__bf16)h4.x, (__bf16)h4.y, (__bf16)h4.z, (__bf16)h4.w};
   };
   float *buf0 = smem, *buf1 = smem + G::BUF;
   if (it0 < it1) stage(it0, buf0);

@@ -828,6 +828,11 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
 // LDS-DMA and rounded at fragment read, G staged in bf16 by 16-byte LDS-DMA
 // into rows of 5 slots (the fifth an OOB zero pad: 80-byte pitch, conflict-free
 // ds_read_b128 straight into the MFMA B fragment, no conversion).
+// Staging runs through an NS-slot LDS ring: items it+1 .. it+NS-2 stay in
+// flight while item it computes; each wave waits only for its own DMAs of item
+// it (vmcnt retires loads in order) and one barrier publishes the item (a
+// fenced __syncthreads would drain the ring). The item's fragments are read
+// first as 16-byte vectors (one LDS wait), then converted and multiplied.
 // ---------------------------------------------------------------------------
 template <int TR>
 struct WgGkGeo {
@@ -839,9 +844,26 @@ struct WgGkGeo {
   static constexpr int NWR = TR / 64, NW = NWR * 4, NTH = NW * 64;
   static constexpr int PROUNDS = (PSZ + NTH - 1) / NTH;
   static constexpr int QROUNDS = (QSLOTS + NTH - 1) / NTH;
+  // LDS-DMAs every wave issues per item (the P rounds are whole; a partial last
+  // Q round adds one on the first waves only): the ring's vmcnt allowance per
+  // item still in flight (a wave issuing more waits slightly more, never less)
+  static constexpr int DMIN = PROUNDS + QSLOTS / NTH;
+  static_assert(PSZ % NTH == 0, "whole P rounds");
 };
 
-template <int TR>
+// s_waitcnt vmcnt(ahead * D) (immediates only), then one unfenced barrier
+template <int D>
+__device__ __forceinline__ void gk_ring_wait(int ahead) {
+  static_assert(2 * D < 64, "vmcnt range");
+  if (ahead >= 2)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D) : "memory");
+  else if (ahead == 1)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(D) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int TR, int NS>
 __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
   using G = WgGkGeo<TR>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -919,33 +941,56 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  char *buf0 = lds, *buf1 = lds + G::BUF;
-  if (it0 < it1) stage(it0, buf0);
-  __syncthreads();
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+#pragma unroll
+  for (int k = 0; k < NS - 1; ++k)
+    if (it0 + k < it1) stage(it0 + k, lds + k * G::BUF);
+  int sl = 0;  // ring slot of item it
   for (int it = it0; it < it1; ++it) {
-    const bool odd = (it - it0) & 1;
-    const char *cur = odd ? buf1 : buf0;
-    if (it + 1 < it1) stage(it + 1, odd ? buf0 : buf1);
+    // items it+1 .. it+NS-2 may stay in flight; the barrier also retires every
+    // wave's reads of item it-1, whose slot the next staging reuses
+    gk_ring_wait<G::DMIN>(min(NS - 2, it1 - 1 - it));
+    if (it + NS - 1 < it1) stage(it + NS - 1, lds + (sl == 0 ? NS - 1 : sl - 1) * G::BUF);
+    const char *cur = lds + sl * G::BUF;
+    sl = sl + 1 == NS ? 0 : sl + 1;
     const float *pa = reinterpret_cast<const float *>(cur) + (wr * 64 + lo) * G::PITCH + 8 * hi;
     const char *qb = cur + G::PSZ * 4 + ((wc * 64 + lo) * 5 + hi) * 16;
+    // every fragment of the item first, as 16-byte reads (rows are 16-byte
+    // aligned: PITCH * 4 = 144 B), one LDS wait, then the conversions and the
+    // MFMAs (element-wise reads compiled to b96 + b32 pieces, each waited on
+    // before its conversion: the loop was LDS-latency bound)
+    constexpr int NKS = G::KC / 16;
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    f32x4v pf[NKS][2][2];
+    bf16x8f b[NKS][2];
 #pragma unroll
-    for (int s = 0; s < G::KC / 16; ++s) {
-      bf16x8f a[2], b[2];
+    for (int s = 0; s < NKS; ++s)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float *src = pa + i * 32 * G::PITCH + 16 * s;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a[i][u] = (__bf16)src[u];
+        const f32x4v *src = reinterpret_cast<const f32x4v *>(
+            __builtin_assume_aligned(pa + i * 32 * G::PITCH + 16 * s, 16));
+        pf[s][i][0] = src[0];
+        pf[s][i][1] = src[1];
       }
 #pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
       for (int j = 0; j < 2; ++j)
-        b[j] = *reinterpret_cast<const bf16x8f *>(qb + j * 32 * 5 * 16 + s * 32);
+        b[s][j] = *reinterpret_cast<const bf16x8f *>(qb + j * 32 * 5 * 16 + s * 32);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      bf16x8f a[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4v lo4 = pf[s][i][0], hi4 = pf[s][i][1];
+        a[i] = bf16x8f{(__bf16)lo4.x, (__bf16)lo4.y, (__bf16)lo4.z, (__bf16)lo4.w,
+                       (__bf16)hi4.x, (__bf16)hi4.y, (__bf16)hi4.z, (__bf16)hi4.w};
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_bf(a[i], b[s][j], acc[i][j]);
     }
-    __syncthreads();  // retires this wave's LDS-DMA and publishes the next item
   }
   float *slab = p.slab + (int64_t)split * p.R * p.C;
 #pragma unroll
@@ -975,12 +1020,22 @@ void plan_wgrad_gk(WgradParams &w, int T) {
 
 hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s) {
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
-  if (p.CT == 128)
-    hipLaunchKernelGGL((k_wgrad_gemm_gk<128>), dim3(nblk), dim3(WgGkGeo<128>::NTH),
-                       2 * WgGkGeo<128>::BUF, s, p);
-  else
-    hipLaunchKernelGGL((k_wgrad_gemm_gk<64>), dim3(nblk), dim3(WgGkGeo<64>::NTH),
-                       2 * WgGkGeo<64>::BUF, s, p);
+  // ring depth 4 (155.6 / 118.8 KiB, one workgroup per CU, three items in
+  // flight): cfg3 5289 vs 5155-5187, cfg5 2352 vs 2301-2303 clips/s against 2
+  // slots (two workgroups per CU, one item of lookahead each) in one A/B call.
+  // (Before the fragment reads were 16-byte vectors the loop was LDS-latency
+  // bound and 2 slots won: 5141 vs 5063.) STGCN_GK_SLOTS=2: A/B only.
+  static const bool two = getenv("STGCN_GK_SLOTS") && atoi(getenv("STGCN_GK_SLOTS")) == 2;
+  static_assert(4 * WgGkGeo<128>::BUF <= 160 * 1024, "LDS budget");
+#define GK_LAUNCH(TR, NS) \
+  hipLaunchKernelGGL((k_wgrad_gemm_gk<TR, NS>), dim3(nblk), dim3(WgGkGeo<TR>::NTH), \
+                     NS * WgGkGeo<TR>::BUF, s, p)
+  if (p.CT == 128) {
+    if (two) GK_LAUNCH(128, 2); else GK_LAUNCH(128, 4);
+  } else {
+    if (two) GK_LAUNCH(64, 2); else GK_LAUNCH(64, 4);
+  }
+#undef GK_LAUNCH
   return hipGetLastError();
 }
 

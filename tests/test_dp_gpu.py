@@ -40,3 +40,25 @@ def test_dp_two_ranks_on_hip(tmp_path, world):
     assert res["grad_err"] < 1e-6, res
     assert res["grad_err_A"] < 1e-3, res
     assert res["step_err"] < 1e-6, res
+
+
+def test_bench_two_ranks_rehearsal():
+    """bench.py's own N>1 branch (the one the driver launches per GPU over RCCL)
+    run end to end with 2 ranks sharing the one GPU over gloo
+    (STGCN_DIST_BACKEND=gloo): barrier + max-over-ranks timing, bucket-view
+    all-reduce, FusedAdam, one JSON line from rank 0 with the whole-job value."""
+    env = dict(os.environ, STGCN_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "8", "--no-roofline", "--no-repeats"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    print(out)
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 16
+    assert out["config"]["parallelism"] == "dp2" and out["scaling"] == "weak"
+    assert out["value"] > 0 and out["loss"] == out["loss"]  # finite, not NaN
+    assert "cpu_baseline" not in out  # rank 0 at N=1 only
