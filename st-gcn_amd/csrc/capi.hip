@@ -149,6 +149,8 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   w.S = wgrad_splits(w.n_rtiles * w.n_jtiles, d->N * w.n_mtiles);
   if (wgrad_sp_applies(w)) plan_wgrad_sp(w);
   if (bf16(d)) plan_wgrad_bf16(w);  // k_wgrad_bf16 where it covers the shape
+  // fp32 path of STGCN_F_F32X3: the spatial dW' on exact bf16 splits (k_wgrad_sp<.., X3>)
+  if (f32x3(d) && wgrad_sp_applies(w) && !getenv("STGCN_WSP_F32")) w.bf16 = 3;
   return w;
 }
 

@@ -1045,8 +1045,44 @@ bool wgrad_supported(const WgradParams &p) { return wgrad_lds_bytes(p) <= 160 * 
 // operand feeds 4 MFMAs: lane (i, h) holds k = kb + 4h + u for MFMA u, the same
 // k permutation on both operands. Workgroups of one split are consecutive in
 // the (XCD-remapped) grid, so the tiles sharing a chunk share an L2.
+// X3 (STGCN_F_F32X3 blocks): the same staging, the products as exact 3-way bf16
+// splits on v_mfma_f32_32x32x16_bf16 (six products, h*h apart; kernels_x3.hip):
+// 16-deep k-steps, lane half h holding k = kb + 8h + u (u < 8) of both operands
+// (two 16-byte reads per operand), split in registers at fragment read.
 // ---------------------------------------------------------------------------
-template <int CT, bool X4>
+typedef __bf16 wsp_bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 wsp_bf2 __attribute__((ext_vector_type(2)));
+typedef float wsp_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ unsigned wsp_pk(float a, float b) {
+  const wsp_bf2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+// 8 floats (two 16-byte LDS reads) -> exact bf16 planes h, m, l (x == h + m + l)
+__device__ __forceinline__ void wsp_planes(const float *src, uint4 &h, uint4 &m, uint4 &l) {
+  const wsp_f4 *v = reinterpret_cast<const wsp_f4 *>(__builtin_assume_aligned(src, 16));
+  const wsp_f4 x0 = v[0], x1 = v[1];
+  const float f[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  unsigned hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = f[2 * i], b = f[2 * i + 1];
+    hh[i] = wsp_pk(a, b);
+    const float ra = a - __builtin_bit_cast(float, hh[i] << 16);
+    const float rb = b - __builtin_bit_cast(float, hh[i] & 0xffff0000u);
+    mm[i] = wsp_pk(ra, rb);
+    ll[i] = wsp_pk(ra - __builtin_bit_cast(float, mm[i] << 16),
+                   rb - __builtin_bit_cast(float, mm[i] & 0xffff0000u));
+  }
+  h = uint4{hh[0], hh[1], hh[2], hh[3]};
+  m = uint4{mm[0], mm[1], mm[2], mm[3]};
+  l = uint4{ll[0], ll[1], ll[2], ll[3]};
+}
+__device__ __forceinline__ floatx16 wsp_mfma(uint4 a, uint4 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(wsp_bf8, a),
+                                                 __builtin_bit_cast(wsp_bf8, b), c, 0, 0, 0);
+}
+
+template <int CT, bool X4, bool X3>
 __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
   constexpr int KC = CT == 64 ? 64 : 32, PITCH = KC + 4;
   static_assert((PITCH / 4) % 2 == 1, "ds_read_b128 conflict-free pitch");
@@ -1120,11 +1156,11 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
   };
 
   const int mi = wave & 1, nj = wave >> 1;
-  floatx16 acc[NJ];
+  floatx16 acc[NJ], acl[NJ];
 #pragma unroll
   for (int t = 0; t < NJ; ++t)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    for (int i = 0; i < 16; ++i) acc[t][i] = acl[t][i] = 0.f;
   if (it0 < it1) stage(it0, Ps0, Qs0);
   __syncthreads();
   for (int it = it0; it < it1; ++it) {
@@ -1132,6 +1168,28 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
     const float *Ps = odd ? Ps1 : Ps0;
     const float *Qs = odd ? Qs1 : Qs0;
     if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
+    if constexpr (X3) {
+      const float *pa = Ps + (mi * 32 + lo) * PITCH + 8 * hi;
+      const float *qb = Qs + (nj * (CT / 2) + lo) * PITCH + 8 * hi;
+#pragma unroll
+      for (int s = 0; s < KC / 16; ++s) {
+        uint4 ah, am, al, bh[NJ], bm[NJ], bl[NJ];
+        wsp_planes(pa + 16 * s, ah, am, al);
+#pragma unroll
+        for (int t = 0; t < NJ; ++t) wsp_planes(qb + t * 32 * PITCH + 16 * s, bh[t], bm[t], bl[t]);
+#pragma unroll
+        for (int t = 0; t < NJ; ++t) {
+          acc[t] = wsp_mfma(ah, bh[t], acc[t]);
+          acl[t] = wsp_mfma(ah, bm[t], acl[t]);
+          acl[t] = wsp_mfma(am, bh[t], acl[t]);
+          acl[t] = wsp_mfma(ah, bl[t], acl[t]);
+          acl[t] = wsp_mfma(am, bm[t], acl[t]);
+          acl[t] = wsp_mfma(al, bh[t], acl[t]);
+        }
+      }
+      __syncthreads();  // retires this wave's LDS-DMA and publishes the next chunk
+      continue;
+    }
     const float *pa = Ps + (mi * 32 + lo) * PITCH + 4 * hi;
     const float *qb = Qs + (nj * (CT / 2) + lo) * PITCH + 4 * hi;
     // element-wise reads (merged into ds_read_b128 by the backend; a float4
@@ -1169,7 +1227,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-      if (row < p.R && c < p.C) dst[(int64_t)row * p.C + c] = acc[t][i];
+      if (row < p.R && c < p.C) dst[(int64_t)row * p.C + c] = X3 ? acc[t][i] + acl[t][i] : acc[t][i];
     }
   }
 }
@@ -1195,17 +1253,21 @@ static hipError_t launch_wgrad_sp(const WgradParams &p, hipStream_t s) {
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const int KC = wgrad_sp_kc(p.CT);
   const size_t lds = sizeof(float) * 2 * (size_t)(64 + p.CT) * (KC + 4);
+  const bool x3 = p.bf16 == 3;
+#define WSP_LAUNCH(CT, X4, X3) \
+  hipLaunchKernelGGL((k_wgrad_sp<CT, X4, X3>), dim3(nblk), dim3(256), lds, s, p)
   if (p.CT == 64) {
     if (x4)
-      hipLaunchKernelGGL((k_wgrad_sp<64, true>), dim3(nblk), dim3(256), lds, s, p);
+      { if (x3) WSP_LAUNCH(64, true, true); else WSP_LAUNCH(64, true, false); }
     else
-      hipLaunchKernelGGL((k_wgrad_sp<64, false>), dim3(nblk), dim3(256), lds, s, p);
+      { if (x3) WSP_LAUNCH(64, false, true); else WSP_LAUNCH(64, false, false); }
   } else {
     if (x4)
-      hipLaunchKernelGGL((k_wgrad_sp<128, true>), dim3(nblk), dim3(256), lds, s, p);
+      { if (x3) WSP_LAUNCH(128, true, true); else WSP_LAUNCH(128, true, false); }
     else
-      hipLaunchKernelGGL((k_wgrad_sp<128, false>), dim3(nblk), dim3(256), lds, s, p);
+      { if (x3) WSP_LAUNCH(128, false, true); else WSP_LAUNCH(128, false, false); }
   }
+#undef WSP_LAUNCH
   return hipGetLastError();
 }
 
@@ -1214,6 +1276,7 @@ bool wgrad_sp_applies(const WgradParams &p) {
 }
 
 hipError_t launch_wgrad(const WgradParams &p, hipStream_t s) {
+  if (p.bf16 == 3 && wgrad_sp_applies(p)) return launch_wgrad_sp(p, s);  // x3 products
   if (p.bf16) return launch_wgrad_bf16(p, s);
   if (wgrad_sp_applies(p)) return launch_wgrad_sp(p, s);
   if (!wgrad_supported(p)) return hipErrorInvalidValue;

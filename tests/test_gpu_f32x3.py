@@ -1,6 +1,6 @@
 """GPU parity of the fp32 block with STGCN_F_F32X3: the temporal conv forward /
-data-grad GEMMs (k_conv_x3) and the stride-1 V=18 weight gradient (k_wgrad_x3)
-as exact 3-way bf16 operand splits with six partial products on the bf16
+data-grad GEMMs (k_conv_x3), the stride-1 V=18 weight gradient (k_wgrad_x3)
+and the spatial 1x1 weight gradient dW' (k_wgrad_sp<.., X3>) as exact 3-way bf16 operand splits with six partial products on the bf16
 matrix cores (st-gcn_amd/csrc/kernels_x3.hip).
 
 The mode claims fp32-GEMM accuracy, so it is held to the SAME gate as the fp32
@@ -62,6 +62,9 @@ def test_f32x3_block_random(pkg, case):
         if V == 18:  # k_wgrad_x3 (temporal weight gradient, stride 1 and 2)
             k = "grad.temporalConv.weight"
             assert not torch.equal(got[k], ref[k]), "k_wgrad_x3 did not run"
+        # spatial dW' = dZ G^T on the split products (k_wgrad_sp<.., X3>)
+        k = "grad.spatialConv.W.weight"
+        assert not torch.equal(got[k], ref[k]), "k_wgrad_sp X3 did not run"
 
 
 def test_f32x3_full_size_block(pkg):
