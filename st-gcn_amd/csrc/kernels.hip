@@ -1082,7 +1082,20 @@ __device__ __forceinline__ floatx16 wsp_mfma(uint4 a, uint4 b, floatx16 c) {
                                                  __builtin_bit_cast(wsp_bf8, b), c, 0, 0, 0);
 }
 
-template <int CT, bool X4, bool X3>
+// NS > 2 (X3 only): an NS-slot LDS-DMA ring with hand-counted waits (items
+// it+1 .. it+NS-2 in flight while item it computes; one workgroup per CU).
+template <int CT, bool X4>
+struct WspGeo {
+  static constexpr int KC = CT == 64 ? 64 : 32, PITCH = KC + 4;
+  static constexpr int PSZ = 64 * PITCH, QSZ = CT * PITCH;
+  static constexpr int G = X4 ? 4 : 1;
+  // DMA wave-instructions per item; every wave issues at least DMIN of them
+  static constexpr int NPW = (PSZ / G + 63) / 64, NQW = (QSZ / G + 63) / 64;
+  static constexpr int DMIN = NPW / 4 + NQW / 4;
+  static constexpr int RING = 2 * DMIN < 64 ? 4 : 3;  // vmcnt allowance (NS-2)*DMIN < 64
+};
+
+template <int CT, bool X4, bool X3, int NS = 2>
 __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
   constexpr int KC = CT == 64 ? 64 : 32, PITCH = KC + 4;
   static_assert((PITCH / 4) % 2 == 1, "ds_read_b128 conflict-free pitch");
@@ -1091,6 +1104,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
   constexpr int G = X4 ? 4 : 1;             // floats per lane per DMA
   constexpr int PN = (PSZ / G + 255) / 256;  // DMA rounds per wave (upper bound)
   constexpr int QN = (QSZ / G + 255) / 256;
+  static_assert(NS == 2 || (X3 && NS <= WspGeo<CT, X4>::RING), "ring only on the x3 path");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *Ps0 = smem, *Qs0 = smem + PSZ, *Ps1 = smem + PSZ + QSZ, *Qs1 = Ps1 + PSZ;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1161,6 +1175,49 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
   for (int t = 0; t < NJ; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = acl[t][i] = 0.f;
+  // x3 products of one staged item (P rows at Ps, Q rows at Qs)
+  auto x3_item = [&](const float *Ps, const float *Qs) {
+    const float *pa = Ps + (mi * 32 + lo) * PITCH + 8 * hi;
+    const float *qb = Qs + (nj * (CT / 2) + lo) * PITCH + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < KC / 16; ++s) {
+      uint4 ah, am, al, bh[NJ], bm[NJ], bl[NJ];
+      wsp_planes(pa + 16 * s, ah, am, al);
+#pragma unroll
+      for (int t = 0; t < NJ; ++t) wsp_planes(qb + t * 32 * PITCH + 16 * s, bh[t], bm[t], bl[t]);
+#pragma unroll
+      for (int t = 0; t < NJ; ++t) {
+        acc[t] = wsp_mfma(ah, bh[t], acc[t]);
+        acl[t] = wsp_mfma(ah, bm[t], acl[t]);
+        acl[t] = wsp_mfma(am, bh[t], acl[t]);
+        acl[t] = wsp_mfma(ah, bl[t], acl[t]);
+        acl[t] = wsp_mfma(am, bm[t], acl[t]);
+        acl[t] = wsp_mfma(al, bh[t], acl[t]);
+      }
+    }
+  };
+  if constexpr (NS > 2) {
+    constexpr int D = WspGeo<CT, X4>::DMIN, SLOT = PSZ + QSZ;
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k)
+      if (it0 + k < it1) stage(it0 + k, smem + k * SLOT, smem + k * SLOT + PSZ);
+    int sl = 0;
+    for (int it = it0; it < it1; ++it) {
+      const int ahead = min(NS - 2, it1 - 1 - it);  // items staged after this one
+      if (ahead >= 2)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * D) : "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(D) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (it + NS - 1 < it1) {
+        float *nx = smem + (sl == 0 ? NS - 1 : sl - 1) * SLOT;
+        stage(it + NS - 1, nx, nx + PSZ);
+      }
+      x3_item(smem + sl * SLOT, smem + sl * SLOT + PSZ);
+      sl = sl + 1 == NS ? 0 : sl + 1;
+    }
+  } else {
   if (it0 < it1) stage(it0, Ps0, Qs0);
   __syncthreads();
   for (int it = it0; it < it1; ++it) {
@@ -1169,24 +1226,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
     const float *Qs = odd ? Qs1 : Qs0;
     if (it + 1 < it1) stage(it + 1, odd ? Ps0 : Ps1, odd ? Qs0 : Qs1);
     if constexpr (X3) {
-      const float *pa = Ps + (mi * 32 + lo) * PITCH + 8 * hi;
-      const float *qb = Qs + (nj * (CT / 2) + lo) * PITCH + 8 * hi;
-#pragma unroll
-      for (int s = 0; s < KC / 16; ++s) {
-        uint4 ah, am, al, bh[NJ], bm[NJ], bl[NJ];
-        wsp_planes(pa + 16 * s, ah, am, al);
-#pragma unroll
-        for (int t = 0; t < NJ; ++t) wsp_planes(qb + t * 32 * PITCH + 16 * s, bh[t], bm[t], bl[t]);
-#pragma unroll
-        for (int t = 0; t < NJ; ++t) {
-          acc[t] = wsp_mfma(ah, bh[t], acc[t]);
-          acl[t] = wsp_mfma(ah, bm[t], acl[t]);
-          acl[t] = wsp_mfma(am, bh[t], acl[t]);
-          acl[t] = wsp_mfma(ah, bl[t], acl[t]);
-          acl[t] = wsp_mfma(am, bm[t], acl[t]);
-          acl[t] = wsp_mfma(al, bh[t], acl[t]);
-        }
-      }
+      x3_item(Ps, Qs);
       __syncthreads();  // retires this wave's LDS-DMA and publishes the next chunk
       continue;
     }
@@ -1219,6 +1259,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_sp(WgradParams p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // retires this wave's LDS-DMA and publishes the next chunk
+  }
   }
   float *dst = p.slab + (int64_t)split * p.R * p.C;
 #pragma unroll
@@ -1254,8 +1295,20 @@ static hipError_t launch_wgrad_sp(const WgradParams &p, hipStream_t s) {
   const int KC = wgrad_sp_kc(p.CT);
   const size_t lds = sizeof(float) * 2 * (size_t)(64 + p.CT) * (KC + 4);
   const bool x3 = p.bf16 == 3;
-#define WSP_LAUNCH(CT, X4, X3) \
-  hipLaunchKernelGGL((k_wgrad_sp<CT, X4, X3>), dim3(nblk), dim3(256), lds, s, p)
+  // x3: STGCN_WSP_RING=1 selects the LDS-DMA ring (WspGeo::RING slots, one
+  // workgroup per CU): measured 1% SLOWER on cfg2 than the two-buffer schedule
+  // at two workgroups per CU (4356-4375 vs 4403-4415 clips/s in one A/B call);
+  // A/B measurement only
+  static const bool ring = getenv("STGCN_WSP_RING") && atoi(getenv("STGCN_WSP_RING")) == 1;
+#define WSP_LAUNCH(CT, X4, X3)                                                              \
+  do {                                                                                      \
+    constexpr int NSR = WspGeo<CT, X4>::RING;                                               \
+    if (X3 && ring)                                                                         \
+      hipLaunchKernelGGL((k_wgrad_sp<CT, X4, X3, X3 ? NSR : 2>), dim3(nblk), dim3(256),     \
+                         sizeof(float) * NSR * (size_t)(64 + CT) * (WspGeo<CT, X4>::KC + 4), s, p); \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_wgrad_sp<CT, X4, X3>), dim3(nblk), dim3(256), lds, s, p);       \
+  } while (0)
   if (p.CT == 64) {
     if (x4)
       { if (x3) WSP_LAUNCH(64, true, true); else WSP_LAUNCH(64, true, false); }
