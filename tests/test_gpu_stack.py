@@ -119,6 +119,52 @@ def test_stack_cfg1_matches_reference(pkg):
             assert rel_to_max(v.cpu().numpy(), ref["after." + k]) < 1e-4, k
 
 
+@pytest.mark.skip(reason="written at the end of round 2 while the GPU pool had no box to run "
+                         "it on; not yet run on hardware - enable next round")
+@pytest.mark.parametrize("residual", [False, True])
+def test_stack_chain_small_bn2_gamma(pkg, residual):
+    """The chain link with BN2 gammas at 0 and 1e-4 on some channels of every
+    block: rebuilding uhat = (y - b2) / g2 from the block
+    output is ill-conditioned there, so the link must read U for those channels.
+    Chained and unchained runs agree at the same gates as above."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    torch.manual_seed(11)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 10, A, residual=residual).cuda().train()
+        m2 = pkg.STGCNStack(3, 10, A, residual=residual).cuda().train()
+    with torch.no_grad():
+        for blk in m1.conv:
+            g = blk.batch_n_2.weight
+            g[0:2] = 0.0
+            g[2:4] = 1e-4
+            g[4:6] = -1e-4
+            blk.batch_n_2.bias[0:6] = torch.linspace(-0.5, 0.5, 6)
+    m2.load_state_dict(m1.state_dict())
+    x = torch.randn(6, 3, 40, 18, generator=torch.Generator().manual_seed(12)).cuda()
+    lab = torch.randint(0, 10, (6,), generator=torch.Generator().manual_seed(13)).cuda()
+    out1 = m1.forward_nctv(x)                      # chained
+    h = x
+    for blk in m2.conv:                            # unchained
+        h = blk(h)
+    out2 = m2.fc_layer(h.flatten(2).mean(dim=2))
+    torch.nn.functional.cross_entropy(out1, lab).backward()
+    torch.nn.functional.cross_entropy(out2, lab).backward()
+    torch.cuda.synchronize()
+    assert rel_to_max(out1.detach().cpu().numpy(), out2.detach().cpu().numpy()) < 1e-5
+    bad = []
+    for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
+        assert np.isfinite(ga).all(), k
+        if np.abs(gb).max() == 0:
+            continue
+        tol = 2e-3 if k.endswith("spatialConv.A") else 1e-4
+        err = rel_to_max(ga, gb)
+        if err > tol:
+            bad.append(f"{k}: {err:.2e} > {tol:.0e}")
+    assert not bad, "; ".join(bad)
+
+
 @pytest.mark.parametrize("residual,drop", [(False, 0), (True, 0), (False, 0.5), (True, 0.3)])
 def test_stack_chain_matches_unchained(pkg, residual, drop):
     """Cross-block fusion (network.StackChain: BN1 stats from the previous
