@@ -119,8 +119,6 @@ def test_stack_cfg1_matches_reference(pkg):
             assert rel_to_max(v.cpu().numpy(), ref["after." + k]) < 1e-4, k
 
 
-@pytest.mark.skip(reason="written at the end of round 2 while the GPU pool had no box to run "
-                         "it on; not yet run on hardware - enable next round")
 @pytest.mark.parametrize("residual", [False, True])
 def test_stack_chain_small_bn2_gamma(pkg, residual):
     """The chain link with BN2 gammas at 0 and 1e-4 on some channels of every
