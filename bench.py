@@ -48,7 +48,6 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense (no sparsity)
 # MFMAs per fp32 product (kernels_x3.hip), so the fp32-work ceiling is 1/6 of BF16
 X3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
-HBM_PEAK_GBS = 8000.0
 
 
 def adjacency(pkg, cfg):
@@ -71,13 +70,36 @@ def build_model(pkg, cfg, device):
     return model.to(device)
 
 
-def cpu_baseline(cfg, seconds=12.0):
-    """The oracle (CPU restatement of the reference, fp32 torch ops) timed on
-    this host's cores on a bounded sample of the same workload."""
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), or platform.processor()."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, seconds=8.0):
+    """The oracle (CPU restatement of the reference, fp32 torch ops, pinned at
+    0.945 of the reference's own speed: profiles/cpu_baseline_pin.json) timed
+    on this host's cores on a bounded sample of the same workload
+    (torch.set_num_threads(os.cpu_count())). A GPU box's
+    process may be confined to a share of the machine's cores (16 per GPU on
+    this pool), where os.cpu_count() threads oversubscribe it: both thread
+    counts are timed and the faster one is reported (the best the reference
+    path does on this host)."""
     from oracle import ref_cpu
     pkg = load()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
+    ncpu = os.cpu_count() or 1
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = ncpu
+    cands = sorted({ncpu, max(1, min(16, share))}, reverse=True)
     A = adjacency(pkg, cfg)
     p, b = ref_cpu.init_stack_params(cfg["C"], cfg["classes"], A, seed=0)
     p = {k: v.clone().requires_grad_(True) for k, v in p.items()}
@@ -90,17 +112,27 @@ def cpu_baseline(cfg, seconds=12.0):
         loss = torch.nn.functional.cross_entropy(st.forward(x), y)
         loss.backward()
 
-    step()  # warm-up
-    iters, t0 = 0, time.perf_counter()
-    while iters < 2 or time.perf_counter() - t0 < seconds:
-        step()
-        iters += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * iters / dt, 3), "unit": "clips/s", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle/ref_cpu.py fp32 stack fwd+bwd+loss, N={n} clips x {iters} iters "
+    prev = torch.get_num_threads()
+    res = []
+    for threads in cands:
+        torch.set_num_threads(threads)
+        step()  # warm-up
+        iters, t0 = 0, time.perf_counter()
+        while iters < 2 or time.perf_counter() - t0 < seconds:
+            step()
+            iters += 1
+        dt = time.perf_counter() - t0
+        res.append((n * iters / dt, threads, iters, dt))
+    torch.set_num_threads(prev)
+    best = max(res)
+    return {"value": round(best[0], 3), "unit": "clips/s", "cores": best[1],
+            "kind": "port", "cpu_model": cpu_model(), "os_cpu_count": ncpu,
+            "affinity_cpus": share,
+            "per_thread_count": {str(t): round(v, 3) for v, t, _, _ in res},
+            "sample": f"oracle/ref_cpu.py fp32 stack fwd+bwd+loss, N={n} clips x {best[2]} iters "
                       f"(T={cfg['T']}, V={cfg['V']}, K={cfg['K']}, {cfg['classes']} classes), "
-                      f"{threads} threads, {dt:.1f}s"}
+                      f"{best[1]} threads, {best[3]:.1f}s; timed at "
+                      f"{' and '.join(str(t) for t in cands)} threads, the faster reported"}
 
 
 # cfg2 stack layers (lightning_model.py:65-86): (C_in, C_out, T_in, stride)
@@ -117,12 +149,26 @@ KERNEL_KINDS = {0: "tconv_fwd", 1: "tconv_dgrad", 2: "tconv_wgrad", 3: "spatial_
                 4: "spatial_bwd"}
 
 
+def joint_bwd_symbol(cfg, ci, t):
+    """rocprof short name of the unfused spatial backward's joint kernel
+    (kernels.hip launch_spatial_dx: k_spatial_bwd5 / _bwd6, else k_spatial_bwd3)."""
+    V, K = cfg["V"], cfg["K"]
+    if V in (18, 25) and K * ((V + 1) // 2) * ((V + 31) // 32) <= 48:
+        for rb in (128, 64):
+            if (ci * t) % rb == 0:
+                return f"k_spatial_bwd5<{V},{rb},{K}>"
+    if V == 50 and (ci * t) % 64 == 0:
+        return f"k_spatial_bwd6<50,{K},{'true' if cfg['bf16'] else 'false'}>"
+    return f"k_spatial_bwd3<{V}>"
+
+
 def kernel_roofline(pkg, device, cfg, iters=10):
     """Per-kernel timing with HIP events on the launch stream (the library's
     stgcn_time_kernel entry point, same launch parameters as the block), over
-    every layer of the stack. Returns {kind: (total_ms, total_flops, launches)}
-    and the same aggregated per kernel symbol (rocprof names: k_tconv<9,2,V,1>
-    = temporal forward + data-grad of the stride-1 layers)."""
+    every layer of the stack. Returns {kind: (total_ms, total_flops, launches,
+    bytes)} and the same aggregated per kernel symbol (rocprof short names), so
+    the dominant kernel is chosen among every GEMM-type kernel of the step,
+    the two halves of an unfused spatial backward included (which 5 / 6)."""
     import ctypes
     hl = pkg.hip_lib
     lib = hl.lib()
@@ -137,8 +183,10 @@ def kernel_roofline(pkg, device, cfg, iters=10):
         x3 = cfg.get("f32_gemm") == "bf16x3" and not cfg["bf16"]
         d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
                                 bf16=cfg["bf16"], f32x3=x3)
-        for which, kind in KERNEL_KINDS.items():
+        for which in range(7):
             nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
+            if nbytes == 0:  # 5 / 6 where the spatial backward is one fused kernel
+                continue
             scratch = torch.randn(nbytes // 4 + 1, device=device)
             ms, fl = ctypes.c_float(0), ctypes.c_double(0)
             hl.check(lib.stgcn_time_kernel(ctypes.byref(d), which, hl.ptr(scratch), nbytes, iters,
@@ -148,26 +196,37 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # algorithmic HBM bytes of the timed launch(es): fp32 activations in
             # and out (the kept G of the fused spatial forward in bf16)
             N, to = cfg["N"], (t - 1) // s + 1
+            V, K = cfg["V"], cfg["K"]
             # bf16 storage of Z and dU (capi.hip act_bf16: bf16 path, stride-1
             # non-residual blocks whose spatial forward is fused, C_in >= 16):
             # those operands move 2 bytes per element
             ab = cfg["bf16"] and s == 1 and ci >= 16
-            V2 = cfg["V"] * 2 if ab else V4
+            V2 = V * 2 if ab else V4
             act = {0: N * (co * t * V2 + co * to * V4), 1: N * (co * to * V2 + co * t * V4),
                    2: N * (co * to + co * t) * V2,
-                   3: N * (ci * t * V4 + co * t * V2) + (N * cfg["K"] * ci * t * cfg["V"] * 2
+                   3: N * (ci * t * V4 + co * t * V2) + (N * K * ci * t * V * 2
                                                        if cfg["bf16"] and ci >= 16 else
-                                                       N * cfg["K"] * ci * t * V4),
-                   4: N * (co * t + 2 * ci * t) * V4}[which]  # dZ, x in; dx out
-            add(kinds, kind, ms.value, fl.value, 1, act)
-            V, K = cfg["V"], cfg["K"]
+                                                       N * K * ci * t * V4),
+                   4: N * (co * t + 2 * ci * t) * V4,  # dZ, x in; dx out
+                   5: N * (co * t + K * ci * t) * V4,  # dZ in; H out
+                   6: N * (K * ci * t + 2 * ci * t) * V4}[which]  # H, x in; dx out
+            if which <= 4:
+                add(kinds, KERNEL_KINDS[which], ms.value, fl.value, 1, act)
             # rocprof short names of the kernel each timing runs
             if which == 4:
                 # the fused spatial backward (bf16, V = 25, K = 3); the unfused
-                # H GEMM + joint kernel pair is two kernels: kind only
-                if cfg["bf16"] and V == 25 and K == 3 and ci % 32 == 0 and co % 16 == 0 \
-                        and co >= 64:
-                    add(symbols, "k_sp_bwd_fused<25,3,false>", ms.value, fl.value, 1, act)
+                # pair is timed per kernel by which 5 / 6
+                if lib.stgcn_time_kernel_bytes(ctypes.byref(d), 5) == 0:
+                    add(symbols, f"k_sp_bwd_fused<{V},{K},{'true' if x3 else 'false'}>",
+                        ms.value, fl.value, 1, act)
+                continue
+            if which == 6:
+                add(symbols, joint_bwd_symbol(cfg, ci, t), ms.value, fl.value, 1, act)
+                continue
+            if which == 5:  # the stacked H GEMM (NQ = 1 over C_out channels)
+                sym = (f"k_conv_bf16<1,16,{V},1>" if cfg["bf16"] and co >= 16
+                       else f"k_tconv<1,8,{V},1>")
+                add(symbols, sym, ms.value, fl.value, 1, act)
                 continue
             if cfg["bf16"]:
                 # temporal GEMMs: k_conv_x3 with one operand plane (NPL = 1)
@@ -221,20 +280,40 @@ def per_block_rates(model, cfg, device, iters=5):
     return out
 
 
-def traffic_from_profiles(symbol, key="hbm_bytes_per_launch"):
-    """HBM bytes per launch of `symbol` from the committed rocprofv3 PMC pass
-    (profiles/pmc_*.json: FETCH_SIZE doubled per the gfx950 correction +
-    WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None. key="mfma_busy":
-    the kernel's MFMA-busy fraction of SIMD cycles from the same file."""
+def source_sha16():
+    """sha256 (first 16 hex) over the kernel sources and the C-ABI header: the
+    tree tag a PMC file must carry for its counters to describe this build."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
-    if not files:
-        return None
-    try:
-        data = json.load(open(files[-1]))
-        return data.get(key, {}).get(symbol)
-    except (OSError, ValueError):
-        return None
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "st-gcn_amd", "csrc", "*"))) + \
+        [os.path.join(ROOT, "include", "stgcn_hip.h")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_profile(config):
+    """The committed rocprofv3 PMC summary (profiles/pmc_<tag>_<config>.json,
+    scripts/pmc_traffic.py) of THIS config measured on THIS kernel-source tree
+    (its src_sha16), or (None, reason)."""
+    import glob
+    sha = source_sha16()
+    found = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_*_{config}.json"))):
+        try:
+            data = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if data.get("config") == config:
+            found.append((f, data))
+    for f, data in reversed(found):
+        if data.get("src_sha16") == sha:
+            return data, os.path.relpath(f, ROOT)
+    return None, (f"no PMC pass of {config} on this kernel-source tree (src_sha16 {sha}); "
+                  f"newest: {os.path.relpath(found[-1][0], ROOT) if found else 'none'}")
 
 
 def main():
@@ -391,7 +470,9 @@ def main():
             kinds, symbols = kernel_roofline(pkg, device, cfg)
             sym = max(symbols, key=lambda k: symbols[k][0])
             ms_tot, fl_tot, nl, nb_tot = symbols[sym]
-            traffic = traffic_from_profiles(sym)
+            pmc, pmc_src = pmc_profile(args.config)
+            traffic = pmc["hbm_bytes_per_launch"].get(sym) if pmc else None
+            mfma_busy = pmc.get("mfma_busy", {}).get(sym) if pmc else None
             fpeak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
                      X3_PEAK_TFLOPS if sym.startswith("k_conv_x3") else MFMA_F32_PEAK_TFLOPS)
             # the roof that bounds the kernel's algorithmic work: MFMA or HBM
@@ -406,7 +487,8 @@ def main():
                 "kernel": sym, "bound": "hbm" if hbm else "mfma", "achieved": round(ach, 2),
                 "peak": peak, "unit": unit,
                 "frac": round(ach / peak, 4), "traffic": traffic,
-                "mfma_busy": traffic_from_profiles(sym, "mfma_busy"),
+                "traffic_source": pmc_src, "src_sha16": source_sha16(),
+                "mfma_busy": mfma_busy,
                 "algorithmic_bytes_per_launch": round(nb_tot / nl),
                 "algorithmic_flops_per_launch": round(fl_tot / nl),
                 "tflops": round(fl_tot / (ms_tot * 1e-3) / 1e12, 2),
@@ -415,7 +497,9 @@ def main():
                 "per_kind_tflops": {k: round(v[1] / (v[0] * 1e-3) / 1e12, 1)
                                     for k, v in kinds.items()},
                 "per_kind_gbs": {k: round(v[3] / (v[0] * 1e-3) / 1e9, 1) for k, v in kinds.items()},
-                "per_kind_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()}}
+                "per_kind_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()},
+                "per_symbol_ms_per_step": {k: round(v[0], 3) for k, v in
+                                           sorted(symbols.items(), key=lambda kv: -kv[1][0])}}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(out), flush=True)

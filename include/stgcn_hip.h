@@ -57,15 +57,22 @@ extern "C" {
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
 #define STGCN_F_BF16 2     /* channel GEMMs (W, temporal conv fwd/dgrad/wgrad, projection)
                             * on bf16 MFMA: operands rounded to bf16, fp32 accumulate;
-                            * tensors stay fp32, A / BatchNorm stay fp32 (BASELINE cfg3/5).
+                            * A / BatchNorm stay fp32 (BASELINE cfg3/5). x, y, U, stats and
+                            * every gradient the caller receives are fp32. Z (the saved
+                            * spatial output) is OPAQUE under this flag: on stride-1
+                            * non-residual blocks with C_in >= 16 it holds bf16 values in
+                            * the first half of its fp32-sized buffer (every reader rounds
+                            * it to bf16 anyway), so only stgcn_block_bwd may read it.
                             * Applies for V in {18, 25, 50} and reductions over >= 16
                             * channels; other GEMMs run the fp32 kernels. */
 #define STGCN_F_F32X3 4    /* fp32 channel GEMMs on the bf16 matrix cores by exact 3-way
                             * operand splits (x = h + m + l, six partial products, fp32
                             * accumulate): fp32-GEMM accuracy at up to 2.67x the fp32
-                            * MFMA rate. Applies to the temporal conv forward (stride 1
-                            * and 2) and data-grad for V in {18, 25} over >= 16 channels;
-                            * other GEMMs run the fp32 kernels. Exclusive with STGCN_F_BF16. */
+                            * MFMA rate. Applies for V in {18, 25} over >= 16 channels to
+                            * the temporal conv forward (stride 1 and 2), data-grad and
+                            * weight-grad, and to the spatial weight-grad dW'; other GEMMs
+                            * run the fp32 kernels. Every tensor stays fp32. Exclusive with
+                            * STGCN_F_BF16. */
 
 enum {
   STGCN_OK = 0,
@@ -84,7 +91,7 @@ typedef struct stgcn_desc {
   float momentum;      /* BatchNorm momentum 0.1                             */
   int32_t training;    /* 1: batch statistics + running-stat update          */
   int32_t need_dx;     /* backward: write dx (0 for the network's first block)*/
-  int32_t flags;       /* STGCN_F_RESIDUAL | STGCN_F_BF16 (or 0)             */
+  int32_t flags;       /* STGCN_F_RESIDUAL | (STGCN_F_BF16 or STGCN_F_F32X3) */
 } stgcn_desc_t;
 
 /* Forward arguments. Saved tensors (Z, U, stats; residual: Z, Za, y, stats)
@@ -100,7 +107,8 @@ typedef struct stgcn_fwd_args {
   const float *g1, *b1, *g2, *b2;       /* batch_n / batch_n_2 affine         */
   float *rm1, *rv1, *rm2, *rv2;         /* running stats (updated if training)*/
   float *y;                             /* out: N,C_out,T_out,V               */
-  float *Z;                             /* saved: spatial output N,C_out,T,V  */
+  float *Z;                             /* saved: spatial output N,C_out,T,V
+                                         * (fp32-sized; opaque under STGCN_F_BF16) */
   float *U;                             /* saved: temporal output N,C_out,T_out,V */
   float *stats;                         /* saved: 2*C_in + 2*C_out floats     */
   /* ABI 2 (residual block; null otherwise) */
@@ -199,7 +207,10 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
  * launched `iters` times with the exact parameters the block uses for this
  * descriptor, between two hipEvents on `stream`. which: 0 temporal conv fwd,
  * 1 temporal conv data-grad, 2 temporal conv weight-grad, 3 spatial channel
- * GEMM, 4 spatial backward (dZ -> dx, dA, BN1 sums). scratch (>= stgcn_time_kernel_bytes) supplies operand memory.
+ * GEMM (the fused SpatialConv forward where it runs), 4 spatial backward
+ * (dZ -> dx, dA, BN1 sums), 5 / 6 the H GEMM / the joint kernel of a spatial
+ * backward that runs unfused (STGCN_E_UNSUPPORTED where it is one kernel).
+ * scratch (>= stgcn_time_kernel_bytes) supplies operand memory.
  * *flops receives the algorithmic FLOPs of one launch. */
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which);
 int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t scratch_bytes,

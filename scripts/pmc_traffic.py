@@ -14,8 +14,14 @@ keeps the value of the first directory that has it (cfg2 first). A pass with
 SQ_VALU_MFMA_BUSY_CYCLES and GRBM_GUI_ACTIVE adds `mfma_busy` per kernel: MFMA
 busy cycles over the 1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs).
 
-Usage: python scripts/pmc_traffic.py profiles/pmc_<tag>.json <pass dir> [<pass dir> ...]
+Round 3 on: one file per config, profiles/pmc_<tag>_<config>.json, carrying
+"config" and "src_sha16" (bench.source_sha16() of the tree the passes ran on,
+written by the GPU script into <pass dir>/../src_sha16.txt); bench.py only uses
+the file of its config whose src_sha16 matches its own tree.
+
+Usage: python scripts/pmc_traffic.py profiles/pmc_<tag>_<config>.json <pass dir> [...]
 """
+import os
 import csv
 import glob
 import json
@@ -48,8 +54,16 @@ def main(dst, *srcs):
             for c, v in cs.items():
                 if c not in vals[k]:
                     vals[k][c] = v
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
-                     "bench.py --steps 2 --warmup 1 --no-roofline",
+    base = os.path.basename(dst)[:-5]  # pmc_<tag>_<config>
+    tag, config = base.split("_")[1], base.split("_")[-1]
+    sha = None
+    for src in srcs:
+        p = os.path.join(os.path.dirname(os.path.normpath(src)), "src_sha16.txt")
+        if os.path.exists(p):
+            sha = open(p).read().strip()
+    out = {"tag": tag, "config": config, "src_sha16": sha,
+           "source": f"rocprofv3 --pmc (separate passes) over bench.py --config {config} "
+                     "--steps 2 --warmup 1 --no-roofline",
            "formula": "2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (bytes per launch)",
            "hbm_bytes_per_launch": {}, "raw_kib": {}, "mfma_busy": {}}
     for k, cs in sorted(vals.items()):
@@ -67,7 +81,7 @@ def main(dst, *srcs):
             if gg > 0:
                 out["mfma_busy"][k] = round(mb / (gg * 1024), 4)
     stats = [k for k in out["raw_kib"] if k.startswith("k_bn_stats")]
-    if stats:
+    if stats and config == "cfg2":
         # with stack chaining only block 0 runs its own BN1 statistics pass
         # (the other blocks take them from the previous block's output pass):
         # one launch per step reading the 3-channel input once

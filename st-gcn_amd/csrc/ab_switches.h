@@ -1,0 +1,48 @@
+// Compile-time A/B alternates of the tuned kernel paths.
+//
+// The shipped library (build.py default) has exactly one path per
+// configuration: every switch below is 0. A measurement build turns one on with
+// a -D define (`build.py`: build(variant="name", defines=("STGCN_AB_UNFUSED_SP=1",)),
+// loaded as lib/libstgcn_hip_<variant>.so by scripts/), so no environment
+// variable can route the product library to an untested kernel.
+#pragma once
+
+#ifndef STGCN_AB_UNFUSED_SP     // the unfused gather + W' GEMM instead of k_sp_fwd_*
+#define STGCN_AB_UNFUSED_SP 0
+#endif
+#ifndef STGCN_AB_UNFUSED_SPB    // the H GEMM + k_spatial_bwd5/6 pair instead of k_sp_bwd_fused
+#define STGCN_AB_UNFUSED_SPB 0
+#endif
+#ifndef STGCN_AB_SPB_X3         // k_sp_bwd_fused on exact splits for the fp32 path (cfg2)
+#define STGCN_AB_SPB_X3 0
+#endif
+#ifndef STGCN_AB_WSP_F32        // the fp32-MFMA spatial dW' on STGCN_F_F32X3 blocks
+#define STGCN_AB_WSP_F32 0
+#endif
+#ifndef STGCN_AB_WSP_RING       // k_wgrad_sp<.., X3> with the LDS-DMA ring
+#define STGCN_AB_WSP_RING 0
+#endif
+#ifndef STGCN_AB_ACT_FP32       // fp32 storage of Z / dU on the bf16 path
+#define STGCN_AB_ACT_FP32 0
+#endif
+#ifndef STGCN_AB_X3_MR1         // 64-row tiles only in k_conv_x3
+#define STGCN_AB_X3_MR1 0
+#endif
+#ifndef STGCN_AB_OLD_BF16CONV   // k_conv_bf16 for the 9/5/4-tap bf16 GEMMs
+#define STGCN_AB_OLD_BF16CONV 0
+#endif
+#ifndef STGCN_AB_GK_SLOTS2      // two-slot staging in k_wgrad_gemm_gk
+#define STGCN_AB_GK_SLOTS2 0
+#endif
+#ifndef STGCN_AB_SPF_NARROW25   // the 64-row k_sp_fwd_bf16 for V = 25, K = 3
+#define STGCN_AB_SPF_NARROW25 0
+#endif
+#ifndef STGCN_AB_GENERIC_CONV   // the runtime-geometry conv kernels for every V
+#define STGCN_AB_GENERIC_CONV 0
+#endif
+#ifndef STGCN_AB_JOINT3         // k_spatial_bwd3 / gather3 instead of the MFMA joint kernels
+#define STGCN_AB_JOINT3 0
+#endif
+#ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
+#define STGCN_AB_BWD6_EXACT 0
+#endif

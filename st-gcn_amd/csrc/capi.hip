@@ -89,15 +89,15 @@ Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
   return dr;
 }
 // the fused spatial forward (kernels_fused.hip) of the bf16 path applies
-// (STGCN_UNFUSED_SP: the unfused gather + GEMM kernels, A/B measurement only)
+// (STGCN_AB_UNFUSED_SP build: the unfused gather + GEMM kernels, A/B measurement only)
 bool fused_sp(const stgcn_desc_t *d) {
-  static const bool off = getenv("STGCN_UNFUSED_SP") != nullptr;
+  constexpr bool off = STGCN_AB_UNFUSED_SP != 0;
   return !off && bf16(d) && sp_fwd_bf16_supported(d->C_in, d->V, d->K, d->C_out, residual(d));
 }
 // the fused spatial backward (kernels_spbwd.hip) applies: bf16 path, or the fp32
-// split path (STGCN_UNFUSED_SPB: the H GEMM + k_spatial_bwd5/6 pair, A/B only)
+// split path (STGCN_AB_UNFUSED_SPB build: the H GEMM + k_spatial_bwd5/6 pair, A/B only)
 bool fused_spb(const stgcn_desc_t *d) {
-  static const bool off = getenv("STGCN_UNFUSED_SPB") != nullptr;
+  constexpr bool off = STGCN_AB_UNFUSED_SPB != 0;
   return !off && (bf16(d) || f32x3(d)) &&
          sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T, f32x3(d));
 }
@@ -150,7 +150,7 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
   if (wgrad_sp_applies(w)) plan_wgrad_sp(w);
   if (bf16(d)) plan_wgrad_bf16(w);  // k_wgrad_bf16 where it covers the shape
   // fp32 path of STGCN_F_F32X3: the spatial dW' on exact bf16 splits (k_wgrad_sp<.., X3>)
-  if (f32x3(d) && wgrad_sp_applies(w) && !getenv("STGCN_WSP_F32")) w.bf16 = 3;
+  if (f32x3(d) && wgrad_sp_applies(w) && !STGCN_AB_WSP_F32) w.bf16 = 3;
   return w;
 }
 
@@ -285,10 +285,9 @@ void conv_tiles(ConvGemmParams &p) {
 // the bytes move; the bias / BN gradients use the fp32 sums of the producing
 // passes. The tensors keep their fp32-sized buffers (the first half holds the
 // bf16 data). Producers: the fused spatial forward's epilogues (so C_in >= 16)
-// and the BN2 + ReLU backward pass. (STGCN_ACT_FP32: fp32 storage, A/B only)
+// and the BN2 + ReLU backward pass. (STGCN_AB_ACT_FP32 build: fp32 storage, A/B only)
 bool act_bf16(const stgcn_desc_t *d) {
-  static const bool off =
-      getenv("STGCN_ACT_FP32") != nullptr || getenv("STGCN_GENERIC_CONV") != nullptr;
+  constexpr bool off = STGCN_AB_ACT_FP32 != 0 || STGCN_AB_GENERIC_CONV != 0;
   // Stride-2 blocks keep fp32: their weight gradient (k_wgrad_bf16<9,V,2>) staged
   // bf16 pairs slower than fp32 (cfg5 2.19 -> 2.66 ms per step), more than the
   // strided forward and data-gradient phases gained.
@@ -818,6 +817,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 //         4: spatial backward dZ -> dx, dA, BN1 sums (k_sp_bwd_fused where it
 //            applies, else the stacked H GEMM + the joint kernel; H GEMM and
 //            joint contraction FLOPs)
+//         5: the stacked H GEMM of the unfused spatial backward alone
+//         6: the joint kernel of the unfused spatial backward alone
+//            (k_spatial_bwd5 / _bwd6 / _bwd3: dx, dA, BN1 sums from H)
+//         (5 and 6 fail with STGCN_E_UNSUPPORTED where k_sp_bwd_fused runs)
 // flops = the algorithmic FLOPs of one launch (SURVEY.md §8d terms).
 // ---------------------------------------------------------------------------
 namespace {
@@ -832,8 +835,8 @@ struct TimedPlan {
   void *wpk = nullptr;
   float *Z = nullptr;
   __bf16 *Gk = nullptr;
-  // which 4: the spatial backward
-  bool spb = false;
+  // which 4: the spatial backward (5: its H GEMM only, 6: its joint kernel only)
+  bool spb = false, spb_gemm = true, spb_joint = true;
   const float *dZ = nullptr;
   float *H = nullptr, *dx = nullptr, *dA = nullptr;
   double *sd = nullptr;
@@ -923,8 +926,10 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.wp = w;
     P.wgrad = true;
     P.flops = tflops;
-  } else if (which == 4) {
+  } else if (which >= 4) {
     P.spb = true;
+    P.spb_gemm = which != 6;
+    P.spb_joint = which != 5;
     P.wpk = wpk;
     P.x = c.take<float>((size_t)N * C * T * V);
     P.st = c.take<float>((size_t)4 * C);
@@ -958,7 +963,8 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       conv_tiles(p);
       P.cp[P.ncp++] = p;
     }
-    P.flops = 2.0 * K * C * (double)R * T * V * N + 4.0 * K * C * (double)T * V * V * N;
+    P.flops = (P.spb_gemm ? 2.0 * K * C * (double)R * T * V * N : 0.0) +
+              (P.spb_joint ? 4.0 * K * C * (double)T * V * V * N : 0.0);
   } else if (fused_sp(d)) {
     // the forward's fused spatial kernel (G kept in bf16 as in the stack)
     P.spf = true;
@@ -1004,7 +1010,8 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
 extern "C" {
 
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which) {
-  if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 4) return 0;
+  if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 6) return 0;
+  if (which >= 5 && fused_spb(d)) return 0;
   return plan_timed(d, which, nullptr).bytes;
 }
 
@@ -1012,8 +1019,10 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
                       int iters, void *stream, float *avg_ms, double *flops) {
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
-  if (which < 0 || which > 4 || iters <= 0 || !avg_ms || !flops)
+  if (which < 0 || which > 6 || iters <= 0 || !avg_ms || !flops)
     return fail(STGCN_E_INVALID, "bad timing request");
+  if (which >= 5 && fused_spb(d))
+    return fail(STGCN_E_UNSUPPORTED, "the spatial backward is one fused kernel here (which 4)");
   TimedPlan P = plan_timed(d, which, scratch);
   if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
   hipStream_t s = (hipStream_t)stream;
@@ -1025,8 +1034,10 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
         return launch_sp_bwd_fused(P.dZ, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A,
                                    P.W, P.wpk, P.dx, P.dA, P.sd, P.sd + C, d->N, C, d->C_out,
                                    d->T, d->V, d->K, 1, residual(d) ? 1 : 0, f32x3(d), s);
-      hipError_t e = launch_conv_gemm(P.cp[0], s);
-      if (e != hipSuccess) return e;
+      if (P.spb_gemm) {
+        hipError_t e = launch_conv_gemm(P.cp[0], s);
+        if (e != hipSuccess || !P.spb_joint) return e;
+      }
       return launch_spatial_dx(P.H, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A, P.dx,
                                P.dA, P.sd, P.sd + C, d->N, C, d->T, d->V, d->K, 1,
                                residual(d) ? 1 : 0, bf16(d) ? 1 : 0, s);

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ab_switches.h"
+
 namespace stgcn {
 
 // Fused dropout (st_graphconv.py:53-58, :107-109): element e of the block

@@ -400,14 +400,12 @@ __global__ __launch_bounds__(256, 2) void k_tconv(ConvGemmParams p) {
 
 
 
-static bool env_flag(const char *name) { return getenv(name) != nullptr; }
 
 // The (V, stride, NQ) combinations with a specialised k_tconv instantiation:
 // the joint counts of the reference's skeleton graphs (coco18, body25,
 // two-person body25), input stride 1 (and 2 for the strided temporal forward).
 static bool tconv_specialised(const ConvGemmParams &p) {
-  static const bool generic = env_flag("STGCN_GENERIC_CONV");  // A/B measurement only
-  if (generic) return false;
+  if (STGCN_AB_GENERIC_CONV) return false;  // A/B builds only (ab_switches.h)
   if (p.V != 18 && p.V != 25 && p.V != 50) return false;
   if (p.FT != kTileCols / p.V) return false;
   if (p.s_in == 2) return p.NQ == 9;
@@ -987,8 +985,7 @@ hipError_t launch_wgrad_taps(const WgradParams &p, hipStream_t s) {
   if (!wgrad_taps_supported(p)) return hipErrorInvalidValue;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   const size_t lds = wgrad_taps_lds_bytes(p);
-  static const bool generic = getenv("STGCN_GENERIC_CONV") != nullptr;  // A/B measurement only
-  if (!generic) {
+  if (!STGCN_AB_GENERIC_CONV) {
     // the plans make_wgrad_taps builds for the reference's graphs (FT = 80 / V,
     // reduced until the double-buffered images fit in LDS)
     if (p.V == 18 && p.FT == 4 && p.s_in == 1)
@@ -1295,11 +1292,11 @@ static hipError_t launch_wgrad_sp(const WgradParams &p, hipStream_t s) {
   const int KC = wgrad_sp_kc(p.CT);
   const size_t lds = sizeof(float) * 2 * (size_t)(64 + p.CT) * (KC + 4);
   const bool x3 = p.bf16 == 3;
-  // x3: STGCN_WSP_RING=1 selects the LDS-DMA ring (WspGeo::RING slots, one
+  // x3: STGCN_AB_WSP_RING builds select the LDS-DMA ring (WspGeo::RING slots, one
   // workgroup per CU): measured 1% SLOWER on cfg2 than the two-buffer schedule
   // at two workgroups per CU (4356-4375 vs 4403-4415 clips/s in one A/B call);
   // A/B measurement only
-  static const bool ring = getenv("STGCN_WSP_RING") && atoi(getenv("STGCN_WSP_RING")) == 1;
+  constexpr bool ring = STGCN_AB_WSP_RING != 0;
 #define WSP_LAUNCH(CT, X4, X3)                                                              \
   do {                                                                                      \
     constexpr int NSR = WspGeo<CT, X4>::RING;                                               \
@@ -2794,7 +2791,7 @@ static bool joint_fast(int V) { return V == 18 || V == 25 || V == 50; }
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, int relu, hipStream_t s) {
-  static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
+  constexpr bool joint3 = STGCN_AB_JOINT3 != 0;  // A/B builds only (ab_switches.h)
   if (!joint3 && K > 1 && (V == 25 || V == 50) && ((uintptr_t)x & 15) == 0 &&
       ((uintptr_t)G & 15) == 0) {  // partitioned graphs: contraction on MFMA
     const int64_t rows = (int64_t)N * C * T;
@@ -3038,9 +3035,9 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b, const float *A,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
                              int V, int K, int write_dx, int relu, int bf16ops, hipStream_t s) {
-  static const bool joint3 = env_flag("STGCN_JOINT3");  // A/B measurement only
-  // (STGCN_BWD6_EXACT: the exact-split k_spatial_bwd6 for bf16 blocks too, A/B only)
-  static const bool exact6 = env_flag("STGCN_BWD6_EXACT");
+  constexpr bool joint3 = STGCN_AB_JOINT3 != 0;  // A/B builds only (ab_switches.h)
+  // (STGCN_AB_BWD6_EXACT: the exact-split k_spatial_bwd6 for bf16 blocks too)
+  constexpr bool exact6 = STGCN_AB_BWD6_EXACT != 0;
   const bool bf6 = bf16ops && !exact6;
   const bool aligned = ((int64_t)N * C * T * V) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
                        ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0;

@@ -740,8 +740,8 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
                               hipStream_t s) {
   if (!sp_fwd_bf16_supported(C, V, K, R, relu != 0)) return hipErrorInvalidValue;
   // all output channels per workgroup: the two-person graph, and V = 25 with
-  // K = 3 (STGCN_SPF_NARROW25: the 64-row k_sp_fwd_bf16 there, A/B only)
-  static const bool narrow25 = getenv("STGCN_SPF_NARROW25") != nullptr;
+  // K = 3 (STGCN_AB_SPF_NARROW25 build: the 64-row k_sp_fwd_bf16 there, A/B only)
+  constexpr bool narrow25 = STGCN_AB_SPF_NARROW25 != 0;
   const bool wide = V == 50 || (V == 25 && K == 3 && !narrow25 && (R <= 128 || !relu));
   const int nch = (C + 15) / 16;
   const int rows = !wide ? 64 : (R <= 64 ? 64 : (R <= 128 ? 128 : 256));
@@ -1024,8 +1024,8 @@ hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s) {
   // flight): cfg3 5289 vs 5155-5187, cfg5 2352 vs 2301-2303 clips/s against 2
   // slots (two workgroups per CU, one item of lookahead each) in one A/B call.
   // (Before the fragment reads were 16-byte vectors the loop was LDS-latency
-  // bound and 2 slots won: 5141 vs 5063.) STGCN_GK_SLOTS=2: A/B only.
-  static const bool two = getenv("STGCN_GK_SLOTS") && atoi(getenv("STGCN_GK_SLOTS")) == 2;
+  // bound and 2 slots won: 5141 vs 5063.) STGCN_AB_GK_SLOTS2 builds: A/B only.
+  constexpr bool two = STGCN_AB_GK_SLOTS2 != 0;
   static_assert(4 * WgGkGeo<128>::BUF <= 160 * 1024, "LDS budget");
 #define GK_LAUNCH(TR, NS) \
   hipLaunchKernelGGL((k_wgrad_gemm_gk<TR, NS>), dim3(nblk), dim3(WgGkGeo<TR>::NTH), \

@@ -578,7 +578,7 @@ __global__ void k_pack_spb_a(const float *A, __bf16 *img, int K, int V, int NP) 
 // STGCN_SPB_X3 selects it (A/B only).
 bool sp_bwd_fused_supported(int C, int V, int K, int R, int T, bool x3) {
   constexpr int D = SpBwdGeo<25, 3, false>::D, CMAX = SpBwdGeo<25, 3, false>::CMAX;
-  static const bool x3_on = getenv("STGCN_SPB_X3") != nullptr;
+  constexpr bool x3_on = STGCN_AB_SPB_X3 != 0;
   const bool shape = x3 ? (x3_on && V == 18 && K == 1) : (V == 25 && K == 3);
   return shape && C > 0 && C % 32 == 0 && C <= CMAX && R % 16 == 0 && R / 16 >= D &&
          (int64_t)std::max(R, C) * T * V * 4 < ((int64_t)1 << 31);

@@ -558,9 +558,9 @@ size_t conv_x3_wpk_bytes(const ConvGemmParams &p) {
 // 128-row tiles (two 32-row blocks per wave: half the weight and window
 // staging per MFMA, half the window re-reads over the row tiles) for the
 // 9-tap launches with a whole number of them and unit output stride
-// (STGCN_X3_MR1: 64-row tiles everywhere, A/B measurement only)
+// (STGCN_AB_X3_MR1 build: 64-row tiles everywhere, A/B measurement only)
 static bool x3_wide_rows(const ConvGemmParams &p) {
-  static const bool off = getenv("STGCN_X3_MR1") != nullptr;
+  constexpr bool off = STGCN_AB_X3_MR1 != 0;
   return !off && p.NQ == 9 && p.s_out == 1 && p.R % 128 == 0;
 }
 
@@ -634,9 +634,9 @@ hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
 }
 
 // The bf16 temporal-conv GEMMs (9 taps; stride-2 data-gradient phases 5 / 4) on
-// the one-plane k_conv_x3 (STGCN_OLD_BF16CONV: k_conv_bf16, A/B only)
+// the one-plane k_conv_x3 (STGCN_AB_OLD_BF16CONV build: k_conv_bf16, A/B only)
 bool conv_b1_supported(const ConvGemmParams &p) {
-  static const bool off = getenv("STGCN_OLD_BF16CONV") != nullptr;
+  constexpr bool off = STGCN_AB_OLD_BF16CONV != 0;
   if (off || p.C < 16) return false;
   if (p.V != 18 && p.V != 25 && p.V != 50) return false;
   if (p.FT != kTileCols / p.V) return false;

@@ -19,11 +19,19 @@ Use ``zero_grad()`` (zeroes the flat buffers, keeps the views) instead of
 the bucket view (the caller set ``.grad`` to None or replaced it), the hook
 copies it into the view and re-installs the view.
 
+Exactly one backward per ``synchronize()`` reduces. Gradient accumulation over
+several backward passes runs the earlier ones under ``with dp.no_sync():``
+(they only accumulate into the buckets, as DDP's no_sync); a second backward
+outside it, before ``synchronize()``, would add into a buffer whose
+all-reduce is in flight, so it raises before accumulating.
+
 The reference has no distributed code of its own (only
 PyTorch-Lightning's inherited Trainer flags could enable DDP); this is the
 MI355X-native counterpart of that DDP path. With ~2.7 M fp32 parameters
 (10.8 MB) per step the default 4 MB buckets give 3-4 collectives per step.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -58,8 +66,33 @@ class GradAllReduce:
                 off += p.numel()
             self._flat.append(flat)
         self._install_views()
+        self._sync = True
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
+        self._handles += [p.register_hook(self._guard(p)) for p in params]
         self._reset()
+
+    def _guard(self, p):
+        bi = self._bucket_of[p]
+
+        def check(grad):
+            # runs before autograd accumulates into p.grad (the bucket view)
+            if self._work[bi] is not None:
+                raise RuntimeError(
+                    "GradAllReduce: a second backward before synchronize() would accumulate "
+                    "into a bucket whose all-reduce is in flight; run the earlier "
+                    "micro-batches under `with dp.no_sync():`")
+            return grad
+        return check
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside only accumulate into the bucket views; the
+        next backward outside launches the all-reduce of the accumulated sum."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
 
     def _install_views(self):
         for p, v in self._view.items():
@@ -83,6 +116,8 @@ class GradAllReduce:
         if p.grad is not v:  # not accumulated into the bucket: move it there
             v.copy_(p.grad)
             p.grad = v
+        if not self._sync:
+            return
         bi = self._bucket_of[p]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:

@@ -99,3 +99,80 @@ def test_dp_allreduce_matches_mean_of_shards(world, bucket_bytes):
         assert worst < 1e-5, (rank, worst)
         assert same, rank
         assert nb >= 2
+
+
+def _accum_worker(rank, world, port, out_q):
+    """Two optimizer-free steps with dp.zero_grad() between them, a
+    no_sync() gradient accumulation, and the guard against a second backward
+    before synchronize() (the bucket-view race)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from stgcn_loader import load
+        pkg = load()
+        torch.manual_seed(0)
+        model = nn.Sequential(nn.Linear(6, 5), nn.Tanh(), nn.Linear(5, 3))
+        gen = torch.Generator().manual_seed(7)
+        xs = torch.randn(3, world, 4, 6, generator=gen)  # (micro-batch, rank, N, features)
+
+        def local_grads(*mbs):
+            ref = nn.Sequential(nn.Linear(6, 5), nn.Tanh(), nn.Linear(5, 3))
+            ref.load_state_dict(model.state_dict())
+            for mb in mbs:
+                ref(mb).square().sum().backward()
+            return [p.grad.clone() for p in ref.parameters()]
+
+        def mean_over_ranks(*mb_idx):
+            per = [local_grads(*[xs[i, r] for i in mb_idx]) for r in range(world)]
+            return [sum(g[j] for g in per) / world for j in range(len(per[0]))]
+
+        dp = pkg.dp.GradAllReduce(model, world, bucket_bytes=64)
+        errs = []
+        for step in range(2):  # two steps, zero_grad between them
+            dp.zero_grad()
+            model(xs[step, rank]).square().sum().backward()
+            dp.synchronize()
+            want = mean_over_ranks(step)
+            errs.append(max((p.grad - w).abs().max().item() for p, w in zip(model.parameters(), want)))
+        # accumulation: micro-batch 0 under no_sync, micro-batch 1 reduces the sum
+        dp.zero_grad()
+        with dp.no_sync():
+            model(xs[0, rank]).square().sum().backward()
+        model(xs[1, rank]).square().sum().backward()
+        dp.synchronize()
+        want = mean_over_ranks(0, 1)
+        errs.append(max((p.grad - w).abs().max().item() for p, w in zip(model.parameters(), want)))
+        # a second backward before synchronize() raises before accumulating
+        dp.zero_grad()
+        model(xs[2, rank]).square().sum().backward()
+        raised = False
+        try:
+            model(xs[2, rank]).square().sum().backward()
+        except RuntimeError as e:
+            raised = "no_sync" in str(e)
+        dp.synchronize()
+        want = mean_over_ranks(2)
+        errs.append(max((p.grad - w).abs().max().item() for p, w in zip(model.parameters(), want)))
+        out_q.put((rank, max(errs), raised))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_accumulation_and_double_backward_guard():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_accum_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, raised in res:
+        assert err < 1e-6, (rank, err)
+        assert raised, rank

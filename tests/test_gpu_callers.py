@@ -125,14 +125,25 @@ def _eval_case(pkg, case, residual, seed=0):
     return arrays, x, g
 
 
-@pytest.mark.parametrize("case,residual", [
-    ((64, 64, 1, 18, 1, 3, 40), False),
-    ((64, 128, 2, 25, 3, 2, 33), False),
-    ((3, 64, 1, 50, 3, 2, 20), False),
-    ((64, 64, 1, 18, 1, 3, 40), True),
-    ((64, 128, 2, 18, 1, 2, 37), True),
+@pytest.mark.parametrize("case,residual,gemm", [
+    ((64, 64, 1, 18, 1, 3, 40), False, "fp32"),
+    ((64, 128, 2, 25, 3, 2, 33), False, "fp32"),
+    ((3, 64, 1, 50, 3, 2, 20), False, "fp32"),
+    ((64, 64, 1, 18, 1, 3, 40), True, "fp32"),
+    ((64, 128, 2, 18, 1, 2, 37), True, "fp32"),
+    # eval mode on the fused bf16 spatial forward / backward
+    # (V = 25, K = 3, C_in >= 32: k_sp_fwd_wide + k_sp_bwd_fused, bf16 Z / dU
+    # storage at stride 1, the kept-bf16-G dW'), V = 50 (k_sp_fwd_wide +
+    # k_spatial_bwd6), and on the fp32 split path (x3), residual with a
+    # strided projection included (its dWr / dbr at the fp32 gate). The oracle
+    # takes the HIP run's final ReLU mask (ties at the bf16 resolution).
+    ((64, 64, 1, 25, 3, 2, 40), False, "bf16"),
+    ((64, 128, 2, 25, 3, 2, 33), False, "bf16"),
+    ((64, 64, 1, 50, 3, 2, 17), False, "bf16"),
+    ((64, 64, 1, 18, 1, 3, 40), False, "x3"),
+    ((64, 128, 2, 18, 1, 2, 37), True, "x3"),
 ])
-def test_block_eval_mode_backward(pkg, case, residual):
+def test_block_eval_mode_backward(pkg, case, residual, gemm):
     """Eval mode with gradients (frozen BatchNorm statistics): the backward
     treats the running statistics as constants, like nn.BatchNorm2d.eval()."""
     arrays, x, g = _eval_case(pkg, case, residual)
@@ -142,8 +153,10 @@ def test_block_eval_mode_backward(pkg, case, residual):
     torch.manual_seed(0)
     A = p["spatialConv.A"]
     with contextlib.redirect_stdout(io.StringIO()):
-        blk = pkg.SpatialTemporalConv(C_in, C_out, A, 9, stride, 4, dropout_rate=0.5,
-                                      residual=residual)
+        blk = pkg.SpatialTemporalConv(
+            C_in, C_out, A, 9, stride, 4, dropout_rate=0.5, residual=residual,
+            gemm_dtype=torch.bfloat16 if gemm == "bf16" else torch.float32,
+            f32_gemm="bf16x3" if gemm == "x3" else "mfma")
     sd = {k: v for k, v in p.items()}
     sd.update({k: v for k, v in b.items()})
     blk.load_state_dict(sd)
@@ -152,20 +165,41 @@ def test_block_eval_mode_backward(pkg, case, residual):
     y = blk(xd)
     y.backward(g.to(DEV))
     torch.cuda.synchronize()
-    p64 = {k: v.double().requires_grad_(True) for k, v in p.items()}
-    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
-    x64 = x.double().requires_grad_(True)
-    y64 = ref_cpu.block_forward(x64, p64, b64, stride, residual=residual, training=False,
-                                dtype=torch.float64)
-    y64.backward(g.double())
-    assert rel_to_max(y.detach().cpu().numpy(), y64.detach().numpy()) < TOL
-    assert rel_to_max(xd.grad.cpu().numpy(), x64.grad.numpy()) < TOL
-    names = dict(blk.named_parameters())
-    for k, v in p64.items():
-        err = rel_to_max(names[k].grad.cpu().double().numpy(), v.grad.numpy())
-        if k == "temporalConv.bias" and not residual:
-            err = rel_to_max(names[k].grad.cpu().double().numpy(), v.grad.numpy())
-        assert err < 2 * TOL, (k, err)
+
+    def oracle(dtype, gemm_bf16=False):
+        pp = {k: v.to(dtype).requires_grad_(True) for k, v in p.items()}
+        bb = {k: (v.to(dtype) if v.is_floating_point() else v) for k, v in b.items()}
+        xx = x.to(dtype).requires_grad_(True)
+        yy = ref_cpu.block_forward(xx, pp, bb, stride, residual=residual, training=False,
+                                   dtype=dtype, gemm_bf16=gemm_bf16,
+                                   relu_mask=(y.detach().cpu() > 0).to(dtype))
+        yy.backward(g.to(dtype))
+        out = {"y": yy.detach(), "grad.x": xx.grad}
+        out.update({"grad." + k: v.grad for k, v in pp.items()})
+        return out
+
+    want = oracle(torch.float64)
+    got = {"y": y.detach().cpu(), "grad.x": xd.grad.cpu()}
+    got.update({"grad." + k: v.grad.cpu() for k, v in blk.named_parameters()})
+    if gemm == "bf16":  # SURVEY §8c bf16 gate, or 3x the reference's own bf16-operand error
+        ref16 = oracle(torch.float32, gemm_bf16=True)
+        gate = {k: max(2e-2, 3 * rel_to_max(ref16[k].double().numpy(), w.double().numpy()))
+                for k, w in want.items()}
+        blk.gemm_dtype = torch.float32
+        with torch.no_grad():
+            y32 = blk(x.to(DEV))
+        assert not torch.equal(y32.cpu(), got["y"]), "bf16 kernels did not run"
+    else:
+        gate = {k: (TOL if k in ("y", "grad.x") else 2 * TOL) for k in want}
+    bad = []
+    for k, w in want.items():
+        if k == "grad.temporalConv.bias" and not residual:  # analytically 0
+            assert got[k].abs().max().item() < (1e-3 if gemm == "bf16" else 1e-5), k
+            continue
+        err = rel_to_max(got[k].double().numpy(), w.double().numpy())
+        if not err < gate[k]:
+            bad.append(f"{k}: {err:.2e} >= {gate[k]:.1e}")
+    assert not bad, "; ".join(bad)
     for k, v in blk.named_buffers():  # eval mode leaves the running statistics alone
         if "running" in k:
             assert torch.equal(v.cpu(), b[k]), k

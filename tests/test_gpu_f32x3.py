@@ -65,6 +65,10 @@ def test_f32x3_block_random(pkg, case):
         # spatial dW' = dZ G^T on the split products (k_wgrad_sp<.., X3>)
         k = "grad.spatialConv.W.weight"
         assert not torch.equal(got[k], ref[k]), "k_wgrad_sp X3 did not run"
+    if residual and (C_in != C_out or stride != 1):
+        # the strided projection's dWr / dbr: present in both
+        # runs, so _check held them to the fp32 gate above
+        assert "grad.apply_residual.weight" in got and "grad.apply_residual.bias" in got
 
 
 def test_f32x3_full_size_block(pkg):
