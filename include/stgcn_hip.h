@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 4
+#define STGCN_ABI_VERSION 5
 
 /* stgcn_desc_t.flags */
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
@@ -121,7 +121,11 @@ typedef struct stgcn_fwd_args {
   float *G;
   /* ABI 2, optional stack chaining (training): x_stats = [sum(C_in), sumsq(C_in)]
    * of x over (n,t,v) in fp64 (produced by the previous block's y_stats: the
-   * BN1 statistics pass is skipped); y_stats (out) = the same for y (C_out). */
+   * BN1 statistics pass is skipped); y_stats (out) = the same for y (C_out).
+   * ABI 5: y_stats holds 5 * C_out doubles; a non-residual block without
+   * dropout also writes, with its ReLU mask m = y > 0 and uhat = (U - mean2) *
+   * invstd2, [cnt = sum m | su = sum m uhat | xu = sum y uhat] after the two
+   * (the next block's deferred-dx chain, stgcn_bwd_args_t.x_stats). */
   const double *x_stats;
   double *y_stats;
   /* ABI 2, optional fused dropout on y (training only; st_graphconv.py:53-58,
@@ -162,6 +166,23 @@ typedef struct stgcn_bwd_args {
    * uhat from U instead. Null: reconstruct everywhere. */
   const float *prev_U;
   const float *prev_stats;
+  /* ABI 5, optional deferred dx (training, non-residual block, with the
+   * prev_* chain arguments above and prev_U / prev_stats): this block's BN1
+   * backward apply is folded into the PREVIOUS block's ReLU+BN2 backward
+   * apply. When the library takes it (*dx_deferred = 1; it does where its
+   * spatial-backward kernel reads the previous block's U in place of x), dx
+   * receives dxhat (the gradient at BN1's output) instead of the gradient of
+   * x, dx_coef (5 * C_in floats [a | md | mu | is | mdn]) the BN1 backward
+   * coefficients (dx = a * (dxhat - md - (x - mu) * is * mdn)) and prev_sums
+   * the previous block's dy_sums; the previous block's stgcn_block_bwd then
+   * takes dy = that dxhat with dy_coef = dx_coef and dy_sums = prev_sums.
+   * x_stats: the 5 * C_in y_stats the previous block's forward wrote. */
+  const double *x_stats;
+  float *dx_coef;
+  int32_t *dx_deferred;                 /* host int: 1 deferred, 0 dx written */
+  /* ABI 5, in: dy holds the next block's dxhat, to be combined as above with
+   * these 5 * C_out coefficients (needs dy_sums; non-residual, no dropout) */
+  const float *dy_coef;
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);

@@ -189,6 +189,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
 
 struct BwdLayout {
   double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
+  double *s1, *s2;  // deferred-dx chain: the prev-mode sums of the spatial backward
   float *dU, *dZ, *G, *H, *slab, *wpk;
   float *Wpk;  // W' = [W_0 | ... | W_{K-1}] (C_out, K*C_in) for the stacked H GEMM
   float *Rg;  // residual projection data-grad (N, C_in, T, V)
@@ -205,6 +206,8 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.sd = c.take<double>(C);
   L.sdn = c.take<double>(C);
   L.SdZ = c.take<double>((size_t)R * d->V);
+  L.s1 = c.take<double>(C);
+  L.s2 = c.take<double>(C);
   L.dbl_bytes = c.off;
   L.dU = c.take<float>((size_t)d->N * R * nTo(d));
   L.dZ = c.take<float>((size_t)d->N * R * nT(d));
@@ -565,9 +568,13 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * To * V, d->eps, d->momentum,
                              d->training, a->rm2, a->rv2, mean2, invstd2, s));
   double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
-  if (ys) HIP_TRY(hipMemsetAsync(ys, 0, sizeof(double) * 2 * R, s));
+  const Dropout ydrop = make_dropout(d, a->dropout_p, a->seed);
+  // (ABI 5: y_stats holds 5 * C_out sums; the last three -- over the ReLU mask --
+  // feed the next block's deferred-dx chain, meaningless under dropout)
+  if (ys) HIP_TRY(hipMemsetAsync(ys, 0, sizeof(double) * 5 * R, s));
   HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
-                             ys ? ys + R : nullptr, make_dropout(d, a->dropout_p, a->seed), s));
+                             ys ? ys + R : nullptr, ydrop, s,
+                             (ys && !ydrop.thresh) ? ys + 2 * R : nullptr));
   return STGCN_OK;
 }
 
@@ -589,6 +596,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     return fail(STGCN_E_INVALID, "dy_sums cannot be combined with dropout");
   if (!d->training && (a->dy_sums || a->prev_sums))
     return fail(STGCN_E_INVALID, "stack chaining applies to training mode only");
+  if (a->dy_coef && (!a->dy_sums || res || drop.thresh))
+    return fail(STGCN_E_INVALID, "dy_coef needs dy_sums, a non-residual block, no dropout");
   const BwdLayout L = bwd_layout(d, workspace);
   if (!workspace || workspace_bytes < L.total)
     return fail(STGCN_E_INVALID, "workspace too small");
@@ -611,7 +620,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     }
     HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
                                      L.sdu, N, R, To * V, d->training, drop, s,
-                                     du_bf16(d) ? 1 : 0));
+                                     du_bf16(d) ? 1 : 0, a->dy_coef));
     HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
     // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
@@ -714,11 +723,32 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s));
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
+  // Deferred dx (ABI 5): the BN1 backward apply of this block is folded into the
+  // previous block's ReLU+BN2 backward apply (launch_bn_relu_bwd_apply with
+  // dy_coef). The spatial backward then reads the previous block's U in place of
+  // x (PrevBn: x rebuilt, that block's mask / uhat sums), dx receives dxhat, and
+  // launch_chain_coef forms dg1 / db1, the coefficients and the previous block's
+  // ReLU+BN2 sums: dx never makes its own HBM round trip.
+  const bool defer = d->need_dx && d->training && !res && a->prev_g2 && a->prev_b2 &&
+                     a->prev_sums && a->prev_U && a->prev_stats && a->x_stats && a->dx_coef &&
+                     a->dx_deferred &&
+                     (fused_spb(d) || spatial_dx_prev_supported(N, C, T, V, K));
+  PrevBn pvb;
+  if (defer) {
+    pvb.mean = a->prev_stats;
+    pvb.invstd = a->prev_stats + C;
+    pvb.g = a->prev_g2;
+    pvb.b = a->prev_b2;
+    pvb.s1 = L.s1;
+    pvb.s2 = L.s2;
+  }
+  const float *xin = defer ? a->prev_U : a->x;
+  if (a->dx_deferred) *a->dx_deferred = defer ? 1 : 0;
   if (fused_spb(d)) {
     // H = W'^T dZ, dx = sum_k H_k A_k, dA, BN1 sums in one kernel (H stays on chip)
-    HIP_TRY(launch_sp_bwd_fused(L.dZ, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.wpk,
+    HIP_TRY(launch_sp_bwd_fused(L.dZ, xin, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.wpk,
                                 a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res,
-                                f32x3(d), s));
+                                f32x3(d), s, defer ? &pvb : nullptr));
   } else {
   {
     // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
@@ -750,8 +780,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     conv_tiles(p);
     HIP_TRY(launch_conv_gemm(p, s));
   }
-  HIP_TRY(launch_spatial_dx(L.H, a->x, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
-                            L.sdn, N, C, T, V, K, d->need_dx, res, bf16(d) ? 1 : 0, s));
+  HIP_TRY(launch_spatial_dx(L.H, xin, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
+                            L.sdn, N, C, T, V, K, d->need_dx, res, bf16(d) ? 1 : 0, s,
+                            defer ? &pvb : nullptr));
+  }
+  if (defer) {
+    HIP_TRY(launch_chain_coef(L.sd, L.sdn, mean1, invstd1, a->g1, L.s1, L.s2, a->x_stats, C,
+                              (int64_t)N * T * V, a->dg1, a->db1, a->dx_coef, a->prev_sums, s));
+    return STGCN_OK;
   }
   HIP_TRY(launch_bn_grads_out(L.sd, L.sdn, nullptr, C, a->dg1, a->db1, nullptr, s));
   // residual path gradient (added to dx after the BN1 backward)

@@ -26,6 +26,17 @@ __host__ __device__ inline bool dropout_keep(const Dropout &d, uint64_t e) {
   return (uint32_t)(z >> 32) >= d.thresh;
 }
 
+// Deferred-dx chain (ABI 5; capi.hip "deferred dx"): the spatial backward of
+// block i reads the PREVIOUS block's pre-BN2 tensor U in place of its input x
+// and rebuilds x = ReLU((U - mean) * invstd * g + b) exactly as that block's
+// output pass did; with the mask m = x > 0 and uhat = (U - mean) * invstd it
+// adds s1[c] += sum m * dxhat, s2[c] += sum m * dxhat * uhat (fp64). mean ==
+// nullptr: off (x read as is).
+struct PrevBn {
+  const float *mean = nullptr, *invstd = nullptr, *g = nullptr, *b = nullptr;
+  double *s1 = nullptr, *s2 = nullptr;
+};
+
 constexpr int kTileRows = 64;   // output rows per workgroup (2 MFMA 32-row tiles)
 constexpr int kTileCols = 256;  // max (frames x V) columns per workgroup (8 MFMA 32-col tiles)
 
@@ -140,10 +151,14 @@ hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, dou
 hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M,
                               float eps, float momentum, int training, float *rm, float *rv,
                               float *mean_out, float *invstd_out, hipStream_t s);
-// y = ReLU(BN(U)); ysum/ysq (or null): per-channel sum / sum of squares of y
+// y = ReLU(BN(U)); ysum/ysq (or null): per-channel sum / sum of squares of y;
+// yext (or null, 3*C: [cnt | su | xu]): with the ReLU mask m = y > 0 and
+// uhat = (U - mean) * invstd, cnt += sum m, su += sum m * uhat, xu += sum y * uhat
+// (the deferred-dx chain's forward sums)
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
-                              double *ysum, double *ysq, Dropout drop, hipStream_t s);
+                              double *ysum, double *ysq, Dropout drop, hipStream_t s,
+                              double *yext = nullptr);
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b,
                                      int N, int C, int L, double *sg, double *sgu, Dropout drop,
@@ -152,7 +167,22 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU,
                                     double *sdu, int N, int C, int L, int training,
-                                    Dropout drop, hipStream_t s, int du_bf16 = 0);
+                                    Dropout drop, hipStream_t s, int du_bf16 = 0,
+                                    const float *dy_coef = nullptr);
+// Deferred-dx chain: block i's BN1 backward folded into block i-1's ReLU+BN2
+// backward. dy_coef (5*C: [a | md | mu | is | mdn], launch_chain_coef) makes
+// launch_bn_relu_bwd_apply read dy as the next block's dxhat and form
+//   dy = a * (dxhat - md - (y - mu) * is * mdn),  y = ReLU((U - mean) * invstd * g + b)
+// (k_bn1_bwd_apply's arithmetic) instead of reading a materialised dy.
+// launch_chain_coef (block i, C = its C_in): from its BN1 sums sd / sdn, its BN1
+// statistics (mean1, invstd1, g1), the prev-mode sums s1 / s2 of its spatial
+// backward and xst (5*C: the previous block's output sums [sum | sumsq | cnt |
+// su | xu]) -> dg1 = sdn, db1 = sd, coef (5*C) and psum (2*C: the previous
+// block's [sum m dy | sum m dy uhat]). M = N*T*V.
+hipError_t launch_chain_coef(const double *sd, const double *sdn, const float *mean1,
+                             const float *invstd1, const float *g1, const double *s1,
+                             const double *s2, const double *xst, int C, int64_t M,
+                             float *dg1, float *db1, float *coef, double *psum, hipStream_t s);
 hipError_t launch_bn_grads_out(const double *sg, const double *sgu, const double *sdu, int C,
                                float *dgamma, float *dbeta, float *dbias, hipStream_t s);
 // add (same layout as dx, or null) is added after the BN1 backward (residual path)
@@ -187,7 +217,10 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b,
                              const float *A, float *dx, float *dA, double *sd, double *sdn,
                              int N, int C, int T, int V, int K, int write_dx, int relu,
-                             int bf16ops, hipStream_t s);
+                             int bf16ops, hipStream_t s, const PrevBn *prev = nullptr);
+// launch_spatial_dx takes a PrevBn for this shape (its k_spatial_bwd5 / _bwd6
+// paths; 16-byte aligned tensors assumed, as torch allocates them)
+bool spatial_dx_prev_supported(int N, int C, int T, int V, int K);
 
 // Fused spatial graph convolution of the bf16 path (kernels_fused.hip):
 // Z = W' (f(BN1(x)) A^T) + biasZ in one kernel (BN1 + joint contraction on MFMA
@@ -217,6 +250,7 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
                                const float *invstd, const float *g, const float *b,
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
-                               int write_dx, int relu, bool x3, hipStream_t s);
+                               int write_dx, int relu, bool x3, hipStream_t s,
+                               const PrevBn *prev = nullptr);
 
 }  // namespace stgcn

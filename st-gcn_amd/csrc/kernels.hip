@@ -1489,33 +1489,45 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
                                                      const float *invstd, const float *g,
                                                      const float *b, float *y, int C, int L,
-                                                     double *ysum, double *ysq, Dropout drop) {
+                                                     double *ysum, double *ysq, Dropout drop,
+                                                     double *yext) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
-  const float mu = mean[c], a = invstd[c] * g[c], be = b[c];
-  double s = 0.0, q = 0.0;
+  const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
+  double s = 0.0, q = 0.0, cnt = 0.0, su = 0.0, xu = 0.0;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float v[VEC];
     vld<VEC>(U + base + i, v);
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
+      const float uh = (v[j] - mu) * is;
       const float t = (v[j] - mu) * a + be;
       v[j] = t > 0.f ? t : 0.f;
       if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
       s += (double)v[j];
       q += (double)v[j] * (double)v[j];
+      if (yext && t > 0.f) {
+        cnt += 1.0;
+        su += (double)uh;
+        xu += (double)v[j] * (double)uh;
+      }
     }
     vst<VEC>(y + base + i, v);
   }
   if (ysum) block_sum2_atomic<256>(s, q, ysum + c, ysq + c, red);
+  if (yext) {
+    block_sum2_atomic<256>(cnt, su, yext + c, yext + C + c, red);
+    block_sum2_atomic<256>(xu, 0.0, yext + 2 * C + c, nullptr, red);
+  }
 }
 
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
-                              double *ysum, double *ysq, Dropout drop, hipStream_t s) {
+                              double *ysum, double *ysq, Dropout drop, hipStream_t s,
+                              double *yext) {
   STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, N), U, mean, invstd, g, b, y, C,
-                   L, ysum, ysq, drop);
+                   L, ysum, ysq, drop, yext);
   return hipGetLastError();
 }
 
@@ -1564,17 +1576,34 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
     const float *dy, const float *U, const float *mean, const float *invstd, const float *g,
     const float *b, const double *sg, const double *sgu, float *dU, double *sdu, int C, int L,
-    double invM, Dropout drop, int du_bf16) {
+    double invM, Dropout drop, int du_bf16, const float *dy_coef) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   const float mg = (float)(sg[c] * invM), mgu = (float)(sgu[c] * invM);
+  // deferred dx of the next block: dy = ca * (dxhat - cmd - (y - cmu) * cis * cmdn)
+  float ca = 0.f, cmd = 0.f, cmu = 0.f, cis = 0.f, cmdn = 0.f;
+  if (dy_coef) {
+    ca = dy_coef[c];
+    cmd = dy_coef[C + c];
+    cmu = dy_coef[2 * C + c];
+    cis = dy_coef[3 * C + c];
+    cmdn = dy_coef[4 * C + c];
+  }
   double s = 0.0;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float u[VEC], d[VEC], o[VEC];
     vld<VEC>(U + base + i, u);
     vld<VEC>(dy + base + i, d);
+    if (dy_coef) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float t = (u[j] - mu) * a + be;
+        const float yv = t > 0.f ? t : 0.f;  // this block's output, as k_bn_relu_fwd wrote it
+        d[j] = ca * (d[j] - cmd - (yv - cmu) * cis * cmdn);
+      }
+    }
     if (drop.thresh) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
@@ -1610,11 +1639,50 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU, double *sdu,
                                     int N, int C, int L, int training, Dropout drop,
-                                    hipStream_t s, int du_bf16) {
+                                    hipStream_t s, int du_bf16, const float *dy_coef) {
   // eval mode (constant running statistics): no batch-mean terms
   const double invM = training ? 1.0 / ((double)N * L) : 0.0;
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_apply, slice_vec(L, {dy, U, dU}), dim3(C, N), dy, U, mean,
-                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop, du_bf16);
+                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop, du_bf16, dy_coef);
+  return hipGetLastError();
+}
+
+// The deferred-dx chain's per-channel finalize (see internal.h): with
+// a = invstd1 g1, md = sd / M, mdn = sdn / M the next-to-be-applied dx is
+//   dx = a (dxhat - md - (x - mu1) invstd1 mdn)
+// and, x = ReLU(g2 uhat + b2) being the previous block's output (x = 0 off its
+// mask m), the previous block's ReLU+BN2 backward sums follow from the prev-mode
+// sums s1 = sum m dxhat, s2 = sum m dxhat uhat and that block's forward sums
+// (cnt = sum m, su = sum m uhat, sum x, xu = sum x uhat):
+//   sum m dx       = a (s1 - md cnt - mdn invstd1 (sum x - mu1 cnt))
+//   sum m dx uhat  = a (s2 - md su  - mdn invstd1 (xu    - mu1 su))
+__global__ void k_chain_coef(const double *sd, const double *sdn, const float *mean1,
+                             const float *invstd1, const float *g1, const double *s1,
+                             const double *s2, const double *xst, int C, double invM,
+                             float *dg1, float *db1, float *coef, double *psum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double md = sd[c] * invM, mdn = sdn[c] * invM;
+  const float af = invstd1[c] * g1[c];
+  const double a = (double)af, is = (double)invstd1[c], mu = (double)mean1[c];
+  const double sx = xst[c], cnt = xst[2 * C + c], su = xst[3 * C + c], xu = xst[4 * C + c];
+  dg1[c] = (float)sdn[c];
+  db1[c] = (float)sd[c];
+  coef[c] = af;
+  coef[C + c] = (float)md;
+  coef[2 * C + c] = mean1[c];
+  coef[3 * C + c] = invstd1[c];
+  coef[4 * C + c] = (float)mdn;
+  psum[c] = a * (s1[c] - md * cnt - mdn * is * (sx - mu * cnt));
+  psum[C + c] = a * (s2[c] - md * su - mdn * is * (xu - mu * su));
+}
+
+hipError_t launch_chain_coef(const double *sd, const double *sdn, const float *mean1,
+                             const float *invstd1, const float *g1, const double *s1,
+                             const double *s2, const double *xst, int C, int64_t M,
+                             float *dg1, float *db1, float *coef, double *psum, hipStream_t s) {
+  hipLaunchKernelGGL(k_chain_coef, dim3((C + 255) / 256), dim3(256), 0, s, sd, sdn, mean1,
+                     invstd1, g1, s1, s2, xst, C, 1.0 / (double)M, dg1, db1, coef, psum);
   return hipGetLastError();
 }
 
@@ -2102,6 +2170,35 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
   }
 }
 
+// Row-pass sums of k_spatial_bwd5 / _bwd6 (float sv[4]: sd, sdn and, in prev
+// mode, s1, s2 of PrevBn; ns of them), reduced per channel segment of the
+// block: a wave whose rows share one channel reduces once; LDS segment
+// accumulators (the kernel's __shared__ segv[4][MAXSEG]) when the block spans
+// few channels, else global fp64 atomics. (A macro: the LDS array must stay a
+// visible __shared__ object at the atomics, or hipcc mis-selects them.)
+#define STGCN_ROWPASS_SUMS(sv, ns, seg, ci)                                   \
+  do {                                                                        \
+    const int seg0_ = __builtin_amdgcn_readfirstlane(seg);                    \
+    if (__builtin_amdgcn_ballot_w64((seg) != seg0_) == 0) {                   \
+      for (int i_ = 0; i_ < (ns); ++i_) {                                     \
+        const double w_ = wave_sum((double)(sv)[i_]);                         \
+        if (lane == 0) {                                                      \
+          if (seg_lds)                                                        \
+            atomicAdd(&segv[i_][seg0_], w_);                                  \
+          else                                                                \
+            atomicAdd(gdst[i_] + (ci), w_);                                   \
+        }                                                                     \
+      }                                                                       \
+    } else {                                                                  \
+      for (int i_ = 0; i_ < (ns); ++i_) {                                     \
+        if (seg_lds)                                                          \
+          atomicAdd(&segv[i_][seg], (double)(sv)[i_]);                        \
+        else                                                                  \
+          atomicAdd(gdst[i_] + (ci), (double)(sv)[i_]);                       \
+      }                                                                       \
+    }                                                                         \
+  } while (0)
+
 // k_spatial_bwd5: the spatial backward with both joint contractions on MFMA.
 // Persistent and double-buffered like k_spatial_bwd4 (row blocks of RB rows,
 // contiguous in x, dx and per partition in H; H planes and x by 16-byte
@@ -2124,7 +2221,7 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx, int relu) {
+    int K, int64_t rows, int write_dx, int relu, PrevBn prev) {
   constexpr int VH = (V + 1) / 2;           // MFMA k-steps over v
   constexpr int NW = bwd5_nw(KMAX);         // waves
   constexpr int NH = NW / 4;                // reduction halves of the dx GEMM
@@ -2136,10 +2233,13 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
   constexpr int NRT = RB / 32;                    // 32-row tiles per block
   constexpr bool DREG = KMAX * NT * NT <= 4;      // dA accumulators resident in VGPRs
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
-  const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
+  __shared__ double segv[4][MAXSEG];  // [sd | sdn | s1 | s2] per channel segment
+  const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane (prev mode: U)
   float *dxs = smem + 2 * BUF;   // [RB][V]: reduction half 0, then dx
   float *dxs2 = dxs + PL;        // [RB][V]: reduction half 1 (NH == 2)
+  const bool pv = prev.mean != nullptr;
+  const int ns = pv ? 4 : 2;
+  double *const gdst[4] = {sd, sdn, prev.s1, prev.s2};
   float *dred = dxs + NH * PL;   // [K][DW][DW]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2211,7 +2311,7 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
   for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
     float *buf = smem + (it & 1) * BUF;
     float *Hs = buf, *xs = buf + K * PL;
-    if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
+    if (tid < MAXSEG) segv[0][tid] = segv[1][tid] = segv[2][tid] = segv[3][tid] = 0.0;
     __syncthreads();  // block blk staged (vmcnt(0)); previous block fully retired
     if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * BUF);
     const int r0 = blk * RB;
@@ -2258,40 +2358,38 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
       const int seg = n0 * C + ci - cfirst;
       const float mu = mean[ci], is = invstd[ci];
       const float a = is * g[ci], be = b[ci];
-      float s = 0.f, sn = 0.f;
+      // prev mode: the staged plane is the previous block's U; its output x =
+      // ReLU((U - pmu) * pa + pb) as that block's output pass formed it
+      const float pmu = pv ? prev.mean[ci] : 0.f, pis = pv ? prev.invstd[ci] : 1.f;
+      const float pa = pv ? pis * prev.g[ci] : 1.f, pb = pv ? prev.b[ci] : 0.f;
+      float sv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < (V + TPR - 1) / TPR; ++j) {
         const int w = part + j * TPR;
         if (w < V) {
-          const float xv = xs[rl * V + w];
+          float xv = xs[rl * V + w];
+          float uh = 0.f;
+          bool pm = false;
+          if (pv) {
+            const float t = (xv - pmu) * pa + pb;
+            uh = (xv - pmu) * pis;
+            pm = t > 0.f;
+            xv = pm ? t : 0.f;
+          }
           float d = NH == 2 ? dxs[rl * V + w] + dxs2[rl * V + w] : dxs[rl * V + w];
           const float bn = (xv - mu) * a + be;
           if (relu && bn <= 0.f) d = 0.f;  // ReLU'(BN1(x))
           dxs[rl * V + w] = d;
-          s += d;
-          sn = fmaf(d, (xv - mu) * is, sn);
+          sv[0] += d;
+          sv[1] = fmaf(d, (xv - mu) * is, sv[1]);
+          if (pm) {
+            sv[2] += d;
+            sv[3] = fmaf(d, uh, sv[3]);
+          }
           xs[rl * V + w] = relu ? fmaxf(bn, 0.f) : bn;
         }
       }
-      const int seg0 = __builtin_amdgcn_readfirstlane(seg);
-      if (__builtin_amdgcn_ballot_w64(seg != seg0) == 0) {
-        const double ws = wave_sum((double)s), wn = wave_sum((double)sn);
-        if (lane == 0) {
-          if (seg_lds) {
-            atomicAdd(&seg_s[seg0], ws);
-            atomicAdd(&seg_n[seg0], wn);
-          } else {
-            atomicAdd(sd + ci, ws);
-            atomicAdd(sdn + ci, wn);
-          }
-        }
-      } else if (seg_lds) {
-        atomicAdd(&seg_s[seg], (double)s);
-        atomicAdd(&seg_n[seg], (double)sn);
-      } else {
-        atomicAdd(sd + ci, (double)s);
-        atomicAdd(sdn + ci, (double)sn);
-      }
+      STGCN_ROWPASS_SUMS(sv, ns, seg, ci);
     }
     __syncthreads();  // BN1(x) rows and segment sums complete
     if (seg_lds && tid < MAXSEG) {
@@ -2300,8 +2398,7 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
       const int glast = (rlast / CT) * C + (rlast % CT) / T;
       if (gc <= glast) {
         const int cc = gc % C;
-        atomicAdd(sd + cc, seg_s[tid]);
-        atomicAdd(sdn + cc, seg_n[tid]);
+        for (int i = 0; i < ns; ++i) atomicAdd(gdst[i] + cc, segv[i][tid]);
       }
     }
     // dA partials on MFMA: wave takes row pairs kk = wave + 8j; accumulators
@@ -2359,14 +2456,16 @@ template <int V, int RB, int KT>
 static bool launch_bwd5(const float *H, const float *x, const float *mean, const float *invstd,
                         const float *g, const float *b, const float *A, float *dx, float *dA,
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
-                        int write_dx, int relu, hipStream_t s) {
+                        int write_dx, int relu, hipStream_t s, const PrevBn &prev,
+                        bool dry = false) {
   const size_t lds = bwd5_lds<V, RB>(K);
-  if (lds > 160 * 1024 - 512 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
-  const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 512))));
+  if (lds > 160 * 1024 - 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
+  const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 1024))));
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
   if (K != KT) return false;
+  if (dry) return true;
   hipLaunchKernelGGL((k_spatial_bwd5<V, RB, KT>), grid, dim3(bwd5_nw(KT) * 64), lds, s, H, x, mean, invstd, g,
-                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
+                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, prev);
   return true;
 }
 
@@ -2414,16 +2513,19 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx, int relu) {
+    int K, int64_t rows, int write_dx, int relu, PrevBn prev) {
   constexpr int RB = 64, NW = 8;
   static_assert(V > 32 && V <= 64, "two 32-column tiles");
   constexpr int MAXSEG = 32;
   constexpr int PL = (RB * V + 255) / 256 * 256;  // plane pitch: whole 16-byte DMA rounds
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ double seg_s[MAXSEG], seg_n[MAXSEG];
-  const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane
+  __shared__ double segv[4][MAXSEG];  // [sd | sdn | s1 | s2] per channel segment
+  const int BUF = (K + 1) * PL;  // one buffer: K H planes + x plane (prev mode: U)
   float *dxs = smem + 2 * BUF;   // [RB][V]: reduction half 0, then dx
   float *dxs2 = dxs + PL;        // [RB][V]: reduction half 1
+  const bool pv = prev.mean != nullptr;
+  const int ns = pv ? 4 : 2;
+  double *const gdst[4] = {sd, sdn, prev.s1, prev.s2};
   // f(BN1(x)) split into 3 bf16 planes, joint-major [w][row] (pitch XTP: 16-byte
   // row groups at an odd 16-byte stride), the dA GEMM's B operand
   constexpr int XTP = RB + 8, XTPL = V * XTP * 2;
@@ -2485,7 +2587,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
   for (int it = 0; blk < nblocks; ++it, blk += gridDim.x) {
     float *buf = smem + (it & 1) * BUF;
     float *Hs = buf, *xs = buf + K * PL;
-    if (tid < MAXSEG) seg_s[tid] = seg_n[tid] = 0.0;
+    if (tid < MAXSEG) segv[0][tid] = segv[1][tid] = segv[2][tid] = segv[3][tid] = 0.0;
     __syncthreads();  // block blk staged (vmcnt(0)); previous block fully retired
     if (blk + (int)gridDim.x < nblocks) stage(blk + gridDim.x, smem + ((it + 1) & 1) * BUF);
     const int r0 = blk * RB;
@@ -2540,18 +2642,32 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       const int seg = n0 * C + ci - cfirst;
       const float mu = mean[ci], is = invstd[ci];
       const float a = is * g[ci], be = b[ci];
-      float s = 0.f, sn = 0.f;
+      const float pmu = pv ? prev.mean[ci] : 0.f, pis = pv ? prev.invstd[ci] : 1.f;
+      const float pa = pv ? pis * prev.g[ci] : 1.f, pb = pv ? prev.b[ci] : 0.f;
+      float sv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < (V + TPR - 1) / TPR; ++j) {
         const int w = part + j * TPR;
         if (w < V) {
-          const float xv = xs[rl * V + w];
+          float xv = xs[rl * V + w];
+          float uh = 0.f;
+          bool pm = false;
+          if (pv) {  // prev mode: the staged plane is the previous block's U (see bwd5)
+            const float t = (xv - pmu) * pa + pb;
+            uh = (xv - pmu) * pis;
+            pm = t > 0.f;
+            xv = pm ? t : 0.f;
+          }
           float d = dxs[rl * V + w] + dxs2[rl * V + w];
           const float bn = (xv - mu) * a + be;
           if (relu && bn <= 0.f) d = 0.f;
           dxs[rl * V + w] = d;
-          s += d;
-          sn = fmaf(d, (xv - mu) * is, sn);
+          sv[0] += d;
+          sv[1] = fmaf(d, (xv - mu) * is, sv[1]);
+          if (pm) {
+            sv[2] += d;
+            sv[3] = fmaf(d, uh, sv[3]);
+          }
           const float f = relu ? fmaxf(bn, 0.f) : bn;
           const __bf16 fh = (__bf16)f;
           __bf16 *xt = reinterpret_cast<__bf16 *>(XT) + w * XTP + rl;
@@ -2564,25 +2680,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
           }
         }
       }
-      const int seg0 = __builtin_amdgcn_readfirstlane(seg);
-      if (__builtin_amdgcn_ballot_w64(seg != seg0) == 0) {
-        const double ws = wave_sum((double)s), wn = wave_sum((double)sn);
-        if (lane == 0) {
-          if (seg_lds) {
-            atomicAdd(&seg_s[seg0], ws);
-            atomicAdd(&seg_n[seg0], wn);
-          } else {
-            atomicAdd(sd + ci, ws);
-            atomicAdd(sdn + ci, wn);
-          }
-        }
-      } else if (seg_lds) {
-        atomicAdd(&seg_s[seg], (double)s);
-        atomicAdd(&seg_n[seg], (double)sn);
-      } else {
-        atomicAdd(sd + ci, (double)s);
-        atomicAdd(sdn + ci, (double)sn);
-      }
+      STGCN_ROWPASS_SUMS(sv, ns, seg, ci);
     }
     __syncthreads();  // BN1(x) rows, dx and segment sums complete
     if (seg_lds && tid < MAXSEG) {
@@ -2591,8 +2689,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       const int glast = (rlast / CT) * C + (rlast % CT) / T;
       if (gc <= glast) {
         const int cc = gc % C;
-        atomicAdd(sd + cc, seg_s[tid]);
-        atomicAdd(sdn + cc, seg_n[tid]);
+        for (int i = 0; i < ns; ++i) atomicAdd(gdst[i] + cc, segv[i][tid]);
       }
     }
     // dA tiles: dA_k[v in p2][w in q2] += sum_rows H_k[row][v] f(BN1(x))[row][w],
@@ -2663,16 +2760,18 @@ template <int V, int KT, bool BF>
 static bool launch_bwd6(const float *H, const float *x, const float *mean, const float *invstd,
                         const float *g, const float *b, const float *A, float *dx, float *dA,
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
-                        int write_dx, int relu, hipStream_t s) {
+                        int write_dx, int relu, hipStream_t s, const PrevBn &prev,
+                        bool dry = false) {
   constexpr int RB = 64;
   constexpr int PL = (RB * V + 255) / 256 * 256;
   const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 2) * PL) + 3 * (size_t)V * (RB + 8) * 2;
-  if (K != KT || lds > 160 * 1024 - 512 || ((int64_t)C * T) % RB != 0 ||
+  if (K != KT || lds > 160 * 1024 - 1024 || ((int64_t)C * T) % RB != 0 ||
       rows >= (int64_t)1 << 31)
     return false;
+  if (dry) return true;
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256));
   hipLaunchKernelGGL((k_spatial_bwd6<V, KT, BF>), grid, dim3(512), lds, s, H, x, mean, invstd, g, b,
-                     A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
+                     A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, prev);
   return true;
 }
 
@@ -3031,14 +3130,12 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
   for (int e = tid; e < KVV; e += 256) atomicAdd(dA + e, dAs[e]);
 }
 
-hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
-                             const float *invstd, const float *g, const float *b, const float *A,
-                             float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
-                             int V, int K, int write_dx, int relu, int bf16ops, hipStream_t s) {
+// the bwd5 / bwd6 launch (or, dry, whether one of them takes this shape)
+static bool launch_bwd56(const float *H, const float *x, const float *mean, const float *invstd,
+                         const float *g, const float *b, const float *A, float *dx, float *dA,
+                         double *sd, double *sdn, int N, int C, int T, int V, int K, int write_dx,
+                         int relu, bool bf6, hipStream_t s, const PrevBn &prev, bool dry) {
   constexpr bool joint3 = STGCN_AB_JOINT3 != 0;  // A/B builds only (ab_switches.h)
-  // (STGCN_AB_BWD6_EXACT: the exact-split k_spatial_bwd6 for bf16 blocks too)
-  constexpr bool exact6 = STGCN_AB_BWD6_EXACT != 0;
-  const bool bf6 = bf16ops && !exact6;
   const bool aligned = ((int64_t)N * C * T * V) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
                        ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0;
   if (!joint3 && aligned && K <= 3 && K * ((V + 1) / 2) * ((V + 31) / 32) <= 48) {
@@ -3046,7 +3143,7 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
     bool done = false;
 #define STGCN_BWD5(VV, RR, KK)                                                              \
   launch_bwd5<VV, RR, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, \
-                          relu, s)
+                          relu, s, prev, dry)
     // partitions K: 1 (uniform), 2 (distance), 3 (spatial) labelling
     if (V == 18)
       done = STGCN_BWD5(18, 128, 1) || STGCN_BWD5(18, 64, 1) || STGCN_BWD5(18, 128, 2) ||
@@ -3057,21 +3154,44 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
     else if (V == 50)
       done = STGCN_BWD5(50, 64, 1) || STGCN_BWD5(50, 64, 2) || STGCN_BWD5(50, 64, 3);
 #undef STGCN_BWD5
-    if (done) return hipGetLastError();
+    if (done) return true;
   }
   if (!joint3 && aligned && V == 50 && K <= 3) {  // two-person graph, 2 or 3 partitions
     const int64_t rows = (int64_t)N * C * T;
     bool done = false;
 #define STGCN_BWD6(KK, BF)                                                                     \
   launch_bwd6<50, KK, BF>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, \
-                          relu, s)
+                          relu, s, prev, dry)
     if (bf6)
       done = STGCN_BWD6(1, true) || STGCN_BWD6(2, true) || STGCN_BWD6(3, true);
     else
       done = STGCN_BWD6(1, false) || STGCN_BWD6(2, false) || STGCN_BWD6(3, false);
 #undef STGCN_BWD6
-    if (done) return hipGetLastError();
+    if (done) return true;
   }
+  return false;
+}
+
+bool spatial_dx_prev_supported(int N, int C, int T, int V, int K) {
+  // (16-byte aligned operands: any non-null aligned stand-in pointer)
+  const float *p = reinterpret_cast<const float *>(uintptr_t(256));
+  return launch_bwd56(p, p, nullptr, nullptr, nullptr, nullptr, nullptr, const_cast<float *>(p),
+                      nullptr, nullptr, nullptr, N, C, T, V, K, 1, 0, true, nullptr, PrevBn(), true);
+}
+
+hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
+                             const float *invstd, const float *g, const float *b, const float *A,
+                             float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
+                             int V, int K, int write_dx, int relu, int bf16ops, hipStream_t s,
+                             const PrevBn *prev) {
+  // (STGCN_AB_BWD6_EXACT: the exact-split k_spatial_bwd6 for bf16 blocks too)
+  constexpr bool exact6 = STGCN_AB_BWD6_EXACT != 0;
+  const bool bf6 = bf16ops && !exact6;
+  const PrevBn pv = prev ? *prev : PrevBn();
+  if (launch_bwd56(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, N, C, T, V, K, write_dx, relu,
+                   bf6, s, pv, false))
+    return hipGetLastError();
+  if (pv.mean) return hipErrorInvalidValue;  // (callers check spatial_dx_prev_supported)
   if (joint_fast(V) && K <= 3) {
     const int VP = (V + 3) & ~3;
     const int RB = bwd3_rows(V, K);

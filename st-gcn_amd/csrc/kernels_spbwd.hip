@@ -174,9 +174,10 @@ struct SpBwdGeo {
   static constexpr int OFF_X = OFF_W + D * W_BYTES;                        // fp32 [ci][RP]
   static constexpr int OFF_ST = OFF_X + CB * RP * 4;                        // fp32 [ci][SP]
   static constexpr int OFF_XB = (OFF_ST + CB * SP * 4 + 15) & ~15;          // bf16 image
-  static constexpr int OFF_TAB = (OFF_XB + NPLX * XB_PLANE + 15) & ~15;  // [mean|invstd|a|beta][CMAX]
-  static constexpr int OFF_SUM = OFF_TAB + 4 * CMAX * 4;  // [s | sn][CMAX] fp64
-  static constexpr int LDS = OFF_SUM + 2 * CMAX * 8;
+  // [mean|invstd|a|beta][CMAX] of BN1, then (prev mode) the same of the previous block's BN2
+  static constexpr int OFF_TAB = (OFF_XB + NPLX * XB_PLANE + 15) & ~15;
+  static constexpr int OFF_SUM = OFF_TAB + 8 * CMAX * 4;  // [s | sn | s1 | s2][CMAX] fp64
+  static constexpr int LDS = OFF_SUM + 4 * CMAX * 8;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(K * V * V * 4 <= D * RING_SLOT, "dA reduction fits the ring");
   static_assert(W_BYTES % 128 == 0 && WPW <= 64, "W' pieces per wave");
@@ -190,6 +191,7 @@ struct SpBwdParams {
   float *dx, *dA;
   double *sd, *sdn;
   int C, R, T, ncb, nft, nitems, write_dx, relu;
+  PrevBn prev;  // prev mode (internal.h): x is the previous block's U
 };
 
 template <int V, int K, bool X3>
@@ -210,14 +212,24 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
   // ---- prologue: BN tables of all channels, zeroed sums and zero row, A image
   float *tab = reinterpret_cast<float *>(lds + G::OFF_TAB);
   double *sums = reinterpret_cast<double *>(lds + G::OFF_SUM);
+  const bool pv = P.prev.mean != nullptr;
   for (int c = tid; c < P.C; c += 512) {
     const float is = P.invstd[c];
     tab[c] = P.mean[c];
     tab[G::CMAX + c] = is;
     tab[2 * G::CMAX + c] = is * P.g[c];
     tab[3 * G::CMAX + c] = P.b[c];
+    if (pv) {
+      const float pis = P.prev.invstd[c];
+      tab[4 * G::CMAX + c] = P.prev.mean[c];
+      tab[5 * G::CMAX + c] = pis;
+      tab[6 * G::CMAX + c] = pis * P.prev.g[c];
+      tab[7 * G::CMAX + c] = P.prev.b[c];
+    }
     sums[c] = 0.0;
     sums[G::CMAX + c] = 0.0;
+    sums[2 * G::CMAX + c] = 0.0;
+    sums[3 * G::CMAX + c] = 0.0;
   }
   for (int e = tid; e < G::NPLX * (G::XBP / 4); e += 512) {
     const int p = e / (G::XBP / 4), q = e - p * (G::XBP / 4);
@@ -405,6 +417,11 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       const int c = cb * G::CB + ci;
       const float mu = tab[c], is = tab[G::CMAX + c];
       const float a = tab[2 * G::CMAX + c], be = tab[3 * G::CMAX + c];
+      // prev mode: the x slice holds the previous block's U; x = ReLU((U - pmu) pa + pb)
+      // as that block's output pass formed it, mask m = x > 0, uhat = (U - pmu) pis
+      const float pmu = pv ? tab[4 * G::CMAX + c] : 0.f, pis = pv ? tab[5 * G::CMAX + c] : 1.f;
+      const float pa = pv ? tab[6 * G::CMAX + c] : 1.f, pb = pv ? tab[7 * G::CMAX + c] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
       // slot of channel ci: 16 ks + 8 hi + j for ci = 16 ks + (j & 3) + 8 (j >> 2) + 4 hi
       const int rr = ci & 15;
       const int slot = 16 * (ci >> 4) + 8 * ((rr >> 2) & 1) + (rr & 3) + 4 * (rr >> 3);
@@ -425,11 +442,23 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       for (int q = 0; q < NQ; ++q) {
         const int pos = part + 16 * q;
         const bool live = pos < nlive;
+        bool pm = false;
+        float uh = 0.f;
+        if (pv) {
+          const float t = (xq[q] - pmu) * pa + pb;
+          uh = (xq[q] - pmu) * pis;
+          pm = t > 0.f;
+          xq[q] = pm ? t : 0.f;
+        }
         const float bn = (xq[q] - mu) * a + be;
         float d = live ? dq[q] : 0.f;
         if (P.relu && bn <= 0.f) d = 0.f;  // ReLU'(BN1(x))
         s += d;
         sn = fmaf(d, (xq[q] - mu) * is, sn);
+        if (pm) {
+          s1 += d;
+          s2 = fmaf(d, uh, s2);
+        }
         if (P.write_dx && live) dst[pos] = d;
         if (pos < G::NPOS) {
           const float fx = live ? (P.relu ? fmaxf(bn, 0.f) : bn) : 0.f;
@@ -444,15 +473,23 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
           }
         }
       }
-      double ds = s, dn = sn;
+      double ds = s, dn = sn, d1 = s1, d2 = s2;
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) {
         ds += __shfl_xor(ds, o, 64);
         dn += __shfl_xor(dn, o, 64);
+        if (pv) {
+          d1 += __shfl_xor(d1, o, 64);
+          d2 += __shfl_xor(d2, o, 64);
+        }
       }
       if (part == 0) {  // one writer per channel per item
         sums[c] += ds;
         sums[G::CMAX + c] += dn;
+        if (pv) {
+          sums[2 * G::CMAX + c] += d1;
+          sums[3 * G::CMAX + c] += d2;
+        }
       }
     }
     spb_barrier();  // f(BN1(x)) image complete; the x slice and dx row image free
@@ -511,6 +548,10 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     for (int c = tid; c < P.C; c += 512) {
       atomicAdd(P.sd + c, sums[c]);
       atomicAdd(P.sdn + c, sums[G::CMAX + c]);
+      if (pv) {
+        atomicAdd(P.prev.s1 + c, sums[2 * G::CMAX + c]);
+        atomicAdd(P.prev.s2 + c, sums[3 * G::CMAX + c]);
+      }
     }
   }
 }
@@ -608,7 +649,8 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
                                const float *invstd, const float *g, const float *b,
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
-                               int write_dx, int relu, bool x3, hipStream_t s) {
+                               int write_dx, int relu, bool x3, hipStream_t s,
+                               const PrevBn *prev) {
   if (!sp_bwd_fused_supported(C, V, K, R, T, x3)) return hipErrorInvalidValue;
   const int npw = x3 ? 3 : 1, npa = x3 ? 3 : 2;
   __bf16 *aimg = reinterpret_cast<__bf16 *>(wpk);
@@ -637,6 +679,7 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
   P.nitems = N;
   P.write_dx = write_dx;
   P.relu = relu;
+  if (prev) P.prev = *prev;
   if (x3) return launch_spb<18, 1, true>(P, s);
   return launch_spb<25, 3, false>(P, s);
 }

@@ -44,12 +44,20 @@ class Link:
     """Hand-over between two chained blocks in backward: the later block
     computes the earlier block's ReLU+BN2 backward sums while writing its dx
     (``sums``); the earlier block uses them only if the gradient it receives is
-    that very dx tensor, unmodified (``dx_ref`` / ``dx_version``)."""
+    that very dx tensor, unmodified (``dx_ref`` / ``dx_version``).
+
+    Deferred dx (ABI 5, ``coef`` set): the later block left dxhat in that
+    tensor (its BN1 backward apply is folded into the earlier block's ReLU+BN2
+    backward pass, which takes ``coef``). Within ``model.STGCNStack`` the tensor
+    goes straight from one block's backward to the other's; if anything
+    replaced or modified it in between, the true gradient was never formed and
+    the earlier block raises instead of using it."""
 
     def __init__(self):
         self.sums = None
         self.dx_ref = None
         self.dx_version = None
+        self.coef = None
 
     def valid_for(self, dy):
         return (self.sums is not None and self.dx_ref is not None and self.dx_ref() is dy
@@ -75,20 +83,32 @@ class ChainCtx:
 
 
 def _chain_bwd_args(cc, dy, need_dx, C_in, dev):
-    """(dy_sums, prev_g2, prev_b2, prev_sums, prev_U, prev_stats) for stgcn_block_bwd."""
+    """(dy_sums, dy_coef, prev_g2, prev_b2, prev_sums, prev_U, prev_stats, x_stats,
+    dx_coef) for stgcn_block_bwd."""
+    none = (None,) * 9
     if cc is None:
-        return None, None, None, None, None, None
-    dy_sums = cc.out_link.sums if (cc.out_link is not None and cc.out_link.valid_for(dy)) \
-        else None
+        return none
+    dy_sums = dy_coef = None
+    link = cc.out_link
+    if link is not None and link.sums is not None:
+        if link.valid_for(dy):
+            dy_sums, dy_coef = link.sums, link.coef
+        elif link.coef is not None:
+            raise RuntimeError(
+                "STGCNStack chain: the gradient between two chained blocks was replaced or "
+                "modified in backward (a hook?); the deferred-dx chain cannot form it")
     if cc.in_link is not None and need_dx:
         prev_sums = torch.empty(2 * C_in, device=dev, dtype=torch.float64)
-        return dy_sums, cc.prev_g2, cc.prev_b2, prev_sums, cc.prev_U, cc.prev_stats
-    return dy_sums, None, None, None, None, None
+        dx_coef = torch.empty(5 * C_in, device=dev, dtype=torch.float32)
+        return (dy_sums, dy_coef, cc.prev_g2, cc.prev_b2, prev_sums, cc.prev_U, cc.prev_stats,
+                cc.x_stats, dx_coef)
+    return (dy_sums, dy_coef) + (None,) * 7
 
 
-def _chain_publish(cc, prev_sums, dx):
+def _chain_publish(cc, prev_sums, dx, dx_coef=None):
     if prev_sums is not None:
         cc.in_link.sums = prev_sums
+        cc.in_link.coef = dx_coef
         cc.in_link.dx_ref = weakref.ref(dx)
         cc.in_link.dx_version = dx._version
 
@@ -179,8 +199,9 @@ class StgcnBlockFn(torch.autograd.Function):
         C_out = Wt.shape[0]
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
                          need_dx=need_dx, **_gemm_flags(ctx.gemm))
-        dy_sums, pg2, pb2, psums, pU, pst = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1],
-                                                            x.device)
+        dy_sums, dy_coef, pg2, pb2, psums, pU, pst, xst, dx_coef = _chain_bwd_args(
+            ctx.cc, dy, need_dx, x.shape[1], x.device)
+        deferred = ctypes.c_int32(0)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
         dbWt = torch.empty(C_out, device=x.device, dtype=torch.float32)
@@ -191,11 +212,14 @@ class StgcnBlockFn(torch.autograd.Function):
             dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
             None, None, None, None, None, G, dy_sums, pg2, pb2, psums)], *ctx.drop,
-            prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst))
+            prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst), x_stats=hip_lib.ptr(xst),
+            dx_coef=hip_lib.ptr(dx_coef),
+            dx_deferred=ctypes.addressof(deferred) if dx_coef is not None else None,
+            dy_coef=hip_lib.ptr(dy_coef))
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))
-        _chain_publish(ctx.cc, psums, dx)
+        _chain_publish(ctx.cc, psums, dx, dx_coef if deferred.value else None)
         dA, dW, dbW, dWt = grads
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,
                 None, None, None, None, None, None, None, None, None, None, None, None)
@@ -271,7 +295,8 @@ class StgcnResBlockFn(torch.autograd.Function):
         dg1, db1, dg2, db2 = (torch.empty_like(t) for t in (g1, b1, g2, b2))
         dWr = torch.empty_like(Wr) if Wr is not None else None
         dbr = torch.empty(C_out, device=dev, dtype=torch.float32) if Wr is not None else None
-        _, pg2, pb2, psums, pU, pst = _chain_bwd_args(ctx.cc, dy, need_dx, x.shape[1], dev)
+        _, _, pg2, pb2, psums, pU, pst, _, _ = _chain_bwd_args(ctx.cc, dy, need_dx,
+                                                               x.shape[1], dev)
         nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         args = _args(hip_lib.BwdArgs, [hip_lib.ptr(t) for t in (

@@ -17,8 +17,11 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libstgcn_hip.so")
 if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in-tree only
+    # an explicitly built A/B variant (build.py variant=...); loading it says so
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
-ABI_VERSION = 4
+    import sys
+    print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
+ABI_VERSION = 5
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -54,7 +57,9 @@ class BwdArgs(ctypes.Structure):
         "G",                                   # ABI 2: optional kept joint contraction
         "dy_sums", "prev_g2", "prev_b2", "prev_sums")  # ABI 2: optional stack chaining
     ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)  # ABI 2: fused dropout
-         ] + [("prev_U", _vp), ("prev_stats", _vp)]  # ABI 4: chain conditioning fallback
+         ] + [("prev_U", _vp), ("prev_stats", _vp)  # ABI 4: chain conditioning fallback
+              ] + [("x_stats", _vp), ("dx_coef", _vp), ("dx_deferred", _vp),  # ABI 5:
+                   ("dy_coef", _vp)]                                         # deferred dx
 
 
 class SpatialDesc(ctypes.Structure):  # ABI 4: SpatialConv on its own

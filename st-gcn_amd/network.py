@@ -128,7 +128,8 @@ class SpatialTemporalConv(nn.Module):
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:
             # not with dropout on that output, nor for the residual block)
-            cc = ChainCtx(y_stats=torch.empty(2 * self.temporalConv.out_channels,
+            # (y_stats: [sum | sumsq | cnt | su | xu] per output channel, ABI 5)
+            cc = ChainCtx(y_stats=torch.empty(5 * self.temporalConv.out_channels,
                                               device=x.device, dtype=torch.float64),
                           out_link=None if (self.residual or drop > 0) else Link())
             if chain.y is not None and x is chain.y and x._version == chain.y_version:

@@ -222,6 +222,87 @@ def test_stack_chain_matches_unchained(pkg, residual, drop):
             assert rel_to_max(a.cpu().numpy(), b.cpu().numpy()) < 1e-5, k
 
 
+@pytest.mark.parametrize("V,K,gemm,T", [(18, 1, "fp32", 40), (18, 1, "x3", 300),
+                                         (25, 3, "bf16", 40), (50, 3, "bf16", 24),
+                                         (25, 3, "fp32", 40)])
+def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
+    """ABI 5 deferred dx: inside the chained stack every block's BN1 backward
+    apply is folded into the previous block's ReLU+BN2 backward pass (dx keeps
+    dxhat; the spatial backward reads the previous block's U: k_spatial_bwd5 at
+    V = 18 / 25 fp32, k_sp_bwd_fused at V = 25 bf16, k_spatial_bwd6 at V = 50).
+    The chained stack must equal the blocks run one by one, and the deferral
+    must have run on every link."""
+    gr = pkg.graph
+    if K == 1:
+        A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(V))
+    else:
+        A = gr.get_normalized_adjacency_matrices(2, 1, distances=gr.synthetic_distances(V),
+                                                 graph=gr.graph_for(V))
+    kw = dict(gemm_dtype=torch.bfloat16 if gemm == "bf16" else torch.float32,
+              f32_gemm="bf16x3" if gemm == "x3" else "mfma")
+    deferred = []
+    orig = pkg.fused._chain_publish
+
+    def spy(cc, prev_sums, dx, dx_coef=None):
+        if prev_sums is not None:
+            deferred.append(dx_coef is not None)
+        return orig(cc, prev_sums, dx, dx_coef)
+
+    monkeypatch.setattr(pkg.fused, "_chain_publish", spy)
+    torch.manual_seed(5)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 10, A, **kw).cuda().train()
+        m2 = pkg.STGCNStack(3, 10, A, **kw).cuda().train()
+    m2.load_state_dict(m1.state_dict())
+    N = 4
+    x = torch.randn(N, 3, T, V, generator=torch.Generator().manual_seed(6)).cuda()
+    lab = torch.randint(0, 10, (N,), generator=torch.Generator().manual_seed(7)).cuda()
+    out1 = m1.forward_nctv(x)                      # chained (deferred dx)
+    h = x
+    for blk in m2.conv:                            # unchained
+        h = blk(h)
+    out2 = m2.fc_layer(h.flatten(2).mean(dim=2))
+    torch.nn.functional.cross_entropy(out1, lab).backward()
+    torch.nn.functional.cross_entropy(out2, lab).backward()
+    torch.cuda.synchronize()
+    assert deferred == [True] * 9, deferred        # blocks 9..1 each deferred their dx
+    assert rel_to_max(out1.detach().cpu().numpy(), out2.detach().cpu().numpy()) < \
+        (1e-3 if gemm == "bf16" else 1e-5)
+    bad = []
+    for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
+        assert np.isfinite(ga).all(), k
+        if np.abs(gb).max() == 0 or k.endswith("temporalConv.bias"):  # (analytically 0)
+            continue
+        if gemm == "bf16":  # summation order through bf16 roundings
+            tol = 2e-2
+        else:
+            tol = 2e-3 if k.endswith("spatialConv.A") else 5e-4 if ".batch_n" in k else 1e-4
+        err = rel_to_max(ga, gb)
+        if err > tol:
+            bad.append(f"{k}: {err:.2e} > {tol:.0e}")
+    assert not bad, "; ".join(bad)
+
+
+def test_stack_deferred_dx_guard(pkg):
+    """A gradient hook that replaces the tensor between two chained blocks
+    (where dx holds dxhat) makes the earlier block raise, not compute garbage."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    torch.manual_seed(5)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = pkg.STGCNStack(3, 10, A).cuda().train()
+    x = torch.randn(2, 3, 20, 18, generator=torch.Generator().manual_seed(6)).cuda()
+    chain = pkg.network.StackChain()
+    h = x
+    for i, blk in enumerate(m.conv):
+        h = blk(h, chain=chain)
+        if i == 4:
+            h.register_hook(lambda g: g * 1.0)     # a new tensor replaces the chain's dx
+    with pytest.raises(RuntimeError, match="deferred-dx"):
+        h.sum().backward()
+
+
 def test_stack_bf16_cfg3_shape(pkg):
     """cfg3 (NTU V=25, K=3 spatial partitioning, 60 classes) stack with bf16
     channel GEMMs at N=4, T=40, one training step: logits and loss against the
