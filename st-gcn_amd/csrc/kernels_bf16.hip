@@ -304,7 +304,8 @@ hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s) {
 // NQ = 9 (temporal taps) or 1 (spatial W, residual projection). Output tile
 // 64 rows x CB channels x NQ taps; waves = (row half) x (32-channel block) x
 // (tap group: taps 0-4 / 5-8 for NQ = 9). Work item = (clip n, FT frames of P);
-// the split-K over items is S-way (grid = tiles x S), items s, s+S, ...
+// the split-K over items is S-way (grid = S x tiles, a split's tiles adjacent),
+// each split a contiguous run of items
 // The reduction index is the (frame, joint) position with the joint axis
 // padded to Vp = round4(V) (P's pad positions are zero, so Q's are don't-care).
 // k-step s (16 positions): lane half h takes the position 4-groups 2s, 2s+1 of
@@ -360,11 +361,15 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hi = lane >> 5, lo = lane & 31;
-  int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = bid % p.S;
-  bid /= p.S;
-  const int jt = bid % p.n_jtiles;
-  const int rt = bid / p.n_jtiles;
+  // the tiles of one split are adjacent in the XCD-remapped grid (they read the
+  // same items: P rows shared by the column tiles, Q rows by the row tiles, in
+  // one L2), and a split takes a CONTIGUOUS run of items (consecutive frame
+  // tiles of a clip: the next item's Q halo is mostly this item's frames, L2-hot)
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = p.n_rtiles * p.n_jtiles;
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int jt = tile % p.n_jtiles;
+  const int rt = tile / p.n_jtiles;
   const int r0 = rt * 64, c0 = jt * CB;
   const int mi = wave & 1;
   const int cj = (wave >> 1) % (CB / 32);
@@ -372,6 +377,8 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
   // first tap and tap count of this wave's group
   const int q0 = G::TG == 2 ? 5 * tq : (G::TG == 4 ? (tq ? 1 + 2 * tq : 0) : 0);
   const int nitems = p.N * p.n_mtiles;
+  const int per = (nitems + p.S - 1) / p.S;
+  const int it0 = min(nitems, split * per), it1 = min(nitems, it0 + per);
 
   // lane bases (elements) of the A (P) and B (Q) fragments
   const int pa = (mi * 32 + lo) * G::PPITCH + hi * G::HF * G::Vp;
@@ -527,9 +534,8 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
     }
   };
 
-  int item = split;
-  if (item < nitems) {
-    const ItemRef ir = item_ref(item);
+  if (it0 < it1) {
+    const ItemRef ir = item_ref(it0);
     load_part(ir, std::integral_constant<int, 0>{});
     write_part(lds, std::integral_constant<int, 0>{});
     load_part(ir, std::integral_constant<int, 1>{});
@@ -551,12 +557,12 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-    for (int it = 0, itm = item; itm < nitems; ++it, itm += p.S) {
+    for (int it = 0, itm = it0; itm < it1; ++it, ++itm) {
       __syncthreads();
       const char *cur = lds + (it & 1) * G::BUF;
       char *nxt = lds + ((it + 1) & 1) * G::BUF;
-      const bool more = itm + p.S < nitems;
-      const ItemRef nir = item_ref(more ? itm + p.S : itm);
+      const bool more = itm + 1 < it1;
+      const ItemRef nir = item_ref(more ? itm + 1 : itm);
       item_body(acc, cur, nxt, more, nir, nt_c);
     }
     // partial tile -> slab[split][r][c*NQ + q]

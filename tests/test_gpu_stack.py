@@ -169,6 +169,9 @@ def test_stack_chain_small_bn2_gamma(pkg, residual, gemm):
         assert np.isfinite(ga).all(), k
         if np.abs(gb).max() == 0:
             continue
+        if k.endswith("temporalConv.bias") and not residual:  # analytically 0: rounding noise
+            assert np.abs(ga).max() < 1e-4, (k, np.abs(ga).max())
+            continue
         if gemm == "bf16":  # chain-vs-unchained summation order through bf16 roundings
             tol = 2e-2
         else:
@@ -211,6 +214,9 @@ def test_stack_chain_matches_unchained(pkg, residual, drop):
     for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
         if np.abs(gb).max() == 0:
+            continue
+        if k.endswith("temporalConv.bias") and not residual:  # analytically 0: rounding noise
+            assert np.abs(ga).max() < 1e-4, (k, np.abs(ga).max())
             continue
         tol = 2e-3 if k.endswith("spatialConv.A") else 1e-4
         err = rel_to_max(ga, gb)
@@ -272,7 +278,10 @@ def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
     for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
         assert np.isfinite(ga).all(), k
-        if np.abs(gb).max() == 0 or k.endswith("temporalConv.bias"):  # (analytically 0)
+        if k.endswith("temporalConv.bias"):  # analytically 0: rounding noise
+            assert np.abs(ga).max() < (1e-3 if gemm == "bf16" else 1e-4), (k, np.abs(ga).max())
+            continue
+        if np.abs(gb).max() == 0:
             continue
         if gemm == "bf16":  # summation order through bf16 roundings
             tol = 2e-2
