@@ -1,5 +1,5 @@
 """Time the spatial backward (stgcn_time_kernel which=4: k_sp_bwd_fused, or the
-H GEMM + joint kernel with STGCN_UNFUSED_SPB) at the cfg3 / cfg5 layer shapes
+H GEMM + joint kernel in an STGCN_AB_UNFUSED_SPB=1 variant build) at the cfg3 / cfg5 layer shapes
 (bf16 path, K = 3) or the cfg2 shapes (KB_V=18: fp32 split path, K = 1).
 Usage: KB_V=25 python scripts/kbench_spb.py [iters]"""
 import ctypes
