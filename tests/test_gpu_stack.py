@@ -173,7 +173,9 @@ def test_stack_chain_small_bn2_gamma(pkg, residual, gemm):
             assert np.abs(ga).max() < 1e-4, (k, np.abs(ga).max())
             continue
         if gemm == "bf16":  # chain-vs-unchained summation order through bf16 roundings
-            tol = 2e-2
+            # (the first block's BN1 parameters end the deepest backward path: bf16
+            # noise there reaches ~20% vs exact, test_stack_bf16_cfg3_shape)
+            tol = 1e-1 if k.startswith("conv.0.batch_n.") else 2e-2
         else:
             tol = 2e-3 if k.endswith("spatialConv.A") else 1e-4
         err = rel_to_max(ga, gb)
@@ -283,8 +285,8 @@ def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
             continue
         if np.abs(gb).max() == 0:
             continue
-        if gemm == "bf16":  # summation order through bf16 roundings
-            tol = 2e-2
+        if gemm == "bf16":  # summation order through bf16 roundings (deep end: see above)
+            tol = 1e-1 if k.startswith("conv.0.batch_n.") else 2e-2
         else:
             tol = 2e-3 if k.endswith("spatialConv.A") else 5e-4 if ".batch_n" in k else 1e-4
         err = rel_to_max(ga, gb)
