@@ -78,6 +78,51 @@ def gate_stack_grads(model, g64, g32, skip=("temporalConv.bias",)):
     assert not bad, "; ".join(bad)
 
 
+def snapshot_stack(model):
+    """(params, buffers) of a stack in state_dict naming, on the CPU: the
+    oracle's starting point for a run of ``model``."""
+    p0 = {k: v.detach().cpu().clone() for k, v in model.named_parameters()}
+    b0 = {k: v.detach().cpu().clone() for k, v in model.named_buffers()}
+    return p0, b0
+
+
+def gate_chained_vs_oracle(model, p0, b0, x_nctv, lab, masks, gemm, residual=False):
+    """The deferred-dx chain changes the arithmetic of the BN2 backward sums
+    (formed from the spatial backward's mask sums instead of summing a
+    materialised dx), so a chained run is no longer bit-close to the unchained
+    one on the BN-affine / A gradients, which the 10-block stack conditions
+    badly (the fp32 reference's own error reaches several %).
+    Both are held to the fp64 oracle instead, through the chained run's ReLU
+    masks: fp32 modes at max(1e-4, 3x the fp32 oracle's error) per tensor,
+    bf16 at max(2e-2, 4x the bf16-operand oracle's error)."""
+    x_ntvc = x_nctv.detach().cpu().permute(0, 2, 3, 1).contiguous()
+    lab = lab.cpu()
+
+    def run(dtype, bf16):
+        p = {k: v.clone().to(dtype).requires_grad_(True) for k, v in p0.items()}
+        b = {k: (v.clone().to(dtype) if v.is_floating_point() else v.clone())
+             for k, v in b0.items()}
+        st = ref_cpu.Stack(p, b, residual=residual)
+        lg = st.forward(x_ntvc, dtype=dtype, gemm_bf16=bf16,
+                        relu_masks=[m.to(dtype) for m in masks])
+        torch.nn.functional.cross_entropy(lg, lab).backward()
+        return {k: v.grad for k, v in p.items()}
+
+    g64 = run(torch.float64, False)
+    gref = run(torch.float32, gemm == "bf16")
+    lim, fac = (2e-2, 4.0) if gemm == "bf16" else (1e-4, 3.0)
+    bad = []
+    for k, v in model.named_parameters():
+        if k.startswith("Masks.") or k.endswith("temporalConv.bias"):
+            continue
+        want = g64[k].detach().double().numpy()
+        floor = rel_to_max(gref[k].detach().double().numpy(), want)
+        err = rel_to_max(v.grad.detach().cpu().double().numpy(), want)
+        if err > max(lim, fac * floor):
+            bad.append(f"{k}: {err:.2e} (ref {floor:.2e})")
+    assert not bad, "; ".join(bad)
+
+
 def test_stack_cfg1_matches_reference(pkg):
     ref = load_npz("stack_cfg1.npz")
     A = torch.from_numpy(load_npz("adjacency.npz")["V18_s0_d1"])
@@ -151,9 +196,12 @@ def test_stack_chain_small_bn2_gamma(pkg, residual, gemm):
             g[4:6] = -1e-4
             blk.batch_n_2.bias[0:6] = torch.linspace(-0.5, 0.5, 6)
     m2.load_state_dict(m1.state_dict())
+    p0, b0 = snapshot_stack(m1)
     x = torch.randn(6, 3, 40, V, generator=torch.Generator().manual_seed(12)).cuda()
     lab = torch.randint(0, 10, (6,), generator=torch.Generator().manual_seed(13)).cuda()
+    masks, unhook = capture_relu_masks(m1)
     out1 = m1.forward_nctv(x)                      # chained
+    unhook()
     h = x
     for blk in m2.conv:                            # unchained
         h = blk(h)
@@ -163,21 +211,17 @@ def test_stack_chain_small_bn2_gamma(pkg, residual, gemm):
     torch.cuda.synchronize()
     assert rel_to_max(out1.detach().cpu().numpy(), out2.detach().cpu().numpy()) < \
         (1e-3 if gemm == "bf16" else 1e-5)
+    for k, a in m1.named_parameters():
+        assert torch.isfinite(a.grad).all(), k
+    if not residual:  # deferred dx: both runs against the fp64 oracle
+        gate_chained_vs_oracle(m1, p0, b0, x, lab, masks, gemm)
+        return
     bad = []
     for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
         ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
-        assert np.isfinite(ga).all(), k
         if np.abs(gb).max() == 0:
             continue
-        if k.endswith("temporalConv.bias") and not residual:  # analytically 0: rounding noise
-            assert np.abs(ga).max() < 1e-4, (k, np.abs(ga).max())
-            continue
-        if gemm == "bf16":  # chain-vs-unchained summation order through bf16 roundings
-            # (the first block's BN1 parameters end the deepest backward path: bf16
-            # noise there reaches ~20% vs exact, test_stack_bf16_cfg3_shape)
-            tol = 1e-1 if k.startswith("conv.0.batch_n.") else 2e-2
-        else:
-            tol = 2e-3 if k.endswith("spatialConv.A") else 1e-4
+        tol = 2e-3 if k.endswith("spatialConv.A") else 1e-4
         err = rel_to_max(ga, gb)
         if err > tol:
             bad.append(f"{k}: {err:.2e} > {tol:.0e}")
@@ -197,10 +241,13 @@ def test_stack_chain_matches_unchained(pkg, residual, drop):
         m1 = pkg.STGCNStack(3, 10, A, dropout_rate=drop, residual=residual).cuda().train()
         m2 = pkg.STGCNStack(3, 10, A, dropout_rate=drop, residual=residual).cuda().train()
     m2.load_state_dict(m1.state_dict())
+    p0, b0 = snapshot_stack(m1)
     x = torch.randn(6, 3, 40, 18, generator=torch.Generator().manual_seed(4)).cuda()
     lab = torch.randint(0, 10, (6,), generator=torch.Generator().manual_seed(5)).cuda()
+    masks, unhook = capture_relu_masks(m1)
     torch.manual_seed(9)
     out1 = m1.forward_nctv(x)                      # chained
+    unhook()
     torch.manual_seed(9)
     h = x
     for blk in m2.conv:                            # unchained
@@ -210,6 +257,12 @@ def test_stack_chain_matches_unchained(pkg, residual, drop):
     torch.nn.functional.cross_entropy(out2, lab).backward()
     torch.cuda.synchronize()
     assert rel_to_max(out1.detach().cpu().numpy(), out2.detach().cpu().numpy()) < 1e-5
+    for (k, a), (_, b) in zip(m1.named_buffers(), m2.named_buffers()):
+        if a.is_floating_point():
+            assert rel_to_max(a.cpu().numpy(), b.cpu().numpy()) < 1e-5, k
+    if not residual and drop == 0:  # deferred dx: both runs against the fp64 oracle
+        gate_chained_vs_oracle(m1, p0, b0, x, lab, masks, "fp32")
+        return
     # dA of the deep blocks is a small difference of large terms (BN makes the
     # loss invariant to A's scale: |dA| ~ 1e-11 here) -- gated looser
     bad = []
@@ -262,10 +315,13 @@ def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
         m1 = pkg.STGCNStack(3, 10, A, **kw).cuda().train()
         m2 = pkg.STGCNStack(3, 10, A, **kw).cuda().train()
     m2.load_state_dict(m1.state_dict())
+    p0, b0 = snapshot_stack(m1)
     N = 4
     x = torch.randn(N, 3, T, V, generator=torch.Generator().manual_seed(6)).cuda()
     lab = torch.randint(0, 10, (N,), generator=torch.Generator().manual_seed(7)).cuda()
+    masks, unhook = capture_relu_masks(m1)
     out1 = m1.forward_nctv(x)                      # chained (deferred dx)
+    unhook()
     h = x
     for blk in m2.conv:                            # unchained
         h = blk(h)
@@ -276,23 +332,11 @@ def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
     assert deferred == [True] * 9, deferred        # blocks 9..1 each deferred their dx
     assert rel_to_max(out1.detach().cpu().numpy(), out2.detach().cpu().numpy()) < \
         (1e-3 if gemm == "bf16" else 1e-5)
-    bad = []
-    for (k, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
-        ga, gb = a.grad.detach().cpu().double().numpy(), b.grad.detach().cpu().double().numpy()
-        assert np.isfinite(ga).all(), k
+    for k, a in m1.named_parameters():
+        assert torch.isfinite(a.grad).all(), k
         if k.endswith("temporalConv.bias"):  # analytically 0: rounding noise
-            assert np.abs(ga).max() < (1e-3 if gemm == "bf16" else 1e-4), (k, np.abs(ga).max())
-            continue
-        if np.abs(gb).max() == 0:
-            continue
-        if gemm == "bf16":  # summation order through bf16 roundings (deep end: see above)
-            tol = 1e-1 if k.startswith("conv.0.batch_n.") else 2e-2
-        else:
-            tol = 2e-3 if k.endswith("spatialConv.A") else 5e-4 if ".batch_n" in k else 1e-4
-        err = rel_to_max(ga, gb)
-        if err > tol:
-            bad.append(f"{k}: {err:.2e} > {tol:.0e}")
-    assert not bad, "; ".join(bad)
+            assert a.grad.abs().max().item() < (1e-3 if gemm == "bf16" else 1e-4), k
+    gate_chained_vs_oracle(m1, p0, b0, x, lab, masks, gemm)
 
 
 def test_stack_deferred_dx_guard(pkg):
