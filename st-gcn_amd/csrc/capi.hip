@@ -307,6 +307,28 @@ bool act_bf16(const stgcn_desc_t *d) {
 bool z_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
 bool du_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
 
+// dZ (the gradient at the SpatialConv output) stored in bf16 on the bf16 path's
+// non-residual blocks whose SpatialConv backward is the fused kernel and whose
+// dW' reads the kept bf16 G: both of those readers round dZ to bf16 anyway
+// (k_sp_bwd_fused's H GEMM operand, k_wgrad_gemm_gk's P operand), so they see
+// the same values at half the bytes (and the fused kernel's ring doubles in
+// depth); the third reader, the bias-type sums sum_{n,t} dZ (k_sum_nt4_bf16),
+// accumulates the bf16 values in fp64. Producer: the temporal data-gradient
+// (one-plane k_conv_x3, bf16 epilogue store). The buffer keeps its fp32 size.
+// (STGCN_AB_DZ_FP32 build: fp32 dZ, A/B only)
+bool dz_bf16(const stgcn_desc_t *d) {
+  constexpr bool off = STGCN_AB_DZ_FP32 != 0;
+  if (off || !bf16(d) || residual(d) || !fused_sp(d) || !fused_spb(d)) return false;
+  ConvGemmParams p = conv_base(d, nullptr);  // the data gradient's launch(es)
+  p.C = d->C_out;
+  p.R = d->C_out;
+  p.s_in = 1;
+  p.NQ = d->stride == 1 ? 9 : 5;
+  if (!conv_b1_supported(p)) return false;
+  p.NQ = 4;
+  return d->stride == 1 || conv_b1_supported(p);
+}
+
 }  // namespace
 
 // Every GEMM launch of the block fits its LDS budget.
@@ -631,12 +653,15 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                                 nullptr, s));
   }
 
+  // dZ in bf16 where every reader takes it (needs the kept G: k_wgrad_gemm_gk)
+  const bool dzb = dz_bf16(d) && a->G != nullptr;
   // Temporal conv data-gradient: dZ = conv^T(dU)
   {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = L.dU;
     p.in_bf16 = du_bf16(d) ? 1 : 0;
     p.out = L.dZ;
+    p.out_bf16 = dzb ? 1 : 0;
     p.in_bstride = (int64_t)R * To * V;
     p.out_bstride = (int64_t)R * T * V;
     p.w_sr = 9;
@@ -706,6 +731,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     w.T_src = T;
     w.V = V;
     w.N = N;
+    w.p_bf16 = dzb ? 1 : 0;
     plan_wgrad_gk(w, T);
     HIP_TRY(launch_wgrad_gk(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));
@@ -721,7 +747,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_wgrad(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));
   }
-  HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s));
+  HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s, dzb ? 1 : 0));
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
   // Deferred dx (ABI 5): the BN1 backward apply of this block is folded into the
   // previous block's ReLU+BN2 backward apply (launch_bn_relu_bwd_apply with
@@ -748,7 +774,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     // H = W'^T dZ, dx = sum_k H_k A_k, dA, BN1 sums in one kernel (H stays on chip)
     HIP_TRY(launch_sp_bwd_fused(L.dZ, xin, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.wpk,
                                 a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res,
-                                f32x3(d), s, defer ? &pvb : nullptr));
+                                f32x3(d), s, defer ? &pvb : nullptr, dzb ? 1 : 0));
   } else {
   {
     // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
@@ -919,6 +945,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     p.in_bf16 = du_bf16(d) ? 1 : 0;
     const float *w = c.take<float>((size_t)R * R * 9);
     p.out = c.take<float>((size_t)N * R * T * V);
+    p.out_bf16 = dz_bf16(d) ? 1 : 0;  // (the stack keeps G, so dZ is bf16 there)
     p.in_bstride = (int64_t)R * To * V;
     p.out_bstride = (int64_t)R * T * V;
     p.w_sr = 9;
@@ -1069,7 +1096,8 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
       if (fused_spb(d))
         return launch_sp_bwd_fused(P.dZ, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A,
                                    P.W, P.wpk, P.dx, P.dA, P.sd, P.sd + C, d->N, C, d->C_out,
-                                   d->T, d->V, d->K, 1, residual(d) ? 1 : 0, f32x3(d), s);
+                                   d->T, d->V, d->K, 1, residual(d) ? 1 : 0, f32x3(d), s,
+                                   nullptr, dz_bf16(d) ? 1 : 0);
       if (P.spb_gemm) {
         hipError_t e = launch_conv_gemm(P.cp[0], s);
         if (e != hipSuccess || !P.spb_joint) return e;

@@ -210,7 +210,7 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, int relu, hipStream_t s);
 hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out,
-                         hipStream_t s);
+                         hipStream_t s, int x_bf16 = 0);
 hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K,
                                 int R, int V, float *dbW, float *dA, hipStream_t s);
 hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
@@ -251,6 +251,6 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
                                int write_dx, int relu, bool x3, hipStream_t s,
-                               const PrevBn *prev = nullptr);
+                               const PrevBn *prev = nullptr, int dz_bf16 = 0);
 
 }  // namespace stgcn

@@ -3005,7 +3005,52 @@ __global__ __launch_bounds__(256) void k_sum_nt4(const float *X, int C, int T, i
   }
 }
 
-hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out, hipStream_t s) {
+// k_sum_nt4 over a bf16 tensor (capi.hip dz_bf16): 4 bf16 = 8 bytes per load,
+// the same period / shift bookkeeping (8-byte boundary below a row's start)
+__global__ __launch_bounds__(256) void k_sum_nt4_bf16(const __bf16 *X, int C, int T, int V,
+                                                      double *out) {
+  __shared__ double part[1024];
+  const int c = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const int L = T * V;
+  const int per = V / (V % 4 == 0 ? 4 : (V % 2 == 0 ? 2 : 1));
+  const int A = 256 / per * per;
+  const int64_t start = ((int64_t)n * C + c) * L;
+  const int shift = (int)(start & 3);
+  const uint2 *src = reinterpret_cast<const uint2 *>(X + (start - shift));
+  const int nf = (L + shift + 3) / 4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  auto f0 = [](unsigned w) { return __builtin_bit_cast(float, w << 16); };
+  auto f1 = [](unsigned w) { return __builtin_bit_cast(float, w & 0xffff0000u); };
+  if (tid < A) {
+    for (int f = tid; f < nf; f += A) {
+      const uint2 q = src[f];
+      const int p0 = 4 * f - shift;
+      if (p0 >= 0 && p0 < L) a0 += f0(q.x);
+      if (p0 + 1 >= 0 && p0 + 1 < L) a1 += f1(q.x);
+      if (p0 + 2 >= 0 && p0 + 2 < L) a2 += f0(q.y);
+      if (p0 + 3 >= 0 && p0 + 3 < L) a3 += f1(q.y);
+    }
+  }
+  part[4 * tid] = a0;
+  part[4 * tid + 1] = a1;
+  part[4 * tid + 2] = a2;
+  part[4 * tid + 3] = a3;
+  __syncthreads();
+  if (tid < V) {
+    double acc = 0.0;
+    for (int q = (tid + shift) % V; q < 4 * A; q += V) acc += part[q];
+    atomicAdd(out + c * V + tid, acc);
+  }
+}
+
+hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out, hipStream_t s,
+                         int x_bf16) {
+  if (x_bf16) {  // (a bf16 tensor in an fp32-sized, 16-byte aligned buffer)
+    if (V > 256 || ((int64_t)N * C * T * V) % 4 != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sum_nt4_bf16, dim3(C, N), dim3(256), 0, s,
+                       reinterpret_cast<const __bf16 *>(X), C, T, V, out);
+    return hipGetLastError();
+  }
   // (rows of any alignment: the float4 kernel reads from the 16-byte boundary
   // below a row's start; X 16-byte aligned and a whole number of float4 in
   // total, so no read passes the tensor's end)

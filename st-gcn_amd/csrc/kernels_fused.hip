@@ -833,14 +833,20 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
 // it (vmcnt retires loads in order) and one barrier publishes the item (a
 // fenced __syncthreads would drain the ring). The item's fragments are read
 // first as 16-byte vectors (one LDS wait), then converted and multiplied.
+// PB: dZ is stored in bf16 (capi.hip dz_bf16): staged by 2-byte LDS-DMA into a
+// bf16 image (80-byte rows), each fragment one ds_read_b128, no conversion --
+// the same bf16 operand values as rounding the fp32 dZ at fragment read.
 // ---------------------------------------------------------------------------
-template <int TR>
+template <int TR, bool PB = false>
 struct WgGkGeo {
-  static constexpr int TC = 256, KC = 32, PITCH = KC + 4;  // P pitch (floats)
-  static constexpr int PSZ = TR * PITCH;                    // floats
+  static constexpr int TC = 256, KC = 32;
+  static constexpr int PITCH = PB ? KC + 8 : KC + 4;        // P pitch (elements)
+  static constexpr int ESZ = PB ? 2 : 4;                    // P element bytes
+  static constexpr int PSZ = TR * PITCH;                    // elements
   static constexpr int QSLOTS = TC * 5;                     // 16-byte slots of the G image
   static constexpr int QBYTES = QSLOTS * 16;
-  static constexpr int BUF = PSZ * 4 + QBYTES;              // bytes per buffer
+  static constexpr int PBYTES = (PSZ * ESZ + 15) / 16 * 16;
+  static constexpr int BUF = PBYTES + QBYTES;               // bytes per buffer
   static constexpr int NWR = TR / 64, NW = NWR * 4, NTH = NW * 64;
   static constexpr int PROUNDS = (PSZ + NTH - 1) / NTH;
   static constexpr int QROUNDS = (QSLOTS + NTH - 1) / NTH;
@@ -863,9 +869,9 @@ __device__ __forceinline__ void gk_ring_wait(int ahead) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <int TR, int NS>
+template <int TR, int NS, bool PB>
 __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
-  using G = WgGkGeo<TR>;
+  using G = WgGkGeo<TR, PB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -905,16 +911,23 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     const int mt = rem >> 3, kc = rem & 7;
     const int l0 = mt * FTV + kc * G::KC;
     const int lim = min(min(G::KC, FTV - kc * G::KC), L - l0);  // valid positions of the piece
+    // (PB: a resource over the bf16 tensor, in fp32 units of its bytes)
     const __amdgpu_buffer_rsrc_t rs_p =
-        make_rsrc(p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * L, (int64_t)prow_lim * L);
-    float *pb = reinterpret_cast<float *>(buf);
+        PB ? make_rsrc(reinterpret_cast<const float *>(reinterpret_cast<const __bf16 *>(p.P) +
+                                                       (int64_t)n * p.p_bstride + (int64_t)r0 * L),
+                       ((int64_t)prow_lim * L + 1) / 2)
+           : make_rsrc(p.P + (int64_t)n * p.p_bstride + (int64_t)r0 * L, (int64_t)prow_lim * L);
 #pragma unroll
     for (int i = 0; i < G::PROUNDS; ++i) {
       const int base = (i * G::NW + wave) * 64;  // wave-uniform
       if (base < G::PSZ) {
         const bool ok = prow[i] >= 0 && prow[i] < prow_lim && pcol[i] < lim;
-        const unsigned voff = ok ? (unsigned)(prow[i] * L + l0 + pcol[i]) * 4u : kOOB;
-        blds_f32(rs_p, voff, pb + base);
+        const unsigned voff = ok ? (unsigned)(prow[i] * L + l0 + pcol[i]) * (unsigned)G::ESZ : kOOB;
+        if constexpr (PB)  // 2-byte LDS-DMA: lane l lands at base + 2 l
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              rs_p, reinterpret_cast<float *>(buf + base * 2), 2, voff, 0, 0, 0);
+        else
+          blds_f32(rs_p, voff, reinterpret_cast<float *>(buf) + base);
       }
     }
     // Gk rows of this clip / column tile: (c0 + row) * nmt * 256 + mt * 256 + kc * 32
@@ -929,7 +942,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
         const unsigned voff =
             ok ? (unsigned)((qrow[i] * nmt + mt) * 256 + kc * G::KC + qpc[i] * 8) * 2u : kOOB;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs_q, reinterpret_cast<float *>(buf + G::PSZ * 4 + base * 16), 16, voff, 0, 0, 0);
+            rs_q, reinterpret_cast<float *>(buf + G::PBYTES + base * 16), 16, voff, 0, 0, 0);
       }
     }
   };
@@ -954,7 +967,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     const char *cur = lds + sl * G::BUF;
     sl = sl + 1 == NS ? 0 : sl + 1;
     const float *pa = reinterpret_cast<const float *>(cur) + (wr * 64 + lo) * G::PITCH + 8 * hi;
-    const char *qb = cur + G::PSZ * 4 + ((wc * 64 + lo) * 5 + hi) * 16;
+    const __bf16 *pab = reinterpret_cast<const __bf16 *>(cur) + (wr * 64 + lo) * G::PITCH + 8 * hi;
+    const char *qb = cur + G::PBYTES + ((wc * 64 + lo) * 5 + hi) * 16;
     // every fragment of the item first, as 16-byte reads (rows are 16-byte
     // aligned: PITCH * 4 = 144 B), one LDS wait, then the conversions and the
     // MFMAs (element-wise reads compiled to b96 + b32 pieces, each waited on
@@ -962,15 +976,21 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     constexpr int NKS = G::KC / 16;
     typedef float f32x4v __attribute__((ext_vector_type(4)));
     f32x4v pf[NKS][2][2];
+    bf16x8f pbf[NKS][2];
     bf16x8f b[NKS][2];
 #pragma unroll
     for (int s = 0; s < NKS; ++s)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4v *src = reinterpret_cast<const f32x4v *>(
-            __builtin_assume_aligned(pa + i * 32 * G::PITCH + 16 * s, 16));
-        pf[s][i][0] = src[0];
-        pf[s][i][1] = src[1];
+        if constexpr (PB) {
+          pbf[s][i] = *reinterpret_cast<const bf16x8f *>(
+              __builtin_assume_aligned(pab + i * 32 * G::PITCH + 16 * s, 16));
+        } else {
+          const f32x4v *src = reinterpret_cast<const f32x4v *>(
+              __builtin_assume_aligned(pa + i * 32 * G::PITCH + 16 * s, 16));
+          pf[s][i][0] = src[0];
+          pf[s][i][1] = src[1];
+        }
       }
 #pragma unroll
     for (int s = 0; s < NKS; ++s)
@@ -982,9 +1002,13 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
       bf16x8f a[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4v lo4 = pf[s][i][0], hi4 = pf[s][i][1];
-        a[i] = bf16x8f{(__bf16)lo4.x, (__bf16)lo4.y, (__bf16)lo4.z, (__bf16)lo4.w,
-                       (__bf16)hi4.x, (__bf16)hi4.y, (__bf16)hi4.z, (__bf16)hi4.w};
+        if constexpr (PB) {
+          a[i] = pbf[s][i];
+        } else {
+          const f32x4v lo4 = pf[s][i][0], hi4 = pf[s][i][1];
+          a[i] = bf16x8f{(__bf16)lo4.x, (__bf16)lo4.y, (__bf16)lo4.z, (__bf16)lo4.w,
+                         (__bf16)hi4.x, (__bf16)hi4.y, (__bf16)hi4.z, (__bf16)hi4.w};
+        }
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -1027,13 +1051,15 @@ hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s) {
   // bound and 2 slots won: 5141 vs 5063.) STGCN_AB_GK_SLOTS2 builds: A/B only.
   constexpr bool two = STGCN_AB_GK_SLOTS2 != 0;
   static_assert(4 * WgGkGeo<128>::BUF <= 160 * 1024, "LDS budget");
-#define GK_LAUNCH(TR, NS) \
-  hipLaunchKernelGGL((k_wgrad_gemm_gk<TR, NS>), dim3(nblk), dim3(WgGkGeo<TR>::NTH), \
-                     NS * WgGkGeo<TR>::BUF, s, p)
-  if (p.CT == 128) {
-    if (two) GK_LAUNCH(128, 2); else GK_LAUNCH(128, 4);
+#define GK_LAUNCH(TR, NS, PB)                                                                \
+  hipLaunchKernelGGL((k_wgrad_gemm_gk<TR, NS, PB>), dim3(nblk), dim3((WgGkGeo<TR, PB>::NTH)), \
+                     (NS * WgGkGeo<TR, PB>::BUF), s, p)
+  if (p.p_bf16) {  // bf16 dZ (capi.hip dz_bf16)
+    if (p.CT == 128) GK_LAUNCH(128, 4, true); else GK_LAUNCH(64, 4, true);
+  } else if (p.CT == 128) {
+    if (two) GK_LAUNCH(128, 2, false); else GK_LAUNCH(128, 4, false);
   } else {
-    if (two) GK_LAUNCH(64, 2); else GK_LAUNCH(64, 4);
+    if (two) GK_LAUNCH(64, 2, false); else GK_LAUNCH(64, 4, false);
   }
 #undef GK_LAUNCH
   return hipGetLastError();

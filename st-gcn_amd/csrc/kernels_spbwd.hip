@@ -90,7 +90,12 @@ __device__ __forceinline__ void spb_wait_vm(int n) {
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -142,7 +147,9 @@ __device__ __forceinline__ void spb_mfma6(const uint4 (&a)[3], const uint4 (&b)[
 // X3 = false: the bf16 path (bf16 W', dZ rounded to bf16; H, A to 2^-16).
 // X3 = true : the fp32 path of STGCN_F_F32X3 (every operand as its exact 3-way
 //             bf16 split, six products per fp32 product, h*h accumulated apart).
-template <int V, int K, bool X3>
+// DZB: dZ is stored in bf16 (capi.hip dz_bf16; the values the fp32 path rounds
+//      it to): half-size ring slots, so the ring is 6 chunks deep instead of 4.
+template <int V, int K, bool X3, bool DZB = false>
 struct SpBwdGeo {
   static_assert(V <= 32, "one 32-joint tile");
   static constexpr int NPLW = X3 ? 3 : 1;           // W' planes
@@ -156,11 +163,16 @@ struct SpBwdGeo {
   static constexpr int NPC = (NPOS + 3 + 3) / 4;
   static constexpr int CB = 32;                     // input channels per item
   static constexpr int CR = 16;                     // dZ channels per chunk (one k-step)
-  static constexpr int D = 4;                       // ring depth (chunks)
+  static constexpr int D = DZB ? 6 : 4;             // ring depth (chunks)
   // row pitch (floats): whole pieces, and 8 rows apart = 32 banks apart
   static constexpr int RP = (NPC * 4) % 8 == 0 ? NPC * 4 + 4 : NPC * 4;
-  static_assert(NPOS % 4 == 0, "item starts p0 16-byte aligned within a row");
-  static constexpr int RING_SLOT = CR * RP * 4;     // fp32 [r][RP]
+  static_assert(NPOS % 8 == 0, "item starts p0 16-byte aligned within a row (fp32 and bf16)");
+  // the dZ ring rows: fp32 as the x slice, or bf16 (NPCZ 8-element pieces from
+  // the 16-byte boundary below the row start; pitch = 8 mod 16 elements)
+  static constexpr int NPCZ = DZB ? (NPOS + 7 + 7) / 8 : NPC;
+  static constexpr int RPZ = DZB ? ((NPCZ * 8) % 16 == 0 ? NPCZ * 8 + 8 : NPCZ * 8) : RP;
+  static constexpr int ZSZ = DZB ? 2 : 4;
+  static constexpr int RING_SLOT = CR * RPZ * ZSZ;  // [r][RPZ]
   static constexpr int W_BYTES = K * NPLW * CR * 64;  // W' chunk [k][plane][octet 2][ci 32][8]
   static constexpr int WPW = W_BYTES / 16 / 8;      // W' pieces per wave
   static constexpr int XBP = 80;                    // f(BN1(x)) image row pitch, bytes
@@ -181,7 +193,7 @@ struct SpBwdGeo {
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(K * V * V * 4 <= D * RING_SLOT, "dA reduction fits the ring");
   static_assert(W_BYTES % 128 == 0 && WPW <= 64, "W' pieces per wave");
-  static_assert(NPC <= 64, "one DMA instruction per row");
+  static_assert(NPC <= 64 && NPCZ <= 64, "one DMA instruction per row");
 };
 
 struct SpBwdParams {
@@ -194,9 +206,9 @@ struct SpBwdParams {
   PrevBn prev;  // prev mode (internal.h): x is the previous block's U
 };
 
-template <int V, int K, bool X3>
+template <int V, int K, bool X3, bool DZB>
 __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
-  using G = SpBwdGeo<V, K, X3>;
+  using G = SpBwdGeo<V, K, X3, DZB>;
   constexpr int D = G::D, NACC = G::NACC;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
@@ -261,14 +273,18 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     decode(first + k * NG, n, ft, cb);
     const int p0 = ft * G::FT * V;
     const int slot = gch % D;
-    const spb_i4 rz = spb_rsrc(P.dZ + (int64_t)n * P.R * TV, (int64_t)P.R * TV * 4);
+    const spb_i4 rz =
+        DZB ? spb_rsrc(reinterpret_cast<const __bf16 *>(P.dZ) + (int64_t)n * P.R * TV,
+                       (int64_t)P.R * TV * 2)
+            : spb_rsrc(P.dZ + (int64_t)n * P.R * TV, (int64_t)P.R * TV * 4);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int r = 2 * wave + h;
-      const int start = (c * G::CR + r) * TV + p0;  // from (start & ~3): the row's shift
-      const unsigned voff = (unsigned)(((start & ~3) + 4 * lane) * 4);
-      if (lane < G::NPC)
-        spb_dma16(rz, voff, lds0 + G::OFF_RING + slot * G::RING_SLOT + r * G::RP * 4);
+      const int start = (c * G::CR + r) * TV + p0;  // from the 16-byte boundary below: the row's shift
+      constexpr int EPP = 16 / G::ZSZ;              // elements per 16-byte piece
+      const unsigned voff = (unsigned)(((start & ~(EPP - 1)) + EPP * lane) * G::ZSZ);
+      if (lane < G::NPCZ)
+        spb_dma16(rz, voff, lds0 + G::OFF_RING + slot * G::RING_SLOT + r * G::RPZ * G::ZSZ);
     }
     if (lane < G::WPW)
       spb_dma16(rw, (unsigned)((cb * NCH + c) * G::W_BYTES + wave * G::WPW * 16 + lane * 16),
@@ -329,20 +345,36 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       // A operand: dZ[r = 8 hi + j][frame f, joint lo] (0 past V: read at a
       // clamped joint, then selected, so the 8 reads issue back to back); row
       // 8 hi + j starts (8 hi + j) * TV mod 4 = j * TV mod 4 floats into its LDS row
-      const float *rz = reinterpret_cast<const float *>(lds + G::OFF_RING + slot * G::RING_SLOT) +
-                        8 * hi * G::RP + f * V + (lo < V ? lo : V - 1);
-      float dv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = rz[j * G::RP + ((j * TV) & 3)];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = lo < V ? dv[j] : 0.f;
       const char *wb = lds + G::OFF_W + slot * G::W_BYTES + hi * 512 + lo * 16;
-      if constexpr (!X3) {
-        uint4 a;  // dZ rounded to bf16
+      float dv[8];
+      uint4 a;  // dZ rounded to bf16 (the X3 path splits dv instead)
+      if constexpr (DZB) {  // stored in bf16: the same values, read as shorts
+        const unsigned short *rz =
+            reinterpret_cast<const unsigned short *>(lds + G::OFF_RING + slot * G::RING_SLOT) +
+            8 * hi * G::RPZ + f * V + (lo < V ? lo : V - 1);
+        unsigned hv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = rz[j * G::RPZ + ((j * TV) & 7)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hv[j] = lo < V ? hv[j] : 0u;
+        a.x = hv[0] | (hv[1] << 16);
+        a.y = hv[2] | (hv[3] << 16);
+        a.z = hv[4] | (hv[5] << 16);
+        a.w = hv[6] | (hv[7] << 16);
+      } else {
+        const float *rz =
+            reinterpret_cast<const float *>(lds + G::OFF_RING + slot * G::RING_SLOT) +
+            8 * hi * G::RPZ + f * V + (lo < V ? lo : V - 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv[j] = rz[j * G::RPZ + ((j * TV) & 3)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dv[j] = lo < V ? dv[j] : 0.f;
         a.x = spb_pk(dv[0], dv[1]);
         a.y = spb_pk(dv[2], dv[3]);
         a.z = spb_pk(dv[4], dv[5]);
         a.w = spb_pk(dv[6], dv[7]);
+      }
+      if constexpr (!X3) {
 #pragma unroll
         for (int kk = 0; kk < K; ++kk) {
           const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
@@ -632,16 +664,16 @@ size_t sp_bwd_fused_wpk_bytes(int C, int R, int K, int V) {
   return kSpbAimgBytes + (size_t)K * R * C * 2 * 3 + 256;
 }
 
-template <int V, int K, bool X3>
+template <int V, int K, bool X3, bool DZB = false>
 static hipError_t launch_spb(const SpBwdParams &P0, hipStream_t s) {
-  using G = SpBwdGeo<V, K, X3>;
+  using G = SpBwdGeo<V, K, X3, DZB>;
   SpBwdParams P = P0;
   P.nft = (P.T + G::FT - 1) / G::FT;
   const int64_t items = (int64_t)P.ncb * P.nft * P.nitems;  // (nitems: N on entry)
   if (items >= (int64_t)1 << 31) return hipErrorInvalidValue;
   P.nitems = (int)items;
   const int grid = (int)std::min<int64_t>(items, 256);
-  hipLaunchKernelGGL((k_sp_bwd_fused<V, K, X3>), dim3(grid), dim3(512), G::LDS, s, P);
+  hipLaunchKernelGGL((k_sp_bwd_fused<V, K, X3, DZB>), dim3(grid), dim3(512), G::LDS, s, P);
   return hipGetLastError();
 }
 
@@ -650,7 +682,7 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
                                int write_dx, int relu, bool x3, hipStream_t s,
-                               const PrevBn *prev) {
+                               const PrevBn *prev, int dz_bf16) {
   if (!sp_bwd_fused_supported(C, V, K, R, T, x3)) return hipErrorInvalidValue;
   const int npw = x3 ? 3 : 1, npa = x3 ? 3 : 2;
   __bf16 *aimg = reinterpret_cast<__bf16 *>(wpk);
@@ -680,7 +712,8 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
   P.write_dx = write_dx;
   P.relu = relu;
   if (prev) P.prev = *prev;
-  if (x3) return launch_spb<18, 1, true>(P, s);
+  if (x3) return dz_bf16 ? hipErrorInvalidValue : launch_spb<18, 1, true>(P, s);
+  if (dz_bf16) return launch_spb<25, 3, false, true>(P, s);
   return launch_spb<25, 3, false>(P, s);
 }
 

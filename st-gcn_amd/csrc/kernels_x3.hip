@@ -480,8 +480,10 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
       for (int j = 0; j < 2; ++j)
         acc_to_img(smem, acc[rb * 2 + j], mi * 32 * MR + rb * 32, (nj0 + j) * 32);
     __syncthreads();
-    conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS>(p, smem, smem + G::ROWS * kEpiPitch, n, r0,
-                                                      m0);
+    // (one-plane bf16 path: the output may be stored in bf16, p.out_bf16 -- the
+    // data gradient dZ of capi.hip dz_bf16)
+    conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS, NPL == 1>(
+        p, smem, smem + G::ROWS * kEpiPitch, n, r0, m0);
     return;
   }
   if constexpr (MR == 2) return;  // (never: 128-row tiles are launched for s_out == 1 only)
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[2 + j][i] = ho[(j * 16 + i) * 64 + lane];
-    conv_tile_epilogue<V, G::NCOLS>(p, acc, n, r0, m0, smem);
+    conv_tile_epilogue<V, G::NCOLS, false, NPL == 1>(p, acc, n, r0, m0, smem);
   } else if (p.stat_sum) {
     __syncthreads();  // the epilogue's one barrier (statistics)
   }
