@@ -25,6 +25,9 @@
 #ifndef STGCN_AB_ACT_FP32       // fp32 storage of Z / dU on the bf16 path
 #define STGCN_AB_ACT_FP32 0
 #endif
+#ifndef STGCN_AB_NO_SLICE       // the unfused spatial backward over the whole batch at once
+#define STGCN_AB_NO_SLICE 0
+#endif
 #ifndef STGCN_AB_DZ_FP32        // fp32 storage of dZ on the bf16 path (capi.hip dz_bf16)
 #define STGCN_AB_DZ_FP32 0
 #endif

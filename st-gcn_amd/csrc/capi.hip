@@ -101,6 +101,20 @@ bool fused_spb(const stgcn_desc_t *d) {
   return !off && (bf16(d) || f32x3(d)) &&
          sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T, f32x3(d));
 }
+// Clips per slice of the unfused spatial backward (H GEMM + joint kernel): the
+// slice's H, dZ, x and dx (fp32) within ~160 MiB, so the Infinity Cache (256
+// MiB; it keeps a line resident while the bytes moved between two uses of it
+// fit, MI355X_MICROARCH.md) serves H's read-back. At least 8 clips a slice
+// (enough workgroups per launch). STGCN_AB_NO_SLICE build: one slice.
+int spatial_bwd_slice(const stgcn_desc_t *d) {
+  constexpr bool off = STGCN_AB_NO_SLICE != 0;
+  if (off) return d->N;
+  const int64_t per_clip =
+      (int64_t)4 * d->T * d->V * ((int64_t)d->K * d->C_in + d->C_out + 2 * d->C_in);
+  const int64_t budget = (int64_t)160 << 20;
+  const int ns = (int)std::max<int64_t>(8, budget / std::max<int64_t>(per_clip, 1));
+  return std::min(ns, d->N);
+}
 // residual block with a 1x1 projection (apply_residual Conv2d, st_graphconv.py:27)
 bool projection(const stgcn_desc_t *d) {
   return residual(d) && (d->C_in != d->C_out || d->stride != 1);
@@ -776,16 +790,25 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                                 a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res,
                                 f32x3(d), s, defer ? &pvb : nullptr, dzb ? 1 : 0));
   } else {
+  // Clip slices (spatial_bwd_slice): the H GEMM and the joint kernel run on ns
+  // clips at a time, so the slice of H they hand over (and the dZ / x / dx
+  // slices around it) stay within the 256 MiB Infinity Cache: H is written and
+  // read back on-die instead of through HBM (the buffer is reused per slice).
+  const float *Wz = a->W;
+  if (K > 1) {
+    HIP_TRY(launch_pack_w(a->W, L.Wpk, K, R, C, s));
+    Wz = L.Wpk;
+  }
+  const int NSL = spatial_bwd_slice(d);
+  for (int n0 = 0; n0 < N; n0 += NSL) {
+  const int ns = std::min(NSL, N - n0);
+  const int64_t xo = (int64_t)n0 * C * T * V;
   {
     // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
     // the channels of H_k): dZ is read once instead of K times
-    const float *Wz = a->W;
-    if (K > 1) {
-      HIP_TRY(launch_pack_w(a->W, L.Wpk, K, R, C, s));
-      Wz = L.Wpk;
-    }
     ConvGemmParams p = conv_base(d, L.wpk);
-    p.in = L.dZ;
+    p.N = ns;
+    p.in = L.dZ + (int64_t)n0 * R * T * V;
     p.w = Wz;
     p.out = L.H;
     p.in_bstride = (int64_t)R * T * V;
@@ -806,9 +829,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     conv_tiles(p);
     HIP_TRY(launch_conv_gemm(p, s));
   }
-  HIP_TRY(launch_spatial_dx(L.H, xin, mean1, invstd1, a->g1, a->b1, a->A, a->dx, a->dA, L.sd,
-                            L.sdn, N, C, T, V, K, d->need_dx, res, bf16(d) ? 1 : 0, s,
-                            defer ? &pvb : nullptr));
+  HIP_TRY(launch_spatial_dx(L.H, xin + xo, mean1, invstd1, a->g1, a->b1, a->A,
+                            a->dx ? a->dx + xo : nullptr, a->dA, L.sd, L.sdn, ns, C, T, V, K,
+                            d->need_dx, res, bf16(d) ? 1 : 0, s, defer ? &pvb : nullptr));
+  }
   }
   if (defer) {
     HIP_TRY(launch_chain_coef(L.sd, L.sdn, mean1, invstd1, a->g1, L.s1, L.s2, a->x_stats, C,
