@@ -322,17 +322,26 @@ bool z_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
 bool du_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
 
 // dZ (the gradient at the SpatialConv output) stored in bf16 on the bf16 path's
-// non-residual blocks whose SpatialConv backward is the fused kernel and whose
-// dW' reads the kept bf16 G: both of those readers round dZ to bf16 anyway
-// (k_sp_bwd_fused's H GEMM operand, k_wgrad_gemm_gk's P operand), so they see
-// the same values at half the bytes (and the fused kernel's ring doubles in
-// depth); the third reader, the bias-type sums sum_{n,t} dZ (k_sum_nt4_bf16),
-// accumulates the bf16 values in fp64. Producer: the temporal data-gradient
-// (one-plane k_conv_x3, bf16 epilogue store). The buffer keeps its fp32 size.
+// non-residual blocks whose dW' reads the kept bf16 G: its readers round dZ to
+// bf16 anyway (k_sp_bwd_fused's H GEMM operand -- or, unfused, the H GEMM
+// k_conv_bf16<1, .., IB> -- and k_wgrad_gemm_gk's P operand), so they see the
+// same values at half the bytes (and the fused kernel's ring is 6 chunks deep
+// instead of 4); the remaining reader, the bias-type sums sum_{n,t} dZ
+// (k_sum_nt4_bf16), accumulates the bf16 values in fp64. Producer: the temporal
+// data-gradient (one-plane k_conv_x3, bf16 epilogue store). The buffer keeps
+// its fp32 size.
 // (STGCN_AB_DZ_FP32 build: fp32 dZ, A/B only)
 bool dz_bf16(const stgcn_desc_t *d) {
   constexpr bool off = STGCN_AB_DZ_FP32 != 0;
-  if (off || !bf16(d) || residual(d) || !fused_sp(d) || !fused_spb(d)) return false;
+  if (off || !bf16(d) || residual(d) || !fused_sp(d)) return false;
+  if (!fused_spb(d)) {  // the unfused spatial backward: its H GEMM reads dZ (k_conv_bf16<.., IB>)
+    ConvGemmParams h = conv_base(d, nullptr);
+    h.C = d->C_out;
+    h.R = d->K * d->C_in;
+    h.NQ = 1;
+    h.s_in = 1;
+    if (!conv_bf16_supported(h)) return false;
+  }
   ConvGemmParams p = conv_base(d, nullptr);  // the data gradient's launch(es)
   p.C = d->C_out;
   p.R = d->C_out;
@@ -808,7 +817,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     // the channels of H_k): dZ is read once instead of K times
     ConvGemmParams p = conv_base(d, L.wpk);
     p.N = ns;
-    p.in = L.dZ + (int64_t)n0 * R * T * V;
+    p.in_bf16 = dzb ? 1 : 0;  // (element offsets: the bf16 kernel halves them)
+    p.in = dzb ? reinterpret_cast<const float *>(reinterpret_cast<const __bf16 *>(L.dZ) +
+                                                 (int64_t)n0 * R * T * V)
+               : L.dZ + (int64_t)n0 * R * T * V;
     p.w = Wz;
     p.out = L.H;
     p.in_bstride = (int64_t)R * T * V;
@@ -1030,6 +1042,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       P.H = c.take<float>((size_t)N * K * C * T * V);
       ConvGemmParams p = conv_base(d, wpk);
       p.in = P.dZ;
+      p.in_bf16 = dz_bf16(d) ? 1 : 0;
       p.w = c.take<float>((size_t)R * K * C);  // (the packed W' of the block)
       p.out = P.H;
       p.in_bstride = (int64_t)R * T * V;

@@ -492,6 +492,8 @@ hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
   if (p0.bf16 == 3 && conv_x3_supported(p0)) return launch_conv_x3(p0, s);
   if (p0.bf16 == 1 && conv_b1_supported(p0)) return launch_conv_b1(p0, s);
   if (p0.bf16 == 1 && conv_bf16_supported(p0)) return launch_conv_bf16(p0, s);
+  // (bf16-stored operands: only the kernels above read / write them)
+  if (p0.in_bf16 || p0.out_bf16) return hipErrorInvalidValue;
   ConvGemmParams p = p0;
   if (!conv_gemm_supported(p) || !p.wpk) return hipErrorInvalidValue;
   p.Cpad = conv_gemm_cpad(p);

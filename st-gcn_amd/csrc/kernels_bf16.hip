@@ -101,7 +101,9 @@ struct ConvBf16Geo {
 #define STGCN_CB1_MINB 2
 #endif
 
-template <int NQ, int CK, int V, int SIN>
+// IB: the input is stored in bf16 (p.in_bf16; the NQ = 1 GEMM over a bf16 dZ,
+// capi.hip dz_bf16): loaded as zero-extended shorts, packed without conversion
+template <int NQ, int CK, int V, int SIN, bool IB = false>
 __global__ __launch_bounds__(256, NQ == 1 ? STGCN_CB1_MINB : 2) void k_conv_bf16(ConvGemmParams p) {
   using G = ConvBf16Geo<NQ, CK, V, SIN>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -149,12 +151,27 @@ __global__ __launch_bounds__(256, NQ == 1 ? STGCN_CB1_MINB : 2) void k_conv_bf16
       make_rsrc(reinterpret_cast<const float *>(wblk), (int64_t)nchunks * G::WCH / 4);
   float st[G::IPT][8];
   auto load_img = [&](int chunk) {
-    const __amdgpu_buffer_rsrc_t rs =
-        make_rsrc(inN + (int64_t)chunk * CK * cstride, (int64_t)(p.C - chunk * CK) * cstride);
+    if constexpr (IB) {
+      const __bf16 *inb = reinterpret_cast<const __bf16 *>(p.in) + (int64_t)n * p.in_bstride +
+                          (int64_t)chunk * CK * cstride;
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(
+          reinterpret_cast<const float *>(inb), ((int64_t)(p.C - chunk * CK) * cstride + 1) / 2);
 #pragma unroll
-    for (int k = 0; k < G::IPT; ++k)
+      for (int k = 0; k < G::IPT; ++k)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) st[k][j] = ld_f32(rs, voff[k] + (unsigned)(j * cstride * 4));
+        for (int j = 0; j < 8; ++j)
+          st[k][j] = __builtin_bit_cast(
+              float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(
+                         rs, voff[k] == kOOB ? (int)kOOB : (int)((voff[k] >> 1) + j * cstride * 2),
+                         0, 0));
+    } else {
+      const __amdgpu_buffer_rsrc_t rs =
+          make_rsrc(inN + (int64_t)chunk * CK * cstride, (int64_t)(p.C - chunk * CK) * cstride);
+#pragma unroll
+      for (int k = 0; k < G::IPT; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st[k][j] = ld_f32(rs, voff[k] + (unsigned)(j * cstride * 4));
+    }
   };
   auto dma_w = [&](int chunk, char *dst) {
     for (int d = wave; d < G::WDMA; d += 4)
@@ -167,10 +184,18 @@ __global__ __launch_bounds__(256, NQ == 1 ? STGCN_CB1_MINB : 2) void k_conv_bf16
     for (int k = 0; k < G::IPT; ++k)
       if (loff[k] >= 0) {
         uint4 v;
-        v.x = pk_bf16(st[k][0], st[k][1]);
-        v.y = pk_bf16(st[k][2], st[k][3]);
-        v.z = pk_bf16(st[k][4], st[k][5]);
-        v.w = pk_bf16(st[k][6], st[k][7]);
+        if constexpr (IB) {  // already bf16 (zero-extended shorts)
+          const auto u = [&](int j) { return __builtin_bit_cast(unsigned, st[k][j]); };
+          v.x = u(0) | (u(1) << 16);
+          v.y = u(2) | (u(3) << 16);
+          v.z = u(4) | (u(5) << 16);
+          v.w = u(6) | (u(7) << 16);
+        } else {
+          v.x = pk_bf16(st[k][0], st[k][1]);
+          v.y = pk_bf16(st[k][2], st[k][3]);
+          v.z = pk_bf16(st[k][4], st[k][5]);
+          v.w = pk_bf16(st[k][6], st[k][7]);
+        }
         *reinterpret_cast<uint4 *>(dst + loff[k]) = v;
       }
   };
@@ -262,6 +287,13 @@ template <int NQ, int V, int SIN>
 static bool launch_cb_if(const ConvGemmParams &p, int nblk, size_t lds, hipStream_t s) {
   if (p.V != V || p.s_in != SIN) return false;
   constexpr int CK = NQ == 1 ? STGCN_CB1_CK : 16;
+  if constexpr (NQ == 1 && SIN == 1) {
+    if (p.in_bf16) {
+      hipLaunchKernelGGL((k_conv_bf16<NQ, CK, V, SIN, true>), dim3(nblk), dim3(256), lds, s, p);
+      return true;
+    }
+  }
+  if (p.in_bf16) return false;
   hipLaunchKernelGGL((k_conv_bf16<NQ, CK, V, SIN>), dim3(nblk), dim3(256), lds, s, p);
   return true;
 }
@@ -273,7 +305,10 @@ static bool launch_cb_v(const ConvGemmParams &p, int nblk, size_t lds, hipStream
 }
 
 hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s) {
-  if (!conv_bf16_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  // (bf16 input: the NQ = 1 stride-1 GEMM only; no bf16 output here)
+  if (!conv_bf16_supported(p) || !p.wpk || p.out_bf16 ||
+      (p.in_bf16 && (p.NQ != 1 || p.s_in != 1)))
+    return hipErrorInvalidValue;
   const int CK = conv_bf16_ck(p.NQ);
   const int nch = (p.C + CK - 1) / CK;
   {
