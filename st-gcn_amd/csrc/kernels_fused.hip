@@ -833,19 +833,23 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
 // it (vmcnt retires loads in order) and one barrier publishes the item (a
 // fenced __syncthreads would drain the ring). The item's fragments are read
 // first as 16-byte vectors (one LDS wait), then converted and multiplied.
-// PB: dZ is stored in bf16 (capi.hip dz_bf16): staged by 2-byte LDS-DMA into a
-// bf16 image (80-byte rows), each fragment one ds_read_b128, no conversion --
-// the same bf16 operand values as rounding the fp32 dZ at fragment read.
+// PB: dZ is stored in bf16 (capi.hip dz_bf16): staged as bf16 PAIRS by 4-byte
+// LDS-DMA (a row's piece from the even element at or below its start: rows
+// of an odd-length clip row start at odd elements on odd rows), rows of 20
+// dwords (17 used, 80-byte pitch); a fragment = one ds_read_b128 + one
+// ds_read_b32, shifted by 16 bits on odd-start rows, positions past the piece
+// masked to 0 -- the same bf16 operand values as rounding the fp32 dZ at
+// fragment read.
 // ---------------------------------------------------------------------------
 template <int TR, bool PB = false>
 struct WgGkGeo {
   static constexpr int TC = 256, KC = 32;
-  static constexpr int PITCH = PB ? KC + 8 : KC + 4;        // P pitch (elements)
-  static constexpr int ESZ = PB ? 2 : 4;                    // P element bytes
-  static constexpr int PSZ = TR * PITCH;                    // elements
+  static constexpr int PITCH = PB ? 20 : KC + 4;            // P pitch (dwords)
+  static constexpr int PUSED = KC / 2 + 1;                  // (PB) pairs staged per row
+  static constexpr int PSZ = TR * PITCH;                    // dwords
   static constexpr int QSLOTS = TC * 5;                     // 16-byte slots of the G image
   static constexpr int QBYTES = QSLOTS * 16;
-  static constexpr int PBYTES = (PSZ * ESZ + 15) / 16 * 16;
+  static constexpr int PBYTES = PSZ * 4;
   static constexpr int BUF = PBYTES + QBYTES;               // bytes per buffer
   static constexpr int NWR = TR / 64, NW = NWR * 4, NTH = NW * 64;
   static constexpr int PROUNDS = (PSZ + NTH - 1) / NTH;
@@ -911,7 +915,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     const int mt = rem >> 3, kc = rem & 7;
     const int l0 = mt * FTV + kc * G::KC;
     const int lim = min(min(G::KC, FTV - kc * G::KC), L - l0);  // valid positions of the piece
-    // (PB: a resource over the bf16 tensor, in fp32 units of its bytes)
+    // (PB: a resource over the bf16 tensor, in fp32 units of its bytes; r0 and the
+    // clip stride are even, so pair boundaries are dword boundaries)
     const __amdgpu_buffer_rsrc_t rs_p =
         PB ? make_rsrc(reinterpret_cast<const float *>(reinterpret_cast<const __bf16 *>(p.P) +
                                                        (int64_t)n * p.p_bstride + (int64_t)r0 * L),
@@ -921,13 +926,17 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     for (int i = 0; i < G::PROUNDS; ++i) {
       const int base = (i * G::NW + wave) * 64;  // wave-uniform
       if (base < G::PSZ) {
-        const bool ok = prow[i] >= 0 && prow[i] < prow_lim && pcol[i] < lim;
-        const unsigned voff = ok ? (unsigned)(prow[i] * L + l0 + pcol[i]) * (unsigned)G::ESZ : kOOB;
-        if constexpr (PB)  // 2-byte LDS-DMA: lane l lands at base + 2 l
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              rs_p, reinterpret_cast<float *>(buf + base * 2), 2, voff, 0, 0, 0);
-        else
-          blds_f32(rs_p, voff, reinterpret_cast<float *>(buf) + base);
+        unsigned voff;
+        if constexpr (PB) {  // pair pcol of the row's piece, from element (row start - sh)
+          const int sh = (prow[i] & 1) & (L & 1);
+          const int e = 2 * pcol[i] - sh;  // first element of the pair, rel. to the piece
+          const bool ok = prow[i] >= 0 && prow[i] < prow_lim && pcol[i] < G::PUSED && e < lim;
+          voff = ok ? (unsigned)(prow[i] * L + l0 + e) * 2u : kOOB;
+        } else {
+          const bool ok = prow[i] >= 0 && prow[i] < prow_lim && pcol[i] < lim;
+          voff = ok ? (unsigned)(prow[i] * L + l0 + pcol[i]) * 4u : kOOB;
+        }
+        blds_f32(rs_p, voff, reinterpret_cast<float *>(buf) + base);
       }
     }
     // Gk rows of this clip / column tile: (c0 + row) * nmt * 256 + mt * 256 + kc * 32
@@ -967,7 +976,16 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     const char *cur = lds + sl * G::BUF;
     sl = sl + 1 == NS ? 0 : sl + 1;
     const float *pa = reinterpret_cast<const float *>(cur) + (wr * 64 + lo) * G::PITCH + 8 * hi;
-    const __bf16 *pab = reinterpret_cast<const __bf16 *>(cur) + (wr * 64 + lo) * G::PITCH + 8 * hi;
+    // (PB: dword 4 hi of the row = its pairs from element 8 hi - sh; sh = 1 on odd
+    // rows of an odd-length clip row; the item's valid positions: lim_b)
+    const unsigned *pab = reinterpret_cast<const unsigned *>(cur) + (wr * 64 + lo) * G::PITCH + 4 * hi;
+    const bool shb = PB && (lo & 1) && (L & 1);  // rows wr*64 + i*32 + lo: parity of lo
+    int lim_b = G::KC;
+    if constexpr (PB) {
+      const int n_it = it / p.n_mtiles, rem_it = it - n_it * p.n_mtiles;
+      const int l0b = (rem_it >> 3) * FTV + (rem_it & 7) * G::KC;
+      lim_b = min(min(G::KC, FTV - (rem_it & 7) * G::KC), L - l0b);
+    }
     const char *qb = cur + G::PBYTES + ((wc * 64 + lo) * 5 + hi) * 16;
     // every fragment of the item first, as 16-byte reads (rows are 16-byte
     // aligned: PITCH * 4 = 144 B), one LDS wait, then the conversions and the
@@ -976,15 +994,17 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
     constexpr int NKS = G::KC / 16;
     typedef float f32x4v __attribute__((ext_vector_type(4)));
     f32x4v pf[NKS][2][2];
-    bf16x8f pbf[NKS][2];
+    uint4 pq[NKS][2];
+    unsigned pe[NKS][2];
     bf16x8f b[NKS][2];
 #pragma unroll
     for (int s = 0; s < NKS; ++s)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (PB) {
-          pbf[s][i] = *reinterpret_cast<const bf16x8f *>(
-              __builtin_assume_aligned(pab + i * 32 * G::PITCH + 16 * s, 16));
+          const unsigned *src = pab + i * 32 * G::PITCH + 8 * s;
+          pq[s][i] = *reinterpret_cast<const uint4 *>(__builtin_assume_aligned(src, 16));
+          pe[s][i] = src[4];
         } else {
           const f32x4v *src = reinterpret_cast<const f32x4v *>(
               __builtin_assume_aligned(pa + i * 32 * G::PITCH + 16 * s, 16));
@@ -1003,7 +1023,28 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_gemm_gk(WgradParams p) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         if constexpr (PB) {
-          a[i] = pbf[s][i];
+          const uint4 q = pq[s][i];
+          uint4 w = q;
+          if (shb) {  // odd-start row: elements from the high half of dword 0
+            w.x = __builtin_amdgcn_alignbit(q.y, q.x, 16);
+            w.y = __builtin_amdgcn_alignbit(q.z, q.y, 16);
+            w.z = __builtin_amdgcn_alignbit(q.w, q.z, 16);
+            w.w = __builtin_amdgcn_alignbit(pe[s][i], q.w, 16);
+          }
+          // positions k = 16 s + 8 hi + j past the piece (lim_b) are 0 (the pair
+          // at the boundary and, on shifted rows, the element after it)
+          const int k0 = 16 * s + 8 * hi;
+          if (k0 + 8 > lim_b) {
+            unsigned m[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+              m[d] = (k0 + 2 * d < lim_b ? 0xffffu : 0u) | (k0 + 2 * d + 1 < lim_b ? 0xffff0000u : 0u);
+            w.x &= m[0];
+            w.y &= m[1];
+            w.z &= m[2];
+            w.w &= m[3];
+          }
+          a[i] = __builtin_bit_cast(bf16x8f, w);
         } else {
           const f32x4v lo4 = pf[s][i][0], hi4 = pf[s][i][1];
           a[i] = bf16x8f{(__bf16)lo4.x, (__bf16)lo4.y, (__bf16)lo4.z, (__bf16)lo4.w,
