@@ -70,6 +70,12 @@ def build_model(pkg, cfg, device):
     return model.to(device)
 
 
+def progress(msg):
+    """A progress line on stderr (long phases must keep writing: a GPU run
+    silent for 3 minutes is taken to be hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_model():
     """The host CPU's model name (/proc/cpuinfo), or platform.processor()."""
     try:
@@ -99,7 +105,7 @@ def cpu_baseline(cfg, seconds=8.0):
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = ncpu
-    cands = sorted({ncpu, max(1, min(16, share))}, reverse=True)
+    cands = sorted({ncpu, max(1, min(16, share))})
     A = adjacency(pkg, cfg)
     p, b = ref_cpu.init_stack_params(cfg["C"], cfg["classes"], A, seed=0)
     p = {k: v.clone().requires_grad_(True) for k, v in p.items()}
@@ -114,15 +120,29 @@ def cpu_baseline(cfg, seconds=8.0):
 
     prev = torch.get_num_threads()
     res = []
+    import threading
+    done = threading.Event()
+
+    def beat():  # one oversubscribed step can outlast the 3-minute silence limit
+        while not done.wait(45):
+            progress("cpu baseline: running")
+    threading.Thread(target=beat, daemon=True).start()
     for threads in cands:
         torch.set_num_threads(threads)
+        t0 = time.perf_counter()
         step()  # warm-up
+        tw = time.perf_counter() - t0
+        progress(f"cpu baseline: {threads} threads, warm-up step {tw:.1f}s")
+        if res and tw > 4 * n / res[-1][0]:  # far slower than the smaller thread count
+            res.append((n / tw, threads, 1, tw))  # (oversubscribed: one step is the sample)
+            continue
         iters, t0 = 0, time.perf_counter()
         while iters < 2 or time.perf_counter() - t0 < seconds:
             step()
             iters += 1
         dt = time.perf_counter() - t0
         res.append((n * iters / dt, threads, iters, dt))
+    done.set()
     torch.set_num_threads(prev)
     best = max(res)
     return {"value": round(best[0], 3), "unit": "clips/s", "cores": best[1],
@@ -179,7 +199,8 @@ def kernel_roofline(pkg, device, cfg, iters=10):
         d[key] = (t[0] + ms, t[1] + fl, t[2] + n, t[3] + nb)
 
     V4 = cfg["V"] * 4
-    for ci, co, t, s in stack_layers(cfg):
+    for li, (ci, co, t, s) in enumerate(stack_layers(cfg)):
+        progress(f"kernel timing: layer {li}")
         x3 = cfg.get("f32_gemm") == "bf16x3" and not cfg["bf16"]
         d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
                                 bf16=cfg["bf16"], f32x3=x3)
@@ -222,14 +243,16 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 # the fused spatial backward (bf16, V = 25, K = 3); the unfused
                 # pair is timed per kernel by which 5 / 6
                 if lib.stgcn_time_kernel_bytes(ctypes.byref(d), 5) == 0:
-                    add(symbols, f"k_sp_bwd_fused<{V},{K},{'true' if x3 else 'false'}>",
+                    add(symbols, f"k_sp_bwd_fused<{V},{K},{'true' if x3 else 'false'},"
+                                 f"{'true' if dzb else 'false'}>",
                         ms.value, fl.value, 1, act)
                 continue
             if which == 6:
                 add(symbols, joint_bwd_symbol(cfg, ci, t), ms.value, fl.value, 1, act)
                 continue
             if which == 5:  # the stacked H GEMM (NQ = 1 over C_out channels)
-                sym = (f"k_conv_bf16<1,16,{V},1>" if cfg["bf16"] and co >= 16
+                sym = (f"k_conv_bf16<1,16,{V},1,{'true' if dzb else 'false'}>"
+                       if cfg["bf16"] and co >= 16
                        else f"k_tconv<1,8,{V},1>")
                 add(symbols, sym, ms.value, fl.value, 1, act)
                 continue
@@ -241,7 +264,7 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                        1: (f"k_conv_x3<9,3,{V},1,1,1,{ib}>" if s == 1 else
                            f"k_conv_x3<5|4,{V},1,1,1,false>"),
                        2: f"k_wgrad_bf16<9,{V},{s},{ft},{cb},{ib}>",
-                       3: (f"k_conv_bf16<1,16,{V},1>" if ci < 16 else
+                       3: (f"k_conv_bf16<1,16,{V},1,false>" if ci < 16 else
                            f"k_sp_fwd_bf16<{V},{K}>" if not (V == 50 or (V == 25 and K == 3)) else
                            f"k_sp_fwd_wide<{V},3,{64 if co <= 64 else 128 if co <= 128 else 256}>")
                        }[which]
@@ -385,6 +408,7 @@ def main():
         opt.step()
         return loss
 
+    progress(f"{args.config}: model built, {args.warmup} warm-up steps")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -427,6 +451,7 @@ def main():
             d1 = t.item()
         runs.append(cfg["N"] * world * args.steps / d1)
     gf_clip = pkg.flops_per_clip(cfg["C"], cfg["T"], cfg["V"], cfg["K"], cfg["classes"]) / 1e9
+    progress(f"{args.config}: {clips:.1f} clips/s ({[round(r, 1) for r in runs]})")
 
     # the exact fp32-MFMA path (every GEMM on v_mfma_f32_32x32x2_f32) timed
     # beside the default bf16x3 path, same model and inputs (N=1 only)
@@ -471,7 +496,9 @@ def main():
         if alt is not None:
             out["fp32_mfma_path"] = alt
         if not args.no_roofline:
+            progress("per-block rates")
             out["per_block_clips_s"] = per_block_rates(model, cfg, device)
+            progress("per-kernel timing (roofline)")
             kinds, symbols = kernel_roofline(pkg, device, cfg)
             sym = max(symbols, key=lambda k: symbols[k][0])
             ms_tot, fl_tot, nl, nb_tot = symbols[sym]
@@ -506,6 +533,7 @@ def main():
                 "per_symbol_ms_per_step": {k: round(v[0], 3) for k, v in
                                            sorted(symbols.items(), key=lambda kv: -kv[1][0])}}
         if world == 1 and not args.no_cpu_baseline:
+            progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(cfg)
         print(json.dumps(out), flush=True)
     if world > 1:
