@@ -223,10 +223,9 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # those operands move 2 bytes per element
             ab = cfg["bf16"] and s == 1 and ci >= 16
             V2 = V * 2 if ab else V4
-            # bf16 storage of dZ (capi.hip dz_bf16: kept bf16 G, C_in >= 16; the
-            # fused spatial backward at V = 25, K = 3, the bf16-input H GEMM at V = 50):
-            # the data gradient's output, the spatial backward's input
-            dzb = cfg["bf16"] and ci >= 16 and (V == 50 or (V == 25 and K == 3 and ci % 32 == 0))
+            # bf16 storage of dZ (capi.hip dz_bf16) is an A/B build only
+            # (STGCN_AB_DZ_BF16): the shipped library stores dZ in fp32
+            dzb = False
             VZ = V * 2 if dzb else V4
             act = {0: N * (co * t * V2 + co * to * V4), 1: N * (co * to * V2 + co * t * VZ),
                    2: N * (co * to + co * t) * V2,

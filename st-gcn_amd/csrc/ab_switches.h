@@ -25,11 +25,11 @@
 #ifndef STGCN_AB_ACT_FP32       // fp32 storage of Z / dU on the bf16 path
 #define STGCN_AB_ACT_FP32 0
 #endif
-#ifndef STGCN_AB_NO_SLICE       // the unfused spatial backward over the whole batch at once
-#define STGCN_AB_NO_SLICE 0
+#ifndef STGCN_AB_SLICE          // the unfused spatial backward in Infinity-Cache-sized clip slices
+#define STGCN_AB_SLICE 0
 #endif
-#ifndef STGCN_AB_DZ_FP32        // fp32 storage of dZ on the bf16 path (capi.hip dz_bf16)
-#define STGCN_AB_DZ_FP32 0
+#ifndef STGCN_AB_DZ_BF16        // bf16 storage of dZ on the bf16 path (capi.hip dz_bf16)
+#define STGCN_AB_DZ_BF16 0
 #endif
 #ifndef STGCN_AB_X3_MR1         // 64-row tiles only in k_conv_x3
 #define STGCN_AB_X3_MR1 0

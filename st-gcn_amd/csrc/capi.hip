@@ -101,14 +101,17 @@ bool fused_spb(const stgcn_desc_t *d) {
   return !off && (bf16(d) || f32x3(d)) &&
          sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T, f32x3(d));
 }
-// Clips per slice of the unfused spatial backward (H GEMM + joint kernel): the
-// slice's H, dZ, x and dx (fp32) within ~160 MiB, so the Infinity Cache (256
-// MiB; it keeps a line resident while the bytes moved between two uses of it
-// fit, MI355X_MICROARCH.md) serves H's read-back. At least 8 clips a slice
-// (enough workgroups per launch). STGCN_AB_NO_SLICE build: one slice.
+// Clips per slice of the unfused spatial backward (H GEMM + joint kernel). The
+// shipped build runs the whole batch as one slice. STGCN_AB_SLICE build (A/B
+// only): the slice's H, dZ, x and dx (fp32) within ~160 MiB, so the Infinity
+// Cache (256 MiB; MI355X_MICROARCH.md) could serve H's read-back -- measured
+// SLOWER in one A/B call (round 3: cfg5 2126 vs 2324, cfg2 4182 vs 4432 clips/s):
+// the persistent joint kernels (k_spatial_bwd5/6) flush their dA accumulators
+// and BN1 sums once per launch, so 16 launches per layer (8-clip slices at cfg5)
+// multiply that tail and underfill the grid.
 int spatial_bwd_slice(const stgcn_desc_t *d) {
-  constexpr bool off = STGCN_AB_NO_SLICE != 0;
-  if (off) return d->N;
+  constexpr bool on = STGCN_AB_SLICE != 0;
+  if (!on) return d->N;
   const int64_t per_clip =
       (int64_t)4 * d->T * d->V * ((int64_t)d->K * d->C_in + d->C_out + 2 * d->C_in);
   const int64_t budget = (int64_t)160 << 20;
@@ -330,10 +333,12 @@ bool du_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
 // (k_sum_nt4_bf16), accumulates the bf16 values in fp64. Producer: the temporal
 // data-gradient (one-plane k_conv_x3, bf16 epilogue store). The buffer keeps
 // its fp32 size.
-// (STGCN_AB_DZ_FP32 build: fp32 dZ, A/B only)
+// Not the shipped default: measured in one A/B call (round 3) fp32 dZ ran cfg3
+// 5415 vs 5285 and cfg5 2137 vs 2126 clips/s, so bf16 dZ is the STGCN_AB_DZ_BF16
+// build only (A/B measurement).
 bool dz_bf16(const stgcn_desc_t *d) {
-  constexpr bool off = STGCN_AB_DZ_FP32 != 0;
-  if (off || !bf16(d) || residual(d) || !fused_sp(d)) return false;
+  constexpr bool on = STGCN_AB_DZ_BF16 != 0;
+  if (!on || !bf16(d) || residual(d) || !fused_sp(d)) return false;
   if (!fused_spb(d)) {  // the unfused spatial backward: its H GEMM reads dZ (k_conv_bf16<.., IB>)
     ConvGemmParams h = conv_base(d, nullptr);
     h.C = d->C_out;
