@@ -227,14 +227,19 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # (STGCN_AB_DZ_BF16): the shipped library stores dZ in fp32
             dzb = False
             VZ = V * 2 if dzb else V4
+            # the two-person graph's fused spatial backward: two kernels, each
+            # reading dZ and x (k_sp50_dx also writes dx), timed as which 5 / 6
+            f50 = cfg["bf16"] and V == 50 and K == 3 and ci % 32 == 0 and ci <= 128
             act = {0: N * (co * t * V2 + co * to * V4), 1: N * (co * to * V2 + co * t * VZ),
                    2: N * (co * to + co * t) * V2,
                    3: N * (ci * t * V4 + co * t * V2) + (N * K * ci * t * V * 2
                                                        if cfg["bf16"] and ci >= 16 else
                                                        N * K * ci * t * V4),
                    4: N * (co * t * VZ + 2 * ci * t * V4),  # dZ, x in; dx out
-                   5: N * (co * t * VZ + K * ci * t * V4),  # dZ in; H out
-                   6: N * (K * ci * t + 2 * ci * t) * V4}[which]  # H, x in; dx out
+                   5: (N * (co * t * VZ + 2 * ci * t * V4) if f50 else  # dZ, x in; dx out
+                       N * (co * t * VZ + K * ci * t * V4)),  # dZ in; H out
+                   6: (N * (co * t * VZ + ci * t * V4) if f50 else  # dZ, x in
+                       N * (K * ci * t + 2 * ci * t) * V4)}[which]  # H, x in; dx out
             if which <= 4:
                 add(kinds, KERNEL_KINDS[which], ms.value, fl.value, 1, act)
             # rocprof short names of the kernel each timing runs
@@ -247,7 +252,11 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                         ms.value, fl.value, 1, act)
                 continue
             if which == 6:
-                add(symbols, joint_bwd_symbol(cfg, ci, t), ms.value, fl.value, 1, act)
+                add(symbols, f"k_sp50_dA<{K}>" if f50 else joint_bwd_symbol(cfg, ci, t),
+                    ms.value, fl.value, 1, act)
+                continue
+            if which == 5 and f50:
+                add(symbols, f"k_sp50_dx<{K}>", ms.value, fl.value, 1, act)
                 continue
             if which == 5:  # the stacked H GEMM (NQ = 1 over C_out channels)
                 sym = (f"k_conv_bf16<1,16,{V},1,{'true' if dzb else 'false'}>"

@@ -22,12 +22,18 @@ shapes = [("L1 64->64 T300", 64, 64, 300), ("L4 64->128 T300", 64, 128, 300),
           ("L5 128->128 T150", 128, 128, 150), ("L8 256->256 T75", 256, 256, 75)]
 for label, ci, co, T in shapes:
     d = pkg.fused.make_desc((128, ci, T, V), co, K, 1, 4, 1e-5, 0.1, True, bf16=not x3, f32x3=x3)
-    nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), 4)
-    scratch = torch.randn(nbytes // 4 + 1, device=dev) * 0.1
-    ms, fl = ctypes.c_float(0), ctypes.c_double(0)
-    hl.check(lib.stgcn_time_kernel(ctypes.byref(d), 4, hl.ptr(scratch), nbytes, iters,
-                                   hl.stream_handle(dev), ctypes.byref(ms), ctypes.byref(fl)))
-    mb = 4 * 128 * T * V * (co + 2 * ci) / 1e6
-    print(f"{label:18s} {ms.value * 1e3:8.1f} us  {fl.value / ms.value / 1e9:6.1f} TF/s  "
-          f"{mb / ms.value / 1e3:6.2f} TB/s (dZ + x + dx)", flush=True)
-    del scratch
+    out = []
+    for which in (4, 5, 6):  # whole backward; its two kernels (H GEMM / joint, or V = 50 dx / dA)
+        nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
+        if nbytes == 0:
+            continue
+        scratch = torch.randn(nbytes // 4 + 1, device=dev) * 0.1
+        ms, fl = ctypes.c_float(0), ctypes.c_double(0)
+        hl.check(lib.stgcn_time_kernel(ctypes.byref(d), which, hl.ptr(scratch), nbytes, iters,
+                                       hl.stream_handle(dev), ctypes.byref(ms), ctypes.byref(fl)))
+        out.append(f"w{which} {ms.value * 1e3:7.1f} us")
+        if which == 4:
+            mb = 4 * 128 * T * V * (co + 2 * ci) / 1e6
+            out.append(f"({mb / ms.value / 1e3:5.2f} TB/s of dZ + x + dx)")
+        del scratch
+    print(f"{label:18s} " + "  ".join(out), flush=True)

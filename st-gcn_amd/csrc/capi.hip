@@ -101,6 +101,9 @@ bool fused_spb(const stgcn_desc_t *d) {
   return !off && (bf16(d) || f32x3(d)) &&
          sp_bwd_fused_supported(d->C_in, d->V, d->K, d->C_out, d->T, f32x3(d));
 }
+// the fused backward of the two-person graph: two kernels (k_sp50_dx, k_sp50_dA),
+// timed apart as which 5 / 6
+bool fused_spb50(const stgcn_desc_t *d) { return fused_spb(d) && d->V == 50; }
 // Clips per slice of the unfused spatial backward (H GEMM + joint kernel). The
 // shipped build runs the whole batch as one slice. STGCN_AB_SLICE build (A/B
 // only): the slice's H, dZ, x and dx (fp32) within ~160 MiB, so the Infinity
@@ -339,6 +342,7 @@ bool du_bf16(const stgcn_desc_t *d) { return act_bf16(d); }
 bool dz_bf16(const stgcn_desc_t *d) {
   constexpr bool on = STGCN_AB_DZ_BF16 != 0;
   if (!on || !bf16(d) || residual(d) || !fused_sp(d)) return false;
+  if (fused_spb(d) && d->V == 50) return false;  // (k_sp50_dx / _dA read fp32 dZ)
   if (!fused_spb(d)) {  // the unfused spatial backward: its H GEMM reads dZ (k_conv_bf16<.., IB>)
     ConvGemmParams h = conv_base(d, nullptr);
     h.C = d->C_out;
@@ -921,9 +925,11 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 //            applies, else the stacked H GEMM + the joint kernel; H GEMM and
 //            joint contraction FLOPs)
 //         5: the stacked H GEMM of the unfused spatial backward alone
+//            (V = 50 fused: its dx kernel k_sp50_dx alone)
 //         6: the joint kernel of the unfused spatial backward alone
+//            (V = 50 fused: its dA kernel k_sp50_dA alone)
 //            (k_spatial_bwd5 / _bwd6 / _bwd3: dx, dA, BN1 sums from H)
-//         (5 and 6 fail with STGCN_E_UNSUPPORTED where k_sp_bwd_fused runs)
+//         (5 and 6 fail with STGCN_E_UNSUPPORTED where k_sp_bwd_fused<25> runs)
 // flops = the algorithmic FLOPs of one launch (SURVEY.md §8d terms).
 // ---------------------------------------------------------------------------
 namespace {
@@ -1070,6 +1076,8 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     }
     P.flops = (P.spb_gemm ? 2.0 * K * C * (double)R * T * V * N : 0.0) +
               (P.spb_joint ? 4.0 * K * C * (double)T * V * V * N : 0.0);
+    if (fused_spb50(d) && which >= 5)  // k_sp50_dx / _dA: each its H GEMM + its contraction
+      P.flops = 2.0 * K * C * (double)R * T * V * N + 2.0 * K * C * (double)T * V * V * N;
   } else if (fused_sp(d)) {
     // the forward's fused spatial kernel (G kept in bf16 as in the stack)
     P.spf = true;
@@ -1116,7 +1124,7 @@ extern "C" {
 
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which) {
   if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 6) return 0;
-  if (which >= 5 && fused_spb(d)) return 0;
+  if (which >= 5 && fused_spb(d) && !fused_spb50(d)) return 0;
   return plan_timed(d, which, nullptr).bytes;
 }
 
@@ -1126,7 +1134,7 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
   if (rc) return rc;
   if (which < 0 || which > 6 || iters <= 0 || !avg_ms || !flops)
     return fail(STGCN_E_INVALID, "bad timing request");
-  if (which >= 5 && fused_spb(d))
+  if (which >= 5 && fused_spb(d) && !fused_spb50(d))
     return fail(STGCN_E_UNSUPPORTED, "the spatial backward is one fused kernel here (which 4)");
   TimedPlan P = plan_timed(d, which, scratch);
   if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
@@ -1139,7 +1147,8 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
         return launch_sp_bwd_fused(P.dZ, P.x, P.st, P.st + C, P.st + 2 * C, P.st + 3 * C, P.A,
                                    P.W, P.wpk, P.dx, P.dA, P.sd, P.sd + C, d->N, C, d->C_out,
                                    d->T, d->V, d->K, 1, residual(d) ? 1 : 0, f32x3(d), s,
-                                   nullptr, dz_bf16(d) ? 1 : 0);
+                                   nullptr, dz_bf16(d) ? 1 : 0,
+                                   P.spb_gemm && P.spb_joint ? 0 : (P.spb_gemm ? 1 : 2));
       if (P.spb_gemm) {
         hipError_t e = launch_conv_gemm(P.cp[0], s);
         if (e != hipSuccess || !P.spb_joint) return e;

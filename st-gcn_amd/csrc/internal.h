@@ -251,6 +251,8 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
                                int write_dx, int relu, bool x3, hipStream_t s,
-                               const PrevBn *prev = nullptr, int dz_bf16 = 0);
+                               const PrevBn *prev = nullptr, int dz_bf16 = 0, int only = 0);
+// V = 50 runs the fused backward as two kernels (k_sp50_dx, k_sp50_dA); only = 1 / 2
+// launches just the first / second of them (timing entry point), 0 both.
 
 }  // namespace stgcn

@@ -266,29 +266,43 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     n = r / P.nft;
   };
   const spb_i4 rw = spb_rsrc(P.wpk, (int64_t)P.ncb * NCH * G::W_BYTES);
-  // DMA of global chunk gch (3 instructions per wave: dZ rows 2w, 2w+1 and 1/8 of W')
-  auto issue_chunk = [&](int gch) {
-    const int k = gch / NCH, c = gch - k * NCH;
-    int n, ft, cb;
-    decode(first + k * NG, n, ft, cb);
-    const int p0 = ft * G::FT * V;
-    const int slot = gch % D;
-    const spb_i4 rz =
-        DZB ? spb_rsrc(reinterpret_cast<const __bf16 *>(P.dZ) + (int64_t)n * P.R * TV,
-                       (int64_t)P.R * TV * 2)
-            : spb_rsrc(P.dZ + (int64_t)n * P.R * TV, (int64_t)P.R * TV * 4);
+  // issue cursor: the next chunk to DMA (item ik of this workgroup, chunk ic, ring
+  // slot islot); the item's dZ resource, first-row offset and W' base are formed
+  // once per item (no run-time divisions per chunk)
+  int ik = 0, ic = 0, islot = 0, irow = 0, iwb = 0;
+  spb_i4 rz;
+  auto start_item = [&]() {
+    int n = 0, ft = 0, cb = 0;
+    if (ik < myitems) decode(first + ik * NG, n, ft, cb);
+    rz = DZB ? spb_rsrc(reinterpret_cast<const __bf16 *>(P.dZ) + (int64_t)n * P.R * TV,
+                        (int64_t)P.R * TV * 2)
+             : spb_rsrc(P.dZ + (int64_t)n * P.R * TV, (int64_t)P.R * TV * 4);
+    irow = ft * G::FT * V;
+    iwb = cb * NCH * G::W_BYTES;
+  };
+  start_item();
+  // DMA of the cursor's chunk (3 instructions per wave: dZ rows 2w, 2w+1 and 1/8 of
+  // W'), then advance the cursor
+  auto issue_chunk = [&]() {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int r = 2 * wave + h;
-      const int start = (c * G::CR + r) * TV + p0;  // from the 16-byte boundary below: the row's shift
-      constexpr int EPP = 16 / G::ZSZ;              // elements per 16-byte piece
+      const int start = irow + r * TV;  // from the 16-byte boundary below: the row's shift
+      constexpr int EPP = 16 / G::ZSZ;  // elements per 16-byte piece
       const unsigned voff = (unsigned)(((start & ~(EPP - 1)) + EPP * lane) * G::ZSZ);
       if (lane < G::NPCZ)
-        spb_dma16(rz, voff, lds0 + G::OFF_RING + slot * G::RING_SLOT + r * G::RPZ * G::ZSZ);
+        spb_dma16(rz, voff, lds0 + G::OFF_RING + islot * G::RING_SLOT + r * G::RPZ * G::ZSZ);
     }
     if (lane < G::WPW)
-      spb_dma16(rw, (unsigned)((cb * NCH + c) * G::W_BYTES + wave * G::WPW * 16 + lane * 16),
-                lds0 + G::OFF_W + slot * G::W_BYTES + wave * G::WPW * 16);
+      spb_dma16(rw, (unsigned)(iwb + ic * G::W_BYTES + wave * G::WPW * 16 + lane * 16),
+                lds0 + G::OFF_W + islot * G::W_BYTES + wave * G::WPW * 16);
+    islot = islot + 1 == D ? 0 : islot + 1;
+    irow += G::CR * TV;
+    if (++ic == NCH) {
+      ic = 0;
+      ++ik;
+      start_item();
+    }
   };
   // DMA of an item's x slice: 32 channel rows (4 per wave)
   auto issue_x = [&](int item) {
@@ -316,7 +330,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
   const float *xs = reinterpret_cast<const float *>(lds + G::OFF_X);
 
   if (myitems > 0) issue_x(first);
-  for (int gch = 0; gch < D - 1 && gch < nchunks; ++gch) issue_chunk(gch);
+  for (int gch = 0; gch < D - 1 && gch < nchunks; ++gch) issue_chunk();
 
   int gch = 0;
   for (int k = 0; k < myitems; ++k) {
@@ -339,7 +353,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       const int after = 3 * min(D - 2, nchunks - 1 - gch) + (k > 0 && c <= D - 2 ? 4 : 0);
       spb_wait_vm(after);
       spb_barrier();  // chunk gch in LDS for every wave; chunk gch - 1 retired
-      if (gch + D - 1 < nchunks) issue_chunk(gch + D - 1);
+      if (gch + D - 1 < nchunks) issue_chunk();
       const int slot = gch % D;
       if (STGCN_SPB_EXP & 1) continue;
       // A operand: dZ[r = 8 hi + j][frame f, joint lo] (0 past V: read at a
@@ -641,6 +655,580 @@ __global__ void k_pack_spb_a(const float *A, __bf16 *img, int K, int V, int NP) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// The two-person graph (V = 50, two 32-joint tiles), bf16 path: the SpatialConv
+// backward as TWO kernels that each recompute H = W'^T dZ from dZ on MFMA and
+// keep it in registers (H never reaches HBM; the unfused pair wrote H in fp32 --
+// K * C_in channels, 3x dZ at C_in = C_out -- and read it back):
+//   k_sp50_dx<K>: dx = sum_k H_k A_k and the BN1 backward sums (+ the deferred-dx
+//                 chain's mask sums), wave = (frame f, output joint tile wt):
+//                 T_k = H_k^T for both joint tiles (the B operand of
+//                 dx^T = A_k^T H_k^T, lane = ci), the A image [k][wt][vt][ks]
+//                 [plane] in LDS, the row pass on the accumulator registers
+//                 (lane = ci, 16 joints of frame f: mask, sums, 8-byte stores).
+//   k_sp50_dA<K>: dA_k += sum H_k^T f(BN1(x)), wave = (frame f, joint tile vt):
+//                 S_k = H_k (the A operand, lane = v), f(BN1(x)) as a bf16 image
+//                 (row (frame, w), channel slots in the accumulator order), the
+//                 12 dA tiles of the workgroup resident for the whole loop.
+// One 8-wave workgroup per CU each; item = (clip, 4 frames, 32 input channels),
+// every item of a workgroup in the same 32-channel block (grid a multiple of the
+// block count), so the per-lane BN tables and sums stay in registers. dZ chunks
+// (16 channels x 4 frames x 50 joints) and the packed W' chunk move by LDS-DMA
+// through a 6-deep ring that runs across items; the item's x values are loaded
+// into registers under the next item's chunk loop. Every wait counts this wave's
+// own vector-memory instructions (`issued`, marks per ring slot), so the ring
+// stays full across the per-item phases.
+// Numerics as k_sp_bwd_fused / k_spatial_bwd6<.., BF = true>: H from bf16 dZ and
+// W' with fp32 accumulation, H and A to 2^-16 (h + m planes, three products) in
+// dx, H to 2^-16 and f(BN1(x)) to bf16 (two products) in dA.
+// ---------------------------------------------------------------------------
+#ifndef STGCN_SP50_EXP  // timing experiments only (bits skip work; results wrong): 1 x
+#define STGCN_SP50_EXP 0  // loads, 2 dx stores, 4 dx / dA MFMAs, 8 chunk MFMAs
+#endif
+template <int K>
+struct Sp50Geo {
+  static constexpr int V = 50, FT = 4, NPOS = FT * V;         // 200 positions per item
+  static constexpr int NPC = (NPOS + 3 + 3) / 4;              // 16-byte pieces per dZ row
+  static constexpr int RP = (NPC * 4) % 8 == 0 ? NPC * 4 + 4 : NPC * 4;  // row pitch (floats)
+  static constexpr int CB = 32, CR = 16, D = 6;               // ci per item, dZ rows per chunk, ring depth
+  static constexpr int RING_SLOT = CR * RP * 4;
+  static constexpr int W_BYTES = K * CR * 64;                 // W' chunk [k][octet][ci 32][8] bf16
+  static constexpr int WPW = W_BYTES / 16 / 8;                // W' pieces per wave
+  static constexpr int AIMG = K * 2 * 2 * 2 * 2 * 1024;       // [k][wt][vt][ks][plane] fragments
+  static constexpr int XBP = 80, XB_ROWS = NPOS + 1;          // f(BN1(x)) image (+ a zero row)
+  static constexpr int XB_BYTES = (XB_ROWS * XBP + 15) & ~15;
+  static constexpr int NQ2 = (NPOS + 15) / 16;                // dA kernel: x values per thread
+  // k_sp50_dx: A image | dZ ring | W' ring (the sum reduction reuses the ring)
+  static constexpr int L1_RING = AIMG, L1_W = L1_RING + D * RING_SLOT;
+  static constexpr int LDS1 = L1_W + D * W_BYTES;
+  // k_sp50_dA: dZ ring | W' ring | f(BN1(x)) image (the dA reduction reuses the ring)
+  static constexpr int L2_W = D * RING_SLOT, L2_XB = L2_W + D * W_BYTES;
+  static constexpr int LDS2 = L2_XB + XB_BYTES;
+  static_assert(LDS1 <= 160 * 1024 && LDS2 <= 160 * 1024, "LDS budget");
+  static_assert(8 * 32 * 4 * 8 <= D * RING_SLOT, "sum reduction fits the ring");
+  static_assert(K * V * V * 4 <= D * RING_SLOT, "dA reduction fits the ring");
+  static_assert(NPC <= 64 && WPW <= 64, "one DMA instruction per row / W' piece");
+};
+
+struct Sp50Params {
+  const float *dZ, *x, *mean, *invstd, *g, *b;
+  const __bf16 *wpk;   // [cb][chunk][k][octet][ci 32][8]
+  const __bf16 *aimg;  // [k][wt][vt][ks][plane][lane][8]
+  float *dx, *dA;
+  double *sd, *sdn;
+  int C, R, T, ncb, nft, nitems, write_dx, relu;
+  PrevBn prev;
+};
+
+// s_waitcnt vmcnt(q) for a run-time n, q = n rounded down to a multiple of 4
+// (at most 60): waiting for up to 3 more instructions than asked is safe and
+// keeps the dispatch to a 16-way branch tree
+__device__ __forceinline__ void sp50_wait_vm(int n) {
+  const int q = n < 0 ? 0 : (n > 63 ? 15 : n >> 2);
+  switch (q) {
+#define SP50_W(i) \
+  case i: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * i) : "memory"); break;
+    SP50_W(0) SP50_W(1) SP50_W(2) SP50_W(3) SP50_W(4) SP50_W(5) SP50_W(6) SP50_W(7)
+    SP50_W(8) SP50_W(9) SP50_W(10) SP50_W(11) SP50_W(12) SP50_W(13) SP50_W(14) SP50_W(15)
+#undef SP50_W
+  }
+}
+
+// Shared chunk pipeline of the two kernels: the ring of dZ chunks (2 rows per
+// wave) and W' chunks (1/8 per wave), 3 DMA instructions per wave and chunk.
+template <int K>
+struct Sp50Ring {
+  using G = Sp50Geo<K>;
+  const Sp50Params &P;
+  unsigned lds0;
+  int ring_off, w_off, first, NG, NCH, TV, wave, lane, myitems;
+  spb_i4 rw;
+  // issue cursor: the next chunk to DMA (item ik of this workgroup, chunk ic,
+  // ring slot islot); the item's dZ resource, first-row offset and W' base are
+  // formed once per item (no divisions per chunk)
+  int ik = 0, ic = 0, islot = 0, irow = 0, iwb = 0;
+  spb_i4 rz;
+  __device__ Sp50Ring(const Sp50Params &P_, unsigned lds0_, int ring_off_, int w_off_, int first_,
+                      int wave_, int lane_, int myitems_)
+      : P(P_), lds0(lds0_), ring_off(ring_off_), w_off(w_off_), first(first_), NG(gridDim.x),
+        NCH(P_.R / 16), TV(P_.T * 50), wave(wave_), lane(lane_), myitems(myitems_) {
+    rw = spb_rsrc(P.wpk, (int64_t)P.ncb * NCH * G::W_BYTES);
+    start_item();
+  }
+  __device__ void decode(int it, int &n, int &ft, int &cb) const {
+    cb = it % P.ncb;
+    const int r = it / P.ncb;
+    ft = r % P.nft;
+    n = r / P.nft;
+  }
+  __device__ void start_item() {
+    int n = 0, ft = 0, cb = 0;
+    if (ik < myitems) decode(first + ik * NG, n, ft, cb);
+    rz = spb_rsrc(P.dZ + (int64_t)n * P.R * TV, (int64_t)P.R * TV * 4);
+    irow = ft * G::NPOS;  // element offset of chunk ic's row 0 (rows of a chunk TV apart)
+    iwb = cb * NCH * G::W_BYTES;
+  }
+  // DMA of the cursor's chunk (3 instructions per wave), then advance the cursor
+  __device__ void issue_next() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 2 * wave + h;
+      const int start = irow + r * TV;  // from the 16-byte boundary below
+      if (lane < G::NPC)
+        spb_dma16(rz, (unsigned)(((start & ~3) + 4 * lane) * 4),
+                  lds0 + ring_off + islot * G::RING_SLOT + r * G::RP * 4);
+    }
+    if (lane < G::WPW)
+      spb_dma16(rw, (unsigned)(iwb + ic * G::W_BYTES + wave * G::WPW * 16 + lane * 16),
+                lds0 + w_off + islot * G::W_BYTES + wave * G::WPW * 16);
+    islot = islot + 1 == G::D ? 0 : islot + 1;
+    irow += G::CR * TV;
+    if (++ic == NCH) {
+      ic = 0;
+      ++ik;
+      start_item();
+    }
+  }
+  // dZ fragment of joint tile vt, frame f: rows r = 8 hi + j of the chunk in
+  // slot `slot`, joint 32 vt + lo (0 past V), rounded to bf16 -- the A operand
+  // [row v][k r] of T = dZ^T W, or the B operand [k r][col v] of S = W^T dZ
+  __device__ uint4 dz_frag(const char *lds, int slot, int f, int vt, int hi, int lo) const {
+    const int v = 32 * vt + lo;
+    const float *rz = reinterpret_cast<const float *>(lds + ring_off + slot * G::RING_SLOT) +
+                      8 * hi * G::RP + f * 50 + (v < 50 ? v : 49);
+    float dv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = rz[j * G::RP + ((j * TV) & 3)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dv[j] = v < 50 ? dv[j] : 0.f;
+    uint4 a;
+    a.x = spb_pk(dv[0], dv[1]);
+    a.y = spb_pk(dv[2], dv[3]);
+    a.z = spb_pk(dv[4], dv[5]);
+    a.w = spb_pk(dv[6], dv[7]);
+    return a;
+  }
+};
+
+template <int K>
+__global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
+  using G = Sp50Geo<K>;
+  constexpr int D = G::D;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int f = wave & 3, wt = wave >> 2;  // this wave's frame and output joint tile
+  const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(lds);
+  const int first = xcd_remap(blockIdx.x, gridDim.x);
+  const int myitems =
+      first < P.nitems ? (P.nitems - 1 - first) / (int)gridDim.x + 1 : 0;
+  Sp50Ring<K> ring(P, lds0, G::L1_RING, G::L1_W, first, wave, lane, myitems);
+  const int NCH = ring.NCH, NG = ring.NG, TV = ring.TV;
+  const int nchunks = myitems * NCH;
+  const bool pv = P.prev.mean != nullptr;
+  // this lane's channel (every item of the workgroup is in block first % ncb)
+  const int cb = first % P.ncb, c = cb * 32 + lo;
+  const float mu = P.mean[c], is = P.invstd[c], ga = is * P.g[c], be = P.b[c];
+  const float pmu = pv ? P.prev.mean[c] : 0.f, pis = pv ? P.prev.invstd[c] : 1.f;
+  const float pa = pv ? pis * P.prev.g[c] : 1.f, pb = pv ? P.prev.b[c] : 0.f;
+  {  // A image (48 KiB) by LDS-DMA
+    const spb_i4 ra = spb_rsrc(P.aimg, G::AIMG);
+    for (int i = wave; i < G::AIMG / 1024; i += 8)
+      spb_dma16(ra, (unsigned)(i * 1024 + lane * 16), lds0 + i * 1024);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // x (prev mode: the previous block's U) of this lane's 16 (frame f, joint w)
+  // positions, w = 32 wt + 8 gq + 4 hi + {0..3}: two 8-byte loads per group
+  // (one dword load per value: with 8-byte loads into float2 pairs hipcc copied
+  // the odd halves out of the registers before the loads had landed)
+  float xr[16];
+  // byte offset of the pair (group gq, half h2) of this lane in its clip's x / dx
+  auto xoff = [&](int ft, int gq, int h2) -> unsigned {
+    const int t = ft * G::FT + f, w = 32 * wt + 8 * gq + 4 * hi + 2 * h2;
+    const bool ok = t < P.T && w < 50;
+    return ok ? (unsigned)(((int64_t)c * TV + (int64_t)t * 50 + w) * 4) : kOOB;
+  };
+  auto load_x = [&](int item) {
+    if (STGCN_SP50_EXP & 1) return;
+    int n, ft, cbb;
+    ring.decode(item, n, ft, cbb);
+    const spb_i4 rx = spb_rsrc(P.x + (int64_t)n * P.C * TV, (int64_t)P.C * TV * 4);
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq)
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const unsigned o = xoff(ft, gq, h2);
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                       : "=v"(xr[4 * gq + 2 * h2 + e])
+                       : "v"(o == kOOB ? kOOB : o + 4u * e), "s"(rx)
+                       : "memory");
+      }
+  };
+
+  int issued = 0;  // vector-memory instructions this wave has issued
+  int mk[D - 1];   // `issued` just after the DMA of each chunk in flight (oldest first)
+  int mark_x = 0;
+  if (myitems > 0) {
+    load_x(first);
+    issued += (STGCN_SP50_EXP & 1) ? 0 : 16;
+    mark_x = issued;
+  }
+#pragma unroll
+  for (int i = 0; i < D - 1; ++i) {
+    if (i < nchunks) {
+      ring.issue_next();
+      issued += 3;
+    }
+    mk[i] = issued;
+  }
+  double ds = 0.0, dn = 0.0, d1 = 0.0, d2 = 0.0;
+  const char *aim = lds + lane * 16;
+  int gch = 0, rslot = 0;
+  for (int k = 0; k < myitems; ++k) {
+    const int item = first + k * NG;
+    int n, ft, cbb;
+    ring.decode(item, n, ft, cbb);
+    floatx16 T[K][2];
+#pragma unroll
+    for (int kk = 0; kk < K; ++kk)
+#pragma unroll
+      for (int vt = 0; vt < 2; ++vt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) T[kk][vt][i] = 0.f;
+    // ---- T_k = H_k^T = dZ^T W_k over the chunks, both joint tiles
+    for (int cc = 0; cc < NCH; ++cc, ++gch) {
+      sp50_wait_vm(issued - mk[0]);
+      spb_barrier();  // chunk gch in LDS for every wave; chunk gch - 1 retired
+#pragma unroll
+      for (int i = 0; i < D - 2; ++i) mk[i] = mk[i + 1];
+      if (gch + D - 1 < nchunks) {
+        ring.issue_next();
+        issued += 3;
+      }
+      mk[D - 2] = issued;
+      const int slot = rslot;
+      rslot = rslot + 1 == D ? 0 : rslot + 1;
+      const char *wb = lds + G::L1_W + slot * G::W_BYTES + hi * 512 + lo * 16;
+      const uint4 a0 = ring.dz_frag(lds, slot, f, 0, hi, lo);
+      const uint4 a1 = ring.dz_frag(lds, slot, f, 1, hi, lo);
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
+        if (STGCN_SP50_EXP & 8) { T[kk][0][0] += __builtin_bit_cast(float, a0.x ^ w.y); T[kk][1][0] += __builtin_bit_cast(float, a1.x); continue; }
+        T[kk][0] = spb_mfma(a0, w, T[kk][0]);  // [v][ci] = sum_r dZ[r][v] W_k[r][ci]
+        T[kk][1] = spb_mfma(a1, w, T[kk][1]);
+      }
+    }
+    // ---- dx^T[w][ci] = sum_k sum_v A_k[v][w] H_k^T[v][ci], w in tile wt
+    floatx16 dxa;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dxa[i] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < K; ++kk)
+#pragma unroll
+      for (int vt = 0; vt < 2; ++vt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          float tv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) tv[j] = T[kk][vt][8 * ks + j];
+          uint4 bpl[2];
+          spb_planes<2>(tv, bpl);
+          const int fr = (((kk * 2 + wt) * 2 + vt) * 2 + ks) * 2;
+          const uint4 am0 = *reinterpret_cast<const uint4 *>(aim + fr * 1024);
+          const uint4 am1 = *reinterpret_cast<const uint4 *>(aim + (fr + 1) * 1024);
+          if (STGCN_SP50_EXP & 4) { dxa[ks] += __builtin_bit_cast(float, am0.x ^ am1.y ^ bpl[0].x ^ bpl[1].y); continue; }
+          dxa = spb_mfma(am0, bpl[0], dxa);
+          dxa = spb_mfma(am1, bpl[0], dxa);
+          dxa = spb_mfma(am0, bpl[1], dxa);
+        }
+    // ---- row pass on the registers: lane = channel c, joints w of frame f
+    sp50_wait_vm(issued - mark_x);
+    asm volatile("" : "+v"(xr[0]), "+v"(xr[1]), "+v"(xr[2]), "+v"(xr[3]), "+v"(xr[4]),
+                 "+v"(xr[5]), "+v"(xr[6]), "+v"(xr[7]), "+v"(xr[8]), "+v"(xr[9]), "+v"(xr[10]),
+                 "+v"(xr[11]), "+v"(xr[12]), "+v"(xr[13]), "+v"(xr[14]), "+v"(xr[15]));
+    const bool tlive = ft * G::FT + f < P.T;
+    float s = 0.f, sn = 0.f, s1 = 0.f, s2 = 0.f;
+    float dv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int w = 32 * wt + (i & 3) + 8 * (i >> 2) + 4 * hi;
+      const bool live = tlive && w < 50;
+      float xv = xr[i];
+      bool pm = false;
+      float uh = 0.f;
+      if (pv) {  // x = ReLU((U - pmu) pa + pb) as the previous block's output pass formed it
+        const float t = (xv - pmu) * pa + pb;
+        uh = (xv - pmu) * pis;
+        pm = t > 0.f;
+        xv = pm ? t : 0.f;
+      }
+      const float bn = (xv - mu) * ga + be;
+      float d = live ? dxa[i] : 0.f;
+      if (P.relu && bn <= 0.f) d = 0.f;  // ReLU'(BN1(x)) of the residual block
+      dv[i] = d;
+      s += d;
+      sn = fmaf(d, (xv - mu) * is, sn);
+      if (pm) {
+        s1 += d;
+        s2 = fmaf(d, uh, s2);
+      }
+    }
+    ds += s;
+    dn += sn;
+    d1 += s1;
+    d2 += s2;
+    if (P.write_dx && !(STGCN_SP50_EXP & 2)) {  // (dx stores: masked positions go past the clip's resource)
+      const spb_i4 rdx = spb_rsrc(P.dx + (int64_t)n * P.C * TV, (int64_t)P.C * TV * 4);
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const float2 v2 = {dv[4 * gq + 2 * h2], dv[4 * gq + 2 * h2 + 1]};
+          asm volatile("buffer_store_dwordx2 %0, %1, %2, 0 offen"
+                       :
+                       : "v"(v2), "v"(xoff(ft, gq, h2)), "s"(rdx)
+                       : "memory");
+        }
+      issued += 8;
+    }
+    if (k + 1 < myitems) {
+      load_x(item + NG);
+      issued += (STGCN_SP50_EXP & 1) ? 0 : 16;
+      mark_x = issued;
+    }
+  }
+  // ---- BN1 sums: lanes lo and lo + 32 hold the same channel; 8 waves -> LDS -> global
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  double sv[4] = {ds, dn, d1, d2};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sv[i] += __shfl_xor(sv[i], 32, 64);
+  double *red = reinterpret_cast<double *>(lds + G::L1_RING);
+  if (hi == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[(wave * 32 + lo) * 4 + i] = sv[i];
+  __syncthreads();
+  if (myitems > 0 && tid < 32 * (pv ? 4 : 2)) {
+    const int ci = tid & 31, i = tid >> 5;
+    double t = 0.0;
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) t += red[(w8 * 32 + ci) * 4 + i];
+    double *dst = i == 0 ? P.sd : i == 1 ? P.sdn : i == 2 ? P.prev.s1 : P.prev.s2;
+    atomicAdd(dst + cb * 32 + ci, t);
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(512, 1) void k_sp50_dA(Sp50Params P) {
+  using G = Sp50Geo<K>;
+  constexpr int D = G::D, NQ = G::NQ2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int f = wave & 3, vt = wave >> 2;  // this wave's frame and joint tile of H
+  const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(lds);
+  const int first = xcd_remap(blockIdx.x, gridDim.x);
+  const int myitems =
+      first < P.nitems ? (P.nitems - 1 - first) / (int)gridDim.x + 1 : 0;
+  Sp50Ring<K> ring(P, lds0, 0, G::L2_W, first, wave, lane, myitems);
+  const int NCH = ring.NCH, NG = ring.NG, TV = ring.TV;
+  const int nchunks = myitems * NCH;
+  const bool pv = P.prev.mean != nullptr;
+  // row pass thread: channel ci of the block, positions part + 16 q
+  const int ci = tid >> 4, part = tid & 15;
+  const int cb = first % P.ncb, c = cb * 32 + ci;
+  const float mu = P.mean[c], ga = P.invstd[c] * P.g[c], be = P.b[c];
+  const float pmu = pv ? P.prev.mean[c] : 0.f;
+  const float pa = pv ? P.prev.invstd[c] * P.prev.g[c] : 1.f, pb = pv ? P.prev.b[c] : 0.f;
+  // zero row of the f(BN1(x)) image (joints past V read it)
+  for (int e = tid; e < G::XBP / 4; e += 512)
+    reinterpret_cast<unsigned *>(lds + G::L2_XB + G::NPOS * G::XBP)[e] = 0u;
+  float xr[NQ];
+  auto load_x = [&](int item) {
+    if (STGCN_SP50_EXP & 1) return;
+    int n, ft, cbb;
+    ring.decode(item, n, ft, cbb);
+    const spb_i4 rx = spb_rsrc(P.x + (int64_t)n * P.C * TV, (int64_t)P.C * TV * 4);
+    const int64_t base = (int64_t)c * TV + (int64_t)ft * G::NPOS;
+    const int live = min(G::NPOS, TV - ft * G::NPOS);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int pos = part + 16 * q;
+      const unsigned off = pos < live ? (unsigned)((base + pos) * 4) : kOOB;
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                   : "=v"(xr[q])
+                   : "v"(off), "s"(rx)
+                   : "memory");
+    }
+  };
+  int issued = 0;
+  int mk[D - 1];
+  int mark_x = 0;
+  if (myitems > 0) {
+    load_x(first);
+    issued += (STGCN_SP50_EXP & 1) ? 0 : NQ;
+    mark_x = issued;
+  }
+#pragma unroll
+  for (int i = 0; i < D - 1; ++i) {
+    if (i < nchunks) {
+      ring.issue_next();
+      issued += 3;
+    }
+    mk[i] = issued;
+  }
+  floatx16 dacc[K][2];
+#pragma unroll
+  for (int kk = 0; kk < K; ++kk)
+#pragma unroll
+    for (int wt = 0; wt < 2; ++wt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dacc[kk][wt][i] = 0.f;
+  // channel slot of ci in the image rows: 16 ks + 8 hi + j for
+  // ci = 16 ks + (j & 3) + 8 (j >> 2) + 4 hi (the S accumulator's row order)
+  const int rr = ci & 15;
+  const int cslot = 16 * (ci >> 4) + 8 * ((rr >> 2) & 1) + (rr & 3) + 4 * (rr >> 3);
+  __bf16 *xbi = reinterpret_cast<__bf16 *>(lds + G::L2_XB) + cslot;
+  int gch = 0, rslot = 0;
+  for (int k = 0; k < myitems; ++k) {
+    const int item = first + k * NG;
+    int n, ft, cbb;
+    ring.decode(item, n, ft, cbb);
+    floatx16 S[K];
+#pragma unroll
+    for (int kk = 0; kk < K; ++kk)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) S[kk][i] = 0.f;
+    // ---- S_k = H_k = W_k^T dZ over the chunks (joint tile vt)
+    for (int cc = 0; cc < NCH; ++cc, ++gch) {
+      sp50_wait_vm(issued - mk[0]);
+      spb_barrier();
+#pragma unroll
+      for (int i = 0; i < D - 2; ++i) mk[i] = mk[i + 1];
+      if (gch + D - 1 < nchunks) {
+        ring.issue_next();
+        issued += 3;
+      }
+      mk[D - 2] = issued;
+      const int slot = rslot;
+      rslot = rslot + 1 == D ? 0 : rslot + 1;
+      const char *wb = lds + G::L2_W + slot * G::W_BYTES + hi * 512 + lo * 16;
+      const uint4 bz = ring.dz_frag(lds, slot, f, vt, hi, lo);
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
+        if (STGCN_SP50_EXP & 8) { S[kk][0] += __builtin_bit_cast(float, w.x ^ bz.y); continue; }
+        S[kk] = spb_mfma(w, bz, S[kk]);  // [ci][v] = sum_r W_k[r][ci] dZ[r][v]
+      }
+    }
+    // ---- f(BN1(x)) of the item into the image (row (frame, w) = position)
+    sp50_wait_vm(issued - mark_x);
+    asm volatile("" : "+v"(xr[0]), "+v"(xr[1]), "+v"(xr[2]), "+v"(xr[3]), "+v"(xr[4]),
+                 "+v"(xr[5]), "+v"(xr[6]), "+v"(xr[7]), "+v"(xr[8]), "+v"(xr[9]), "+v"(xr[10]),
+                 "+v"(xr[11]), "+v"(xr[12]));
+    static_assert(NQ == 13, "the register pin above names 13 values");
+    {
+      const int live = min(G::NPOS, TV - ft * G::NPOS);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int pos = part + 16 * q;
+        if (pos < G::NPOS) {
+          float xv = xr[q];
+          if (pv) {
+            const float t = (xv - pmu) * pa + pb;
+            xv = t > 0.f ? t : 0.f;
+          }
+          const float bn = (xv - mu) * ga + be;
+          const float fx = pos < live ? (P.relu ? fmaxf(bn, 0.f) : bn) : 0.f;
+          xbi[pos * (G::XBP / 2)] = (__bf16)fx;
+        }
+      }
+    }
+    spb_barrier();  // f(BN1(x)) image complete
+    if (k + 1 < myitems) {
+      load_x(item + NG);
+      issued += (STGCN_SP50_EXP & 1) ? 0 : NQ;
+      mark_x = issued;
+    }
+    // ---- dA_k[v][w] += sum_ci H_k[ci][v] f(BN1(x))[ci][w], v in tile vt
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 xv[2];
+#pragma unroll
+      for (int wt = 0; wt < 2; ++wt) {
+        const int w = 32 * wt + lo;
+        const int row = w < 50 ? f * 50 + w : G::NPOS;
+        xv[wt] = *reinterpret_cast<const uint4 *>(lds + G::L2_XB + row * G::XBP + hi * 16 + ks * 32);
+      }
+#pragma unroll
+      for (int kk = 0; kk < K; ++kk) {
+        float sv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sv[j] = S[kk][8 * ks + j];
+        uint4 sp[2];
+        spb_planes<2>(sv, sp);
+#pragma unroll
+        for (int wt = 0; wt < 2; ++wt) {
+          if (STGCN_SP50_EXP & 4) { dacc[kk][wt][ks] += __builtin_bit_cast(float, sp[0].x ^ sp[1].y ^ xv[wt].z); continue; }
+          dacc[kk][wt] = spb_mfma(sp[0], xv[wt], dacc[kk][wt]);
+          dacc[kk][wt] = spb_mfma(sp[1], xv[wt], dacc[kk][wt]);
+        }
+      }
+    }
+  }
+  // ---- flush: dA tiles -> LDS (the ring) -> one global atomic per element
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float *dred = reinterpret_cast<float *>(lds);
+  for (int e = tid; e < K * 50 * 50; e += 512) dred[e] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int kk = 0; kk < K; ++kk)
+#pragma unroll
+    for (int wt = 0; wt < 2; ++wt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int v = 32 * vt + (i & 3) + 8 * (i >> 2) + 4 * hi, w = 32 * wt + lo;
+        if (v < 50 && w < 50) atomicAdd(dred + (kk * 50 + v) * 50 + w, dacc[kk][wt][i]);
+      }
+  __syncthreads();
+  if (myitems > 0)
+    for (int e = tid; e < K * 50 * 50; e += 512) atomicAdd(P.dA + e, dred[e]);
+}
+
+// A (K, 50, 50) -> the k_sp50_dx A-operand image [k][wt][vt][ks][plane h, m][lane][8]:
+// lane (lo, hi), j -> A_k[v = 32 vt + 16 ks + (j & 3) + 8 (j >> 2) + 4 hi][w = 32 wt + lo]
+__global__ void k_pack_sp50_a(const float *A, __bf16 *img, int K) {
+  const int total = K * 2 * 2 * 2 * 2 * 512;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    int r = e;
+    const int j = r % 8;
+    r /= 8;
+    const int lane = r % 64;
+    r /= 64;
+    const int plane = r % 2;
+    r /= 2;
+    const int ks = r % 2;
+    r /= 2;
+    const int vt = r % 2;
+    r /= 2;
+    const int wt = r % 2;
+    const int k = r / 2;
+    const int lo = lane & 31, hi = lane >> 5;
+    const int v = 32 * vt + 16 * ks + (j & 3) + 8 * (j >> 2) + 4 * hi, w = 32 * wt + lo;
+    const float a = (v < 50 && w < 50) ? A[((int64_t)k * 50 + v) * 50 + w] : 0.f;
+    const __bf16 h = (__bf16)a;
+    img[e] = plane == 0 ? h : (__bf16)(a - (float)h);
+  }
+}
+
 // instantiated shapes: the NTU graph with spatial partitioning on the bf16 path
 // (BASELINE cfg3) and the Kinetics graph, uniform partition, on the fp32 split
 // path (cfg2)
@@ -652,12 +1240,18 @@ __global__ void k_pack_spb_a(const float *A, __bf16 *img, int K, int V, int NP) 
 bool sp_bwd_fused_supported(int C, int V, int K, int R, int T, bool x3) {
   constexpr int D = SpBwdGeo<25, 3, false>::D, CMAX = SpBwdGeo<25, 3, false>::CMAX;
   constexpr bool x3_on = STGCN_AB_SPB_X3 != 0;
-  const bool shape = x3 ? (x3_on && V == 18 && K == 1) : (V == 25 && K == 3);
+  // V = 50: the k_sp50_dx / _dA pair re-reads dZ once per 32-channel block, so it
+  // is selected up to C_in = 128 (cfg5 layer timings, kbench_spb.py: L1 1241 vs
+  // 1516 us for the unfused H GEMM + k_spatial_bwd6, L4 1471 vs 1507, L5 1438 vs
+  // 1596, but L8 (C_in = 256) 2156 vs 1819)
+  const bool shape = x3 ? (x3_on && V == 18 && K == 1)
+                        : (K == 3 && (V == 25 || (V == 50 && C <= 128)));
   return shape && C > 0 && C % 32 == 0 && C <= CMAX && R % 16 == 0 && R / 16 >= D &&
          (int64_t)std::max(R, C) * T * V * 4 < ((int64_t)1 << 31);
 }
 
-static constexpr size_t kSpbAimgBytes = 3 * 2 * 3 * 1024;
+// A-operand image bytes: V = 25 [k][ks][plane] (3 planes max), V = 50 [k][wt][vt][ks][plane]
+static constexpr size_t kSpbAimgBytes = std::max<size_t>(3 * 2 * 3 * 1024, Sp50Geo<3>::AIMG);
 
 size_t sp_bwd_fused_wpk_bytes(int C, int R, int K, int V) {
   (void)V;
@@ -682,7 +1276,7 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
                                const float *A, const float *W, void *wpk, float *dx, float *dA,
                                double *sd, double *sdn, int N, int C, int R, int T, int V, int K,
                                int write_dx, int relu, bool x3, hipStream_t s,
-                               const PrevBn *prev, int dz_bf16) {
+                               const PrevBn *prev, int dz_bf16, int only) {
   if (!sp_bwd_fused_supported(C, V, K, R, T, x3)) return hipErrorInvalidValue;
   const int npw = x3 ? 3 : 1, npa = x3 ? 3 : 2;
   __bf16 *aimg = reinterpret_cast<__bf16 *>(wpk);
@@ -712,6 +1306,41 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
   P.write_dx = write_dx;
   P.relu = relu;
   if (prev) P.prev = *prev;
+  if (V == 50) {  // the two-person graph: k_sp50_dx + k_sp50_dA (fp32 dZ only)
+    if (dz_bf16 || x3) return hipErrorInvalidValue;
+    using G = Sp50Geo<3>;
+    hipLaunchKernelGGL(k_pack_sp50_a, dim3(48), dim3(256), 0, s, A, aimg, K);
+    Sp50Params Q{};
+    Q.dZ = dZ;
+    Q.x = x;
+    Q.mean = mean;
+    Q.invstd = invstd;
+    Q.g = g;
+    Q.b = b;
+    Q.wpk = wp;
+    Q.aimg = aimg;
+    Q.dx = dx;
+    Q.dA = dA;
+    Q.sd = sd;
+    Q.sdn = sdn;
+    Q.C = C;
+    Q.R = R;
+    Q.T = T;
+    Q.ncb = C / 32;
+    Q.nft = (T + G::FT - 1) / G::FT;
+    const int64_t items = (int64_t)Q.ncb * Q.nft * N;
+    if (items >= (int64_t)1 << 31) return hipErrorInvalidValue;
+    Q.nitems = (int)items;
+    Q.write_dx = write_dx && dx != nullptr;
+    Q.relu = relu;
+    if (prev) Q.prev = *prev;
+    // (a grid of 256 is a multiple of the channel-block count C / 32 <= 8: every
+    // item of a workgroup is in one block)
+    const int grid = (int)std::min<int64_t>(items, 256);
+    if (only != 2) hipLaunchKernelGGL((k_sp50_dx<3>), dim3(grid), dim3(512), G::LDS1, s, Q);
+    if (only != 1) hipLaunchKernelGGL((k_sp50_dA<3>), dim3(grid), dim3(512), G::LDS2, s, Q);
+    return hipGetLastError();
+  }
   if (x3) return dz_bf16 ? hipErrorInvalidValue : launch_spb<18, 1, true>(P, s);
   if (dz_bf16) return launch_spb<25, 3, false, true>(P, s);
   return launch_spb<25, 3, false>(P, s);
