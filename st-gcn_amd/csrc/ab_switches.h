@@ -49,6 +49,9 @@
 #ifndef STGCN_AB_JOINT3         // k_spatial_bwd3 / gather3 instead of the MFMA joint kernels
 #define STGCN_AB_JOINT3 0
 #endif
+#ifndef STGCN_AB_WG_REGSTAGE    // register staging in k_wgrad_bf16 for bf16 P / Q at even V
+#define STGCN_AB_WG_REGSTAGE 0
+#endif
 #ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
 #define STGCN_AB_BWD6_EXACT 0
 #endif

@@ -29,6 +29,25 @@ namespace stgcn {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+// One 4-byte LDS-DMA piece per lane: LDS[lds_wave + 4 lane] = src[voff] (kOOB
+// -> 0). Inline asm, so hipcc neither counts it nor waits for it before LDS
+// reads of other buffers (the caller waits with an explicit s_waitcnt vmcnt).
+__device__ __forceinline__ void dma_b32(int4v rs, unsigned voff, unsigned lds_wave) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+      "buffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(__builtin_amdgcn_readfirstlane(lds_wave)), "v"(voff), "s"(rs)
+      : "memory");
+}
+// (wave-uniform values the compiler cannot prove uniform, for "s" operands)
+__device__ __forceinline__ int4v uniform4(int4v v) {
+  return int4v{__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+               __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w)};
+}
 
 __device__ __forceinline__ floatx16 mfma_bf16(bf16x8 a, bf16x8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -569,7 +588,73 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
     }
   };
 
-  if (it0 < it1) {
+  // LDS-DMA staging (bf16 P and Q, even V: a frame's joints are whole dwords, so
+  // 4-byte LDS-DMA pieces land in the padded frame image without realignment).
+  // Dword d of a buffer's P image (Q image) is (row, frame f, joint pair j) of
+  // the same layout the register staging writes; its source element offset
+  // within the clip minus the item's frame base is fixed per lane and wave
+  // round, kept in a register as (f << 26 | offset) (~0: pitch pad, pad joint
+  // or row past the tensor -> OOB -> 0). An item's whole staging is in flight
+  // under the previous item's k-steps; one vmcnt(0) + barrier per item.
+  constexpr bool DMA = BI && NQ == 9 && V % 2 == 0 && !STGCN_AB_WG_REGSTAGE;
+  constexpr int PW = G::PPITCH / 2, QW = G::QPITCH / 2, VW = G::Vp / 2;  // dwords
+  constexpr int PRN = 64 * PW / 64, QRN = CB * QW / 64;  // wave rounds of 64 dwords
+  constexpr int PR = (PRN + G::NW - 1) / G::NW, QR = (QRN + G::NW - 1) / G::NW;
+  static_assert(!DMA || (G::PBYTES == 64 * PW * 4 && (CB * QW) % 64 == 0), "whole wave rounds");
+  // (offsets must fit 26 bits; block-uniform, else the register staging runs)
+  const bool dma_ok = DMA && (int64_t)p.R * MV < (1 << 26) && (int64_t)p.C * TV < (1 << 26);
+  unsigned ptab[DMA ? PR : 1], qtab[DMA ? QR : 1];
+  if constexpr (DMA) {
+#pragma unroll
+    for (int i = 0; i < PR; ++i) {
+      const int d = (i * G::NW + wave) * 64 + lane;
+      const int row = d / PW, w = d - row * PW, f = w / VW, j = w - f * VW;
+      const bool ok = i * G::NW + wave < PRN && f < FT && 2 * j < V && r0 + row < p.R;
+      ptab[i] = ok ? ((unsigned)f << 26) | (unsigned)((r0 + row) * MV + f * V + 2 * j) : ~0u;
+    }
+#pragma unroll
+    for (int i = 0; i < QR; ++i) {
+      const int d = (i * G::NW + wave) * 64 + lane;
+      const int c = d / QW, w = d - c * QW, f = w / VW, j = w - f * VW;
+      const bool ok = i * G::NW + wave < QRN && f < G::QF && 2 * j < V && c0 + c < p.C;
+      qtab[i] = ok ? ((unsigned)f << 26) | (unsigned)((c0 + c) * TV + f * V + 2 * j) : ~0u;
+    }
+  }
+  const unsigned lds_addr = (unsigned)reinterpret_cast<uintptr_t>(lds);
+  auto dma_stage = [&](int item, int bufi) __attribute__((always_inline)) {
+    const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * FT;
+    const uint64_t sp = reinterpret_cast<uint64_t>(reinterpret_cast<const __bf16 *>(p.P) +
+                                                   (int64_t)n * p.p_bstride);
+    const uint64_t sq = reinterpret_cast<uint64_t>(reinterpret_cast<const __bf16 *>(p.Q) +
+                                                   (int64_t)n * p.q_bstride);
+    const int4v rp = uniform4(int4v{(int)(uint32_t)sp, (int)((sp >> 32) & 0xffff),
+                               (int)std::min<int64_t>(p.p_bstride * 2, 0x7fffffff), 0x00020000});
+    const int4v rq = uniform4(int4v{(int)(uint32_t)sq, (int)((sq >> 32) & 0xffff),
+                               (int)std::min<int64_t>(p.q_bstride * 2, 0x7fffffff), 0x00020000});
+    const int t0 = SIN * m0 + p.off;
+    const unsigned lb =
+        (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_addr + (unsigned)(bufi * G::BUF)));
+    asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
+#pragma unroll
+    for (int i = 0; i < PR; ++i)
+      if (i * G::NW + wave < PRN) {
+        const unsigned e = ptab[i];
+        const bool ok = e != ~0u && m0 + (int)(e >> 26) < p.M;
+        const unsigned voff = ok ? ((e & 0x3ffffffu) + (unsigned)(m0 * V)) * 2u : kOOB;
+        dma_b32(rp, voff, lb + (unsigned)((i * G::NW + wave) * 256));
+      }
+#pragma unroll
+    for (int i = 0; i < QR; ++i)
+      if (i * G::NW + wave < QRN) {
+        const unsigned e = qtab[i];
+        const int t = t0 + (int)(e >> 26);
+        const bool ok = e != ~0u && t >= 0 && t < p.T_src;
+        const unsigned voff = ok ? (unsigned)((int)(e & 0x3ffffffu) + t0 * V) * 2u : kOOB;
+        dma_b32(rq, voff, lb + (unsigned)(G::PBYTES + (i * G::NW + wave) * 256));
+      }
+  };
+
+  if (!dma_ok && it0 < it1) {
     const ItemRef ir = item_ref(it0);
     load_part(ir, std::integral_constant<int, 0>{});
     write_part(lds, std::integral_constant<int, 0>{});
@@ -592,6 +677,17 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    if (dma_ok) {
+      if (it0 < it1) dma_stage(it0, 0);
+      for (int it = 0, itm = it0; itm < it1; ++it, ++itm) {
+        // item it landed (every wave's pieces), and every wave is done reading
+        // item it-1's buffer, which item it+1's pieces overwrite
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (itm + 1 < it1) dma_stage(itm + 1, (it + 1) & 1);
+        compute(acc, lds + (it & 1) * G::BUF, nt_c, std::integral_constant<int, 0>{},
+                std::integral_constant<int, G::KSTEPS>{});
+      }
+    } else
     for (int it = 0, itm = it0; itm < it1; ++it, ++itm) {
       __syncthreads();
       const char *cur = lds + (it & 1) * G::BUF;
