@@ -221,7 +221,8 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # bf16 storage of Z and dU (capi.hip act_bf16: bf16 path, stride-1
             # non-residual blocks whose spatial forward is fused, C_in >= 16):
             # those operands move 2 bytes per element
-            ab = cfg["bf16"] and s == 1 and ci >= 16
+            # (stride-2 blocks too at even V: their weight gradient stages bf16 by LDS-DMA)
+            ab = cfg["bf16"] and (s == 1 or V % 2 == 0) and ci >= 16
             V2 = V * 2 if ab else V4
             # bf16 storage of dZ (capi.hip dz_bf16) is an A/B build only
             # (STGCN_AB_DZ_BF16): the shipped library stores dZ in fp32
@@ -270,7 +271,7 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 ft, cb = {18: (8, 64), 25: (4, 64), 50: (4, 32)}.get(V, (0, 0))
                 sym = {0: f"k_conv_x3<9,3,{V},{s},1,1,{ib}>",
                        1: (f"k_conv_x3<9,3,{V},1,1,1,{ib}>" if s == 1 else
-                           f"k_conv_x3<5|4,{V},1,1,1,false>"),
+                           f"k_conv_x3<5|4,{V},1,1,1,{ib}>"),
                        2: f"k_wgrad_bf16<9,{V},{s},{ft},{cb},{ib}>",
                        3: (f"k_conv_bf16<1,16,{V},1,false>" if ci < 16 else
                            f"k_sp_fwd_bf16<{V},{K}>" if not (V == 50 or (V == 25 and K == 3)) else

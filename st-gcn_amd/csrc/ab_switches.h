@@ -52,6 +52,9 @@
 #ifndef STGCN_AB_WG_REGSTAGE    // register staging in k_wgrad_bf16 for bf16 P / Q at even V
 #define STGCN_AB_WG_REGSTAGE 0
 #endif
+#ifndef STGCN_AB_S2_ACT_FP32     // fp32 Z / dU on stride-2 bf16 blocks at even V
+#define STGCN_AB_S2_ACT_FP32 0
+#endif
 #ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
 #define STGCN_AB_BWD6_EXACT 0
 #endif

@@ -311,15 +311,17 @@ void conv_tiles(ConvGemmParams &p) {
 // and the BN2 + ReLU backward pass. (STGCN_AB_ACT_FP32 build: fp32 storage, A/B only)
 bool act_bf16(const stgcn_desc_t *d) {
   constexpr bool off = STGCN_AB_ACT_FP32 != 0 || STGCN_AB_GENERIC_CONV != 0;
-  // Stride-2 blocks keep fp32: their weight gradient (k_wgrad_bf16<9,V,2>) staged
-  // bf16 pairs slower than fp32 (cfg5 2.19 -> 2.66 ms per step), more than the
-  // strided forward and data-gradient phases gained.
-  if (off || !fused_sp(d) || residual(d) || d->stride != 1) return false;
+  // Stride-2 blocks at odd V keep fp32: their weight gradient (k_wgrad_bf16<9,V,2>)
+  // staged bf16 pairs by registers slower than fp32 (cfg5 2.19 -> 2.66 ms per
+  // step), more than the strided forward and data-gradient phases gained; at even
+  // V it stages them by LDS-DMA (STGCN_AB_S2_ACT_FP32 build: fp32 there, A/B only).
+  const bool s2 = d->stride == 2 && d->V % 2 == 0 && STGCN_AB_S2_ACT_FP32 == 0;
+  if (off || !fused_sp(d) || residual(d) || (d->stride != 1 && !s2)) return false;
   ConvGemmParams p = conv_base(d, nullptr);  // the temporal conv forward and data gradient
   p.C = d->C_out;
   p.R = d->C_out;
   p.NQ = 9;
-  p.s_in = 1;
+  p.s_in = d->stride;
   if (!conv_b1_supported(p)) return false;
   WgradParams w = make_wgrad_taps(d, nullptr, nullptr, nullptr);
   return w.bf16 == 1;

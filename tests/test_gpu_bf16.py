@@ -190,3 +190,12 @@ def test_bf16_cfg5_full_size_block(pkg):
     a realistic grid size."""
     errs = _check_bf16(pkg, (64, 64, 1, 50, 3, 8, 300), seed=11)
     print({k: float(np.format_float_scientific(v, 2)) for k, v in errs.items()})
+
+
+def test_bf16_cfg5_stride2_full_size_block(pkg):
+    """cfg5 L4 shape (V = 50, K = 3, 64 -> 128 channels, stride 2) at T = 300,
+    N = 4: bf16 Z / dU storage on a stride-2 block, read by the strided
+    forward, the two data-gradient phases and the LDS-DMA weight gradient
+    (k_wgrad_bf16<9,50,2,4,32,true>)."""
+    errs = _check_bf16(pkg, (64, 128, 2, 50, 3, 4, 300), seed=13)
+    print({k: float(np.format_float_scientific(v, 2)) for k, v in errs.items()})
