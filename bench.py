@@ -231,8 +231,13 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # the two-person graph's fused spatial backward: two kernels, each
             # reading dZ and x (k_sp50_dx also writes dx), timed as which 5 / 6
             f50 = cfg["bf16"] and V == 50 and K == 3 and ci % 32 == 0 and ci <= 128
-            act = {0: N * (co * t * V2 + co * to * V4), 1: N * (co * to * V2 + co * t * VZ),
-                   2: N * (co * to + co * t) * V2,
+            # the folded block (capi.hip fold_w: fp32 split path, K = 1, V = 18,
+            # C_in >= 16): no spatial / H GEMM, the temporal GEMMs read G (C_in
+            # channels) in place of Z, and the data gradient writes H (C_in)
+            fold = x3 and K == 1 and V == 18 and ci >= 16
+            CZ = ci if fold else co
+            act = {0: N * (CZ * t * V2 + co * to * V4), 1: N * (co * to * V2 + CZ * t * VZ),
+                   2: N * (co * to * V2 + CZ * t * V2),
                    3: N * (ci * t * V4 + co * t * V2) + (N * K * ci * t * V * 2
                                                        if cfg["bf16"] and ci >= 16 else
                                                        N * K * ci * t * V4),
@@ -246,8 +251,9 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # rocprof short names of the kernel each timing runs
             if which == 4:
                 # the fused spatial backward (bf16, V = 25, K = 3); the unfused
-                # pair is timed per kernel by which 5 / 6
-                if lib.stgcn_time_kernel_bytes(ctypes.byref(d), 5) == 0:
+                # pair is timed per kernel by which 5 / 6 (folded: its joint
+                # kernel alone, which 6)
+                if not fold and lib.stgcn_time_kernel_bytes(ctypes.byref(d), 5) == 0:
                     add(symbols, f"k_sp_bwd_fused<{V},{K},{'true' if x3 else 'false'},"
                                  f"{'true' if dzb else 'false'}>",
                         ms.value, fl.value, 1, act)

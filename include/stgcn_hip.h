@@ -71,8 +71,12 @@ extern "C" {
                             * MFMA rate. Applies for V in {18, 25} over >= 16 channels to
                             * the temporal conv forward (stride 1 and 2), data-grad and
                             * weight-grad, and to the spatial weight-grad dW'; other GEMMs
-                            * run the fp32 kernels. Every tensor stays fp32. Exclusive with
-                            * STGCN_F_BF16. */
+                            * run the fp32 kernels. Every tensor stays fp32. On non-residual
+                            * blocks with K = 1, V = 18 and C_in >= 16 the SpatialConv
+                            * channel GEMM is folded into the temporal conv's weights
+                            * (Wc_q = Wt_q W'): Z is never formed, and its buffer is
+                            * OPAQUE (it carries Wc from stgcn_block_fwd to
+                            * stgcn_block_bwd). Exclusive with STGCN_F_BF16. */
 
 enum {
   STGCN_OK = 0,

@@ -55,6 +55,9 @@
 #ifndef STGCN_AB_S2_ACT_FP32     // fp32 Z / dU on stride-2 bf16 blocks at even V
 #define STGCN_AB_S2_ACT_FP32 0
 #endif
+#ifndef STGCN_AB_NO_FOLD        // the unfolded spatial GEMMs on the fp32 split path (capi.hip fold_w)
+#define STGCN_AB_NO_FOLD 0
+#endif
 #ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
 #define STGCN_AB_BWD6_EXACT 0
 #endif

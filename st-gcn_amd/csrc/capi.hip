@@ -104,6 +104,23 @@ bool fused_spb(const stgcn_desc_t *d) {
 // the fused backward of the two-person graph: two kernels (k_sp50_dx, k_sp50_dA),
 // timed apart as which 5 / 6
 bool fused_spb50(const stgcn_desc_t *d) { return fused_spb(d) && d->V == 50; }
+// The folded block (kernels_fold.hip): with one adjacency partition the
+// SpatialConv channel GEMM W' folds into the temporal conv's weights
+// (Wc_q = Wt_q W'), so the temporal conv reads G = BN1(x) A^T (C_in channels)
+// and Z / dZ are never formed; the backward's data gradient yields H directly.
+// fp32 split path (cfg2: V = 18, K = 1), non-residual blocks over >= 16 input
+// channels whose spatial backward is the unfused pair (STGCN_AB_NO_FOLD build:
+// the unfolded kernels, A/B only).
+bool fold_w(const stgcn_desc_t *d) {
+  constexpr bool off = STGCN_AB_NO_FOLD != 0;
+  return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->V == 18 &&
+         !fused_spb(d);
+}
+// The folded forward leaves Wc in the (otherwise unused) Z buffer for the
+// backward when it fits (Z is opaque to the caller under STGCN_F_F32X3 then)
+bool fold_wc_in_z(const stgcn_desc_t *d) {
+  return fold_w(d) && (int64_t)d->N * d->C_out * d->T * d->V >= (int64_t)d->C_out * d->C_in * 9;
+}
 // Clips per slice of the unfused spatial backward (H GEMM + joint kernel). The
 // shipped build runs the whole batch as one slice. STGCN_AB_SLICE build (A/B
 // only): the slice's H, dZ, x and dx (fp32) within ~160 MiB, so the Infinity
@@ -175,17 +192,19 @@ WgradParams make_wgrad(const stgcn_desc_t *d, const float *P, int64_t pb, int R,
 }
 
 // Temporal-conv weight gradient plan (k_wgrad_taps): dWt = sum dU (x) Z(shifted).
+// (Cq: channels of the Q operand, C_out; C_in for the folded block's dWc = sum dU G^T)
 WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float *Z,
-                            float *slab) {
+                            float *slab, int Cq = 0) {
   const int R = d->C_out;
+  if (Cq <= 0) Cq = R;
   WgradParams w{};
   w.P = dU;
   w.Q = Z;
   w.slab = slab;
   w.p_bstride = (int64_t)R * d->T_out * d->V;
-  w.q_bstride = (int64_t)R * d->T * d->V;
+  w.q_bstride = (int64_t)Cq * d->T * d->V;
   w.R = R;
-  w.C = R;
+  w.C = Cq;
   w.NQ = 9;
   w.s_in = d->stride;
   w.off = -d->pad;
@@ -197,7 +216,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
   while (w.FT > 1 && !wgrad_taps_supported(w)) --w.FT;
   w.n_mtiles = (w.M + w.FT - 1) / w.FT;
   w.n_rtiles = (R + 63) / 64;
-  w.n_jtiles = (R + wgrad_taps_cb(w) - 1) / wgrad_taps_cb(w);
+  w.n_jtiles = (Cq + wgrad_taps_cb(w) - 1) / wgrad_taps_cb(w);
   const int tiles = w.n_rtiles * w.n_jtiles;
   w.S = std::max(1, std::min((256 + tiles - 1) / tiles, d->N * w.n_mtiles));
   if (bf16(d)) plan_wgrad_bf16(w);
@@ -213,6 +232,9 @@ struct BwdLayout {
   float *dU, *dZ, *G, *H, *slab, *wpk;
   float *Wpk;  // W' = [W_0 | ... | W_{K-1}] (C_out, K*C_in) for the stacked H GEMM
   float *Rg;  // residual projection data-grad (N, C_in, T, V)
+  // the folded block: dU summed over clips, per-tap sums Tq, dWc, partials, Wc, bZ
+  double *fcs, *ftq, *dWc, *fpart;
+  float *Wc, *bZ;
   size_t dbl_bytes, total;
 };
 
@@ -229,6 +251,14 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.s1 = c.take<double>(C);
   L.s2 = c.take<double>(C);
   L.dbl_bytes = c.off;
+  if (fold_w(d)) {
+    L.fcs = c.take<double>((size_t)R * nTo(d));
+    L.ftq = c.take<double>((size_t)9 * R * d->V);
+    L.dWc = c.take<double>((size_t)R * C * 9);
+    L.fpart = c.take<double>((size_t)9 * R * std::max(C, d->V));
+    L.Wc = c.take<float>((size_t)R * C * 9);
+    L.bZ = c.take<float>((size_t)R * d->V);
+  }
   L.dU = c.take<float>((size_t)d->N * R * nTo(d));
   L.dZ = c.take<float>((size_t)d->N * R * nT(d));
   L.G = c.take<float>((size_t)d->N * K * C * nT(d));
@@ -237,6 +267,10 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   WgradParams w2 =
       make_wgrad(d, nullptr, 0, R, d->T, nullptr, 0, K * C, d->T, 1, 1, 0, nullptr);
   size_t slab = std::max((size_t)w1.S * R * R * 9, (size_t)w2.S * R * K * C);
+  if (fold_w(d)) {
+    WgradParams wf = make_wgrad_taps(d, nullptr, nullptr, nullptr, C);
+    slab = std::max(slab, (size_t)wf.S * R * C * 9);
+  }
   if (fused_sp(d)) {  // dW' from the kept bf16 G (k_wgrad_gemm_gk)
     WgradParams wg{};
     wg.R = R;
@@ -263,6 +297,8 @@ struct FwdLayout {
   double *s1, *q1, *s2, *q2;
   float *G, *Wpk, *biasZ, *wpk;
   float *Rp;  // residual projection output (N, C_out, T_out, V)
+  float *Wc, *BT;  // the folded block: composite weights, per-frame bias table
+  double *bq;      // ... and its per-tap bias products
   size_t dbl_bytes, total;
 };
 
@@ -280,6 +316,11 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
   L.biasZ = c.take<float>((size_t)R * d->V);
   L.wpk = c.take<float>(wpk_floats(d));
   if (projection(d)) L.Rp = c.take<float>((size_t)d->N * R * nTo(d));
+  if (fold_w(d)) {
+    L.Wc = c.take<float>((size_t)R * C * 9);
+    L.BT = c.take<float>((size_t)R * nTo(d));
+    L.bq = c.take<double>((size_t)9 * R * d->V);
+  }
   L.total = c.off;
   return L;
 }
@@ -543,6 +584,9 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
                              a->rm1, a->rv1, mean1, invstd1, s));
   // Spatial graph conv (st_graphconv.py:139-152) in the form (1).
   HIP_TRY(launch_bias_rv(a->A, a->bW, L.biasZ, K, R, V, s));
+  // (the folded block: G only; W' rides on the temporal conv's weights)
+  const bool fold = fold_w(d);
+  const float *Gfold = nullptr;
   const float *Wz = a->W;
   if (K > 1) {
     HIP_TRY(launch_pack_w(a->W, L.Wpk, K, R, C, s));
@@ -559,7 +603,8 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   } else {
   float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
   HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s));
-  {
+  Gfold = G;
+  if (!fold) {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = G;
     p.w = Wz;
@@ -609,6 +654,19 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.w_sq = 1;
     p.C = R;
     p.R = R;
+    if (fold) {  // U = sum_q Wc_q G[s t + q - 4] + BT[o, t, v]  (kernels_fold.hip)
+      float *Wc = fold_wc_in_z(d) ? a->Z : L.Wc;  // (kept for the backward)
+      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, s));
+      HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT, s));
+      p.in = Gfold;
+      p.w = Wc;
+      p.bias_r = nullptr;
+      p.res = L.BT;
+      p.res_shared = 1;
+      p.in_bstride = (int64_t)C * T * V;
+      p.w_sr = (int64_t)C * 9;
+      p.C = C;
+    }
     p.NQ = 9;
     p.s_in = d->stride;
     p.off = -d->pad;
@@ -689,6 +747,67 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 
   // dZ in bf16 where every reader takes it (needs the kept G: k_wgrad_gemm_gk)
   const bool dzb = dz_bf16(d) && a->G != nullptr;
+  if (fold_w(d)) {
+    // The folded block (kernels_fold.hip): Wc_q = Wt_q W'; the data gradient
+    // with Wc gives H = W'^T dZ directly (C_in channels), the weight gradient
+    // over G gives dWc, and dWt, dW', sum_{n,t} dZ follow from dWc and the dU sums.
+    const float *Wc = a->Z;  // (left there by the forward)
+    if (!fold_wc_in_z(d)) {
+      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, s));
+      Wc = L.Wc;
+    }
+    HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));
+    {
+      ConvGemmParams p = conv_base(d, L.wpk);
+      p.in = L.dU;
+      p.out = L.H;
+      p.in_bstride = (int64_t)R * To * V;
+      p.out_bstride = (int64_t)C * T * V;
+      p.w_sr = 9;
+      p.w_sc = (int64_t)C * 9;
+      p.C = R;
+      p.R = C;
+      p.T_src = To;
+      p.T_dst = T;
+      p.s_in = 1;
+      if (d->stride == 1) {
+        p.w = Wc + 8;
+        p.w_sq = -1;
+        p.NQ = 9;
+        p.off = -4;
+        p.s_out = 1;
+        p.p_out = 0;
+        p.M = T;
+        conv_tiles(p);
+        HIP_TRY(launch_conv_gemm(p, s));
+      } else {
+        for (int ph = 0; ph < 2; ++ph) {
+          p.w = Wc + (ph == 0 ? 8 : 7);
+          p.w_sq = -2;
+          p.NQ = ph == 0 ? 5 : 4;
+          p.off = ph == 0 ? -2 : -1;
+          p.s_out = 2;
+          p.p_out = ph;
+          p.M = ph == 0 ? (T + 1) / 2 : T / 2;
+          if (p.M <= 0) continue;
+          conv_tiles(p);
+          HIP_TRY(launch_conv_gemm(p, s));
+        }
+      }
+    }
+    const float *G = a->G;  // kept fp32 G, else recomputed
+    if (!G) {
+      HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K,
+                                res, s));
+      G = L.G;
+    }
+    WgradParams w = make_wgrad_taps(d, L.dU, G, L.slab, C);
+    HIP_TRY(launch_wgrad_taps(w, s));
+    HIP_TRY(launch_fold_du_sums(L.dU, N, R, T, To, V, d->stride, L.fcs, L.ftq, s));
+    HIP_TRY(launch_fold_grads(L.slab, w.S, a->Wt, a->W, L.bZ, L.ftq, R, C, V, L.dWc, L.fpart,
+                              a->dWt,
+                              a->dW, L.SdZ, s));
+  } else {
   // Temporal conv data-gradient: dZ = conv^T(dU)
   {
     ConvGemmParams p = conv_base(d, L.wpk);
@@ -782,6 +901,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));
   }
   HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s, dzb ? 1 : 0));
+  }
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
   // Deferred dx (ABI 5): the BN1 backward apply of this block is folded into the
   // previous block's ReLU+BN2 backward apply (launch_bn_relu_bwd_apply with
@@ -823,7 +943,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   for (int n0 = 0; n0 < N; n0 += NSL) {
   const int ns = std::min(NSL, N - n0);
   const int64_t xo = (int64_t)n0 * C * T * V;
-  {
+  if (!fold_w(d)) {  // (the folded block's data gradient wrote H)
     // H = W'^T dZ for all partitions in one GEMM (rows k*C_in + ci of H are
     // the channels of H_k): dZ is read once instead of K times
     ConvGemmParams p = conv_base(d, L.wpk);
@@ -959,12 +1079,15 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
   TimedPlan P;
   Carve c(scratch);
   const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V, K = d->K;
-  const double tflops = 2.0 * 9 * R * (double)R * To * V * N;
+  // (the folded block: the temporal GEMMs run over C_in channels on the G side)
+  const bool fold = fold_w(d);
+  const int CZ = fold ? C : R;
+  const double tflops = 2.0 * 9 * R * (double)CZ * To * V * N;
   float *wpk = c.take<float>(wpk_floats(d));
   if (which == 0) {
     ConvGemmParams p = conv_base(d, wpk);
-    p.in = c.take<float>((size_t)N * R * T * V);
-    p.w = c.take<float>((size_t)R * R * 9);
+    p.in = c.take<float>((size_t)N * CZ * T * V);
+    p.w = c.take<float>((size_t)R * CZ * 9);
     p.out = c.take<float>((size_t)N * R * To * V);
     p.bias_r = c.take<float>(R);
     p.stat_sum = c.take<double>(R);
@@ -985,6 +1108,14 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     p.T_src = T;
     p.T_dst = To;
     p.in_bf16 = z_bf16(d) ? 1 : 0;
+    if (fold) {
+      p.bias_r = nullptr;
+      p.res = c.take<float>((size_t)R * To * V);
+      p.res_shared = 1;
+      p.in_bstride = (int64_t)C * T * V;
+      p.w_sr = (int64_t)C * 9;
+      p.C = C;
+    }
     conv_tiles(p);
     P.cp[P.ncp++] = p;
     P.flops = tflops;
@@ -992,15 +1123,15 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * R * To * V);
     p.in_bf16 = du_bf16(d) ? 1 : 0;
-    const float *w = c.take<float>((size_t)R * R * 9);
-    p.out = c.take<float>((size_t)N * R * T * V);
+    const float *w = c.take<float>((size_t)R * CZ * 9);
+    p.out = c.take<float>((size_t)N * CZ * T * V);
     p.out_bf16 = dz_bf16(d) ? 1 : 0;  // (the stack keeps G, so dZ is bf16 there)
     p.in_bstride = (int64_t)R * To * V;
-    p.out_bstride = (int64_t)R * T * V;
+    p.out_bstride = (int64_t)CZ * T * V;
     p.w_sr = 9;
-    p.w_sc = (int64_t)R * 9;
+    p.w_sc = (int64_t)CZ * 9;
     p.C = R;
-    p.R = R;
+    p.R = CZ;
     p.T_src = To;
     p.T_dst = T;
     p.s_in = 1;
@@ -1030,17 +1161,17 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.flops = tflops;
   } else if (which == 2) {
     const float *dU = c.take<float>((size_t)N * R * To * V);
-    const float *Z = c.take<float>((size_t)N * R * T * V);
-    WgradParams w = make_wgrad_taps(d, dU, Z, nullptr);
+    const float *Z = c.take<float>((size_t)N * CZ * T * V);
+    WgradParams w = make_wgrad_taps(d, dU, Z, nullptr, CZ);
     w.q_bf16 = z_bf16(d) ? 1 : 0;
     w.p_bf16 = du_bf16(d) ? 1 : 0;
-    w.slab = c.take<float>((size_t)w.S * R * R * 9);
+    w.slab = c.take<float>((size_t)w.S * R * CZ * 9);
     P.wp = w;
     P.wgrad = true;
     P.flops = tflops;
   } else if (which >= 4) {
     P.spb = true;
-    P.spb_gemm = which != 6;
+    P.spb_gemm = which != 6 && !fold;  // (folded: the data gradient wrote H)
     P.spb_joint = which != 5;
     P.wpk = wpk;
     P.x = c.take<float>((size_t)N * C * T * V);
@@ -1053,6 +1184,8 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     P.sd = c.take<double>((size_t)2 * C);
     if (!fused_spb(d)) {
       P.H = c.take<float>((size_t)N * K * C * T * V);
+    }
+    if (!fused_spb(d) && !fold) {
       ConvGemmParams p = conv_base(d, wpk);
       p.in = P.dZ;
       p.in_bf16 = dz_bf16(d) ? 1 : 0;
@@ -1127,6 +1260,7 @@ extern "C" {
 size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which) {
   if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 6) return 0;
   if (which >= 5 && fused_spb(d) && !fused_spb50(d)) return 0;
+  if ((which == 3 || which == 5) && fold_w(d)) return 0;  // (no spatial / H GEMM there)
   return plan_timed(d, which, nullptr).bytes;
 }
 
@@ -1138,6 +1272,8 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
     return fail(STGCN_E_INVALID, "bad timing request");
   if (which >= 5 && fused_spb(d) && !fused_spb50(d))
     return fail(STGCN_E_UNSUPPORTED, "the spatial backward is one fused kernel here (which 4)");
+  if ((which == 3 || which == 5) && fold_w(d))
+    return fail(STGCN_E_UNSUPPORTED, "the folded block has no spatial / H GEMM");
   TimedPlan P = plan_timed(d, which, scratch);
   if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
   hipStream_t s = (hipStream_t)stream;

@@ -120,7 +120,8 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
     }
   }
   const __amdgpu_buffer_rsrc_t rs_res = make_rsrc(
-      p.res ? p.res + (int64_t)n * p.out_bstride : p.out, p.res ? p.out_bstride : 0);
+      p.res ? p.res + (p.res_shared ? 0 : (int64_t)n * p.out_bstride) : p.out,
+      p.res ? p.out_bstride : 0);
   int ocol[4], cv[4];
   bool cok[4];
 #pragma unroll
@@ -268,12 +269,14 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
   const float br = (p.bias_r && rok) ? p.bias_r[row] : 0.f;
   const int64_t obase = (int64_t)n * p.out_bstride + (int64_t)row * ostride + (int64_t)m0 * V;
   float *out = p.out + obase;
-  const float *res = p.res ? p.res + obase : nullptr;
-  const int vec = ((obase & 3) == 0 && (ostride & 3) == 0 &&
+  // (res_shared: one table for every clip, so its offset has no clip term)
+  const int64_t rbase = p.res_shared ? obase - (int64_t)n * p.out_bstride : obase;
+  const float *res = p.res ? p.res + rbase : nullptr;
+  const int vec = ((obase & 3) == 0 && (rbase & 3) == 0 && (ostride & 3) == 0 &&
                    ((reinterpret_cast<uintptr_t>(p.out) & 15) == 0) &&
                    (!p.res || (reinterpret_cast<uintptr_t>(p.res) & 15) == 0))
                       ? 4
-                      : (((obase & 1) == 0 && (ostride & 1) == 0) ? 2 : 1);
+                      : (((obase & 1) == 0 && (rbase & 1) == 0 && (ostride & 1) == 0) ? 2 : 1);
   double s = 0.0, sq = 0.0;
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {

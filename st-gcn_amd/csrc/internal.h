@@ -65,6 +65,8 @@ struct ConvGemmParams {
   int Cpad;  // set by launch_conv_gemm
   // epilogue extras (residual block): out = f(acc + bias + res), f = ReLU if relu_out
   const float *res;  // same layout and clip stride as out, or null
+  int res_shared;    // 1: res has no clip axis (one [R][T_dst][V] table for every clip:
+                     // the folded block's per-frame bias table, capi.hip fold_w)
   int relu_out;
   Dropout drop;      // applied after relu_out (element index = flat index in out)
   int bf16;          // 1: operands rounded to bf16 on v_mfma_f32_32x32x16_bf16 (fp32
@@ -94,6 +96,18 @@ struct WgradParams {
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
+// The folded block (kernels_fold.hip; capi.hip fold_w): composite weights
+// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i], the per-frame bias table, the dU
+// sums (total, boundary frames, per tap Tq) and the weight gradients from dWc.
+hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s);
+hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
+                            int To, int st, double *bq, float *BT, hipStream_t s);
+hipError_t launch_fold_du_sums(const float *dU, int N, int R, int T, int To, int V, int st,
+                               double *cs, double *Tq, hipStream_t s);
+hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
+                             const float *bZ, const double *Tq, int R, int C, int V,
+                             double *dWc, double *part, float *dWt, float *dW, double *SdZ,
+                             hipStream_t s);
 // bf16 path (kernels_bf16.hip): the reference's graphs (V = 18, 25, 50) with
 // the fp32 path's tile plan (FT = kTileCols / V); launch_conv_gemm dispatches here
 // when p.bf16 and conv_bf16_supported(p).

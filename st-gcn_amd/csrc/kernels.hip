@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
       if (rok && cok[j]) {
         float val = acc[j][i] + br;
         if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
-        if (p.res) val += p.res[(int64_t)n * p.out_bstride + row * ostride + ocol[j]];
+        if (p.res) val += p.res[(p.res_shared ? 0 : (int64_t)n * p.out_bstride) + row * ostride + ocol[j]];
         if (p.relu_out) val = fmaxf(val, 0.f);
         if (p.drop.thresh)
           val = dropout_keep(p.drop, (uint64_t)n * p.out_bstride + row * ostride + ocol[j])

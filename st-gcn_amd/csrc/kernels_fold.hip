@@ -1,0 +1,306 @@
+// The folded block (capi.hip fold_w): with one adjacency partition (K = 1) the
+// SpatialConv channel GEMM W' is a 1x1 conv that the (9,1) temporal conv can
+// absorb (st_graphconv.py:99 temporalConv(spatialConv(x)), :148-150):
+//   U[o,t] = sum_q Wt_q (W' G[t'] + bZ)[o]  =  sum_q Wc_q G[t'] + BT[o,t],
+//   Wc_q = Wt_q W'  (C_out x C_in per tap),  t' = s t + q - 4,
+//   BT[o,t,v] = bt[o] + sum_{q : 0 <= t' < T} (Wt_q bZ)[o,v]
+// (bZ = b' rowsum(A), the padded frames of Z carry no bias), so the temporal
+// conv's MFMA GEMM reads G (C_in channels) and Z is never formed. Backward:
+//   dWc_q = sum dU G[t']^T (the temporal weight-gradient kernel over C_in),
+//   dWt_q = dWc_q W'^T + sum_v Tq[o,v] bZ[c,v],   dW' = sum_q Wt_q^T dWc_q,
+//   H = W'^T dZ = sum_q Wc_q^T dU[..]  (the data gradient with Wc: dZ never formed),
+//   sum_{n,t} dZ[c,v] = sum_q sum_o Wt[o,c,q] Tq[o,v],
+// Tq[o,v] = sum over (n, t) with t' in range of dU[o,t,v] = the total minus the
+// boundary frames where tap q reads padding. Small fp64-accumulating kernels
+// here; the big GEMMs are the temporal conv kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "internal.h"
+
+#define HIP_RET(expr)                  \
+  do {                                 \
+    hipError_t e_ = (expr);            \
+    if (e_ != hipSuccess) return e_;   \
+  } while (0)
+
+namespace stgcn {
+
+// out[z][m][n] = sum_{k < K} A[z][m][k] B[z][k][n] + sum_{k < K2} A2[z][m][k] B2[k][n]
+// (element offsets from the strides, z = blockIdx.z adds a_z / b_z / a2_z /
+// o_z). fp64 accumulation; operands and output float or double (run-time
+// flags). Block = 256 threads on a 64 x 64 tile, thread = 4 x 4 outputs; K in
+// chunks of 16 through LDS (A transposed, so both operands are read as
+// 2 x 16-byte vectors per k).
+struct SmallGemm {
+  const void *A, *B, *A2, *B2;
+  void *out;
+  int M, N, K, K2;
+  int a_dbl, b_dbl, a2_dbl, b2_dbl, o_dbl;
+  int64_t am, ak, bk, bn, om, on;
+  int64_t a2m, a2k, b2k, b2n;
+  int64_t a_z, b_z, a2_z, o_z;
+};
+
+__device__ __forceinline__ double ld_fd(const void *p, int dbl, int64_t i) {
+  return dbl ? reinterpret_cast<const double *>(p)[i] : (double)reinterpret_cast<const float *>(p)[i];
+}
+
+__global__ __launch_bounds__(256) void k_small_gemm(SmallGemm g) {
+  __shared__ __attribute__((aligned(16))) double As[16][64];  // [k][m]
+  __shared__ __attribute__((aligned(16))) double Bs[16][64];  // [k][n]
+  const int tid = threadIdx.x, tn = tid & 15, tm = tid >> 4;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int64_t z = blockIdx.z;
+  double acc[4][4] = {};
+  auto run = [&](const void *A, const void *B, int adbl, int bdbl, int K, int64_t am, int64_t ak,
+                 int64_t bk, int64_t bn, int64_t aoff, int64_t boff) {
+    for (int k0 = 0; k0 < K; k0 += 16) {
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int e = r * 256 + tid;
+        {  // A: consecutive threads take consecutive k of one row (strided rows)
+          const int kk = e & 15, mm = e >> 4;
+          const int m = m0 + mm, k = k0 + kk;
+          As[kk][mm] = (m < g.M && k < K) ? ld_fd(A, adbl, aoff + m * am + k * ak) : 0.0;
+        }
+        {
+          const int nn = e & 63, kk = e >> 6;
+          const int k = k0 + kk, n = n0 + nn;
+          Bs[kk][nn] = (k < K && n < g.N) ? ld_fd(B, bdbl, boff + k * bk + n * bn) : 0.0;
+        }
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int kk = 0; kk < 16; ++kk) {
+        double a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a[i] = As[kk][tm * 4 + i];
+          b[i] = Bs[kk][tn * 4 + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+      }
+    }
+  };
+  run(g.A, g.B, g.a_dbl, g.b_dbl, g.K, g.am, g.ak, g.bk, g.bn, z * g.a_z, z * g.b_z);
+  if (g.A2) run(g.A2, g.B2, g.a2_dbl, g.b2_dbl, g.K2, g.a2m, g.a2k, g.b2k, g.b2n, z * g.a2_z, 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + tm * 4 + i;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tn * 4 + j;
+      if (m >= g.M || n >= g.N) continue;
+      const int64_t o = z * g.o_z + m * g.om + n * g.on;
+      if (g.o_dbl)
+        reinterpret_cast<double *>(g.out)[o] = acc[i][j];
+      else
+        reinterpret_cast<float *>(g.out)[o] = (float)acc[i][j];
+    }
+  }
+}
+
+static hipError_t small_gemm(const SmallGemm &g, int nz, hipStream_t s) {
+  hipLaunchKernelGGL(k_small_gemm, dim3((g.N + 63) / 64, (g.M + 63) / 64, nz), dim3(256), 0,
+                     s, g);
+  return hipGetLastError();
+}
+
+// dst[i] = sum_{z < Z} part[z * n + i] (fixed order), as float or double
+__global__ void k_sum_parts(const double *part, int Z, int64_t n, float *dstf, double *dstd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = 0.0;
+  for (int z = 0; z < Z; ++z) a += part[(int64_t)z * n + i];
+  if (dstf) dstf[i] = (float)a;
+  else dstd[i] = a;
+}
+
+// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in)
+hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s) {
+  SmallGemm g{};
+  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.a_z = 1;
+  g.B = W; g.bk = C; g.bn = 1;
+  g.out = Wc; g.om = (int64_t)C * 9; g.on = 9; g.o_z = 1;
+  g.M = R; g.N = C; g.K = R;
+  return small_gemm(g, 9, s);
+}
+
+// Boundary frames of the folded block: output frames t < nb0 and t >= tb1 read
+// padding for some tap (slot t, resp. nb0 + t - tb1; at most 8 slots)
+__device__ __forceinline__ int fold_slot_frame(int slot, int nb0, int tb1) {
+  return slot < nb0 ? slot : tb1 + slot - nb0;
+}
+
+// BT[o][t][v] = bt[o] + sum_{q: 0 <= s t + q - 4 < T} Bq[q][o][v],
+// Bq[q][o][v] = sum_c Wt[o][c][q] bZ[c][v] (small GEMM into `bq`, R * V * 9 doubles)
+__global__ void k_fold_bias(const double *bq, const float *bt, int R, int V, int T, int To, int st,
+                            float *BT) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)R * To * V) return;
+  const int v = (int)(idx % V);
+  const int64_t ot = idx / V;
+  const int t = (int)(ot % To), o = (int)(ot / To);
+  const int t0 = st * t - 4;
+  double a = bt[o];
+#pragma unroll
+  for (int q = 0; q < 9; ++q)
+    if (t0 + q >= 0 && t0 + q < T) a += bq[((int64_t)q * R + o) * V + v];
+  BT[idx] = (float)a;
+}
+
+hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
+                            int To, int st, double *bq, float *BT, hipStream_t s) {
+  SmallGemm g{};
+  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.a_z = 1;
+  g.B = bZ; g.bk = V; g.bn = 1;
+  g.out = bq; g.o_dbl = 1; g.om = V; g.on = 1; g.o_z = (int64_t)R * V;
+  g.M = R; g.N = V; g.K = R;
+  HIP_RET(small_gemm(g, 9, s));
+  const int64_t n = (int64_t)R * To * V;
+  hipLaunchKernelGGL(k_fold_bias, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bq, bt, R, V,
+                     T, To, st, BT);
+  return hipGetLastError();
+}
+
+// cs[o][t][v] = sum_n dU[n, o, t, v] (fp64): block = (o, 1024 consecutive
+// positions of the clip row), thread = VEC consecutive positions, loop over
+// the clips (coalesced VEC-wide loads, no atomics)
+template <int VEC>
+__global__ __launch_bounds__(256) void k_fold_colsum(const float *dU, int N, int R, int L,
+                                                     double *cs) {
+  const int o = blockIdx.x;
+  const int i = (blockIdx.y * 256 + threadIdx.x) * VEC;
+  if (i >= L) return;
+  double a[VEC] = {};
+  const float *p = dU + (int64_t)o * L + i;
+  const int64_t cstr = (int64_t)R * L;
+  int n = 0;
+  for (; n + 2 <= N; n += 2) {
+    float x[VEC], y[VEC];
+    __builtin_memcpy(x, p + n * cstr, sizeof(x));
+    __builtin_memcpy(y, p + (n + 1) * cstr, sizeof(y));
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) a[j] += (double)x[j] + (double)y[j];
+  }
+  if (n < N) {
+    float x[VEC];
+    __builtin_memcpy(x, p + n * cstr, sizeof(x));
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) a[j] += (double)x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) cs[(int64_t)o * L + i + j] = a[j];
+}
+
+// Tq[q][o][v] = sum_t cs[o][t][v] over the frames t whose tap q reads inside
+// [0, T) (all but a few boundary frames): the total minus those frames
+__global__ void k_fold_tq(const double *cs, int R, int V, int T, int To, int st, int nb0, int tb1,
+                          double *Tq) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= R * V) return;
+  const int o = idx / V, v = idx - o * V;
+  const double *c = cs + (int64_t)o * To * V + v;
+  double tot = 0.0;
+  for (int t = 0; t < To; ++t) tot += c[(int64_t)t * V];
+  const int nsl = nb0 + (To - tb1);
+  for (int q = 0; q < 9; ++q) {
+    double a = tot;
+    for (int sl = 0; sl < nsl; ++sl) {
+      const int t = fold_slot_frame(sl, nb0, tb1);
+      const int tt = st * t + q - 4;
+      if (tt < 0 || tt >= T) a -= c[(int64_t)t * V];
+    }
+    Tq[((int64_t)q * R + o) * V + v] = a;
+  }
+}
+
+void fold_slots(int T, int To, int st, int &nb0, int &tb1) {
+  nb0 = std::min(To, (4 + st - 1) / st);                   // frames with s t - 4 < 0
+  tb1 = std::max(nb0, std::min(To, (T - 4 + st - 1) / st));  // frames with s t + 4 >= T
+}
+
+hipError_t launch_fold_du_sums(const float *dU, int N, int R, int T, int To, int V, int st,
+                               double *cs, double *Tq, hipStream_t s) {
+  int nb0, tb1;
+  fold_slots(T, To, st, nb0, tb1);
+  const int L = To * V;
+  const bool a16 = (reinterpret_cast<uintptr_t>(dU) & 15) == 0;
+  const int vec = (L % 4 == 0 && a16) ? 4 : (L % 2 == 0 ? 2 : 1);
+  const dim3 grid(R, (L + 256 * vec - 1) / (256 * vec));
+  if (vec == 4)
+    hipLaunchKernelGGL(k_fold_colsum<4>, grid, dim3(256), 0, s, dU, N, R, L, cs);
+  else if (vec == 2)
+    hipLaunchKernelGGL(k_fold_colsum<2>, grid, dim3(256), 0, s, dU, N, R, L, cs);
+  else
+    hipLaunchKernelGGL(k_fold_colsum<1>, grid, dim3(256), 0, s, dU, N, R, L, cs);
+  hipLaunchKernelGGL(k_fold_tq, dim3((R * V + 127) / 128), dim3(128), 0, s, cs, R, V, T, To, st,
+                     nb0, tb1, Tq);
+  return hipGetLastError();
+}
+
+__global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *dst) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = 0.0;
+  for (int k = 0; k < S; ++k) a += slab[(int64_t)k * n + i];
+  dst[i] = a;
+}
+
+// The folded block's weight gradients from dWc (slab of the temporal weight
+// gradient over C_in channels) and Tq:
+//   dWt[o][c][q] = sum_i dWc[o][i][q] W'[c][i] + sum_v Tq[q][o][v] bZ[c][v]
+//   dW'[c][i]    = sum_q sum_o Wt[o][c][q] dWc[o][i][q]
+//   SdZ[c][v]    = sum_q sum_o Wt[o][c][q] Tq[q][o][v]        (= sum_{n,t} dZ)
+// (the two tap sums as per-tap partial products in `part`, 9 R max(C, V)
+// doubles, summed in fixed order)
+hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
+                             const float *bZ, const double *Tq, int R, int C, int V,
+                             double *dWc, double *part, float *dWt, float *dW, double *SdZ,
+                             hipStream_t s) {
+  const int64_t n = (int64_t)R * C * 9;
+  hipLaunchKernelGGL(k_slab_reduce_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slab,
+                     S, n, dWc);
+  {
+    SmallGemm g{};
+    g.A = dWc; g.a_dbl = 1; g.am = (int64_t)C * 9; g.ak = 9; g.a_z = 1;
+    g.B = W; g.bk = 1; g.bn = C;
+    g.A2 = Tq; g.a2_dbl = 1; g.a2m = V; g.a2k = 1; g.a2_z = (int64_t)R * V;
+    g.B2 = bZ; g.b2k = 1; g.b2n = V;
+    g.K2 = V;
+    g.out = dWt; g.om = (int64_t)R * 9; g.on = 9; g.o_z = 1;
+    g.M = R; g.N = R; g.K = C;
+    HIP_RET(small_gemm(g, 9, s));
+  }
+  {
+    SmallGemm g{};
+    g.A = Wt; g.am = 9; g.ak = (int64_t)R * 9; g.a_z = 1;
+    g.B = dWc; g.b_dbl = 1; g.bk = (int64_t)C * 9; g.bn = 9; g.b_z = 1;
+    g.out = part; g.o_dbl = 1; g.om = C; g.on = 1; g.o_z = (int64_t)R * C;
+    g.M = R; g.N = C; g.K = R;
+    HIP_RET(small_gemm(g, 9, s));
+    const int64_t m = (int64_t)R * C;
+    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
+                       dW, nullptr);
+  }
+  {
+    SmallGemm g{};
+    g.A = Wt; g.am = 9; g.ak = (int64_t)R * 9; g.a_z = 1;
+    g.B = Tq; g.b_dbl = 1; g.bk = V; g.bn = 1; g.b_z = (int64_t)R * V;
+    g.out = part; g.o_dbl = 1; g.om = V; g.on = 1; g.o_z = (int64_t)R * V;
+    g.M = R; g.N = V; g.K = R;
+    HIP_RET(small_gemm(g, 9, s));
+    const int64_t m = (int64_t)R * V;
+    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
+                       nullptr, SdZ);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace stgcn
