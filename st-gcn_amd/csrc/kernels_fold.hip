@@ -48,33 +48,37 @@ __device__ __forceinline__ double ld_fd(const void *p, int dbl, int64_t i) {
 }
 
 __global__ __launch_bounds__(256) void k_small_gemm(SmallGemm g) {
-  __shared__ __attribute__((aligned(16))) double As[16][64];  // [k][m]
-  __shared__ __attribute__((aligned(16))) double Bs[16][64];  // [k][n]
-  const int tid = threadIdx.x, tn = tid & 15, tm = tid >> 4;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  // 32 x 32 output tile; wave w takes k-steps w*16 .. +15 of every 64-deep
+  // chunk (thread = 4 x 4 outputs), the four partial tiles summed in LDS at the end
+  __shared__ __attribute__((aligned(16))) double sm[2 * 64 * 32];
+  double(*As)[32] = reinterpret_cast<double(*)[32]>(sm);            // [k][m]
+  double(*Bs)[32] = reinterpret_cast<double(*)[32]>(sm + 64 * 32);  // [k][n]
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int tm = l >> 3, tn = l & 7;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
   const int64_t z = blockIdx.z;
   double acc[4][4] = {};
   auto run = [&](const void *A, const void *B, int adbl, int bdbl, int K, int64_t am, int64_t ak,
                  int64_t bk, int64_t bn, int64_t aoff, int64_t boff) {
-    for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int k0 = 0; k0 < K; k0 += 64) {
       __syncthreads();
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 8; ++r) {
         const int e = r * 256 + tid;
-        {  // A: consecutive threads take consecutive k of one row (strided rows)
-          const int kk = e & 15, mm = e >> 4;
+        {  // A: consecutive threads take consecutive k of one row
+          const int kk = e & 63, mm = e >> 6;
           const int m = m0 + mm, k = k0 + kk;
           As[kk][mm] = (m < g.M && k < K) ? ld_fd(A, adbl, aoff + m * am + k * ak) : 0.0;
         }
         {
-          const int nn = e & 63, kk = e >> 6;
+          const int nn = e & 31, kk = e >> 5;
           const int k = k0 + kk, n = n0 + nn;
           Bs[kk][nn] = (k < K && n < g.N) ? ld_fd(B, bdbl, boff + k * bk + n * bn) : 0.0;
         }
       }
       __syncthreads();
 #pragma unroll 4
-      for (int kk = 0; kk < 16; ++kk) {
+      for (int kk = w * 16; kk < w * 16 + 16; ++kk) {
         double a[4], b[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -90,25 +94,37 @@ __global__ __launch_bounds__(256) void k_small_gemm(SmallGemm g) {
   };
   run(g.A, g.B, g.a_dbl, g.b_dbl, g.K, g.am, g.ak, g.bk, g.bn, z * g.a_z, z * g.b_z);
   if (g.A2) run(g.A2, g.B2, g.a2_dbl, g.b2_dbl, g.K2, g.a2m, g.a2k, g.b2k, g.b2n, z * g.a2_z, 0);
+  // partial tiles of waves 1-3 -> LDS, wave 0 sums in fixed order and stores
+  __syncthreads();
+  if (w > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sm[((w - 1) * 64 + l) * 16 + i * 4 + j] = acc[i][j];
+  }
+  __syncthreads();
+  if (w > 0) return;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + tm * 4 + i;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + tn * 4 + j;
+      double v = acc[i][j];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) v += sm[(p * 64 + l) * 16 + i * 4 + j];
       if (m >= g.M || n >= g.N) continue;
       const int64_t o = z * g.o_z + m * g.om + n * g.on;
       if (g.o_dbl)
-        reinterpret_cast<double *>(g.out)[o] = acc[i][j];
+        reinterpret_cast<double *>(g.out)[o] = v;
       else
-        reinterpret_cast<float *>(g.out)[o] = (float)acc[i][j];
+        reinterpret_cast<float *>(g.out)[o] = (float)v;
     }
   }
 }
 
 static hipError_t small_gemm(const SmallGemm &g, int nz, hipStream_t s) {
-  hipLaunchKernelGGL(k_small_gemm, dim3((g.N + 63) / 64, (g.M + 63) / 64, nz), dim3(256), 0,
-                     s, g);
+  hipLaunchKernelGGL(k_small_gemm, dim3((g.N + 31) / 32, (g.M + 31) / 32, nz), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
@@ -200,24 +216,31 @@ __global__ __launch_bounds__(256) void k_fold_colsum(const float *dU, int N, int
 }
 
 // Tq[q][o][v] = sum_t cs[o][t][v] over the frames t whose tap q reads inside
-// [0, T) (all but a few boundary frames): the total minus those frames
-__global__ void k_fold_tq(const double *cs, int R, int V, int T, int To, int st, int nb0, int tb1,
-                          double *Tq) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= R * V) return;
-  const int o = idx / V, v = idx - o * V;
-  const double *c = cs + (int64_t)o * To * V + v;
+// [0, T) (all but a few boundary frames): the total minus those frames.
+// Block = o; thread = (frame phase, joint), the phases summed in LDS.
+__global__ __launch_bounds__(256) void k_fold_tq(const double *cs, int R, int V, int T, int To,
+                                                 int st, int nb0, int tb1, double *Tq) {
+  __shared__ double ts[256];
+  const int o = blockIdx.x, tid = threadIdx.x;
+  const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
+  const double *c = cs + (int64_t)o * To * V;
+  double a = 0.0;
+  if (ph < PH)
+    for (int t = ph; t < To; t += PH) a += c[(int64_t)t * V + v];
+  ts[tid] = a;
+  __syncthreads();
+  if (tid >= V) return;
   double tot = 0.0;
-  for (int t = 0; t < To; ++t) tot += c[(int64_t)t * V];
+  for (int p = 0; p < PH; ++p) tot += ts[p * V + tid];
   const int nsl = nb0 + (To - tb1);
   for (int q = 0; q < 9; ++q) {
-    double a = tot;
+    double r = tot;
     for (int sl = 0; sl < nsl; ++sl) {
       const int t = fold_slot_frame(sl, nb0, tb1);
       const int tt = st * t + q - 4;
-      if (tt < 0 || tt >= T) a -= c[(int64_t)t * V];
+      if (tt < 0 || tt >= T) r -= c[(int64_t)t * V + tid];
     }
-    Tq[((int64_t)q * R + o) * V + v] = a;
+    Tq[((int64_t)q * R + o) * V + tid] = r;
   }
 }
 
@@ -240,8 +263,8 @@ hipError_t launch_fold_du_sums(const float *dU, int N, int R, int T, int To, int
     hipLaunchKernelGGL(k_fold_colsum<2>, grid, dim3(256), 0, s, dU, N, R, L, cs);
   else
     hipLaunchKernelGGL(k_fold_colsum<1>, grid, dim3(256), 0, s, dU, N, R, L, cs);
-  hipLaunchKernelGGL(k_fold_tq, dim3((R * V + 127) / 128), dim3(128), 0, s, cs, R, V, T, To, st,
-                     nb0, tb1, Tq);
+  if (V > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fold_tq, dim3(R), dim3(256), 0, s, cs, R, V, T, To, st, nb0, tb1, Tq);
   return hipGetLastError();
 }
 
