@@ -714,6 +714,184 @@ __global__ __launch_bounds__((WgBf16Geo<NQ, V, SIN, FT, CB>::NTH), 1) void k_wgr
 }
 
 // ---------------------------------------------------------------------------
+// k_wgrad_bf16_raw: the stride-1 temporal weight gradient for bf16 P / Q at
+// V = 25 (odd: a frame's joints are not whole dwords, so the padded-frame
+// images of k_wgrad_bf16 cannot be filled by dword LDS-DMA). Same tiles, items
+// (clip, FT = 4 frames), split-K plan and slab as k_wgrad_bf16<9,25,1,4,64>, but
+// the reduction index is the item's RAW position k = f V + v (100 positions,
+// 7 k-steps of 16; P zero past 100), so an item's rows are contiguous runs in
+// HBM that start on even elements whenever the clip's frame counts are even
+// (M = T_src even: the host checks) and move by 4-byte LDS-DMA pieces straight
+// into the images: P [64][120] and the Q window [64 channels][314] (frames
+// m0-4 .. m0+7, zero outside [0, T)). Tap q reads Q at k + 25 q: the B fragment
+// (8 consecutive positions) starts on an odd element for odd q, so it is read as
+// 5 dwords and realigned with v_alignbit (4 aligned dwords for even q). Whole
+// next item in flight under the current one, one vmcnt(0) + barrier per item.
+// ---------------------------------------------------------------------------
+struct WgRawGeo {
+  static constexpr int V = 25, FT = 4, CB = 64, NQ = 9;
+  static constexpr int KP = FT * V;                 // 100 positions
+  static constexpr int KSTEPS = (KP + 15) / 16;     // 7
+  static constexpr int PP = 120;                    // P pitch (elements): PP/8 odd
+  static constexpr int QW = (FT + 8) * V;           // 300 window elements
+  static constexpr int QPD = 157;                   // Q pitch (dwords, odd) >= (111 + 200 + 3) / 2
+  static constexpr int PDW = 64 * PP / 2;           // 3840 dwords
+  static constexpr int QDW = CB * QPD;              // 10048 dwords
+  static constexpr int PBYTES = PDW * 4, BUF = (PDW + QDW) * 4;
+  static constexpr int NW = 8;
+  static constexpr int PRN = PDW / 64, QRN = QDW / 64;  // 60, 157 wave rounds
+  static constexpr int PR = (PRN + NW - 1) / NW, QR = (QRN + NW - 1) / NW;
+  static_assert(PDW % 64 == 0 && QDW % 64 == 0, "whole wave rounds");
+  static_assert(2 * BUF <= 160 * 1024, "LDS budget");
+};
+
+bool wgrad_raw_ok(const WgradParams &p) {
+  return p.NQ == 9 && p.V == 25 && p.s_in == 1 && p.off == -4 && p.FT == 4 && p.p_bf16 &&
+         p.q_bf16 && p.M % 2 == 0 && p.T_src % 2 == 0 && (int64_t)p.R * p.M * 25 < (1 << 23) &&
+         (int64_t)p.C * p.T_src * 25 < (1 << 23) && p.n_jtiles * 64 >= p.C &&
+         !STGCN_AB_WG_REGSTAGE;
+}
+
+__global__ __launch_bounds__(512, 1) void k_wgrad_bf16_raw(WgradParams p) {
+  using G = WgRawGeo;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  char *lds = reinterpret_cast<char *>(smem);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hi = lane >> 5, lo = lane & 31;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntiles = p.n_rtiles * p.n_jtiles;
+  const int tile = bid % ntiles, split = bid / ntiles;
+  const int jt = tile % p.n_jtiles, rt = tile / p.n_jtiles;
+  const int r0 = rt * 64, c0 = jt * G::CB;
+  const int mi = wave & 1, cj = (wave >> 1) & 1, tq = wave >> 2;  // taps 0-4 / 5-8
+  const int nitems = p.N * p.n_mtiles;
+  const int per = (nitems + p.S - 1) / p.S;
+  const int it0 = min(nitems, split * per), it1 = min(nitems, it0 + per);
+  const int MV = p.M * G::V, TV = p.T_src * G::V;
+
+  // per-lane DMA tables: (frame of the dword's first element << 23) | element
+  // offset within the clip (without the item's frame base); ~0: pad / past the tensor
+  unsigned ptab[G::PR], qtab[G::QR];
+#pragma unroll
+  for (int i = 0; i < G::PR; ++i) {
+    const int d = (i * G::NW + wave) * 64 + lane;
+    const int row = d / (G::PP / 2), e = 2 * (d - row * (G::PP / 2));
+    const bool ok = i * G::NW + wave < G::PRN && e < G::KP && r0 + row < p.R;
+    ptab[i] = ok ? ((unsigned)(e / G::V) << 23) | (unsigned)((r0 + row) * MV + e) : ~0u;
+  }
+#pragma unroll
+  for (int i = 0; i < G::QR; ++i) {
+    const int d = (i * G::NW + wave) * 64 + lane;
+    const int c = d / G::QPD, e = 2 * (d - c * G::QPD);
+    const bool ok = i * G::NW + wave < G::QRN && e < G::QW && c0 + c < p.C;
+    qtab[i] = ok ? ((unsigned)(e / G::V) << 23) | (unsigned)((c0 + c) * TV + e) : ~0u;
+  }
+  const unsigned lds_addr = (unsigned)reinterpret_cast<uintptr_t>(lds);
+  auto stage = [&](int item, int bufi) __attribute__((always_inline)) {
+    const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * G::FT;
+    const uint64_t sp = reinterpret_cast<uint64_t>(reinterpret_cast<const __bf16 *>(p.P) +
+                                                   (int64_t)n * p.p_bstride);
+    const uint64_t sq = reinterpret_cast<uint64_t>(reinterpret_cast<const __bf16 *>(p.Q) +
+                                                   (int64_t)n * p.q_bstride);
+    const int4v rp = uniform4(int4v{(int)(uint32_t)sp, (int)((sp >> 32) & 0xffff),
+                                    (int)std::min<int64_t>(p.p_bstride * 2, 0x7fffffff), 0x00020000});
+    const int4v rq = uniform4(int4v{(int)(uint32_t)sq, (int)((sq >> 32) & 0xffff),
+                                    (int)std::min<int64_t>(p.q_bstride * 2, 0x7fffffff), 0x00020000});
+    const int t0 = m0 - 4;
+    const unsigned lb =
+        (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_addr + (unsigned)(bufi * G::BUF)));
+    asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
+#pragma unroll
+    for (int i = 0; i < G::PR; ++i)
+      if (i * G::NW + wave < G::PRN) {
+        const unsigned e = ptab[i];
+        const bool ok = e != ~0u && m0 + (int)(e >> 23) < p.M;
+        const unsigned voff = ok ? ((e & 0x7fffffu) + (unsigned)(m0 * G::V)) * 2u : kOOB;
+        dma_b32(rp, voff, lb + (unsigned)((i * G::NW + wave) * 256));
+      }
+#pragma unroll
+    for (int i = 0; i < G::QR; ++i)
+      if (i * G::NW + wave < G::QRN) {
+        const unsigned e = qtab[i];
+        const int t = t0 + (int)(e >> 23);
+        const bool ok = e != ~0u && t >= 0 && t < p.T_src;
+        const unsigned voff = ok ? (unsigned)((int)(e & 0x7fffffu) + t0 * G::V) * 2u : kOOB;
+        dma_b32(rq, voff, lb + (unsigned)(G::PBYTES + (i * G::NW + wave) * 256));
+      }
+  };
+
+  auto run = [&](auto q0_c, auto nt_c) {
+    constexpr int Q0 = decltype(q0_c)::value, NT = decltype(nt_c)::value;
+    floatx16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    const int pa = (mi * 32 + lo) * G::PP + 8 * hi;            // elements
+    const int qd = (cj * 32 + lo) * G::QPD;                      // dwords
+    auto compute = [&](const char *buf) {
+      const __bf16 *P = reinterpret_cast<const __bf16 *>(buf) + pa;
+      const unsigned *Qd = reinterpret_cast<const unsigned *>(buf + G::PBYTES) + qd;
+      auto ldb = [&](int s, int t) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int q = Q0 + t;
+        const int e0 = 16 * s + 8 * hi + 25 * q;  // first element of the fragment
+        const unsigned *src = Qd + (e0 >> 1);
+        unsigned u[5];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) u[j] = src[j];
+        uint4 w;
+        if (q & 1) {  // odd start: elements from the high half of dword 0
+          u[4] = src[4];
+          w.x = __builtin_amdgcn_alignbit(u[1], u[0], 16);
+          w.y = __builtin_amdgcn_alignbit(u[2], u[1], 16);
+          w.z = __builtin_amdgcn_alignbit(u[3], u[2], 16);
+          w.w = __builtin_amdgcn_alignbit(u[4], u[3], 16);
+        } else {
+          w = make_uint4(u[0], u[1], u[2], u[3]);
+        }
+        return __builtin_bit_cast(bf16x8, w);
+      };
+      bf16x8 a[2], b[2][NT];
+      auto ld = [&](int s, int set) {
+        a[set] = *reinterpret_cast<const bf16x8 *>(P + 16 * s);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) b[set][t] = ldb(s, t);
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        if (s + 1 < G::KSTEPS) ld(s + 1, (s + 1) & 1);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma_bf16(a[s & 1], b[s & 1][t], acc[t]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    if (it0 < it1) stage(it0, 0);
+    for (int it = 0, itm = it0; itm < it1; ++it, ++itm) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (itm + 1 < it1) stage(itm + 1, (it + 1) & 1);
+      compute(lds + (it & 1) * G::BUF);
+    }
+    float *slab = p.slab + (int64_t)split * p.R * p.C * G::NQ;
+    const int c = c0 + cj * 32 + lo;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        if (r < p.R && c < p.C) slab[((int64_t)r * p.C + c) * G::NQ + Q0 + t] = acc[t][i];
+      }
+  };
+  if (tq == 0)
+    run(std::integral_constant<int, 0>{}, std::integral_constant<int, 5>{});
+  else
+    run(std::integral_constant<int, 5>{}, std::integral_constant<int, 4>{});
+}
+
+// ---------------------------------------------------------------------------
 // k_wgrad_gemm_bf16: the NQ = 1, stride-1 weight gradient (the spatial
 // dW' = dZ G^T) as a plain split-K GEMM over the contiguous (t, v) positions of
 // each clip row: slab[split][r][c] = sum_{items} sum_{l in chunk} P[n][r][l] Q[n][c][l].
@@ -897,6 +1075,12 @@ static bool launch_wb_if(const WgradParams &p, hipStream_t s) {
   using G = WgBf16Geo<NQ, V, SIN, FT, CB>;
   const int nblk = p.n_rtiles * p.n_jtiles * p.S;
   if constexpr (NQ == 9) {  // (bf16 P and Q: the temporal weight gradient only)
+    if constexpr (V == 25 && SIN == 1) {
+      if (wgrad_raw_ok(p)) {  // raw positions by LDS-DMA (odd V)
+        hipLaunchKernelGGL(k_wgrad_bf16_raw, dim3(nblk), dim3(512), 2 * WgRawGeo::BUF, s, p);
+        return true;
+      }
+    }
     if (p.p_bf16 && p.q_bf16) {
       hipLaunchKernelGGL((k_wgrad_bf16<NQ, V, SIN, FT, CB, true>), dim3(nblk), dim3(G::NTH),
                          2 * G::BUF, s, p);

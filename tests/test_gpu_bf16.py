@@ -149,6 +149,12 @@ def _check_bf16(pkg, case, residual=False, need_dx=True, seed=0):
     (24, 40, 1, 50, 3, 2, 11),      # partial chunk (24 = 16 + 8) and rows (40 of 64)
     (5, 21, 1, 18, 1, 2, 9),        # odd channel counts: partial tiles and chunks (5: fp32 W)
     (64, 64, 2, 25, 3, 8, 1),       # T = 1 (single frame: all taps but one in the halo)
+    # k_wgrad_bf16_raw (V = 25, stride 1, bf16 Z / dU, even T): ragged last
+    # item (42 = 10 * 4 + 2 frames), partial channel tiles (96 = 64 + 32 rows /
+    # channels), two row tiles, and T = 2 (every tap but one in the halo)
+    (32, 96, 1, 25, 3, 2, 42),
+    (128, 128, 1, 25, 3, 3, 10),
+    (64, 64, 1, 25, 3, 4, 2),
 ])
 def test_bf16_block_matches_oracle(pkg, case):
     errs = _check_bf16(pkg, case)
