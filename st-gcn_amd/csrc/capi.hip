@@ -116,6 +116,14 @@ bool fold_w(const stgcn_desc_t *d) {
   return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->V == 18 &&
          !fused_spb(d);
 }
+// sum_{n,t} dZ from per-tap sums of dU (clip-chunk sums written by the ReLU +
+// BN2 backward apply): the folded block (it has no dZ). Elsewhere the pass over
+// dZ measured faster (cfg3 5684 vs 5643 clips/s in one A/B call: the column
+// apply runs fewer, longer blocks); STGCN_AB_COLS_SUMS builds use the sums on
+// every non-residual block (A/B only).
+bool cols_sums(const stgcn_desc_t *d) {
+  return !residual(d) && (fold_w(d) || STGCN_AB_COLS_SUMS != 0);
+}
 // The folded forward leaves Wc in the (otherwise unused) Z buffer for the
 // backward when it fits (Z is opaque to the caller under STGCN_F_F32X3 then)
 bool fold_wc_in_z(const stgcn_desc_t *d) {
@@ -251,11 +259,15 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.s1 = c.take<double>(C);
   L.s2 = c.take<double>(C);
   L.dbl_bytes = c.off;
-  if (fold_w(d)) {
-    L.fcs = c.take<double>((size_t)R * nTo(d));
+  if (!residual(d)) {  // clip-chunk sums of dU -> Tq -> sum_{n,t} dZ (kernels_fold.hip)
+    L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
     L.ftq = c.take<double>((size_t)9 * R * d->V);
+    L.fpart = c.take<double>(std::max((size_t)9 * R * std::max(C, d->V),
+                                      (size_t)R * apply_cols_chunks(d->N) *
+                                          fold_tot_blocks(d->T_out) * d->V));
+  }
+  if (fold_w(d)) {
     L.dWc = c.take<double>((size_t)R * C * 9);
-    L.fpart = c.take<double>((size_t)9 * R * std::max(C, d->V));
     L.Wc = c.take<float>((size_t)R * C * 9);
     L.bZ = c.take<float>((size_t)R * d->V);
   }
@@ -732,9 +744,19 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
                                         L.sg, L.sgu, drop, s));
     }
-    HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
-                                     L.sdu, N, R, To * V, d->training, drop, s,
-                                     du_bf16(d) ? 1 : 0, a->dy_coef));
+    // (with the clip-chunk sums of dU: sum_{n,t} dZ follows from them per tap,
+    // no pass over dZ)
+    if (cols_sums(d)) {
+      HIP_TRY(launch_bn_relu_bwd_apply_cols(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
+                                            L.dU, L.sdu, N, R, To * V, d->training, drop, s,
+                                            du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs));
+      HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.fpart, L.ftq,
+                             s));
+    } else {
+      HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
+                                       L.sdu, N, R, To * V, d->training, drop, s,
+                                       du_bf16(d) ? 1 : 0, a->dy_coef));
+    }
     HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
     // residual block: final ReLU backward -> dU (= d(conv out) = d(residual));
@@ -803,10 +825,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     }
     WgradParams w = make_wgrad_taps(d, L.dU, G, L.slab, C);
     HIP_TRY(launch_wgrad_taps(w, s));
-    HIP_TRY(launch_fold_du_sums(L.dU, N, R, T, To, V, d->stride, L.fcs, L.ftq, s));
     HIP_TRY(launch_fold_grads(L.slab, w.S, a->Wt, a->W, L.bZ, L.ftq, R, C, V, L.dWc, L.fpart,
-                              a->dWt,
-                              a->dW, L.SdZ, s));
+                              a->dWt, a->dW, s));
   } else {
   // Temporal conv data-gradient: dZ = conv^T(dU)
   {
@@ -900,8 +920,11 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_wgrad(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * K * C, a->dW, 1, R, K, C, s));
   }
-  HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s, dzb ? 1 : 0));
+  if (!cols_sums(d)) HIP_TRY(launch_sum_nt(L.dZ, N, R, T, V, L.SdZ, s, dzb ? 1 : 0));
   }
+  // sum_{n,t} dZ: from the temporal weight and the per-tap dU sums on the
+  // non-residual block (dZ = conv^T(dU)); the residual block's dZ passes BN2
+  if (cols_sums(d)) HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
   HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
   // Deferred dx (ABI 5): the BN1 backward apply of this block is folded into the
   // previous block's ReLU+BN2 backward apply (launch_bn_relu_bwd_apply with

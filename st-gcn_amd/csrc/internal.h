@@ -102,12 +102,23 @@ hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
 hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s);
 hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
                             int To, int st, double *bq, float *BT, hipStream_t s);
-hipError_t launch_fold_du_sums(const float *dU, int N, int R, int T, int To, int V, int st,
-                               double *cs, double *Tq, hipStream_t s);
+int fold_tot_blocks(int To);
+hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
+                          double *part, double *Tq, hipStream_t s);
+hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
+                           double *SdZ, hipStream_t s);
 hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
                              const float *bZ, const double *Tq, int R, int C, int V,
-                             double *dWc, double *part, float *dWt, float *dW, double *SdZ,
-                             hipStream_t s);
+                             double *dWc, double *part, float *dWt, float *dW, hipStream_t s);
+// k_bn_relu_bwd_apply that also writes the clip-chunk sums of dU,
+// cs[z][C][L] for z < apply_cols_chunks(N) (kernels.hip)
+int apply_cols_chunks(int N);
+hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const float *mean,
+                                         const float *invstd, const float *g, const float *b,
+                                         const double *sg, const double *sgu, float *dU,
+                                         double *sdu, int N, int C, int L, int training,
+                                         Dropout drop, hipStream_t s, int du_bf16,
+                                         const float *dy_coef, double *cs);
 // bf16 path (kernels_bf16.hip): the reference's graphs (V = 18, 25, 50) with
 // the fp32 path's tile plan (FT = kTileCols / V); launch_conv_gemm dispatches here
 // when p.bf16 and conv_bf16_supported(p).

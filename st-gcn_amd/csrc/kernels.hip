@@ -1649,6 +1649,123 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
   return hipGetLastError();
 }
 
+// k_bn_relu_bwd_apply with the clip sums of its output (non-residual blocks):
+// block = (channel c, 256 * VEC consecutive positions of the (T_out, V) row,
+// clip chunk z), thread = VEC positions over the chunk's clips, so
+// cs[z][c][pos] = sum_{n in chunk z} dU[n, c, pos] accumulates in registers
+// (fp64, no atomics). Those sums give sum_{n,t} dZ by the per-tap algebra of
+// kernels_fold.hip (SdZ = sum_q Wt_q^T Tq): the separate pass over dZ is gone.
+template <int VEC>
+__global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
+    const float *__restrict__ dy, const float *__restrict__ U, const float *mean,
+    const float *invstd, const float *g, const float *b, const double *sg, const double *sgu,
+    float *__restrict__ dU, double *sdu, int N, int C, int L, double invM, Dropout drop,
+    int du_bf16, const float *dy_coef, double *__restrict__ cs) {
+  __shared__ double red[8];
+  const int c = blockIdx.x;
+  const int i = (blockIdx.y * 256 + threadIdx.x) * VEC;
+  const int nz = gridDim.z, per = (N + nz - 1) / nz;
+  const int n0 = blockIdx.z * per, n1 = min(N, n0 + per);
+  const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
+  const float mg = (float)(sg[c] * invM), mgu = (float)(sgu[c] * invM);
+  float ca = 0.f, cmd = 0.f, cmu = 0.f, cis = 0.f, cmdn = 0.f;
+  if (dy_coef) {
+    ca = dy_coef[c];
+    cmd = dy_coef[C + c];
+    cmu = dy_coef[2 * C + c];
+    cis = dy_coef[3 * C + c];
+    cmdn = dy_coef[4 * C + c];
+  }
+  double s = 0.0, col[VEC] = {};
+  if (i < L) {
+    // (the next clip's operands are loaded before this clip's math and stores)
+    float un[VEC], dn[VEC];
+    if (n0 < n1) {
+      const int64_t base = ((int64_t)n0 * C + c) * L;
+      vld<VEC>(U + base + i, un);
+      vld<VEC>(dy + base + i, dn);
+    }
+    for (int n = n0; n < n1; ++n) {
+      const int64_t base = ((int64_t)n * C + c) * L;
+      float u[VEC], d[VEC], o[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        u[j] = un[j];
+        d[j] = dn[j];
+      }
+      if (n + 1 < n1) {
+        vld<VEC>(U + base + (int64_t)C * L + i, un);
+        vld<VEC>(dy + base + (int64_t)C * L + i, dn);
+      }
+      if (dy_coef) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          const float t = (u[j] - mu) * a + be;
+          const float yv = t > 0.f ? t : 0.f;
+          d[j] = ca * (d[j] - cmd - (yv - cmu) * cis * cmdn);
+        }
+      }
+      if (drop.thresh) {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+          d[j] = dropout_keep(drop, base + i + j) ? d[j] * drop.scale : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        const float uh = (u[j] - mu) * is;
+        const float gg = (u[j] - mu) * a + be > 0.f ? d[j] : 0.f;
+        o[j] = a * (gg - mg - uh * mgu);
+        s += o[j];
+        col[j] += o[j];
+      }
+      if (du_bf16) {
+        __bf16 *ob = reinterpret_cast<__bf16 *>(dU) + base + i;
+        unsigned short h[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) h[j] = __builtin_bit_cast(unsigned short, (__bf16)o[j]);
+        if constexpr (VEC == 4)
+          *reinterpret_cast<uint2 *>(ob) = make_uint2(h[0] | ((unsigned)h[1] << 16),
+                                                      h[2] | ((unsigned)h[3] << 16));
+        else if constexpr (VEC == 2)
+          *reinterpret_cast<unsigned *>(ob) = h[0] | ((unsigned)h[1] << 16);
+        else
+          *reinterpret_cast<unsigned short *>(ob) = h[0];
+      } else {
+        vst<VEC>(dU + base + i, o);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) cs[((int64_t)blockIdx.z * C + c) * L + i + j] = col[j];
+  }
+  block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
+}
+
+int apply_cols_chunks(int N) { return std::min(N, 4); }
+
+hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const float *mean,
+                                         const float *invstd, const float *g, const float *b,
+                                         const double *sg, const double *sgu, float *dU,
+                                         double *sdu, int N, int C, int L, int training,
+                                         Dropout drop, hipStream_t s, int du_bf16,
+                                         const float *dy_coef, double *cs) {
+  const double invM = training ? 1.0 / ((double)N * L) : 0.0;
+  // (whole-row vectors: every row start VEC-aligned needs L % VEC == 0)
+  int vec = slice_vec(L, {dy, U, dU});
+  const int nz = apply_cols_chunks(N);
+#define COLS_LAUNCH(VV)                                                                     \
+  hipLaunchKernelGGL((k_bn_relu_bwd_apply_cols<VV>), dim3(C, (L + 256 * VV - 1) / (256 * VV), nz), \
+                     dim3(256), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, sdu, N, C, L,  \
+                     invM, drop, du_bf16, dy_coef, cs)
+  if (vec == 4)
+    COLS_LAUNCH(4);
+  else if (vec == 2)
+    COLS_LAUNCH(2);
+  else
+    COLS_LAUNCH(1);
+#undef COLS_LAUNCH
+  return hipGetLastError();
+}
+
 // The deferred-dx chain's per-channel finalize (see internal.h): with
 // a = invstd1 g1, md = sd / M, mdn = sdn / M the next-to-be-applied dx is
 //   dx = a (dxhat - md - (x - mu1) invstd1 mdn)

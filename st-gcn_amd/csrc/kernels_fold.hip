@@ -185,62 +185,60 @@ hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, i
   return hipGetLastError();
 }
 
-// cs[o][t][v] = sum_n dU[n, o, t, v] (fp64): block = (o, 1024 consecutive
-// positions of the clip row), thread = VEC consecutive positions, loop over
-// the clips (coalesced VEC-wide loads, no atomics)
-template <int VEC>
-__global__ __launch_bounds__(256) void k_fold_colsum(const float *dU, int N, int R, int L,
-                                                     double *cs) {
-  const int o = blockIdx.x;
-  const int i = (blockIdx.y * 256 + threadIdx.x) * VEC;
-  if (i >= L) return;
-  double a[VEC] = {};
-  const float *p = dU + (int64_t)o * L + i;
-  const int64_t cstr = (int64_t)R * L;
-  int n = 0;
-  for (; n + 2 <= N; n += 2) {
-    float x[VEC], y[VEC];
-    __builtin_memcpy(x, p + n * cstr, sizeof(x));
-    __builtin_memcpy(y, p + (n + 1) * cstr, sizeof(y));
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) a[j] += (double)x[j] + (double)y[j];
-  }
-  if (n < N) {
-    float x[VEC];
-    __builtin_memcpy(x, p + n * cstr, sizeof(x));
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) a[j] += (double)x[j];
-  }
-#pragma unroll
-  for (int j = 0; j < VEC; ++j) cs[(int64_t)o * L + i + j] = a[j];
-}
-
 // Tq[q][o][v] = sum_t cs[o][t][v] over the frames t whose tap q reads inside
 // [0, T) (all but a few boundary frames): the total minus those frames.
-// Block = o; thread = (frame phase, joint), the phases summed in LDS.
-__global__ __launch_bounds__(256) void k_fold_tq(const double *cs, int R, int V, int T, int To,
-                                                 int st, int nb0, int tb1, double *Tq) {
+// cs holds nz clip-chunk partials ([nz][R][To][V], k_bn_relu_bwd_apply_cols).
+// Two steps: k_fold_tot sums frame blocks of 16 (grid R x nz x blocks, one
+// partial per block and joint, fixed order), k_fold_tq adds the partials and
+// subtracts the boundary frames per tap.
+constexpr int kTotFrames = 16;
+
+__global__ __launch_bounds__(256) void k_fold_tot(const double *cs, int R, int V, int To,
+                                                  double *part) {
   __shared__ double ts[256];
-  const int o = blockIdx.x, tid = threadIdx.x;
+  const int o = blockIdx.x, z = blockIdx.y, tb = blockIdx.z, tid = threadIdx.x;
   const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
-  const double *c = cs + (int64_t)o * To * V;
+  const double *c = cs + ((int64_t)z * R + o) * To * V;
   double a = 0.0;
   if (ph < PH)
-    for (int t = ph; t < To; t += PH) a += c[(int64_t)t * V + v];
+    for (int t = tb * kTotFrames + ph; t < min(To, (tb + 1) * kTotFrames); t += PH)
+      a += c[(int64_t)t * V + v];
   ts[tid] = a;
   __syncthreads();
   if (tid >= V) return;
   double tot = 0.0;
   for (int p = 0; p < PH; ++p) tot += ts[p * V + tid];
+  part[(((int64_t)o * gridDim.y + z) * gridDim.z + tb) * V + tid] = tot;
+}
+
+__global__ void k_fold_tq(const double *cs, const double *part, int np, int nz, int R, int V, int T,
+                          int To, int st, int nb0, int tb1, double *Tq) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= R * V) return;
+  const int o = idx / V, v = idx - o * V;
+  const int64_t zs = (int64_t)R * To * V;
+  const double *c = cs + (int64_t)o * To * V + v;
+  double tot = 0.0;
+  for (int k = 0; k < np; ++k) tot += part[((int64_t)o * np + k) * V + v];
   const int nsl = nb0 + (To - tb1);
+  double bnd[8];  // the boundary frames, summed over the clip chunks
+#pragma unroll
+  for (int sl = 0; sl < 8; ++sl) {
+    bnd[sl] = 0.0;
+    if (sl < nsl) {
+      const int t = fold_slot_frame(sl, nb0, tb1);
+      for (int z = 0; z < nz; ++z) bnd[sl] += c[z * zs + (int64_t)t * V];
+    }
+  }
+#pragma unroll
   for (int q = 0; q < 9; ++q) {
     double r = tot;
-    for (int sl = 0; sl < nsl; ++sl) {
-      const int t = fold_slot_frame(sl, nb0, tb1);
-      const int tt = st * t + q - 4;
-      if (tt < 0 || tt >= T) r -= c[(int64_t)t * V + tid];
+#pragma unroll
+    for (int sl = 0; sl < 8; ++sl) {
+      const int tt = st * fold_slot_frame(sl, nb0, tb1) + q - 4;
+      if (sl < nsl && (tt < 0 || tt >= T)) r -= bnd[sl];
     }
-    Tq[((int64_t)q * R + o) * V + tid] = r;
+    Tq[((int64_t)q * R + o) * V + v] = r;
   }
 }
 
@@ -249,22 +247,18 @@ void fold_slots(int T, int To, int st, int &nb0, int &tb1) {
   tb1 = std::max(nb0, std::min(To, (T - 4 + st - 1) / st));  // frames with s t + 4 >= T
 }
 
-hipError_t launch_fold_du_sums(const float *dU, int N, int R, int T, int To, int V, int st,
-                               double *cs, double *Tq, hipStream_t s) {
+int fold_tot_blocks(int To) { return (To + kTotFrames - 1) / kTotFrames; }
+
+// part: R * nz * fold_tot_blocks(To) * V doubles
+hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
+                          double *part, double *Tq, hipStream_t s) {
+  if (V > 256) return hipErrorInvalidValue;
   int nb0, tb1;
   fold_slots(T, To, st, nb0, tb1);
-  const int L = To * V;
-  const bool a16 = (reinterpret_cast<uintptr_t>(dU) & 15) == 0;
-  const int vec = (L % 4 == 0 && a16) ? 4 : (L % 2 == 0 ? 2 : 1);
-  const dim3 grid(R, (L + 256 * vec - 1) / (256 * vec));
-  if (vec == 4)
-    hipLaunchKernelGGL(k_fold_colsum<4>, grid, dim3(256), 0, s, dU, N, R, L, cs);
-  else if (vec == 2)
-    hipLaunchKernelGGL(k_fold_colsum<2>, grid, dim3(256), 0, s, dU, N, R, L, cs);
-  else
-    hipLaunchKernelGGL(k_fold_colsum<1>, grid, dim3(256), 0, s, dU, N, R, L, cs);
-  if (V > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_fold_tq, dim3(R), dim3(256), 0, s, cs, R, V, T, To, st, nb0, tb1, Tq);
+  const int ntb = fold_tot_blocks(To);
+  hipLaunchKernelGGL(k_fold_tot, dim3(R, nz, ntb), dim3(256), 0, s, cs, R, V, To, part);
+  hipLaunchKernelGGL(k_fold_tq, dim3((R * V + 127) / 128), dim3(128), 0, s, cs, part, nz * ntb, nz,
+                     R, V, T, To, st, nb0, tb1, Tq);
   return hipGetLastError();
 }
 
@@ -280,13 +274,11 @@ __global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *d
 // gradient over C_in channels) and Tq:
 //   dWt[o][c][q] = sum_i dWc[o][i][q] W'[c][i] + sum_v Tq[q][o][v] bZ[c][v]
 //   dW'[c][i]    = sum_q sum_o Wt[o][c][q] dWc[o][i][q]
-//   SdZ[c][v]    = sum_q sum_o Wt[o][c][q] Tq[q][o][v]        (= sum_{n,t} dZ)
-// (the two tap sums as per-tap partial products in `part`, 9 R max(C, V)
+// (the tap sum of dW' as per-tap partial products in `part`, 9 R max(C, V)
 // doubles, summed in fixed order)
 hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
                              const float *bZ, const double *Tq, int R, int C, int V,
-                             double *dWc, double *part, float *dWt, float *dW, double *SdZ,
-                             hipStream_t s) {
+                             double *dWc, double *part, float *dWt, float *dW, hipStream_t s) {
   const int64_t n = (int64_t)R * C * 9;
   hipLaunchKernelGGL(k_slab_reduce_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slab,
                      S, n, dWc);
@@ -312,17 +304,22 @@ hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const fl
     hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
                        dW, nullptr);
   }
-  {
-    SmallGemm g{};
-    g.A = Wt; g.am = 9; g.ak = (int64_t)R * 9; g.a_z = 1;
-    g.B = Tq; g.b_dbl = 1; g.bk = V; g.bn = 1; g.b_z = (int64_t)R * V;
-    g.out = part; g.o_dbl = 1; g.om = V; g.on = 1; g.o_z = (int64_t)R * V;
-    g.M = R; g.N = V; g.K = R;
-    HIP_RET(small_gemm(g, 9, s));
-    const int64_t m = (int64_t)R * V;
-    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
-                       nullptr, SdZ);
-  }
+  return hipGetLastError();
+}
+
+// SdZ[c][v] = sum_q sum_o Wt[o][c][q] Tq[q][o][v]  (= sum_{n,t} dZ[c,t,v]; Wt is
+// the temporal weight [R][C][9] with C = its input channels, the Z channels)
+hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
+                           double *SdZ, hipStream_t s) {
+  SmallGemm g{};
+  g.A = Wt; g.am = 9; g.ak = (int64_t)C * 9; g.a_z = 1;
+  g.B = Tq; g.b_dbl = 1; g.bk = V; g.bn = 1; g.b_z = (int64_t)R * V;
+  g.out = part; g.o_dbl = 1; g.om = V; g.on = 1; g.o_z = (int64_t)C * V;
+  g.M = C; g.N = V; g.K = R;
+  HIP_RET(small_gemm(g, 9, s));
+  const int64_t m = (int64_t)C * V;
+  hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
+                     nullptr, SdZ);
   return hipGetLastError();
 }
 
