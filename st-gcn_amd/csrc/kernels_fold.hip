@@ -211,34 +211,39 @@ __global__ __launch_bounds__(256) void k_fold_tot(const double *cs, int R, int V
   part[(((int64_t)o * gridDim.y + z) * gridDim.z + tb) * V + tid] = tot;
 }
 
-__global__ void k_fold_tq(const double *cs, const double *part, int np, int nz, int R, int V, int T,
-                          int To, int st, int nb0, int tb1, double *Tq) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= R * V) return;
-  const int o = idx / V, v = idx - o * V;
-  const int64_t zs = (int64_t)R * To * V;
-  const double *c = cs + (int64_t)o * To * V + v;
-  double tot = 0.0;
-  for (int k = 0; k < np; ++k) tot += part[((int64_t)o * np + k) * V + v];
+// block = o; thread (phase ph, joint v): partial totals over the frame-block
+// partials k = ph, ph + PH, ..., and the boundary frame ph (< nsl) summed over
+// the clip chunks; LDS reduce; threads v < V form the nine taps
+__global__ __launch_bounds__(256) void k_fold_tq(const double *cs, const double *part, int np,
+                                                 int nz, int R, int V, int T, int To, int st,
+                                                 int nb0, int tb1, double *Tq) {
+  __shared__ double ts[256], bs[8 * 64];
+  const int o = blockIdx.x, tid = threadIdx.x;
+  const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
   const int nsl = nb0 + (To - tb1);
-  double bnd[8];  // the boundary frames, summed over the clip chunks
-#pragma unroll
-  for (int sl = 0; sl < 8; ++sl) {
-    bnd[sl] = 0.0;
-    if (sl < nsl) {
+  const int64_t zs = (int64_t)R * To * V;
+  double a = 0.0;
+  if (ph < PH) {
+    for (int k = ph; k < np; k += PH) a += part[((int64_t)o * np + k) * V + v];
+    for (int sl = ph; sl < nsl; sl += PH) {
       const int t = fold_slot_frame(sl, nb0, tb1);
-      for (int z = 0; z < nz; ++z) bnd[sl] += c[z * zs + (int64_t)t * V];
+      double b = 0.0;
+      for (int z = 0; z < nz; ++z) b += cs[z * zs + ((int64_t)o * To + t) * V + v];
+      bs[sl * V + v] = b;
     }
   }
-#pragma unroll
+  ts[tid] = a;
+  __syncthreads();
+  if (tid >= V) return;
+  double tot = 0.0;
+  for (int p = 0; p < PH; ++p) tot += ts[p * V + tid];
   for (int q = 0; q < 9; ++q) {
     double r = tot;
-#pragma unroll
-    for (int sl = 0; sl < 8; ++sl) {
+    for (int sl = 0; sl < nsl; ++sl) {
       const int tt = st * fold_slot_frame(sl, nb0, tb1) + q - 4;
-      if (sl < nsl && (tt < 0 || tt >= T)) r -= bnd[sl];
+      if (tt < 0 || tt >= T) r -= bs[sl * V + tid];
     }
-    Tq[((int64_t)q * R + o) * V + v] = r;
+    Tq[((int64_t)q * R + o) * V + tid] = r;
   }
 }
 
@@ -257,8 +262,9 @@ hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V,
   fold_slots(T, To, st, nb0, tb1);
   const int ntb = fold_tot_blocks(To);
   hipLaunchKernelGGL(k_fold_tot, dim3(R, nz, ntb), dim3(256), 0, s, cs, R, V, To, part);
-  hipLaunchKernelGGL(k_fold_tq, dim3((R * V + 127) / 128), dim3(128), 0, s, cs, part, nz * ntb, nz,
-                     R, V, T, To, st, nb0, tb1, Tq);
+  if (V > 64) return hipErrorInvalidValue;  // (bs: 8 slots x 64 joints)
+  hipLaunchKernelGGL(k_fold_tq, dim3(R), dim3(256), 0, s, cs, part, nz * ntb, nz, R, V, T, To, st,
+                     nb0, tb1, Tq);
   return hipGetLastError();
 }
 
