@@ -58,8 +58,8 @@
 #ifndef STGCN_AB_NO_FOLD        // the unfolded spatial GEMMs on the fp32 split path (capi.hip fold_w)
 #define STGCN_AB_NO_FOLD 0
 #endif
-#ifndef STGCN_AB_COLS_SUMS      // sum_{n,t} dZ from the dU column sums on non-folded blocks too
-#define STGCN_AB_COLS_SUMS 0
+#ifndef STGCN_AB_SUM_NT         // sum_{n,t} dZ by a pass over dZ on unfolded blocks
+#define STGCN_AB_SUM_NT 0
 #endif
 #ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
 #define STGCN_AB_BWD6_EXACT 0

@@ -116,13 +116,13 @@ bool fold_w(const stgcn_desc_t *d) {
   return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->V == 18 &&
          !fused_spb(d);
 }
-// sum_{n,t} dZ from per-tap sums of dU (clip-chunk sums written by the ReLU +
-// BN2 backward apply): the folded block (it has no dZ). Elsewhere the pass over
-// dZ measured faster (cfg3 5684 vs 5643 clips/s in one A/B call: the column
-// apply runs fewer, longer blocks); STGCN_AB_COLS_SUMS builds use the sums on
-// every non-residual block (A/B only).
+// sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
+// sums written by the ReLU + BN2 backward apply, k_fold_tq, one small GEMM with
+// Wt) instead of a pass over dZ (the folded block has no dZ at all): cfg3 5632
+// vs 5604, cfg5 2658 vs 2631 clips/s in one A/B call (STGCN_AB_SUM_NT build:
+// the pass over dZ on unfolded blocks, A/B only).
 bool cols_sums(const stgcn_desc_t *d) {
-  return !residual(d) && (fold_w(d) || STGCN_AB_COLS_SUMS != 0);
+  return !residual(d) && (fold_w(d) || STGCN_AB_SUM_NT == 0);
 }
 // The folded forward leaves Wc in the (otherwise unused) Z buffer for the
 // backward when it fits (Z is opaque to the caller under STGCN_F_F32X3 then)
