@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 5
+#define STGCN_ABI_VERSION 6
 
 /* stgcn_desc_t.flags */
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
@@ -227,6 +227,19 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
                       const float *A, const float *W, const float *bW, float *dx, float *dA,
                       float *dW, float *dbW, void *workspace, size_t workspace_bytes,
                       void *stream);
+
+/* ABI 6: the kernel plan the library selects for a descriptor (a bitmask of
+ * STGCN_PLAN_*), so a caller or a test can pin which path its calls take. */
+#define STGCN_PLAN_FOLD 1          /* K = 1 fp32 split path: the SpatialConv channel GEMM W'
+                                    * folded into the temporal conv's weights (Wc_q = Wt_q W');
+                                    * Z and dZ are never formed (capi.hip fold_w)         */
+#define STGCN_PLAN_SP_FWD_FUSED 2  /* SpatialConv forward in one kernel (k_sp_fwd_*)     */
+#define STGCN_PLAN_SP_BWD_FUSED 4  /* SpatialConv backward in one kernel (H never in HBM) */
+#define STGCN_PLAN_ACT_BF16 8      /* Z / dU stored in bf16 (bf16 path)                  */
+#define STGCN_PLAN_WSP_SPLIT 16    /* spatial dW' on exact split products (k_wgrad_sp X3) */
+#define STGCN_PLAN_TCONV_SPLIT 32  /* temporal conv forward on the split pipeline         */
+#define STGCN_PLAN_TWGRAD_SPLIT 64 /* temporal weight gradient on the split kernel        */
+int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan);
 
 /* Measurement (bench.py roofline): time one of the block's GEMM kernels,
  * launched `iters` times with the exact parameters the block uses for this

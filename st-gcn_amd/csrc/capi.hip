@@ -546,6 +546,34 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   return STGCN_OK;
 }
 
+int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan) {
+  int rc = stgcn_check_desc(d);
+  if (rc) return rc;
+  if (!plan) return fail(STGCN_E_INVALID, "null plan pointer");
+  uint32_t f = 0;
+  if (fold_w(d)) f |= STGCN_PLAN_FOLD;
+  if (fused_sp(d)) f |= STGCN_PLAN_SP_FWD_FUSED;
+  if (fused_spb(d)) f |= STGCN_PLAN_SP_BWD_FUSED;
+  if (act_bf16(d)) f |= STGCN_PLAN_ACT_BF16;
+  if (!fold_w(d) && !fused_sp(d)) {  // the spatial dW' GEMM of the unfolded block
+    WgradParams w = make_wgrad(d, nullptr, 0, d->C_out, d->T, nullptr, 0, d->K * d->C_in, d->T,
+                               1, 1, 0, nullptr);
+    if (w.bf16 == 3) f |= STGCN_PLAN_WSP_SPLIT;
+  }
+  if (f32x3(d)) {
+    ConvGemmParams p = conv_base(d, nullptr);  // the temporal conv forward (capi stgcn_block_fwd)
+    p.C = fold_w(d) ? d->C_in : d->C_out;
+    p.R = d->C_out;
+    p.NQ = 9;
+    p.s_in = d->stride;
+    if (conv_x3_supported(p)) f |= STGCN_PLAN_TCONV_SPLIT;
+    WgradParams w = make_wgrad_taps(d, nullptr, nullptr, nullptr, fold_w(d) ? d->C_in : 0);
+    if (w.bf16 == 3) f |= STGCN_PLAN_TWGRAD_SPLIT;
+  }
+  *plan = f;
+  return STGCN_OK;
+}
+
 size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d) {
   if (stgcn_check_desc(d) != STGCN_OK) return 0;
   return fwd_layout(d, nullptr).total;

@@ -75,6 +75,10 @@ struct ConvGemmParams {
   int in_bf16;       // in[] holds bf16 (same element strides; k_conv_x3 one-plane only)
   int out_bf16;      // out[] is written as bf16 (same element strides; the shared
                      // epilogues; no residual input)
+  // bf16 == 2 (fp32 GEMM as 2-way fp16 splits of power-of-two-scaled operands,
+  // k_conv_x3 NPL = 2): in[] is multiplied by in_scale before the split, the
+  // weights by w_scale, the accumulators by out_scale = 1 / (in_scale w_scale)
+  float in_scale, w_scale, out_scale;
 };
 
 // Weight-gradient GEMM with split-K partial slabs:

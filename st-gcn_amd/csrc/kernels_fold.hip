@@ -30,9 +30,10 @@ namespace stgcn {
 // out[z][m][n] = sum_{k < K} A[z][m][k] B[z][k][n] + sum_{k < K2} A2[z][m][k] B2[k][n]
 // (element offsets from the strides, z = blockIdx.z adds a_z / b_z / a2_z /
 // o_z). fp64 accumulation; operands and output float or double (run-time
-// flags). Block = 256 threads on a 64 x 64 tile, thread = 4 x 4 outputs; K in
-// chunks of 16 through LDS (A transposed, so both operands are read as
-// 2 x 16-byte vectors per k).
+// flags). Block = 256 threads (4 waves) on a 32 x 32 output tile, thread = 4 x 4
+// outputs; K in 64-deep chunks staged in LDS ([k][m] and [k][n]); wave w takes
+// k-steps w*16 .. w*16+15 of each chunk, and the four partial tiles are summed
+// in a fixed order through LDS at the end (deterministic).
 struct SmallGemm {
   const void *A, *B, *A2, *B2;
   void *out;
@@ -217,7 +218,7 @@ __global__ __launch_bounds__(256) void k_fold_tot(const double *cs, int R, int V
 __global__ __launch_bounds__(256) void k_fold_tq(const double *cs, const double *part, int np,
                                                  int nz, int R, int V, int T, int To, int st,
                                                  int nb0, int tb1, double *Tq) {
-  __shared__ double ts[256], bs[8 * 64];
+  __shared__ double ts[256], bs[8 * 256];  // (boundary slots x joints, V <= 256)
   const int o = blockIdx.x, tid = threadIdx.x;
   const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
   const int nsl = nb0 + (To - tb1);
@@ -257,12 +258,11 @@ int fold_tot_blocks(int To) { return (To + kTotFrames - 1) / kTotFrames; }
 // part: R * nz * fold_tot_blocks(To) * V doubles
 hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
                           double *part, double *Tq, hipStream_t s) {
-  if (V > 256) return hipErrorInvalidValue;
+  if (V > 256) return hipErrorInvalidValue;  // (checked before any launch)
   int nb0, tb1;
   fold_slots(T, To, st, nb0, tb1);
   const int ntb = fold_tot_blocks(To);
   hipLaunchKernelGGL(k_fold_tot, dim3(R, nz, ntb), dim3(256), 0, s, cs, R, V, To, part);
-  if (V > 64) return hipErrorInvalidValue;  // (bs: 8 slots x 64 joints)
   hipLaunchKernelGGL(k_fold_tq, dim3(R), dim3(256), 0, s, cs, part, nz * ntb, nz, R, V, T, To, st,
                      nb0, tb1, Tq);
   return hipGetLastError();

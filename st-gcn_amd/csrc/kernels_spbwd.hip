@@ -1334,9 +1334,10 @@ hipError_t launch_sp_bwd_fused(const float *dZ, const float *x, const float *mea
     Q.write_dx = write_dx && dx != nullptr;
     Q.relu = relu;
     if (prev) Q.prev = *prev;
-    // (a grid of 256 is a multiple of the channel-block count C / 32 <= 8: every
-    // item of a workgroup is in one block)
-    const int grid = (int)std::min<int64_t>(items, 256);
+    // (the grid is a multiple of the channel-block count ncb = C / 32, so every
+    // item of a workgroup -- first, first + grid, ... -- is in block first % ncb:
+    // 255 at ncb = 3 (C_in = 96); items is itself a multiple of ncb)
+    const int grid = (int)std::min<int64_t>(items, 256 / Q.ncb * Q.ncb);
     if (only != 2) hipLaunchKernelGGL((k_sp50_dx<3>), dim3(grid), dim3(512), G::LDS1, s, Q);
     if (only != 1) hipLaunchKernelGGL((k_sp50_dA<3>), dim3(grid), dim3(512), G::LDS2, s, Q);
     return hipGetLastError();

@@ -64,6 +64,20 @@ typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ floatx16 mfma_x(bf16x8_t a, bf16x8_t b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+// fp16 operands carried in the same 16-byte fragment registers (NPL = 2)
+__device__ __forceinline__ floatx16 mfma_h(bf16x8_t a, bf16x8_t b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a),
+                                                __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+}
+// the plane products of one MFMA: bf16 (NPL = 1, 3) or fp16 (NPL = 2)
+template <int NPL>
+__device__ __forceinline__ floatx16 mfma_p(bf16x8_t a, bf16x8_t b, floatx16 c) {
+  if constexpr (NPL == 2)
+    return mfma_h(a, b, c);
+  else
+    return mfma_x(a, b, c);
+}
 
 __host__ __device__ __forceinline__ unsigned pk2(float a, float b) {
   const bf16x2_t v = {(__bf16)a, (__bf16)b};
@@ -72,6 +86,23 @@ __host__ __device__ __forceinline__ unsigned pk2(float a, float b) {
 __device__ __forceinline__ float lo_f(unsigned w) { return __builtin_bit_cast(float, w << 16); }
 __device__ __forceinline__ float hi_f(unsigned w) {
   return __builtin_bit_cast(float, w & 0xffff0000u);
+}
+
+__host__ __device__ __forceinline__ unsigned pkh2(float a, float b) {
+  typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+  const h2_t v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float lo_h(unsigned w) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu));
+}
+__device__ __forceinline__ float hi_h(unsigned w) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16));
+}
+// 2-way fp16 split of two (scaled) floats: x = h + l to 2^-22 (RNE twice)
+__device__ __forceinline__ void splith2(float a, float b, unsigned &h, unsigned &l) {
+  h = pkh2(a, b);
+  l = pkh2(a - lo_h(h), b - hi_h(h));
 }
 
 // exact 3-way split of two floats into packed (h, m, l) bf16 pairs
@@ -259,6 +290,15 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
           h.w = pk2(st[k][6], st[k][7]);
         }
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
+      } else if (NPL == 2 && loff[k] >= 0) {  // fp16 (h, l) planes of the scaled input
+        const float sc = p.in_scale;
+        uint4 h, l;
+        splith2(st[k][0] * sc, st[k][1] * sc, h.x, l.x);
+        splith2(st[k][2] * sc, st[k][3] * sc, h.y, l.y);
+        splith2(st[k][4] * sc, st[k][5] * sc, h.z, l.z);
+        splith2(st[k][6] * sc, st[k][7] * sc, h.w, l.w);
+        *reinterpret_cast<uint4 *>(win + loff[k]) = h;
+        *reinterpret_cast<uint4 *>(win + loff[k] + 32) = l;
       } else if (loff[k] >= 0) {
         uint4 h, m, l;
         split2(st[k][0], st[k][1], h.x, m.x, l.x);
@@ -301,7 +341,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // Tile (row block rb, column tile j) -> acc[rb*2 + j] (MR = 1: acc[2..3] are
   // the hand-over registers of the stride-2 epilogue)
   // (NPL = 1: plain bf16 operands, acc only)
-  constexpr int NACL = NPL == 3 ? 2 * MR : 1;
+  constexpr int NACL = NPL >= 2 ? 2 * MR : 1;
   floatx16 acc[4], acl[NACL];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -331,19 +371,21 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   };
   // the six products (plane of A, plane of B) of one tap over the MR x 2 tiles
   // (NPL = 1: the one product)
+  // (NPL = 2: the three fp16 products hh, hl, lh)
   auto mm = [&](const Frag &f) {
     constexpr int PA[6] = {0, 0, 1, 0, 1, 2}, PB[6] = {0, 1, 0, 2, 1, 0};
+    constexpr int NPROD = NPL == 3 ? 6 : (NPL == 2 ? 3 : 1);
 #pragma unroll
-    for (int t = 0; t < (NPL == 3 ? 6 : 1); ++t)
+    for (int t = 0; t < NPROD; ++t)
 #pragma unroll
       for (int rb = 0; rb < MR; ++rb)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (t == 0)
-            acc[rb * 2 + j] = mfma_x(f.a[0][rb], f.b[0][j], acc[rb * 2 + j]);
+            acc[rb * 2 + j] = mfma_p<NPL>(f.a[0][rb], f.b[0][j], acc[rb * 2 + j]);
           else
-            acl[(rb * 2 + j) % NACL] =
-                mfma_x(f.a[PA[t] % NPL][rb], f.b[PB[t] % NPL][j], acl[(rb * 2 + j) % NACL]);
+            acl[(rb * 2 + j) % NACL] = mfma_p<NPL>(f.a[PA[t] % NPL][rb], f.b[PB[t] % NPL][j],
+                                                   acl[(rb * 2 + j) % NACL]);
         }
   };
 
@@ -378,7 +420,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
       if (!(STGCN_X3_EXP & 4) && g == 0) load_img(c + 1);
       if constexpr (MR == 1) {
         // per tap: NR fragment reads, NM MFMAs
-        constexpr int NR = NPL * (MR + 2), NM = (NPL == 3 ? 6 : 1) * 2 * MR;
+        constexpr int NR = NPL * (MR + 2), NM = (NPL == 3 ? 6 : (NPL == 2 ? 3 : 1)) * 2 * MR;
         constexpr int NI = NR < NM ? NR : NM;
 #pragma unroll
         for (int qq = 0; qq < TG; ++qq) {
@@ -410,9 +452,9 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
               if (pa == 0 && pb == 0)
-                acc[rb * 2 + j] = mfma_x(fr.a[0][rb], fr.b[0][j], acc[rb * 2 + j]);
+                acc[rb * 2 + j] = mfma_p<NPL>(fr.a[0][rb], fr.b[0][j], acc[rb * 2 + j]);
               else
-                acl[rb * 2 + j] = mfma_x(fr.a[pa][rb], fr.b[pb][j], acl[rb * 2 + j]);
+                acl[rb * 2 + j] = mfma_p<NPL>(fr.a[pa % NPL][rb], fr.b[pb % NPL][j], acl[rb * 2 + j]);
             }
         };
         auto lda = [&](int qq, int pl) {
@@ -431,26 +473,42 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         for (int qq = 0; qq < TG; ++qq) {
           const bool nx = qq + 1 < TG;
           const int q1 = g * TG + qq + 1;
-          grp(1, 1);
-          __builtin_amdgcn_sched_barrier(0);
-          grp(2, 0);
-          if (nx) lda(qq + 1, 2);
-          __builtin_amdgcn_sched_barrier(0);
-          grp(0, 2);
-          if (nx) ldb(q1, 2);
-          __builtin_amdgcn_sched_barrier(0);
-          grp(1, 0);
-          if (nx) lda(qq + 1, 1);
-          __builtin_amdgcn_sched_barrier(0);
-          grp(0, 1);
-          if (nx) ldb(q1, 1);
-          __builtin_amdgcn_sched_barrier(0);
-          grp(0, 0);
-          if (nx) {
-            lda(qq + 1, 0);
-            ldb(q1, 0);
+          if constexpr (NPL == 2) {
+            // fp16 (h, l): products lh, hl, hh; plane 1 of A / B refilled as it retires
+            grp(1, 0);
+            if (nx) lda(qq + 1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(0, 1);
+            if (nx) ldb(q1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(0, 0);
+            if (nx) {
+              lda(qq + 1, 0);
+              ldb(q1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          } else {
+            grp(1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(2, 0);
+            if (nx) lda(qq + 1, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(0, 2);
+            if (nx) ldb(q1, 2);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(1, 0);
+            if (nx) lda(qq + 1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(0, 1);
+            if (nx) ldb(q1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            grp(0, 0);
+            if (nx) {
+              lda(qq + 1, 0);
+              ldb(q1, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
           }
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
       if (!(STGCN_X3_EXP & 1) && g == G::NG - 1) {
@@ -465,6 +523,10 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   if constexpr (NPL == 3) {
 #pragma unroll
     for (int j = 0; j < 2 * MR; ++j) acc[j] += acl[j];
+  } else if constexpr (NPL == 2) {  // undo the operand scales (powers of two: exact)
+    const float os = p.out_scale;
+#pragma unroll
+    for (int j = 0; j < 2 * MR; ++j) acc[j] = (acc[j] + acl[j]) * os;
   }
   if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
     if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
@@ -515,7 +577,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 // one contiguous run.
 __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int NQ, int TG,
                                  int nch, int rows, int npl, int64_t w_sr, int64_t w_sc,
-                                 int64_t w_sq, int64_t total) {
+                                 int64_t w_sq, int64_t total, float wscale) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int jj = (int)(idx & 7);
@@ -536,6 +598,13 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
   const int r = rt * rows + rl, c = ch * 16 + o * 8 + jj, q = g * TG + qq;
   float v = 0.f;
   if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
+  if (npl == 2) {  // fp16 (h, l) of the scaled weight
+    const float vs = v * wscale;
+    const _Float16 h = (_Float16)vs;
+    const _Float16 l = (_Float16)(vs - (float)h);
+    reinterpret_cast<_Float16 *>(wpk)[idx] = pl == 0 ? h : l;
+    return;
+  }
   const __bf16 h = (__bf16)v;
   const float r1 = v - (float)h;
   const __bf16 m = (__bf16)r1;
@@ -599,7 +668,7 @@ static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
 // npl = 3: fp32 as exact 3-way splits (STGCN_F_F32X3); npl = 1: bf16 operands
 // (STGCN_F_BF16), the same pipeline with one plane and two workgroups per CU
 static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStream_t s) {
-  const bool wide = npl == 3 && x3_wide_rows(p0);
+  const bool wide = npl >= 2 && x3_wide_rows(p0);
   ConvGemmParams p = p0;
   const int rows = wide ? 128 : 64;
   p.n_rtiles = (p.R + rows - 1) / rows;
@@ -608,12 +677,20 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
     const int64_t total = (int64_t)p.n_rtiles * nch * npl * p.NQ * 2 * rows * 8;
     hipLaunchKernelGGL(k_pack_conv_w_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, x3_tg(p.NQ), nch,
-                       rows, npl, p.w_sr, p.w_sc, p.w_sq, total);
+                       rows, npl, p.w_sr, p.w_sc, p.w_sq, total, p.w_scale);
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   bool done = false;
-  if (wide) {
+  if (wide && npl == 2) {
+    done = launch_cx_v<9, 2, 2>(p, nblk, s);
+  } else if (wide) {
     done = launch_cx_v<9, 2, 3>(p, nblk, s);
+  } else if (npl == 2) {
+    switch (p.NQ) {
+      case 4: done = launch_cx_v<4, 1, 2>(p, nblk, s); break;
+      case 5: done = launch_cx_v<5, 1, 2>(p, nblk, s); break;
+      case 9: done = launch_cx_v<9, 1, 2>(p, nblk, s); break;
+    }
   } else if (npl == 3) {
     switch (p.NQ) {
       case 4: done = launch_cx_v<4, 1, 3>(p, nblk, s); break;
@@ -632,6 +709,11 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
 
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
   if (!conv_x3_supported(p) || !p.wpk) return hipErrorInvalidValue;
+  if (STGCN_AB_F16X2) {  // timing experiment: fp16 2-way splits, unit scales
+    ConvGemmParams q = p;
+    q.in_scale = q.w_scale = q.out_scale = 1.f;
+    return launch_conv_planes(q, 2, s);
+  }
   return launch_conv_planes(p, 3, s);
 }
 

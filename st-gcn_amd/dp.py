@@ -75,8 +75,12 @@ class GradAllReduce:
         bi = self._bucket_of[p]
 
         def check(grad):
-            # runs before autograd accumulates into p.grad (the bucket view)
-            if self._work[bi] is not None:
+            # runs before autograd accumulates into p.grad (the bucket view); a
+            # second arrival of p's gradient before synchronize() -- also in a
+            # bucket whose all-reduce never launched because one of its
+            # parameters is unused -- would add into a buffer that is (or will
+            # be) reduced for the first backward only
+            if self._sync and (self._work[bi] is not None or p in self._seen):
                 raise RuntimeError(
                     "GradAllReduce: a second backward before synchronize() would accumulate "
                     "into a bucket whose all-reduce is in flight; run the earlier "
@@ -104,6 +108,7 @@ class GradAllReduce:
     def _reset(self):
         self._pending = [len(ps) for ps in self.buckets]
         self._work = [None] * len(self.buckets)
+        self._seen = set()  # parameters whose gradient arrived since synchronize()
 
     def zero_grad(self):
         """Zero every bucket (one fill per flat buffer) and keep the views."""
@@ -118,6 +123,7 @@ class GradAllReduce:
             p.grad = v
         if not self._sync:
             return
+        self._seen.add(p)
         bi = self._bucket_of[p]
         self._pending[bi] -= 1
         if self._pending[bi] == 0:

@@ -82,9 +82,18 @@ class ChainCtx:
         self.U, self.stats2 = None, None
 
 
-def _chain_bwd_args(cc, dy, need_dx, C_in, dev):
+def _observed(xref):
+    """True when the block input's gradient is observed by the caller: a tensor
+    hook or ``retain_grad()`` on it. Deferred dx would hand such an observer the
+    BN1-side dxhat instead of dL/dx, so those blocks form dx in full."""
+    x = xref() if xref is not None else None
+    return x is not None and (x.retains_grad or bool(getattr(x, "_backward_hooks", None)))
+
+
+def _chain_bwd_args(cc, dy, need_dx, C_in, dev, xref=None):
     """(dy_sums, dy_coef, prev_g2, prev_b2, prev_sums, prev_U, prev_stats, x_stats,
-    dx_coef) for stgcn_block_bwd."""
+    dx_coef) for stgcn_block_bwd. xref: weak reference to the block input; no
+    deferred dx (dx_coef None) when its gradient is observed (``_observed``)."""
     none = (None,) * 9
     if cc is None:
         return none
@@ -99,7 +108,8 @@ def _chain_bwd_args(cc, dy, need_dx, C_in, dev):
                 "modified in backward (a hook?); the deferred-dx chain cannot form it")
     if cc.in_link is not None and need_dx:
         prev_sums = torch.empty(2 * C_in, device=dev, dtype=torch.float64)
-        dx_coef = torch.empty(5 * C_in, device=dev, dtype=torch.float32)
+        dx_coef = (None if _observed(xref)
+                   else torch.empty(5 * C_in, device=dev, dtype=torch.float32))
         return (dy_sums, dy_coef, cc.prev_g2, cc.prev_b2, prev_sums, cc.prev_U, cc.prev_stats,
                 cc.x_stats, dx_coef)
     return (dy_sums, dy_coef) + (None,) * 7
@@ -154,6 +164,8 @@ class StgcnBlockFn(torch.autograd.Function):
     def forward(ctx, x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
                 stride, pad, eps, momentum, training, cc=None, drop=0.0, gemm="fp32"):
         lib = hip_lib.lib()
+        # (the caller's input tensor: a hook / retain_grad() on it turns deferred dx off)
+        ctx.xref = weakref.ref(x) if cc is not None else None
         x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
                  "rm1", "rv1", "rm2", "rv2")
@@ -200,7 +212,7 @@ class StgcnBlockFn(torch.autograd.Function):
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
                          need_dx=need_dx, **_gemm_flags(ctx.gemm))
         dy_sums, dy_coef, pg2, pb2, psums, pU, pst, xst, dx_coef = _chain_bwd_args(
-            ctx.cc, dy, need_dx, x.shape[1], x.device)
+            ctx.cc, dy, need_dx, x.shape[1], x.device, ctx.xref)
         deferred = ctypes.c_int32(0)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]

@@ -21,10 +21,13 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
     import sys
     print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
-ABI_VERSION = 5
+ABI_VERSION = 6
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
+# stgcn_block_plan bits (ABI 6)
+PLAN_FOLD, PLAN_SP_FWD_FUSED, PLAN_SP_BWD_FUSED, PLAN_ACT_BF16 = 1, 2, 4, 8
+PLAN_WSP_SPLIT, PLAN_TCONV_SPLIT, PLAN_TWGRAD_SPLIT = 16, 32, 64
 
 _c_int = ctypes.c_int32
 _c_float = ctypes.c_float
@@ -82,7 +85,8 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_block_fwd", "stgcn_block_bwd", "stgcn_time_kernel_bytes",
             "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
             "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
-            "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes")
+            "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes",
+            "stgcn_block_plan")
 
 _LIB = None
 
@@ -134,6 +138,8 @@ def load_library(path=LIB_PATH):
     lib.stgcn_spatial_bwd.argtypes = [ctypes.POINTER(SpatialDesc)] + [_vp] * 10 + \
         [ctypes.c_size_t, _vp]
     lib.stgcn_spatial_bwd.restype = ctypes.c_int
+    lib.stgcn_block_plan.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(ctypes.c_uint32)]
+    lib.stgcn_block_plan.restype = ctypes.c_int
     if lib.stgcn_abi_version() != ABI_VERSION:
         raise RuntimeError("libstgcn_hip.so ABI version mismatch; rebuild it")
     return lib
@@ -154,6 +160,16 @@ def check(rc):
     if rc != 0:
         msg = lib().stgcn_last_error().decode(errors="replace")
         raise RuntimeError(f"libstgcn_hip error {rc}: {msg}")
+
+
+def block_plan(desc):
+    """stgcn_block_plan: the PLAN_* bitmask the library selects for a descriptor
+    (needs no GPU)."""
+    plan = ctypes.c_uint32(0)
+    rc = load_library().stgcn_block_plan(ctypes.byref(desc), ctypes.byref(plan))
+    if rc != 0:
+        raise RuntimeError(f"stgcn_block_plan failed ({rc})")
+    return plan.value
 
 
 def ptr(t):

@@ -22,7 +22,16 @@ class STGCNStack(nn.Module):
     before the blocks (same RNG consumption), registered as ``Masks.{i}``
     (state_dict interchange), each block built on A * Masks[i]. As in the
     reference the masks only scale the blocks' initial A (each block's
-    ``spatialConv.A`` is its own leaf parameter), so they receive no gradient."""
+    ``spatialConv.A`` is its own leaf parameter), so they receive no gradient.
+
+    Intermediate block outputs: in training the chained backward (deferred dx,
+    fused.Link) hands block i the BN1-side gradient of block i+1 and forms the
+    true gradient of block i's output inside block i's kernels, so that gradient
+    is never materialised. A tensor hook or ``retain_grad()`` on a block output
+    turns the deferral off for that link (the true gradient is formed and seen);
+    ``torch.autograd.grad(loss, block_output)`` cannot be detected from inside
+    the block and is not supported in a chained training step (run the blocks
+    unchained, e.g. one by one, for that)."""
 
     def __init__(self, C_in, nr_classes, A, gamma=9, dropout_rate=0, residual=False,
                  gemm_dtype=torch.float32, f32_gemm="mfma", use_edge_importance=False,

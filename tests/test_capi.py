@@ -29,7 +29,7 @@ def test_header_declares_entry_points(pkg):
 def test_library_exports_every_header_symbol(pkg, lib):
     for name in _header_functions():
         assert hasattr(lib, name), name
-    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 5
+    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 6
 
 
 def _desc(pkg, **kw):
@@ -108,3 +108,26 @@ def test_spatial_desc_workspace_and_rejects(pkg, lib):
     assert lib.stgcn_spatial_fwd(ctypes.byref(d), None, None, None, None, None, None, 0,
                                  None) == -1
     assert b"null" in lib.stgcn_last_error()
+
+
+def test_block_plan_pins_the_paths(pkg, lib):
+    """ABI 6 stgcn_block_plan (host logic, no GPU): the fp32 split path folds W'
+    into the temporal conv on the cfg2 non-residual blocks with C_in >= 16
+    (STGCN_PLAN_FOLD) and keeps the unfolded spatial dW' on split products where
+    it does not fold (residual blocks); the bf16 path fuses both SpatialConv
+    halves at V = 25, K = 3; the exact fp32-MFMA path selects none of these."""
+    hl = pkg.hip_lib
+    plan = lambda **kw: hl.block_plan(_desc(pkg, **kw))  # noqa: E731
+    p = plan(flags=4)  # cfg2 L1-type block (64 -> 64)
+    assert p & hl.PLAN_FOLD and p & hl.PLAN_TCONV_SPLIT and p & hl.PLAN_TWGRAD_SPLIT, p
+    assert plan(flags=4, C_in=128, C_out=256, stride=2, T=150, T_out=75) & hl.PLAN_FOLD
+    assert not plan(flags=4, C_in=3) & hl.PLAN_FOLD          # C_in < 16
+    p = plan(flags=5)                                        # residual: never folded
+    assert not p & hl.PLAN_FOLD and p & hl.PLAN_WSP_SPLIT, p
+    assert not plan(flags=4, V=25, K=3) & hl.PLAN_FOLD       # K = 3
+    p = plan(flags=2, V=25, K=3)
+    assert p & hl.PLAN_SP_FWD_FUSED and p & hl.PLAN_SP_BWD_FUSED and not p & hl.PLAN_FOLD, p
+    assert plan() == 0
+    d = _desc(pkg, N=0)
+    out = ctypes.c_uint32(7)
+    assert lib.stgcn_block_plan(ctypes.byref(d), ctypes.byref(out)) == -1

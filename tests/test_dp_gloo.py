@@ -176,3 +176,70 @@ def test_dp_accumulation_and_double_backward_guard():
     for rank, err, raised in res:
         assert err < 1e-6, (rank, err)
         assert raised, rank
+
+
+class _WithUnused(nn.Module):
+    """Two used parameters and one the forward never touches (so its bucket's
+    all-reduce is not launched by backward: only synchronize() launches it)."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Parameter(torch.linspace(-1.0, 1.0, 6))
+        self.unused = nn.Parameter(torch.ones(2))
+        self.b = nn.Parameter(torch.linspace(0.5, 1.5, 6))
+
+    def forward(self, x):
+        return (x * self.a).tanh() * self.b
+
+
+def _unused_worker(rank, world, port, out_q):
+    """a second backward before synchronize() raises even when
+    the bucket's all-reduce never launched (an unused parameter keeps it
+    pending), instead of adding into the buffer."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from stgcn_loader import load
+        pkg = load()
+        model = _WithUnused()
+        x = torch.randn(world, 4, 6, generator=torch.Generator().manual_seed(3))
+        dp = pkg.dp.GradAllReduce(model, world)  # one bucket (a, unused, b)
+        assert len(dp.buckets) == 1
+        model(x[rank]).square().sum().backward()
+        raised = False
+        try:
+            model(x[rank]).square().sum().backward()
+        except RuntimeError as e:
+            raised = "no_sync" in str(e)
+        dp.synchronize()
+        want = []
+        for r in range(world):
+            ref = _WithUnused()
+            ref(x[r]).square().sum().backward()
+            want.append([ref.a.grad, ref.b.grad])
+        err = max((model.a.grad - (want[0][0] + want[1][0]) / world).abs().max().item(),
+                  (model.b.grad - (want[0][1] + want[1][1]) / world).abs().max().item(),
+                  model.unused.grad.abs().max().item())
+        out_q.put((rank, err, raised))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_second_backward_guard_with_unused_parameter():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unused_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, raised in res:
+        assert raised, rank
+        assert err < 1e-6, (rank, err)

@@ -198,6 +198,15 @@ def test_bf16_cfg5_full_size_block(pkg):
     print({k: float(np.format_float_scientific(v, 2)) for k, v in errs.items()})
 
 
+def test_bf16_v50_three_channel_blocks(pkg):
+    """V = 50 fused spatial backward (k_sp50_dx / _dA) at C_in = 96: three
+    32-channel blocks, more items than the 256-workgroup grid, so each
+    workgroup's strided items must stay in one channel block (the grid is a
+    multiple of 3 there)."""
+    errs = _check_bf16(pkg, (96, 96, 1, 50, 3, 4, 300), seed=17)
+    print({k: float(np.format_float_scientific(v, 2)) for k, v in errs.items()})
+
+
 def test_bf16_cfg5_stride2_full_size_block(pkg):
     """cfg5 L4 shape (V = 50, K = 3, 64 -> 128 channels, stride 2) at T = 300,
     N = 4: bf16 Z / dU storage on a stride-2 block, read by the strided

@@ -116,15 +116,16 @@ def _oracle(arrays, got):
     return want, floor
 
 
-def _random_case(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=False):
-    return _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed, residual)
+def _random_case(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=False, A=None):
+    return _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed, residual, A)
 
 
-def _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=False):
+def _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=False, A=None):
     gr = pkg.graph
     strat = 0 if K == 1 else 2
-    A = gr.get_normalized_adjacency_matrices(strat, 1, distances=gr.synthetic_distances(V),
-                                             graph=gr.graph_for(V))
+    if A is None:
+        A = gr.get_normalized_adjacency_matrices(strat, 1, distances=gr.synthetic_distances(V),
+                                                 graph=gr.graph_for(V))
     torch.manual_seed(seed)
     blk = pkg.SpatialTemporalConv(C_in, C_out, A, 9, stride, 4, dropout_rate=0,
                                   residual=residual)
@@ -160,6 +161,18 @@ def _random_case_once(pkg, C_in, C_out, stride, V, K, N, T, seed=0, residual=Fal
 def test_block_matches_oracle_random(pkg, case):
     C_in, C_out, stride, V, K, N, T = case
     arrays, x, g = _random_case(pkg, C_in, C_out, stride, V, K, N, T)
+    got = _run_hip(pkg, arrays, x, g)
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, floor=floor)
+
+
+@pytest.mark.parametrize("V", [70, 90])
+def test_block_k1_many_joints(pkg, V):
+    """One adjacency partition over more joints than the reference's graphs (a
+    random dense A, V = 70 / 90 <= the descriptor limit K V^2 <= 8192): the
+    backward's per-tap dU sums (k_fold_tq) hold V > 64 joints."""
+    A = np.random.default_rng(5).uniform(0.0, 2.0 / V, size=(1, V, V)).astype(np.float32)
+    arrays, x, g = _random_case(pkg, 16, 32, 1, V, 1, 2, 11, A=A)
     got = _run_hip(pkg, arrays, x, g)
     want, floor = _oracle(arrays, got)
     _compare(got, want, floor=floor)

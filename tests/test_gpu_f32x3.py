@@ -27,6 +27,36 @@ def _check(pkg, arrays, x, g, residual=False, need_dx=True):
     return got
 
 
+def _assert_fold_ran(pkg, arrays, x):
+    """The folded forward writes the composite weights Wc[o][i][q] = sum_c
+    Wt[o][c][q] W'[c][i] into the Z buffer it saves for the backward (capi.hip
+    fold_wc_in_z): the first C_out * C_in * 9 floats of the saved Z must be
+    Wc (fp64 GEMM rounded once to fp32)."""
+    from oracle import ref_cpu
+    p, b = ref_cpu.block_params_from_arrays(arrays, dtype=torch.float32, requires_grad=False)
+    stride = int(arrays["meta"][2])
+    dev = "cuda:0"
+    cu = {k: v.to(dev).contiguous() for k, v in p.items()}
+    bu = {k: v.to(dev).clone() for k, v in b.items() if "num_batches" not in k}
+    xd = x.to(dev).float().contiguous().requires_grad_(True)
+    Wt = cu["temporalConv.weight"].requires_grad_(True)
+    y = pkg.fused.StgcnBlockFn.apply(
+        xd, cu["spatialConv.A"], cu["spatialConv.W.weight"], cu["spatialConv.W.bias"], Wt,
+        cu["temporalConv.bias"], cu["batch_n.weight"], cu["batch_n.bias"],
+        cu["batch_n_2.weight"], cu["batch_n_2.bias"], bu["batch_n.running_mean"],
+        bu["batch_n.running_var"], bu["batch_n_2.running_mean"], bu["batch_n_2.running_var"],
+        stride, 4, 1e-5, 0.1, True, None, 0.0, "f32x3")
+    Z = y.grad_fn.saved_tensors[1]
+    C_out, C_in = Wt.shape[0], xd.shape[1]
+    if Z.numel() < C_out * C_in * 9:
+        return  # (Wc does not fit there: the library keeps it in its workspace)
+    wc = torch.einsum("ocq,ci->oiq", p["temporalConv.weight"].double().reshape(C_out, C_out, 9),
+                      p["spatialConv.W.weight"].double().reshape(C_out, C_in))
+    got = Z.reshape(-1)[:C_out * C_in * 9].double().cpu().reshape(C_out, C_in, 9)
+    assert (got - wc).abs().max().item() <= 1e-6 * wc.abs().max().item(), \
+        "the folded forward did not run (Z does not hold Wc)"
+
+
 @pytest.mark.parametrize("fixture", [f for f in block_fixtures()])
 def test_f32x3_block_fixture(pkg, fixture):
     ref = load_npz(fixture)
@@ -62,9 +92,19 @@ def test_f32x3_block_random(pkg, case):
         if V == 18:  # k_wgrad_x3 (temporal weight gradient, stride 1 and 2)
             k = "grad.temporalConv.weight"
             assert not torch.equal(got[k], ref[k]), "k_wgrad_x3 did not run"
-        # spatial dW' = dZ G^T on the split products (k_wgrad_sp<.., X3>)
-        k = "grad.spatialConv.W.weight"
-        assert not torch.equal(got[k], ref[k]), "k_wgrad_sp X3 did not run"
+        plan = pkg.hip_lib.block_plan(pkg.fused.make_desc(
+            tuple(x.shape), C_out, shape[4], stride, 4, 1e-5, 0.1, True,
+            residual=residual, f32x3=True))
+        if V == 18 and shape[4] == 1 and not residual and C_in >= 16:
+            # the folded block (W' inside the temporal conv's weights): the plan
+            # says so, and the forward left Wc = Wt W' in the (opaque) Z buffer
+            assert plan & pkg.hip_lib.PLAN_FOLD, plan
+            _assert_fold_ran(pkg, arrays, x)
+        else:
+            # spatial dW' = dZ G^T on the split products (k_wgrad_sp<.., X3>)
+            assert not plan & pkg.hip_lib.PLAN_FOLD and plan & pkg.hip_lib.PLAN_WSP_SPLIT, plan
+            k = "grad.spatialConv.W.weight"
+            assert not torch.equal(got[k], ref[k]), "k_wgrad_sp X3 did not run"
     if residual and (C_in != C_out or stride != 1):
         # the strided projection's dWr / dbr: present in both
         # runs, so _check held them to the fp32 gate above

@@ -345,23 +345,59 @@ def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
     gate_chained_vs_oracle(m1, p0, b0, x, lab, masks, gemm)
 
 
-def test_stack_deferred_dx_guard(pkg):
-    """A gradient hook that replaces the tensor between two chained blocks
-    (where dx holds dxhat) makes the earlier block raise, not compute garbage."""
+@pytest.mark.parametrize("observe", ["hook", "retain_grad", "replace"])
+def test_stack_observed_intermediate_gradient(pkg, monkeypatch, observe):
+    """A hook or retain_grad() on a block output between two chained blocks
+    turns the deferred dx off for that link: the observer sees the true
+    gradient of that output (equal to an unchained run's), a hook that
+    replaces the tensor is honoured, and the other eight links still defer."""
     gr = pkg.graph
     A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    deferred = []
+    orig = pkg.fused._chain_publish
+
+    def spy(cc, prev_sums, dx, dx_coef=None):
+        if prev_sums is not None:
+            deferred.append(dx_coef is not None)
+        return orig(cc, prev_sums, dx, dx_coef)
+
+    monkeypatch.setattr(pkg.fused, "_chain_publish", spy)
     torch.manual_seed(5)
     with contextlib.redirect_stdout(io.StringIO()):
-        m = pkg.STGCNStack(3, 10, A).cuda().train()
+        m1 = pkg.STGCNStack(3, 10, A).cuda().train()
+        m2 = pkg.STGCNStack(3, 10, A).cuda().train()
+    m2.load_state_dict(m1.state_dict())
     x = torch.randn(2, 3, 20, 18, generator=torch.Generator().manual_seed(6)).cuda()
-    chain = pkg.network.StackChain()
-    h = x
-    for i, blk in enumerate(m.conv):
-        h = blk(h, chain=chain)
-        if i == 4:
-            h.register_hook(lambda g: g * 1.0)     # a new tensor replaces the chain's dx
-    with pytest.raises(RuntimeError, match="deferred-dx"):
+    seen = []
+
+    def run(m, chained):
+        chain = pkg.network.StackChain() if chained else None
+        h, mid = x, None
+        for i, blk in enumerate(m.conv):
+            h = blk(h, chain=chain) if chained else blk(h)
+            if i == 4:
+                mid = h
+                if observe == "retain_grad":
+                    h.retain_grad()
+                elif observe == "hook":
+                    h.register_hook(lambda g: seen.append(g.detach().clone()))
+                else:
+                    h.register_hook(lambda g: g * 2.0)  # a new tensor replaces the gradient
         h.sum().backward()
+        torch.cuda.synchronize()
+        return mid
+
+    mid1 = run(m1, True)
+    n_chained = len(deferred)
+    mid2 = run(m2, False)
+    assert deferred[:n_chained].count(False) == 1 and deferred[:n_chained].count(True) == 8
+    if observe == "retain_grad":
+        assert rel_to_max(mid1.grad.cpu().numpy(), mid2.grad.cpu().numpy()) < 1e-4
+    elif observe == "hook":
+        assert len(seen) == 2
+        assert rel_to_max(seen[0].cpu().numpy(), seen[1].cpu().numpy()) < 1e-4
+    for (k, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert rel_to_max(a.grad.cpu().numpy(), b.grad.cpu().numpy()) < 2e-2, k
 
 
 def test_stack_bf16_cfg3_shape(pkg):
