@@ -47,6 +47,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 dense (no sparsity)
 # fp32 work on the bf16 matrix cores by exact 3-way operand splits: six bf16
 # MFMAs per fp32 product (kernels_x3.hip), so the fp32-work ceiling is 1/6 of BF16
 X3_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6
+# ... and by 2-way fp16 splits (STGCN_F_F16X2): three fp16 MFMAs (fp16 runs at the
+# bf16 rate) per fp32 product
+F16X2_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
 
 
@@ -87,6 +90,24 @@ def cpu_model():
         pass
     import platform
     return platform.processor() or "unknown"
+
+
+def cgroup_cpu_quota():
+    """The process's cgroup CPU bandwidth limit as (CPUs, raw text), or
+    (None, reason): cgroup v2 /sys/fs/cgroup/cpu.max ("quota period" or
+    "max period"), else v1 cpu.cfs_quota_us / cpu.cfs_period_us."""
+    try:
+        raw = open("/sys/fs/cgroup/cpu.max").read().strip()
+        q, per = raw.split()[:2]
+        return (None if q == "max" else round(int(q) / int(per), 2)), f"cpu.max: {raw}"
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return (None if q <= 0 else round(q / per, 2)), f"cfs_quota_us {q} / period {per}"
+    except (OSError, ValueError):
+        return None, "no cgroup CPU limit readable"
 
 
 def cpu_baseline(cfg, seconds=8.0):
@@ -145,9 +166,18 @@ def cpu_baseline(cfg, seconds=8.0):
     done.set()
     torch.set_num_threads(prev)
     best = max(res)
+    quota, quota_raw = cgroup_cpu_quota()
+    why = None
+    if len(res) > 1 and res[0][0] > 4 * res[-1][0]:
+        why = (f"{res[-1][1]} threads ran {res[0][0] / res[-1][0]:.0f}x slower than {res[0][1]}: "
+               + (f"the process's cgroup limits it to {quota} CPUs ({quota_raw}), so "
+                  f"{res[-1][1]} busy-waiting torch threads are throttled"
+                  if quota is not None and quota < res[-1][1] else
+                  f"oversubscription beyond the process's CPU share ({quota_raw})"))
     return {"value": round(best[0], 3), "unit": "clips/s", "cores": best[1],
             "kind": "port", "cpu_model": cpu_model(), "os_cpu_count": ncpu,
-            "affinity_cpus": share,
+            "affinity_cpus": share, "cgroup_cpu_quota": quota, "cgroup_cpu_limit": quota_raw,
+            "slow_leg_explained": why,
             "per_thread_count": {str(t): round(v, 3) for v, t, _, _ in res},
             "sample": f"oracle/ref_cpu.py fp32 stack fwd+bwd+loss, N={n} clips x {best[2]} iters "
                       f"(T={cfg['T']}, V={cfg['V']}, K={cfg['K']}, {cfg['classes']} classes), "
@@ -201,9 +231,10 @@ def kernel_roofline(pkg, device, cfg, iters=10):
     V4 = cfg["V"] * 4
     for li, (ci, co, t, s) in enumerate(stack_layers(cfg)):
         progress(f"kernel timing: layer {li}")
-        x3 = cfg.get("f32_gemm") == "bf16x3" and not cfg["bf16"]
+        x3 = cfg.get("f32_gemm") in ("bf16x3", "f16x2") and not cfg["bf16"]
+        f16 = cfg.get("f32_gemm") == "f16x2" and not cfg["bf16"]
         d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
-                                bf16=cfg["bf16"], f32x3=x3)
+                                bf16=cfg["bf16"], f32x3=x3 and not f16, f16x2=f16)
         for which in range(7):
             nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
             if nbytes == 0:  # 5 / 6 where the spatial backward is one fused kernel
@@ -285,10 +316,11 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                        }[which]
             elif x3 and V in (18, 25):
                 mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
-                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},3,false>",
-                       1: (f"k_conv_x3<9,3,{V},1,{mr},3,false>" if s == 1 else
-                           f"k_conv_x3<5|4,{V},1,1,3,false>"),
-                       2: f"k_wgrad_x3<{V},{s}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
+                npl = 2 if f16 and fold else 3  # operand planes: fp16 (h, l) or bf16 (h, m, l)
+                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false>",
+                       1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,{npl},false>"),
+                       2: f"k_wgrad_x3<{V},{s},{npl}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
@@ -369,13 +401,16 @@ def main():
                     help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3"], default="bf16x3",
+    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3", "f16x2"], default="bf16x3",
                     help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma) or "
                          "as exact 3-way bf16 operand splits (bf16x3; fp32 accuracy)")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip timing the exact fp32-MFMA path beside the bf16x3 default")
     ap.add_argument("--no-repeats", dest="repeats", action="store_false",
                     help="skip the two extra timed windows (median of three)")
+    ap.add_argument("--no-sweep", dest="sweep", action="store_false",
+                    help="skip the per-GPU batch sweep (SURVEY.md §8(d): N in 32, 64, 256 "
+                         "besides the bench batch; N=1 process only)")
     ap.add_argument("--torch-ops", action="store_true",
                     help="head + cross entropy + Adam from torch instead of the HIP library")
     args = ap.parse_args()
@@ -471,7 +506,7 @@ def main():
     # the exact fp32-MFMA path (every GEMM on v_mfma_f32_32x32x2_f32) timed
     # beside the default bf16x3 path, same model and inputs (N=1 only)
     alt = None
-    if world == 1 and not cfg["bf16"] and cfg["f32_gemm"] == "bf16x3" and not args.no_alt:
+    if world == 1 and not cfg["bf16"] and cfg["f32_gemm"] != "mfma" and not args.no_alt:
         for blk in model.conv:
             blk.f32_gemm = "mfma"
         for _ in range(2):
@@ -485,7 +520,31 @@ def main():
         alt = {"f32_gemm": "mfma", "value": round(cfg["N"] * args.steps / dta, 2),
                "ms_per_step": round(dta / args.steps * 1e3, 3)}
         for blk in model.conv:
-            blk.f32_gemm = "bf16x3"
+            blk.f32_gemm = cfg["f32_gemm"]
+
+    # SURVEY.md §8(d) batch sweep (cfg2: N in {32, 64, 256} clips per GPU beside
+    # the bench batch), same model and step, 5 timed steps each after 2 warm-up
+    # steps; reported as extra keys, `value` stays the bench batch
+    sweep = None
+    if world == 1 and args.sweep and args.config == "cfg2":
+        sweep = {str(cfg["N"]): round(clips, 2)}
+        for nb in (32, 64, 256):
+            if nb == cfg["N"]:
+                continue
+            progress(f"batch sweep: N={nb}")
+            x = torch.randn(nb, cfg["C"], cfg["T"], cfg["V"], generator=gen).to(device)
+            labels = torch.randint(0, cfg["classes"], (nb,), generator=gen).to(device)
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            for _ in range(5):
+                step()
+            torch.cuda.synchronize()
+            sweep[str(nb)] = round(nb * 5 / (time.perf_counter() - ts), 2)
+        sweep = dict(sorted(sweep.items(), key=lambda kv: int(kv[0])))
+        x = torch.randn(cfg["N"], cfg["C"], cfg["T"], cfg["V"], generator=gen).to(device)
+        labels = torch.randint(0, cfg["classes"], (cfg["N"],), generator=gen).to(device)
 
     if rank == 0:
         out = {
@@ -502,7 +561,11 @@ def main():
                                         "fp32: temporal conv fwd/data-grad/weight-grad as exact "
                                         "3-way bf16 splits (6 MFMAs, fp32-gated parity); "
                                         "spatial GEMMs fp32 MFMA"
-                                        if cfg["f32_gemm"] == "bf16x3" else "fp32 MFMA")},
+                                        if cfg["f32_gemm"] == "bf16x3" else
+                                        "fp32: folded temporal GEMMs as 2-way fp16 splits of "
+                                        "power-of-two-scaled operands (3 MFMAs, fp32-gated "
+                                        "parity), other temporal GEMMs 3-way bf16 splits"
+                                        if cfg["f32_gemm"] == "f16x2" else "fp32 MFMA")},
             "model_tflops": round(clips * gf_clip / 1e3, 2),
             "runs_clips_s": [round(r, 2) for r in runs],
             "median_clips_s": round(sorted(runs)[len(runs) // 2], 2),
@@ -510,6 +573,8 @@ def main():
         }
         if alt is not None:
             out["fp32_mfma_path"] = alt
+        if sweep is not None:
+            out["batch_sweep_clips_s"] = sweep
         if not args.no_roofline:
             progress("per-block rates")
             out["per_block_clips_s"] = per_block_rates(model, cfg, device)
@@ -520,8 +585,13 @@ def main():
             pmc, pmc_src = pmc_profile(args.config)
             traffic = pmc["hbm_bytes_per_launch"].get(sym) if pmc else None
             mfma_busy = pmc.get("mfma_busy", {}).get(sym) if pmc else None
+            # split kernels: the fp32-work ceiling is the bf16/fp16 MFMA rate over
+            # the products per fp32 product (6 for bf16 x3, 3 for the fp16 x2 planes)
+            split = sym.startswith("k_conv_x3") or sym.startswith("k_wgrad_x3")
             fpeak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
-                     X3_PEAK_TFLOPS if sym.startswith("k_conv_x3") else MFMA_F32_PEAK_TFLOPS)
+                     (F16X2_PEAK_TFLOPS if sym.rstrip(">").split(",")[-2 if sym.startswith(
+                         "k_conv_x3") else -1].strip() == "2" else X3_PEAK_TFLOPS) if split
+                     else MFMA_F32_PEAK_TFLOPS)
             # the roof that bounds the kernel's algorithmic work: MFMA or HBM
             # (the bf16 GEMMs over fp32 activations at 64-128 channels sit
             # below the bf16 ridge of 2500 / 8 = 312 FLOP/B)

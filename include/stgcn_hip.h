@@ -77,6 +77,13 @@ extern "C" {
                             * (Wc_q = Wt_q W'): Z is never formed, and its buffer is
                             * OPAQUE (it carries Wc from stgcn_block_fwd to
                             * stgcn_block_bwd). Exclusive with STGCN_F_BF16. */
+#define STGCN_F_F16X2 8    /* ABI 6, with STGCN_F_F32X3 only: the folded block's temporal
+                            * GEMMs (forward, data-grad, weight-grad) as 2-way fp16 splits
+                            * (x s = h + l, 22 significant bits, three partial products,
+                            * fp32 accumulate) of operands scaled by powers of two s from
+                            * their max |x| (so h <= 2^14 and no element underflows
+                            * relative to the tensor's maximum); the result is scaled back
+                            * exactly. Same fp32 gate as STGCN_F_F32X3, half its MFMAs. */
 
 enum {
   STGCN_OK = 0,
@@ -95,7 +102,8 @@ typedef struct stgcn_desc {
   float momentum;      /* BatchNorm momentum 0.1                             */
   int32_t training;    /* 1: batch statistics + running-stat update          */
   int32_t need_dx;     /* backward: write dx (0 for the network's first block)*/
-  int32_t flags;       /* STGCN_F_RESIDUAL | (STGCN_F_BF16 or STGCN_F_F32X3) */
+  int32_t flags;       /* STGCN_F_RESIDUAL | (STGCN_F_BF16 or STGCN_F_F32X3
+                        * [| STGCN_F_F16X2])                                  */
 } stgcn_desc_t;
 
 /* Forward arguments. Saved tensors (Z, U, stats; residual: Z, Za, y, stats)
@@ -239,6 +247,7 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
 #define STGCN_PLAN_WSP_SPLIT 16    /* spatial dW' on exact split products (k_wgrad_sp X3) */
 #define STGCN_PLAN_TCONV_SPLIT 32  /* temporal conv forward on the split pipeline         */
 #define STGCN_PLAN_TWGRAD_SPLIT 64 /* temporal weight gradient on the split kernel        */
+#define STGCN_PLAN_F16X2 128       /* the folded GEMMs on 2-way fp16 splits (STGCN_F_F16X2) */
 int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan);
 
 /* Measurement (bench.py roofline): time one of the block's GEMM kernels,

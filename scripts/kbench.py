@@ -25,7 +25,8 @@ if os.environ.get("KB_SHAPES"):
 for label, ci, co, T, s in shapes:
     d = pkg.fused.make_desc((128, ci, T, V), co, K, s, 4, 1e-5, 0.1, True,
                             bf16=os.environ.get("KB_BF16") == "1",
-                            f32x3=os.environ.get("KB_X3") == "1")
+                            f32x3=os.environ.get("KB_X3") == "1",
+                            f16x2=os.environ.get("KB_F16") == "1")
     row = []
     for which in which_set:
         nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)

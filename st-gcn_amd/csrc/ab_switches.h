@@ -64,6 +64,3 @@
 #ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
 #define STGCN_AB_BWD6_EXACT 0
 #endif
-#ifndef STGCN_AB_F16X2          // timing experiment: k_conv_x3 on 2-way fp16 splits (unit scales)
-#define STGCN_AB_F16X2 0
-#endif

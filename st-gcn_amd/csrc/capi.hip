@@ -78,6 +78,7 @@ int64_t nTo(const stgcn_desc_t *d) { return (int64_t)d->T_out * d->V; }
 bool residual(const stgcn_desc_t *d) { return (d->flags & STGCN_F_RESIDUAL) != 0; }
 bool bf16(const stgcn_desc_t *d) { return (d->flags & STGCN_F_BF16) != 0; }
 bool f32x3(const stgcn_desc_t *d) { return (d->flags & STGCN_F_F32X3) != 0; }
+bool f16x2_flag(const stgcn_desc_t *d) { return (d->flags & STGCN_F_F16X2) != 0; }
 // the fused dropout of a call (training and 0 < p < 1; p >= 1: everything dropped)
 Dropout make_dropout(const stgcn_desc_t *d, float p, uint64_t seed) {
   Dropout dr;
@@ -116,6 +117,10 @@ bool fold_w(const stgcn_desc_t *d) {
   return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->V == 18 &&
          !fused_spb(d);
 }
+// The folded block's temporal GEMMs on 2-way fp16 splits (STGCN_F_F16X2; k_conv_x3 /
+// k_wgrad_x3 with NPL = 2), operand scales from max |x| words (launch_absmax)
+bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
+
 // sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
 // sums written by the ReLU + BN2 backward apply, k_fold_tq, one small GEMM with
 // Wt) instead of a pass over dZ (the folded block has no dZ at all): cfg3 5632
@@ -237,6 +242,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
 struct BwdLayout {
   double *sg, *sgu, *sdu, *sd, *sdn, *SdZ;
   double *s1, *s2;  // deferred-dx chain: the prev-mode sums of the spatial backward
+  unsigned *amax;
   float *dU, *dZ, *G, *H, *slab, *wpk;
   float *Wpk;  // W' = [W_0 | ... | W_{K-1}] (C_out, K*C_in) for the stacked H GEMM
   float *Rg;  // residual projection data-grad (N, C_in, T, V)
@@ -258,6 +264,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.SdZ = c.take<double>((size_t)R * d->V);
   L.s1 = c.take<double>(C);
   L.s2 = c.take<double>(C);
+  L.amax = c.take<unsigned>(4);  // f16x2: max |dU|, |Wc|, |G| (zeroed with the sums)
   L.dbl_bytes = c.off;
   if (!residual(d)) {  // clip-chunk sums of dU -> Tq -> sum_{n,t} dZ (kernels_fold.hip)
     L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
@@ -307,6 +314,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
 
 struct FwdLayout {
   double *s1, *q1, *s2, *q2;
+  unsigned *amax;  // f16x2: max |G|, |Wc|
   float *G, *Wpk, *biasZ, *wpk;
   float *Rp;  // residual projection output (N, C_out, T_out, V)
   float *Wc, *BT;  // the folded block: composite weights, per-frame bias table
@@ -322,6 +330,7 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
   L.q1 = c.take<double>(C);
   L.s2 = c.take<double>(R);
   L.q2 = c.take<double>(R);
+  L.amax = c.take<unsigned>(4);
   L.dbl_bytes = c.off;
   L.G = c.take<float>((size_t)d->N * K * C * nT(d));
   L.Wpk = c.take<float>((size_t)R * K * C);
@@ -527,10 +536,12 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   if (!d) return fail(STGCN_E_INVALID, "null descriptor");
   if (d->N <= 0 || d->C_in <= 0 || d->C_out <= 0 || d->T <= 0 || d->V <= 0 || d->K <= 0)
     return fail(STGCN_E_INVALID, "non-positive dimension");
-  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16 | STGCN_F_F32X3)) != 0)
+  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16 | STGCN_F_F32X3 | STGCN_F_F16X2)) != 0)
     return fail(STGCN_E_UNSUPPORTED, "unknown flags");
   if ((d->flags & STGCN_F_BF16) && (d->flags & STGCN_F_F32X3))
     return fail(STGCN_E_INVALID, "STGCN_F_BF16 and STGCN_F_F32X3 are exclusive");
+  if ((d->flags & STGCN_F_F16X2) && !(d->flags & STGCN_F_F32X3))
+    return fail(STGCN_E_INVALID, "STGCN_F_F16X2 needs STGCN_F_F32X3");
   if (d->gamma != 9 || d->pad != 4)
     return fail(STGCN_E_UNSUPPORTED, "only gamma=9, pad=4 (the reference default)");
   if (d->stride != 1 && d->stride != 2) return fail(STGCN_E_UNSUPPORTED, "stride must be 1 or 2");
@@ -570,6 +581,7 @@ int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan) {
     WgradParams w = make_wgrad_taps(d, nullptr, nullptr, nullptr, fold_w(d) ? d->C_in : 0);
     if (w.bf16 == 3) f |= STGCN_PLAN_TWGRAD_SPLIT;
   }
+  if (f16x2(d)) f |= STGCN_PLAN_F16X2;
   *plan = f;
   return STGCN_OK;
 }
@@ -698,6 +710,13 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
       float *Wc = fold_wc_in_z(d) ? a->Z : L.Wc;  // (kept for the backward)
       HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, s));
       HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT, s));
+      if (f16x2(d)) {  // the fp16 splits' operand scales: max |G|, max |Wc|
+        HIP_TRY(launch_absmax(Gfold, (int64_t)N * C * T * V, L.amax, s));
+        HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
+        p.f16x2 = 1;
+        p.amax_in = L.amax;
+        p.amax_w = L.amax + 1;
+      }
       p.in = Gfold;
       p.w = Wc;
       p.bias_r = nullptr;
@@ -807,10 +826,19 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       Wc = L.Wc;
     }
     HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));
+    if (f16x2(d)) {  // the fp16 splits' operand scales: max |dU|, max |Wc|
+      HIP_TRY(launch_absmax(L.dU, (int64_t)N * R * To * V, L.amax, s));
+      HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
+    }
     {
       ConvGemmParams p = conv_base(d, L.wpk);
       p.in = L.dU;
       p.out = L.H;
+      if (f16x2(d)) {
+        p.f16x2 = 1;
+        p.amax_in = L.amax;
+        p.amax_w = L.amax + 1;
+      }
       p.in_bstride = (int64_t)R * To * V;
       p.out_bstride = (int64_t)C * T * V;
       p.w_sr = 9;
@@ -852,6 +880,12 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       G = L.G;
     }
     WgradParams w = make_wgrad_taps(d, L.dU, G, L.slab, C);
+    if (f16x2(d) && w.bf16 == 3) {  // (max |dU| from the data gradient's scale above)
+      HIP_TRY(launch_absmax(G, (int64_t)N * C * T * V, L.amax + 2, s));
+      w.f16x2 = 1;
+      w.amax_p = L.amax;
+      w.amax_q = L.amax + 2;
+    }
     HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_fold_grads(L.slab, w.S, a->Wt, a->W, L.bZ, L.ftq, R, C, V, L.dWc, L.fpart,
                               a->dWt, a->dW, s));
@@ -1122,6 +1156,11 @@ struct TimedPlan {
   const float *dZ = nullptr;
   float *H = nullptr, *dx = nullptr, *dA = nullptr;
   double *sd = nullptr;
+  // f16x2: the operands whose max |x| the fp16 splits scale by (computed once
+  // before the timed launches, as the block does before its GEMMs)
+  unsigned *amax = nullptr;
+  const float *ax[2] = {nullptr, nullptr};
+  int64_t an[2] = {0, 0};
   size_t bytes = 0;
   double flops = 0;
 };
@@ -1135,6 +1174,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
   const int CZ = fold ? C : R;
   const double tflops = 2.0 * 9 * R * (double)CZ * To * V * N;
   float *wpk = c.take<float>(wpk_floats(d));
+  if (f16x2(d) && which <= 2) P.amax = c.take<unsigned>(4);
   if (which == 0) {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * CZ * T * V);
@@ -1167,6 +1207,15 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       p.w_sr = (int64_t)C * 9;
       p.C = C;
     }
+    if (P.amax) {
+      p.f16x2 = 1;
+      p.amax_in = P.amax;
+      p.amax_w = P.amax + 1;
+      P.ax[0] = p.in;
+      P.an[0] = (int64_t)N * C * T * V;
+      P.ax[1] = p.w;
+      P.an[1] = (int64_t)R * C * 9;
+    }
     conv_tiles(p);
     P.cp[P.ncp++] = p;
     P.flops = tflops;
@@ -1186,6 +1235,15 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     p.T_src = To;
     p.T_dst = T;
     p.s_in = 1;
+    if (P.amax) {
+      p.f16x2 = 1;
+      p.amax_in = P.amax;
+      p.amax_w = P.amax + 1;
+      P.ax[0] = p.in;
+      P.an[0] = (int64_t)N * R * To * V;
+      P.ax[1] = w;
+      P.an[1] = (int64_t)R * CZ * 9;
+    }
     if (d->stride == 1) {
       p.w = w ? w + 8 : nullptr;
       p.w_sq = -1;
@@ -1217,6 +1275,15 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     w.q_bf16 = z_bf16(d) ? 1 : 0;
     w.p_bf16 = du_bf16(d) ? 1 : 0;
     w.slab = c.take<float>((size_t)w.S * R * CZ * 9);
+    if (P.amax && w.bf16 == 3) {
+      w.f16x2 = 1;
+      w.amax_p = P.amax;
+      w.amax_q = P.amax + 1;
+      P.ax[0] = dU;
+      P.an[0] = (int64_t)N * R * To * V;
+      P.ax[1] = Z;
+      P.an[1] = (int64_t)N * CZ * T * V;
+    }
     P.wp = w;
     P.wgrad = true;
     P.flops = tflops;
@@ -1358,6 +1425,11 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
     }
     return hipSuccess;
   };
+  if (P.amax) {  // the f16x2 operand scales (not timed)
+    HIP_TRY(hipMemsetAsync(P.amax, 0, 4 * sizeof(unsigned), s));
+    for (int i = 0; i < 2; ++i)
+      if (P.ax[i]) HIP_TRY(launch_absmax(P.ax[i], P.an[i], P.amax + i, s));
+  }
   HIP_TRY(launch());  // warm-up
   hipEvent_t e0, e1;
   HIP_TRY(hipEventCreate(&e0));

@@ -75,10 +75,11 @@ struct ConvGemmParams {
   int in_bf16;       // in[] holds bf16 (same element strides; k_conv_x3 one-plane only)
   int out_bf16;      // out[] is written as bf16 (same element strides; the shared
                      // epilogues; no residual input)
-  // bf16 == 2 (fp32 GEMM as 2-way fp16 splits of power-of-two-scaled operands,
-  // k_conv_x3 NPL = 2): in[] is multiplied by in_scale before the split, the
-  // weights by w_scale, the accumulators by out_scale = 1 / (in_scale w_scale)
-  float in_scale, w_scale, out_scale;
+  // f16x2 (with bf16 == 3): the fp32 GEMM as 2-way fp16 splits (k_conv_x3
+  // NPL = 2, three products) of power-of-two-scaled operands; amax_in / amax_w:
+  // device words holding max |in| / max |w| as float bits (f16x2_scale)
+  int f16x2;
+  const unsigned *amax_in, *amax_w;
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -97,9 +98,16 @@ struct WgradParams {
   int bf16;  // set by plan_wgrad_bf16: run k_wgrad_bf16 (bf16 operands, fp32 accumulate);
              // 3: set by plan_wgrad_x3 (fp32 via exact bf16 splits, k_wgrad_x3)
   int p_bf16, q_bf16;  // P / Q hold bf16 (same element strides; k_wgrad_bf16 only)
+  // f16x2 (with bf16 == 3): k_wgrad_x3 on 2-way fp16 splits (NPL = 2) of the
+  // power-of-two-scaled P / Q; amax_p / amax_q: device max |P| / max |Q| bits
+  int f16x2;
+  const unsigned *amax_p, *amax_q;
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
+// amax[0] = max(amax[0], max |x[i]|) as float bits (x of n floats; amax zeroed
+// by the caller): the operand bound of the fp16-split GEMMs (f16x2)
+hipError_t launch_absmax(const float *x, int64_t n, unsigned *amax, hipStream_t s);
 // The folded block (kernels_fold.hip; capi.hip fold_w): composite weights
 // Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i], the per-frame bias table, the dU
 // sums (total, boundary frames, per tap Tq) and the weight gradients from dWc.

@@ -27,126 +27,129 @@
 
 namespace stgcn {
 
-// out[z][m][n] = sum_{k < K} A[z][m][k] B[z][k][n] + sum_{k < K2} A2[z][m][k] B2[k][n]
-// (element offsets from the strides, z = blockIdx.z adds a_z / b_z / a2_z /
-// o_z). fp64 accumulation; operands and output float or double (run-time
-// flags). Block = 256 threads (4 waves) on a 32 x 32 output tile, thread = 4 x 4
-// outputs; K in 64-deep chunks staged in LDS ([k][m] and [k][n]); wave w takes
-// k-steps w*16 .. w*16+15 of each chunk, and the four partial tiles are summed
-// in a fixed order through LDS at the end (deterministic).
-struct SmallGemm {
+// The fold's small GEMMs as single launches on the fp64 matrix cores
+// (v_mfma_f64_16x16x4_f64; operands float or double, converted exactly, fp64
+// products and accumulation in a fixed order, so the results are deterministic):
+//   out(m, n) = sum_{k < K} A(m, k) B(k, n) + sum_{k < K2} A2(m, k) B2(k, n)
+// Every operand index is a two-level mixed-radix map per dimension,
+//   idx(x) = (x / d) * s1 + (x % d) * s0,
+// so the nine taps ride in M or K of ONE GEMM (no per-tap launches and no
+// per-tap partial sums): e.g. Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i] is the
+// (9 R) x C x R GEMM with m = 9 o + q.
+// Block = 256 threads on a 64 x 64 output tile (wave = 32 x 32 = 2 x 2 MFMA
+// tiles), K in chunks of 16 staged as fp64 in LDS.
+struct Map {
+  int d = 1;
+  int64_t s1 = 0, s0 = 0;
+  __host__ __device__ int64_t operator()(int x) const {
+    return d == 1 ? (int64_t)x * s1 : (int64_t)(x / d) * s1 + (int64_t)(x % d) * s0;
+  }
+};
+struct Gemm64 {
   const void *A, *B, *A2, *B2;
   void *out;
   int M, N, K, K2;
   int a_dbl, b_dbl, a2_dbl, b2_dbl, o_dbl;
-  int64_t am, ak, bk, bn, om, on;
-  int64_t a2m, a2k, b2k, b2n;
-  int64_t a_z, b_z, a2_z, o_z;
+  Map am, ak, bk, bn, a2m, a2k, b2k, b2n, om, on;
 };
 
 __device__ __forceinline__ double ld_fd(const void *p, int dbl, int64_t i) {
   return dbl ? reinterpret_cast<const double *>(p)[i] : (double)reinterpret_cast<const float *>(p)[i];
 }
 
-__global__ __launch_bounds__(256) void k_small_gemm(SmallGemm g) {
-  // 32 x 32 output tile; wave w takes k-steps w*16 .. +15 of every 64-deep
-  // chunk (thread = 4 x 4 outputs), the four partial tiles summed in LDS at the end
-  __shared__ __attribute__((aligned(16))) double sm[2 * 64 * 32];
-  double(*As)[32] = reinterpret_cast<double(*)[32]>(sm);            // [k][m]
-  double(*Bs)[32] = reinterpret_cast<double(*)[32]>(sm + 64 * 32);  // [k][n]
+typedef double double4v __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_gemm_f64(Gemm64 g) {
+  constexpr int KC = 16, TP = 64 + 1;  // chunk depth, LDS pitch (doubles)
+  __shared__ double As[KC][TP], Bs[KC][TP];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int tm = l >> 3, tn = l & 7;
-  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
-  const int64_t z = blockIdx.z;
-  double acc[4][4] = {};
-  auto run = [&](const void *A, const void *B, int adbl, int bdbl, int K, int64_t am, int64_t ak,
-                 int64_t bk, int64_t bn, int64_t aoff, int64_t boff) {
-    for (int k0 = 0; k0 < K; k0 += 64) {
-      __syncthreads();
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
+  double4v acc[2][2];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int e = r * 256 + tid;
-        {  // A: consecutive threads take consecutive k of one row
-          const int kk = e & 63, mm = e >> 6;
-          const int m = m0 + mm, k = k0 + kk;
-          As[kk][mm] = (m < g.M && k < K) ? ld_fd(A, adbl, aoff + m * am + k * ak) : 0.0;
-        }
-        {
-          const int nn = e & 31, kk = e >> 5;
-          const int k = k0 + kk, n = n0 + nn;
-          Bs[kk][nn] = (k < K && n < g.N) ? ld_fd(B, bdbl, boff + k * bk + n * bn) : 0.0;
-        }
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (double4v){0.0, 0.0, 0.0, 0.0};
+  const int Ktot = g.K + (g.A2 ? g.K2 : 0);
+  for (int k0 = 0; k0 < Ktot; k0 += KC) {
+    __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = r * 256 + tid;
+      const int kk = e & (KC - 1), mm = e >> 4;  // A: 16 consecutive k of a row
+      const int k = k0 + kk, m = m0 + mm, n = n0 + mm;
+      double a = 0.0, b = 0.0;
+      if (k < g.K) {
+        if (m < g.M) a = ld_fd(g.A, g.a_dbl, g.am(m) + g.ak(k));
+        if (n < g.N) b = ld_fd(g.B, g.b_dbl, g.bk(k) + g.bn(n));
+      } else if (k < Ktot) {
+        const int k2 = k - g.K;
+        if (m < g.M) a = ld_fd(g.A2, g.a2_dbl, g.a2m(m) + g.a2k(k2));
+        if (n < g.N) b = ld_fd(g.B2, g.b2_dbl, g.b2k(k2) + g.b2n(n));
       }
-      __syncthreads();
-#pragma unroll 4
-      for (int kk = w * 16; kk < w * 16 + 16; ++kk) {
-        double a[4], b[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          a[i] = As[kk][tm * 4 + i];
-          b[i] = Bs[kk][tn * 4 + i];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
-      }
+      As[kk][mm] = a;
+      Bs[kk][mm] = b;
     }
-  };
-  run(g.A, g.B, g.a_dbl, g.b_dbl, g.K, g.am, g.ak, g.bk, g.bn, z * g.a_z, z * g.b_z);
-  if (g.A2) run(g.A2, g.B2, g.a2_dbl, g.b2_dbl, g.K2, g.a2m, g.a2k, g.b2k, g.b2n, z * g.a2_z, 0);
-  // partial tiles of waves 1-3 -> LDS, wave 0 sums in fixed order and stores
-  __syncthreads();
-  if (w > 0) {
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int ks = 0; ks < KC; ks += 4) {
+      // A operand: lane l holds A[row l & 15][k l >> 4]; B: B[k l >> 4][col l & 15]
+      double a[2], b[2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sm[((w - 1) * 64 + l) * 16 + i * 4 + j] = acc[i][j];
-  }
-  __syncthreads();
-  if (w > 0) return;
+      for (int i = 0; i < 2; ++i) a[i] = As[ks + (l >> 4)][wm + i * 16 + (l & 15)];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + tm * 4 + i;
+      for (int j = 0; j < 2; ++j) b[j] = Bs[ks + (l >> 4)][wn + j * 16 + (l & 15)];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + tn * 4 + j;
-      double v = acc[i][j];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) v += sm[(p * 64 + l) * 16 + i * 4 + j];
-      if (m >= g.M || n >= g.N) continue;
-      const int64_t o = z * g.o_z + m * g.om + n * g.on;
-      if (g.o_dbl)
-        reinterpret_cast<double *>(g.out)[o] = v;
-      else
-        reinterpret_cast<float *>(g.out)[o] = (float)v;
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
+  // C/D: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + i * 16 + (l >> 4) + 4 * r, n = n0 + wn + j * 16 + (l & 15);
+        if (m >= g.M || n >= g.N) continue;
+        const int64_t o = g.om(m) + g.on(n);
+        if (g.o_dbl)
+          reinterpret_cast<double *>(g.out)[o] = acc[i][j][r];
+        else
+          reinterpret_cast<float *>(g.out)[o] = (float)acc[i][j][r];
+      }
 }
 
-static hipError_t small_gemm(const SmallGemm &g, int nz, hipStream_t s) {
-  hipLaunchKernelGGL(k_small_gemm, dim3((g.N + 31) / 32, (g.M + 31) / 32, nz), dim3(256), 0, s, g);
+static hipError_t gemm64(const Gemm64 &g, hipStream_t s) {
+  hipLaunchKernelGGL(k_gemm_f64, dim3((g.N + 63) / 64, (g.M + 63) / 64), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
-// dst[i] = sum_{z < Z} part[z * n + i] (fixed order), as float or double
-__global__ void k_sum_parts(const double *part, int Z, int64_t n, float *dstf, double *dstd) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double a = 0.0;
-  for (int z = 0; z < Z; ++z) a += part[(int64_t)z * n + i];
-  if (dstf) dstf[i] = (float)a;
-  else dstd[i] = a;
+static Map mp(int64_t s1) {
+  Map m;
+  m.s1 = s1;
+  return m;
+}
+static Map mp(int d, int64_t s1, int64_t s0) {
+  Map m;
+  m.d = d;
+  m.s1 = s1;
+  m.s0 = s0;
+  return m;
 }
 
-// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in)
+// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in);
+// one (9 R) x C x R GEMM, m = 9 o + q
 hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s) {
-  SmallGemm g{};
-  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.a_z = 1;
-  g.B = W; g.bk = C; g.bn = 1;
-  g.out = Wc; g.om = (int64_t)C * 9; g.on = 9; g.o_z = 1;
-  g.M = R; g.N = C; g.K = R;
-  return small_gemm(g, 9, s);
+  Gemm64 g{};
+  g.A = Wt; g.am = mp(9, (int64_t)R * 9, 1); g.ak = mp(9);
+  g.B = W; g.bk = mp(C); g.bn = mp(1);
+  g.out = Wc; g.om = mp(9, (int64_t)C * 9, 1); g.on = mp(9);
+  g.M = 9 * R; g.N = C; g.K = R;
+  return gemm64(g, s);
 }
 
 // Boundary frames of the folded block: output frames t < nb0 and t >= tb1 read
@@ -174,12 +177,13 @@ __global__ void k_fold_bias(const double *bq, const float *bt, int R, int V, int
 
 hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
                             int To, int st, double *bq, float *BT, hipStream_t s) {
-  SmallGemm g{};
-  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.a_z = 1;
-  g.B = bZ; g.bk = V; g.bn = 1;
-  g.out = bq; g.o_dbl = 1; g.om = V; g.on = 1; g.o_z = (int64_t)R * V;
-  g.M = R; g.N = V; g.K = R;
-  HIP_RET(small_gemm(g, 9, s));
+  // bq[q][o][v]: one (9 R) x V x R GEMM, m = q R + o
+  Gemm64 g{};
+  g.A = Wt; g.am = mp(R, 1, (int64_t)R * 9); g.ak = mp(9);
+  g.B = bZ; g.bk = mp(V); g.bn = mp(1);
+  g.out = bq; g.o_dbl = 1; g.om = mp(R, (int64_t)R * V, V); g.on = mp(1);
+  g.M = 9 * R; g.N = V; g.K = R;
+  HIP_RET(gemm64(g, s));
   const int64_t n = (int64_t)R * To * V;
   hipLaunchKernelGGL(k_fold_bias, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bq, bt, R, V,
                      T, To, st, BT);
@@ -268,6 +272,33 @@ hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V,
   return hipGetLastError();
 }
 
+// amax[0] = max(amax[0], max_i |x[i]|) as float bits (non-negative floats order
+// as unsigned integers): one atomic per wave
+__global__ __launch_bounds__(256) void k_absmax(const float *x, int64_t n, unsigned *amax) {
+  float m = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = i0; i < n4; i += stride) {
+      const float4 v = reinterpret_cast<const float4 *>(x)[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    for (int64_t i = n4 * 4 + i0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  } else {
+    for (int64_t i = i0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(unsigned, m));
+}
+
+hipError_t launch_absmax(const float *x, int64_t n, unsigned *amax, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>(2048, std::max<int64_t>(1, (n / 4 + 255) / 256));
+  hipLaunchKernelGGL(k_absmax, dim3((unsigned)blocks), dim3(256), 0, s, x, n, amax);
+  return hipGetLastError();
+}
+
 __global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -279,54 +310,50 @@ __global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *d
 // The folded block's weight gradients from dWc (slab of the temporal weight
 // gradient over C_in channels) and Tq:
 //   dWt[o][c][q] = sum_i dWc[o][i][q] W'[c][i] + sum_v Tq[q][o][v] bZ[c][v]
-//   dW'[c][i]    = sum_q sum_o Wt[o][c][q] dWc[o][i][q]
-// (the tap sum of dW' as per-tap partial products in `part`, 9 R max(C, V)
-// doubles, summed in fixed order)
+//                  ((9 R) x R GEMM over K = C_in, plus the K2 = V bias term)
+//   dW'[c][i]    = sum_{(o,q)} Wt[o][c][q] dWc[o][i][q]   (R x C GEMM over K = 9 R)
+// (part: unused, kept for the caller's workspace layout)
 hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
                              const float *bZ, const double *Tq, int R, int C, int V,
                              double *dWc, double *part, float *dWt, float *dW, hipStream_t s) {
+  (void)part;
   const int64_t n = (int64_t)R * C * 9;
   hipLaunchKernelGGL(k_slab_reduce_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slab,
                      S, n, dWc);
   {
-    SmallGemm g{};
-    g.A = dWc; g.a_dbl = 1; g.am = (int64_t)C * 9; g.ak = 9; g.a_z = 1;
-    g.B = W; g.bk = 1; g.bn = C;
-    g.A2 = Tq; g.a2_dbl = 1; g.a2m = V; g.a2k = 1; g.a2_z = (int64_t)R * V;
-    g.B2 = bZ; g.b2k = 1; g.b2n = V;
+    Gemm64 g{};
+    g.A = dWc; g.a_dbl = 1; g.am = mp(9, (int64_t)C * 9, 1); g.ak = mp(9);
+    g.B = W; g.bk = mp(1); g.bn = mp(C);
+    g.A2 = Tq; g.a2_dbl = 1; g.a2m = mp(9, V, (int64_t)R * V); g.a2k = mp(1);
+    g.B2 = bZ; g.b2k = mp(1); g.b2n = mp(V);
     g.K2 = V;
-    g.out = dWt; g.om = (int64_t)R * 9; g.on = 9; g.o_z = 1;
-    g.M = R; g.N = R; g.K = C;
-    HIP_RET(small_gemm(g, 9, s));
+    g.out = dWt; g.om = mp(9, (int64_t)R * 9, 1); g.on = mp(9);
+    g.M = 9 * R; g.N = R; g.K = C;
+    HIP_RET(gemm64(g, s));
   }
   {
-    SmallGemm g{};
-    g.A = Wt; g.am = 9; g.ak = (int64_t)R * 9; g.a_z = 1;
-    g.B = dWc; g.b_dbl = 1; g.bk = (int64_t)C * 9; g.bn = 9; g.b_z = 1;
-    g.out = part; g.o_dbl = 1; g.om = C; g.on = 1; g.o_z = (int64_t)R * C;
-    g.M = R; g.N = C; g.K = R;
-    HIP_RET(small_gemm(g, 9, s));
-    const int64_t m = (int64_t)R * C;
-    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
-                       dW, nullptr);
+    Gemm64 g{};
+    g.A = Wt; g.am = mp(9); g.ak = mp(9, (int64_t)R * 9, 1);
+    g.B = dWc; g.b_dbl = 1; g.bk = mp(9, (int64_t)C * 9, 1); g.bn = mp(9);
+    g.out = dW; g.om = mp(C); g.on = mp(1);
+    g.M = R; g.N = C; g.K = 9 * R;
+    HIP_RET(gemm64(g, s));
   }
   return hipGetLastError();
 }
 
 // SdZ[c][v] = sum_q sum_o Wt[o][c][q] Tq[q][o][v]  (= sum_{n,t} dZ[c,t,v]; Wt is
-// the temporal weight [R][C][9] with C = its input channels, the Z channels)
+// the temporal weight [R][C][9] with C = its input channels, the Z channels):
+// one C x V GEMM over K = 9 R (k = 9 o + q). (part: unused)
 hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
                            double *SdZ, hipStream_t s) {
-  SmallGemm g{};
-  g.A = Wt; g.am = 9; g.ak = (int64_t)C * 9; g.a_z = 1;
-  g.B = Tq; g.b_dbl = 1; g.bk = V; g.bn = 1; g.b_z = (int64_t)R * V;
-  g.out = part; g.o_dbl = 1; g.om = V; g.on = 1; g.o_z = (int64_t)C * V;
-  g.M = C; g.N = V; g.K = R;
-  HIP_RET(small_gemm(g, 9, s));
-  const int64_t m = (int64_t)C * V;
-  hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, part, 9, m,
-                     nullptr, SdZ);
-  return hipGetLastError();
+  (void)part;
+  Gemm64 g{};
+  g.A = Wt; g.am = mp(9); g.ak = mp(9, (int64_t)C * 9, 1);
+  g.B = Tq; g.b_dbl = 1; g.bk = mp(9, V, (int64_t)R * V); g.bn = mp(1);
+  g.out = SdZ; g.o_dbl = 1; g.om = mp(V); g.on = mp(1);
+  g.M = C; g.N = V; g.K = 9 * R;
+  return gemm64(g, s);
 }
 
 }  // namespace stgcn

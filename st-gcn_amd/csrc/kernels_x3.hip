@@ -105,6 +105,18 @@ __device__ __forceinline__ void splith2(float a, float b, unsigned &h, unsigned 
   l = pkh2(a - lo_h(h), b - hi_h(h));
 }
 
+// Power-of-two operand scale of the fp16 splits: max |x| (float bits in *amax)
+// maps into [2^13, 2^14), so h <= 2^14 < 65504 and every element keeps 22
+// significant bits down to 2^-24 (fp16's subnormal step) in scaled units; the
+// exponent is clamped to +-100 (0 / denormal / inf maxima). Returns the scale's
+// exponent (scale = 2^se).
+__device__ __forceinline__ int f16x2_se(const unsigned *amax) {
+  const int e = (int)((amax ? *amax : 0x3f800000u) >> 23) & 0xff;
+  const int se = e == 0 ? 0 : 140 - e;
+  return se < -100 ? -100 : (se > 100 ? 100 : se);
+}
+__device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float, (unsigned)(e + 127) << 23); }
+
 // exact 3-way split of two floats into packed (h, m, l) bf16 pairs
 __device__ __forceinline__ void split2(float a, float b, unsigned &h, unsigned &m, unsigned &l) {
   h = pk2(a, b);
@@ -242,6 +254,9 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // kept in bf16 -- loaded as zero-extended shorts at half the byte offsets)
   static_assert(!IB || NPL == 1, "bf16 input: one-plane kernels");
   constexpr bool inb = IB;
+  // NPL = 2: the window's power-of-two scale (f16x2_se of max |in|)
+  const int in_se = NPL == 2 ? f16x2_se(p.amax_in) : 0;
+  const float in_scale = pow2f(in_se);
   auto load_img = [&](int chunk) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
     const int esz = inb ? 2 : 4;
@@ -291,7 +306,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         }
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
       } else if (NPL == 2 && loff[k] >= 0) {  // fp16 (h, l) planes of the scaled input
-        const float sc = p.in_scale;
+        const float sc = in_scale;
         uint4 h, l;
         splith2(st[k][0] * sc, st[k][1] * sc, h.x, l.x);
         splith2(st[k][2] * sc, st[k][3] * sc, h.y, l.y);
@@ -524,9 +539,9 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 #pragma unroll
     for (int j = 0; j < 2 * MR; ++j) acc[j] += acl[j];
   } else if constexpr (NPL == 2) {  // undo the operand scales (powers of two: exact)
-    const float os = p.out_scale;
+    const float ia = pow2f(-in_se), iw = pow2f(-f16x2_se(p.amax_w));
 #pragma unroll
-    for (int j = 0; j < 2 * MR; ++j) acc[j] = (acc[j] + acl[j]) * os;
+    for (int j = 0; j < 2 * MR; ++j) acc[j] = (acc[j] + acl[j]) * ia * iw;
   }
   if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
     if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
@@ -577,7 +592,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 // one contiguous run.
 __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int NQ, int TG,
                                  int nch, int rows, int npl, int64_t w_sr, int64_t w_sc,
-                                 int64_t w_sq, int64_t total, float wscale) {
+                                 int64_t w_sq, int64_t total, const unsigned *amax_w) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int jj = (int)(idx & 7);
@@ -598,8 +613,8 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
   const int r = rt * rows + rl, c = ch * 16 + o * 8 + jj, q = g * TG + qq;
   float v = 0.f;
   if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
-  if (npl == 2) {  // fp16 (h, l) of the scaled weight
-    const float vs = v * wscale;
+  if (npl == 2) {  // fp16 (h, l) of the power-of-two-scaled weight
+    const float vs = v * pow2f(f16x2_se(amax_w));
     const _Float16 h = (_Float16)vs;
     const _Float16 l = (_Float16)(vs - (float)h);
     reinterpret_cast<_Float16 *>(wpk)[idx] = pl == 0 ? h : l;
@@ -677,7 +692,7 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
     const int64_t total = (int64_t)p.n_rtiles * nch * npl * p.NQ * 2 * rows * 8;
     hipLaunchKernelGGL(k_pack_conv_w_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, x3_tg(p.NQ), nch,
-                       rows, npl, p.w_sr, p.w_sc, p.w_sq, total, p.w_scale);
+                       rows, npl, p.w_sr, p.w_sc, p.w_sq, total, p.amax_w);
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   bool done = false;
@@ -709,12 +724,8 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
 
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
   if (!conv_x3_supported(p) || !p.wpk) return hipErrorInvalidValue;
-  if (STGCN_AB_F16X2) {  // timing experiment: fp16 2-way splits, unit scales
-    ConvGemmParams q = p;
-    q.in_scale = q.w_scale = q.out_scale = 1.f;
-    return launch_conv_planes(q, 2, s);
-  }
-  return launch_conv_planes(p, 3, s);
+  if (p.f16x2 && (!p.amax_in || !p.amax_w)) return hipErrorInvalidValue;
+  return launch_conv_planes(p, p.f16x2 ? 2 : 3, s);
 }
 
 // The bf16 temporal-conv GEMMs (9 taps; stride-2 data-gradient phases 5 / 4) on
@@ -756,7 +767,7 @@ namespace stgcn {
 // into registers (4-joint groups, fp32 dwords) under this item's MFMAs, split
 // and written after them; one barrier per item.
 // ---------------------------------------------------------------------------
-template <int V, int SIN>
+template <int V, int SIN, int NPL = 3>
 struct WgX3Geo {
   static constexpr int Vp = (V + 3) & ~3;
   static constexpr int G4 = Vp / 4;
@@ -771,9 +782,9 @@ struct WgX3Geo {
   static constexpr int CB = 32;
   static constexpr int PPL = 64 * PPITCH * 2;  // bytes per P plane
   static constexpr int QPL = CB * QPITCH * 2;  // bytes per Q plane
-  static constexpr int BUF = 3 * (PPL + QPL);
-  // double-buffered where it fits (stride 1); else one buffer written between
-  // two barriers (stride 2: 15 Q frames per item)
+  static constexpr int BUF = NPL * (PPL + QPL);
+  // double-buffered where it fits (stride 1; NPL = 2: stride 2 too); else one
+  // buffer written between two barriers (stride 2, three planes: 15 Q frames)
   static constexpr int NBUF = 2 * BUF <= 160 * 1024 ? 2 : 1;
   static constexpr int LDS = NBUF * BUF;
   static constexpr int PG = FT * G4;  // 4-joint groups per P row
@@ -785,10 +796,15 @@ struct WgX3Geo {
   static_assert(LDS <= 160 * 1024, "LDS budget");
 };
 
-template <int V, int SIN>
+// NPL = 2: fp32 as 2-way fp16 splits of the power-of-two-scaled operands (P and
+// Q by the f16x2_se scales of p.amax_p / p.amax_q, undone on the slab values),
+// three products hh, hl, lh
+template <int V, int SIN, int NPL = 3>
 __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
-  using G = WgX3Geo<V, SIN>;
+  using G = WgX3Geo<V, SIN, NPL>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int p_se = NPL == 2 ? f16x2_se(p.amax_p) : 0, q_se = NPL == 2 ? f16x2_se(p.amax_q) : 0;
+  const float p_scale = pow2f(p_se), q_scale = pow2f(q_se);
   char *lds = reinterpret_cast<char *>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -864,14 +880,23 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 #pragma unroll
     for (int k = K0; k < K1; ++k)
       if (gl[k] >= 0) {
-        uint2 h, m, l;
-        split2(st[k][0], st[k][1], h.x, m.x, l.x);
-        split2(st[k][2], st[k][3], h.y, m.y, l.y);
-        char *dst = buf + (isq[k] ? 3 * G::PPL : 0) + gl[k];
+        char *dst = buf + (isq[k] ? NPL * G::PPL : 0) + gl[k];
         const int pl = isq[k] ? G::QPL : G::PPL;
-        *reinterpret_cast<uint2 *>(dst) = h;
-        *reinterpret_cast<uint2 *>(dst + pl) = m;
-        *reinterpret_cast<uint2 *>(dst + 2 * pl) = l;
+        if constexpr (NPL == 2) {
+          const float sc = isq[k] ? q_scale : p_scale;
+          uint2 h, l;
+          splith2(st[k][0] * sc, st[k][1] * sc, h.x, l.x);
+          splith2(st[k][2] * sc, st[k][3] * sc, h.y, l.y);
+          *reinterpret_cast<uint2 *>(dst) = h;
+          *reinterpret_cast<uint2 *>(dst + pl) = l;
+        } else {
+          uint2 h, m, l;
+          split2(st[k][0], st[k][1], h.x, m.x, l.x);
+          split2(st[k][2], st[k][3], h.y, m.y, l.y);
+          *reinterpret_cast<uint2 *>(dst) = h;
+          *reinterpret_cast<uint2 *>(dst + pl) = m;
+          *reinterpret_cast<uint2 *>(dst + 2 * pl) = l;
+        }
       }
   };
   auto write_item = [&](char *buf) {
@@ -890,16 +915,16 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][i] = acl[t][i] = 0.f;
     struct Frag {
-      bf16x8_t a[3], b[3][NT];
+      bf16x8_t a[NPL], b[NPL][NT];
     };
     auto ld = [&](const char *buf, int s, Frag &f) {
       const __bf16 *P = reinterpret_cast<const __bf16 *>(buf) + pa + 8 * s;
       const int ga = 2 * s, gb = 2 * s + 1;
       const int oa = SIN * (ga / G::G4) * G::Vp + (ga % G::G4) * 4;
       const int ob = SIN * (gb / G::G4) * G::Vp + (gb % G::G4) * 4;
-      const __bf16 *Q = reinterpret_cast<const __bf16 *>(buf + 3 * G::PPL) + qb;
+      const __bf16 *Q = reinterpret_cast<const __bf16 *>(buf + NPL * G::PPL) + qb;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < NPL; ++pl) {
         f.a[pl] = *reinterpret_cast<const bf16x8_t *>(P + pl * (G::PPL / 2));
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -912,17 +937,19 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
     };
     auto mm = [&](const Frag &f) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma_x(f.a[0], f.b[0][t], acc[t]);
+      for (int t = 0; t < NT; ++t) acc[t] = mfma_p<NPL>(f.a[0], f.b[0][t], acc[t]);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0], f.b[1][t], acl[t]);
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_p<NPL>(f.a[0], f.b[1][t], acl[t]);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[1], f.b[0][t], acl[t]);
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_p<NPL>(f.a[1], f.b[0][t], acl[t]);
+      if constexpr (NPL == 3) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0], f.b[2][t], acl[t]);
+        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0], f.b[2 % NPL][t], acl[t]);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[1], f.b[1][t], acl[t]);
+        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[1], f.b[1][t], acl[t]);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[2], f.b[0][t], acl[t]);
+        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[2 % NPL], f.b[0][t], acl[t]);
+      }
     };
     for (int it = it0; it < it1; ++it) {
       const char *cur = lds + (G::NBUF == 2 ? ((it - it0) & 1) * G::BUF : 0);
@@ -970,7 +997,10 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int r = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-        if (r < p.R && c < p.C) slab[((int64_t)r * p.C + c) * 9 + q0 + t] = acc[t][i] + acl[t][i];
+        if (r < p.R && c < p.C)
+          slab[((int64_t)r * p.C + c) * 9 + q0 + t] =
+              NPL == 2 ? (acc[t][i] + acl[t][i]) * pow2f(-p_se) * pow2f(-q_se)
+                       : acc[t][i] + acl[t][i];
       }
   };
   if (it0 < it1) {
@@ -997,9 +1027,19 @@ bool plan_wgrad_x3(WgradParams &w) {
   return true;
 }
 
-hipError_t launch_wgrad_x3(const WgradParams &p, hipStream_t s) {
-  if (p.bf16 != 3 || p.V != 18 || (p.s_in != 1 && p.s_in != 2)) return hipErrorInvalidValue;
-  const int nblk = p.n_rtiles * p.n_jtiles * p.S;
+hipError_t launch_wgrad_x3(const WgradParams &p0, hipStream_t s) {
+  if (p0.bf16 != 3 || p0.V != 18 || (p0.s_in != 1 && p0.s_in != 2)) return hipErrorInvalidValue;
+  const int nblk = p0.n_rtiles * p0.n_jtiles * p0.S;
+  if (p0.f16x2) {  // 2-way fp16 splits (NPL = 2)
+    if (!p0.amax_p || !p0.amax_q) return hipErrorInvalidValue;
+    const WgradParams &p = p0;
+    if (p.s_in == 1)
+      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2>::LDS), s, p);
+    else
+      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2>::LDS), s, p);
+    return hipGetLastError();
+  }
+  const WgradParams &p = p0;
   if (p.s_in == 1) {
     constexpr int lds = WgX3Geo<18, 1>::LDS;
     hipLaunchKernelGGL((k_wgrad_x3<18, 1>), dim3(nblk), dim3(512), lds, s, p);

@@ -47,8 +47,8 @@ def test_check_desc_accepts_north_star_shapes(pkg, lib):
                # STGCN_F_BF16 (cfg3 / cfg5 shapes, residual + bf16)
                dict(flags=2, V=25, K=3), dict(flags=2, V=50, K=3, C_in=128, C_out=256, stride=2,
                                                T_out=150), dict(flags=3, V=18),
-               # STGCN_F_F32X3 (fp32 via bf16 splits), plain and residual
-               dict(flags=4), dict(flags=5, V=25, K=3)):
+               # STGCN_F_F32X3 (fp32 via bf16 splits), plain and residual; + STGCN_F_F16X2
+               dict(flags=4), dict(flags=5, V=25, K=3), dict(flags=12)):
         d = _desc(pkg, **kw)
         assert lib.stgcn_check_desc(ctypes.byref(d)) == 0, kw
         assert lib.stgcn_fwd_workspace_bytes(ctypes.byref(d)) > 0
@@ -56,7 +56,7 @@ def test_check_desc_accepts_north_star_shapes(pkg, lib):
 
 
 @pytest.mark.parametrize("kw,code", [
-    (dict(flags=8), -2), (dict(flags=6), -1), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
+    (dict(flags=16), -2), (dict(flags=8), -1), (dict(flags=10), -1), (dict(flags=6), -1), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
     (dict(T_out=299), -1), (dict(N=0), -1), (dict(V=300), -2)])
 def test_check_desc_rejects(pkg, lib, kw, code):
     d = _desc(pkg, **kw)
@@ -128,6 +128,11 @@ def test_block_plan_pins_the_paths(pkg, lib):
     p = plan(flags=2, V=25, K=3)
     assert p & hl.PLAN_SP_FWD_FUSED and p & hl.PLAN_SP_BWD_FUSED and not p & hl.PLAN_FOLD, p
     assert plan() == 0
+    # STGCN_F_F16X2 (with F32X3): the folded GEMMs on fp16 splits; unfolded blocks unchanged
+    p = plan(flags=12)
+    assert p & hl.PLAN_FOLD and p & hl.PLAN_F16X2, p
+    assert not plan(flags=12, C_in=3) & hl.PLAN_F16X2
+    assert not plan(flags=13) & hl.PLAN_F16X2
     d = _desc(pkg, N=0)
     out = ctypes.c_uint32(7)
     assert lib.stgcn_block_plan(ctypes.byref(d), ctypes.byref(out)) == -1

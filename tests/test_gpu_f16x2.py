@@ -1,0 +1,93 @@
+"""GPU parity of the fp32 block with STGCN_F_F16X2 (``gemm="f16x2"``): the
+folded block's temporal GEMMs (forward, data-grad incl. the stride-2 phases,
+weight-grad; st-gcn_amd/csrc/kernels_x3.hip NPL = 2) as 2-way fp16 splits of
+operands scaled by powers of two from their max |x| (x s = h + l, 22
+significant bits; three partial products hh, hl, lh; fp32 accumulate).
+
+The mode claims fp32-GEMM accuracy, so it is held to the SAME gate as the fp32
+MFMA path and the bf16x3 path (test_gpu_block.py): rel-to-max
+error vs the fp64 oracle below 1e-5 per output and gradient (or below twice
+the fp32 reference's own error where that is larger), ReLU ties as there.
+Each folded case also checks that the plan selected the fp16 splits and that
+their results differ from the bf16x3 path's (the kernels ran). The scale
+cases multiply the input by 1e-6 and 1e5: a fixed scale would underflow or
+overflow fp16 there, the max-derived power-of-two scales must not.
+"""
+import pytest
+import torch
+
+from test_gpu_block import _compare, _oracle, _random_case, _run_hip
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(pkg, arrays, x, g, need_dx=True):
+    got = _run_hip(pkg, arrays, x, g, need_dx=need_dx, gemm="f16x2")
+    want, floor = _oracle(arrays, got)
+    if not need_dx:
+        want.pop("grad.x")
+    _compare(got, want, floor=floor)
+    return got
+
+
+def _plan(pkg, x, C_out, stride, K=1):
+    return pkg.hip_lib.block_plan(pkg.fused.make_desc(
+        tuple(x.shape), C_out, K, stride, 4, 1e-5, 0.1, True, f16x2=True))
+
+
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T
+    (64, 64, 1, 18, 1, 4, 64),      # cfg2 L1-L3 shape (64-row tiles)
+    (64, 128, 2, 18, 1, 3, 37),     # stride 2: the data-grad phases (NQ = 5 / 4), odd T
+    (128, 128, 1, 18, 1, 2, 40),    # 128-row tiles (MR = 2)
+    (128, 256, 2, 18, 1, 2, 30),    # 128-row tiles, stride-2 forward, 8 chunks
+    (256, 256, 1, 18, 1, 2, 19),    # 16 chunks, ragged T
+    (24, 40, 1, 18, 1, 2, 23),      # partial channel chunk (24 = 16 + 8), partial rows
+    (16, 16, 1, 18, 1, 2, 9),       # smallest folded block
+])
+def test_f16x2_block_random(pkg, case):
+    arrays, x, g = _random_case(pkg, *case)
+    got = _check(pkg, arrays, x, g)
+    C_in, C_out, stride = case[:3]
+    plan = _plan(pkg, x, C_out, stride)
+    hl = pkg.hip_lib
+    assert plan & hl.PLAN_FOLD and plan & hl.PLAN_F16X2, plan
+    ref = _run_hip(pkg, arrays, x, g, gemm="f32x3")
+    assert not torch.equal(got["y"], ref["y"]), "fp16-split forward did not run"
+    assert not torch.equal(got["grad.temporalConv.weight"], ref["grad.temporalConv.weight"])
+
+
+@pytest.mark.parametrize("scale", [1e-6, 1e5])
+def test_f16x2_operand_scales(pkg, scale):
+    """Input (hence G) and output gradient far from O(1): the power-of-two
+    operand scales keep every GEMM at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, 64, 128, 1, 18, 1, 2, 33, seed=3)
+    x = x * scale
+    arrays["x"] = x.numpy()
+    g = g * (1.0 / scale)
+    arrays["g"] = g.numpy()
+    _check(pkg, arrays, x, g)
+
+
+def test_f16x2_full_size_block(pkg):
+    """cfg2 L1-type shape at N = 32, T = 300 (the bench layer) at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, 64, 64, 1, 18, 1, 32, 300, seed=7)
+    got = _check(pkg, arrays, x, g)
+    for k, v in got.items():
+        assert torch.isfinite(v).all(), k
+
+
+def test_f16x2_unfolded_blocks_keep_bf16x3(pkg):
+    """Where the block does not fold (first block C_in = 3, residual, K = 3) the
+    flag changes nothing: the plan has no F16X2 bit and the results are
+    bit-identical to the bf16x3 path."""
+    hl = pkg.hip_lib
+    for case, residual in (((3, 64, 1, 18, 1, 2, 30), False), ((64, 64, 1, 18, 1, 2, 30), True)):
+        arrays, x, g = _random_case(pkg, *case, residual=residual)
+        d = pkg.fused.make_desc(tuple(x.shape), case[1], 1, case[2], 4, 1e-5, 0.1, True,
+                                residual=residual, f16x2=True)
+        assert not hl.block_plan(d) & hl.PLAN_F16X2
+        a = _run_hip(pkg, arrays, x, g, gemm="f16x2")
+        b = _run_hip(pkg, arrays, x, g, gemm="f32x3")
+        for k in a:
+            assert torch.equal(a[k], b[k]), k

@@ -171,7 +171,7 @@ def test_stack_cfg1_matches_reference(pkg):
 
 
 @pytest.mark.parametrize("residual,gemm", [(False, "fp32"), (True, "fp32"), (False, "bf16"),
-                                            (False, "x3"), (True, "x3")])
+                                            (False, "x3"), (True, "x3"), (False, "f16")])
 def test_stack_chain_small_bn2_gamma(pkg, residual, gemm):
     """The chain link with BN2 gammas at 0 and 1e-4 on some channels of every
     block: rebuilding uhat = (y - b2) / g2 from the block
@@ -189,7 +189,7 @@ def test_stack_chain_small_bn2_gamma(pkg, residual, gemm):
         A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(V))
     kw = dict(residual=residual,
               gemm_dtype=torch.bfloat16 if gemm == "bf16" else torch.float32,
-              f32_gemm="bf16x3" if gemm == "x3" else "mfma")
+              f32_gemm={"x3": "bf16x3", "f16": "f16x2"}.get(gemm, "mfma"))
     torch.manual_seed(11)
     with contextlib.redirect_stdout(io.StringIO()):
         m1 = pkg.STGCNStack(3, 10, A, **kw).cuda().train()
@@ -290,6 +290,7 @@ def test_stack_chain_matches_unchained(pkg, residual, drop):
 
 
 @pytest.mark.parametrize("V,K,gemm,T", [(18, 1, "fp32", 40), (18, 1, "x3", 300),
+                                         (18, 1, "f16", 300),
                                          (25, 3, "bf16", 40), (50, 3, "bf16", 24),
                                          (25, 3, "fp32", 40)])
 def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
@@ -306,7 +307,7 @@ def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
         A = gr.get_normalized_adjacency_matrices(2, 1, distances=gr.synthetic_distances(V),
                                                  graph=gr.graph_for(V))
     kw = dict(gemm_dtype=torch.bfloat16 if gemm == "bf16" else torch.float32,
-              f32_gemm="bf16x3" if gemm == "x3" else "mfma")
+              f32_gemm={"x3": "bf16x3", "f16": "f16x2"}.get(gemm, "mfma"))
     deferred = []
     orig = pkg.fused._chain_publish
 
@@ -462,9 +463,11 @@ def test_stack_bf16_cfg3_shape(pkg):
 
 # --- the exact benched configuration (round 2) --------------------------------
 
-def test_stack_cfg1_benched_path_matches_reference(pkg):
+@pytest.mark.parametrize("f32_gemm", ["bf16x3", "f16x2"])
+def test_stack_cfg1_benched_path_matches_reference(pkg, f32_gemm):
     """bench.py's step on the cfg1 golden case: STGCNStack(f32_gemm="bf16x3")
-    (temporal GEMMs as exact bf16 splits), StackChain cross-block fusion and the
+    (temporal GEMMs as exact bf16 splits) or "f16x2" (the folded blocks' GEMMs
+    as scaled 2-way fp16 splits), StackChain cross-block fusion and the
     fused HIP head (forward_loss: avg-pool + Linear + cross entropy). Logits and
     loss against the reference's fixture; gradients against the fp64 oracle
     differentiated through the HIP run's ReLU masks (which may differ from
@@ -474,7 +477,7 @@ def test_stack_cfg1_benched_path_matches_reference(pkg):
     A = torch.from_numpy(load_npz("adjacency.npz")["V18_s0_d1"])
     torch.manual_seed(0)
     with contextlib.redirect_stdout(io.StringIO()):
-        model = pkg.STGCNStack(3, 2, A, f32_gemm="bf16x3")
+        model = pkg.STGCNStack(3, 2, A, f32_gemm=f32_gemm)
     model = model.cuda().train()
     masks, unhook = capture_relu_masks(model)
     x = torch.from_numpy(ref["x"]).cuda().permute(0, 3, 1, 2).contiguous()
@@ -499,16 +502,17 @@ def test_stack_cfg1_benched_path_matches_reference(pkg):
             assert rel_to_max(v.cpu().numpy(), ref["after." + k]) < 1e-4, k
 
 
-@pytest.mark.parametrize("residual", [False, True])
-def test_stack_chain_matches_unchained_bf16x3(pkg, residual):
+@pytest.mark.parametrize("residual,f32_gemm", [(False, "bf16x3"), (True, "bf16x3"),
+                                               (False, "f16x2")])
+def test_stack_chain_matches_unchained_bf16x3(pkg, residual, f32_gemm):
     """StackChain in the benched bf16x3 mode (at the bench's T = 300) gives the
     same results as the blocks run one by one, through the fused head."""
     gr = pkg.graph
     A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
     torch.manual_seed(3)
     with contextlib.redirect_stdout(io.StringIO()):
-        m1 = pkg.STGCNStack(3, 400, A, residual=residual, f32_gemm="bf16x3").cuda().train()
-        m2 = pkg.STGCNStack(3, 400, A, residual=residual, f32_gemm="bf16x3").cuda().train()
+        m1 = pkg.STGCNStack(3, 400, A, residual=residual, f32_gemm=f32_gemm).cuda().train()
+        m2 = pkg.STGCNStack(3, 400, A, residual=residual, f32_gemm=f32_gemm).cuda().train()
     m2.load_state_dict(m1.state_dict())
     x = torch.randn(4, 3, 300, 18, generator=torch.Generator().manual_seed(4)).cuda()
     lab = torch.randint(0, 400, (4,), generator=torch.Generator().manual_seed(5)).cuda()
