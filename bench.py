@@ -267,7 +267,11 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # channels) in place of Z, and the data gradient writes H (C_in)
             fold = x3 and K == 1 and V == 18 and ci >= 16
             CZ = ci if fold else co
-            act = {0: N * (CZ * t * V2 + co * to * V4), 1: N * (co * to * V2 + CZ * t * VZ),
+            # (the folded block's data gradient carries the SpatialConv backward:
+            # it reads x and writes dxhat instead of writing H)
+            act = {0: N * (CZ * t * V2 + co * to * V4),
+                   1: (N * (co * to * V2 + 2 * ci * t * V4) if fold else
+                       N * (co * to * V2 + CZ * t * VZ)),
                    2: N * (co * to * V2 + CZ * t * V2),
                    3: N * (ci * t * V4 + co * t * V2) + (N * K * ci * t * V * 2
                                                        if cfg["bf16"] and ci >= 16 else
@@ -306,9 +310,9 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 # temporal GEMMs: k_conv_x3 with one operand plane (NPL = 1)
                 ib = "true" if ab else "false"  # bf16 input instance
                 ft, cb = {18: (8, 64), 25: (4, 64), 50: (4, 32)}.get(V, (0, 0))
-                sym = {0: f"k_conv_x3<9,3,{V},{s},1,1,{ib}>",
-                       1: (f"k_conv_x3<9,3,{V},1,1,1,{ib}>" if s == 1 else
-                           f"k_conv_x3<5|4,{V},1,1,1,{ib}>"),
+                sym = {0: f"k_conv_x3<9,3,{V},{s},1,1,{ib},false>",
+                       1: (f"k_conv_x3<9,3,{V},1,1,1,{ib},false>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,1,{ib},false>"),
                        2: f"k_wgrad_bf16<9,{V},{s},{ft},{cb},{ib}>",
                        3: (f"k_conv_bf16<1,16,{V},1,false>" if ci < 16 else
                            f"k_sp_fwd_bf16<{V},{K}>" if not (V == 50 or (V == 25 and K == 3)) else
@@ -317,9 +321,10 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             elif x3 and V in (18, 25):
                 mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
                 npl = 2 if f16 and fold else 3  # operand planes: fp16 (h, l) or bf16 (h, m, l)
-                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false>",
-                       1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false>" if s == 1 else
-                           f"k_conv_x3<5|4,{V},1,1,{npl},false>"),
+                spb = "true" if fold else "false"  # the fused SpatialConv backward epilogue
+                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false,false>",
+                       1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false,{spb}>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,{npl},false,{spb}>"),
                        2: f"k_wgrad_x3<{V},{s},{npl}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
@@ -589,7 +594,7 @@ def main():
             # the products per fp32 product (6 for bf16 x3, 3 for the fp16 x2 planes)
             split = sym.startswith("k_conv_x3") or sym.startswith("k_wgrad_x3")
             fpeak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
-                     (F16X2_PEAK_TFLOPS if sym.rstrip(">").split(",")[-2 if sym.startswith(
+                     (F16X2_PEAK_TFLOPS if sym.rstrip(">").split(",")[-3 if sym.startswith(
                          "k_conv_x3") else -1].strip() == "2" else X3_PEAK_TFLOPS) if split
                      else MFMA_F32_PEAK_TFLOPS)
             # the roof that bounds the kernel's algorithmic work: MFMA or HBM

@@ -64,3 +64,6 @@
 #ifndef STGCN_AB_BWD6_EXACT     // exact-split k_spatial_bwd6 for bf16 blocks
 #define STGCN_AB_BWD6_EXACT 0
 #endif
+#ifndef STGCN_AB_SPB_PAIR        // the folded block's H stored + k_spatial_bwd5 (no fused epilogue)
+#define STGCN_AB_SPB_PAIR 0
+#endif

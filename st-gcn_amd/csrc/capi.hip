@@ -117,6 +117,11 @@ bool fold_w(const stgcn_desc_t *d) {
   return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->V == 18 &&
          !fused_spb(d);
 }
+// The folded block's SpatialConv backward inside its data gradient (kernels_x3.hip
+// spb_epilogue): dxhat = H A, dA, the BN1 / chain sums from the tile while H is
+// on chip (STGCN_AB_SPB_PAIR build: H stored + k_spatial_bwd5, A/B only)
+bool fold_spb(const stgcn_desc_t *d) { return fold_w(d) && STGCN_AB_SPB_PAIR == 0; }
+
 // The folded block's temporal GEMMs on 2-way fp16 splits (STGCN_F_F16X2; k_conv_x3 /
 // k_wgrad_x3 with NPL = 2), operand scales from max |x| words (launch_absmax)
 bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
@@ -564,7 +569,7 @@ int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan) {
   uint32_t f = 0;
   if (fold_w(d)) f |= STGCN_PLAN_FOLD;
   if (fused_sp(d)) f |= STGCN_PLAN_SP_FWD_FUSED;
-  if (fused_spb(d)) f |= STGCN_PLAN_SP_BWD_FUSED;
+  if (fused_spb(d) || fold_spb(d)) f |= STGCN_PLAN_SP_BWD_FUSED;
   if (act_bf16(d)) f |= STGCN_PLAN_ACT_BF16;
   if (!fold_w(d) && !fused_sp(d)) {  // the spatial dW' GEMM of the unfolded block
     WgradParams w = make_wgrad(d, nullptr, 0, d->C_out, d->T, nullptr, 0, d->K * d->C_in, d->T,
@@ -816,6 +821,27 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
 
   // dZ in bf16 where every reader takes it (needs the kept G: k_wgrad_gemm_gk)
   const bool dzb = dz_bf16(d) && a->G != nullptr;
+  // Deferred dx (ABI 5): the BN1 backward apply of this block is folded into the
+  // previous block's ReLU+BN2 backward apply (launch_bn_relu_bwd_apply with
+  // dy_coef). The spatial backward then reads the previous block's U in place of
+  // x (PrevBn: x rebuilt, that block's mask / uhat sums), dx receives dxhat, and
+  // launch_chain_coef forms dg1 / db1, the coefficients and the previous block's
+  // ReLU+BN2 sums: dx never makes its own HBM round trip.
+  const bool defer = d->need_dx && d->training && !res && a->prev_g2 && a->prev_b2 &&
+                     a->prev_sums && a->prev_U && a->prev_stats && a->x_stats && a->dx_coef &&
+                     a->dx_deferred &&
+                     (fused_spb(d) || fold_spb(d) || spatial_dx_prev_supported(N, C, T, V, K));
+  PrevBn pvb;
+  if (defer) {
+    pvb.mean = a->prev_stats;
+    pvb.invstd = a->prev_stats + C;
+    pvb.g = a->prev_g2;
+    pvb.b = a->prev_b2;
+    pvb.s1 = L.s1;
+    pvb.s2 = L.s2;
+  }
+  const float *xin = defer ? a->prev_U : a->x;
+  if (a->dx_deferred) *a->dx_deferred = defer ? 1 : 0;
   if (fold_w(d)) {
     // The folded block (kernels_fold.hip): Wc_q = Wt_q W'; the data gradient
     // with Wc gives H = W'^T dZ directly (C_in channels), the weight gradient
@@ -826,6 +852,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       Wc = L.Wc;
     }
     HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));
+    if (fold_spb(d)) {  // dbW and the bias part of dA first: the data gradient adds to dA
+      HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
+      HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
+    }
     if (f16x2(d)) {  // the fp16 splits' operand scales: max |dU|, max |Wc|
       HIP_TRY(launch_absmax(L.dU, (int64_t)N * R * To * V, L.amax, s));
       HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
@@ -838,6 +868,20 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
         p.f16x2 = 1;
         p.amax_in = L.amax;
         p.amax_w = L.amax + 1;
+      }
+      if (fold_spb(d)) {  // dxhat -> dx; BN1 / chain sums and dA from the tile (H on chip)
+        p.spb = 1;
+        p.out = d->need_dx ? a->dx : nullptr;
+        p.sx = xin;
+        p.sA = a->A;
+        p.mean1 = mean1;
+        p.invstd1 = invstd1;
+        p.g1 = a->g1;
+        p.b1 = a->b1;
+        if (defer) p.prev = pvb;
+        p.sd = L.sd;
+        p.sdn = L.sdn;
+        p.dA = a->dA;
       }
       p.in_bstride = (int64_t)R * To * V;
       p.out_bstride = (int64_t)C * T * V;
@@ -986,30 +1030,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   }
   // sum_{n,t} dZ: from the temporal weight and the per-tap dU sums on the
   // non-residual block (dZ = conv^T(dU)); the residual block's dZ passes BN2
-  if (cols_sums(d)) HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
-  HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
-  // Deferred dx (ABI 5): the BN1 backward apply of this block is folded into the
-  // previous block's ReLU+BN2 backward apply (launch_bn_relu_bwd_apply with
-  // dy_coef). The spatial backward then reads the previous block's U in place of
-  // x (PrevBn: x rebuilt, that block's mask / uhat sums), dx receives dxhat, and
-  // launch_chain_coef forms dg1 / db1, the coefficients and the previous block's
-  // ReLU+BN2 sums: dx never makes its own HBM round trip.
-  const bool defer = d->need_dx && d->training && !res && a->prev_g2 && a->prev_b2 &&
-                     a->prev_sums && a->prev_U && a->prev_stats && a->x_stats && a->dx_coef &&
-                     a->dx_deferred &&
-                     (fused_spb(d) || spatial_dx_prev_supported(N, C, T, V, K));
-  PrevBn pvb;
-  if (defer) {
-    pvb.mean = a->prev_stats;
-    pvb.invstd = a->prev_stats + C;
-    pvb.g = a->prev_g2;
-    pvb.b = a->prev_b2;
-    pvb.s1 = L.s1;
-    pvb.s2 = L.s2;
+  // (the fused folded backward did both before its data gradient)
+  if (!fold_spb(d)) {
+    if (cols_sums(d)) HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
+    HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
   }
-  const float *xin = defer ? a->prev_U : a->x;
-  if (a->dx_deferred) *a->dx_deferred = defer ? 1 : 0;
-  if (fused_spb(d)) {
+  if (fold_spb(d)) {
+    // (done in the folded block's data gradient: kernels_x3.hip spb_epilogue)
+  } else if (fused_spb(d)) {
     // H = W'^T dZ, dx = sum_k H_k A_k, dA, BN1 sums in one kernel (H stays on chip)
     HIP_TRY(launch_sp_bwd_fused(L.dZ, xin, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.wpk,
                                 a->dx, a->dA, L.sd, L.sdn, N, C, R, T, V, K, d->need_dx, res,
@@ -1244,6 +1272,20 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       P.ax[1] = w;
       P.an[1] = (int64_t)R * CZ * 9;
     }
+    if (fold_spb(d)) {  // the fused SpatialConv backward epilogue and its operands
+      p.spb = 1;
+      p.sx = c.take<float>((size_t)N * C * T * V);
+      p.sA = c.take<float>((size_t)V * V);
+      float *st = c.take<float>((size_t)4 * C);
+      p.mean1 = st;
+      p.invstd1 = st + C;
+      p.g1 = st + 2 * C;
+      p.b1 = st + 3 * C;
+      double *sd = c.take<double>((size_t)2 * C);
+      p.sd = sd;
+      p.sdn = sd + C;
+      p.dA = c.take<float>((size_t)V * V);
+    }
     if (d->stride == 1) {
       p.w = w ? w + 8 : nullptr;
       p.w_sq = -1;
@@ -1267,7 +1309,8 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
         if (p.M > 0) P.cp[P.ncp++] = p;
       }
     }
-    P.flops = tflops;
+    // (fused: + the joint contractions dxhat = H A and dA = H^T BN1(x))
+    P.flops = tflops + (fold_spb(d) ? 4.0 * K * C * (double)T * V * V * N : 0.0);
   } else if (which == 2) {
     const float *dU = c.take<float>((size_t)N * R * To * V);
     const float *Z = c.take<float>((size_t)N * CZ * T * V);
@@ -1379,6 +1422,7 @@ size_t stgcn_time_kernel_bytes(const stgcn_desc_t *d, int which) {
   if (stgcn_check_desc(d) != STGCN_OK || which < 0 || which > 6) return 0;
   if (which >= 5 && fused_spb(d) && !fused_spb50(d)) return 0;
   if ((which == 3 || which == 5) && fold_w(d)) return 0;  // (no spatial / H GEMM there)
+  if (which >= 4 && fold_spb(d)) return 0;  // (inside the data gradient, which 1)
   return plan_timed(d, which, nullptr).bytes;
 }
 
@@ -1392,6 +1436,9 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
     return fail(STGCN_E_UNSUPPORTED, "the spatial backward is one fused kernel here (which 4)");
   if ((which == 3 || which == 5) && fold_w(d))
     return fail(STGCN_E_UNSUPPORTED, "the folded block has no spatial / H GEMM");
+  if (which >= 4 && fold_spb(d))
+    return fail(STGCN_E_UNSUPPORTED, "the folded block's spatial backward runs inside its data "
+                                     "gradient (which 1)");
   TimedPlan P = plan_timed(d, which, scratch);
   if (!scratch || scratch_bytes < P.bytes) return fail(STGCN_E_INVALID, "scratch too small");
   hipStream_t s = (hipStream_t)stream;

@@ -80,6 +80,17 @@ struct ConvGemmParams {
   // device words holding max |in| / max |w| as float bits (f16x2_scale)
   int f16x2;
   const unsigned *amax_in, *amax_w;
+  // spb (the folded block's data gradient, V = 18, K = 1; kernels_x3.hip
+  // spb_epilogue): the tile holds H = W'^T dZ (rows = input channels). Instead of
+  // storing H the epilogue forms dxhat = H A (stored to out, null: not stored),
+  // the BN1 backward sums sd / sdn (and, prev.mean set, the deferred-dx chain's
+  // s1 / s2 over the previous block's U read from sx) and dA += H^T BN1(x):
+  // the SpatialConv backward never round-trips H through HBM.
+  int spb;
+  const float *sx, *sA, *mean1, *invstd1, *g1, *b1;
+  PrevBn prev;
+  double *sd, *sdn;
+  float *dA;
 };
 
 // Weight-gradient GEMM with split-K partial slabs:

@@ -197,9 +197,225 @@ struct ConvX3Geo {
   static_assert((ROWS * kEpiPitch + ROWS * V) * 4 <= LDS, "row-major epilogue image fits");
 };
 
+// ---------------------------------------------------------------------------
+// The folded block's SpatialConv backward fused into its data gradient's
+// epilogue (capi.hip fold_spb; the backward of st_graphconv.py:148-150 with
+// K = 1, V = 18 -- north star: the spatial and temporal halves in one kernel,
+// A pinned in LDS / scalar registers, H never in HBM). The tile's accumulators
+// hold H = sum_q Wc_q^T dU (rows = input channels c, columns = 14 frames x 18
+// joints; frame t = s_out m + p_out covers the stride-2 phases too). In halves
+// of 64 rows (MR = 2: the waves of row half h hand their accumulators over):
+//   1. H -> LDS image; the tile's x rows (deferred dx: the previous block's U)
+//      -> LDS by 4-byte LDS-DMA (column offsets per lane, OOB -> 0);
+//   2. thread (row, frame group): dxhat[w] = sum_v H[v] A[v][w] (A from scalar
+//      registers), x rebuilt as k_spatial_bwd5's row pass does (prev mode: ReLU(
+//      BN2_prev(U)), its mask and uhat), BN1(x) written back over x, the BN1
+//      sums sd += dxhat, sdn += dxhat (x - mu) invstd (prev: s1, s2) reduced
+//      over the row's 8 threads into fp64 atomics, dxhat stored (8-byte stores);
+//   3. dA partials: thread = (6-joint v block, 6-joint w block, 1/56 of the
+//      (row, frame) pairs), 36 register accumulators over both halves;
+// then the partials meet in LDS and each dA entry is summed in a fixed order
+// and added atomically (as k_spatial_bwd5 does). Arithmetic per element is
+// that of k_spatial_bwd5 (fp32, sums in fp64), so the results match it.
+// ---------------------------------------------------------------------------
+constexpr int kSpbAt = 18 * 20;  // A transposed, rows padded to 20 (16-byte aligned)
+// H and x images of one 64-row half + A^T
+constexpr int kSpbLds = (2 * 64 * kEpiPitch + kSpbAt) * 4;
+
+template <int MR>
+__device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
+                                             float *smem, int n, int r0, int m0, int mi,
+                                             int nj0) {
+  constexpr int V = 18, FT = kTileCols / V, NCOLS = FT * V, P = kEpiPitch;
+  constexpr int NSUB = 56;  // threads per (v block, w block) combination of dA
+  float *const Himg = smem, *const Ximg = smem + 64 * P, *const At = smem + 2 * 64 * P;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int C = p.R, T = p.T_dst;
+  const int nvf = min(FT, p.M - m0);  // valid frame slots of the tile
+  // x DMA: compacted column j = k * 64 + lane of a row -> float offset in a channel
+  unsigned coff[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = k * 64 + lane, mf = j / V, w = j - mf * V;
+    const int t = p.s_out * (m0 + mf) + p.p_out;
+    coff[k] = (j < NCOLS && mf < nvf && t < T) ? (unsigned)(t * V + w) : kOOB;
+  }
+  const int64_t cT = (int64_t)T * V;  // floats per channel
+  const uint64_t xsrc = reinterpret_cast<uint64_t>(p.sx + (int64_t)n * C * cT);
+  const int64_t xbytes = (int64_t)C * cT * 4;
+  const int4v rsx = {(int)(uint32_t)xsrc, (int)((xsrc >> 32) & 0xffff),
+                     (int)(xbytes > 0x7fffffff ? 0x7fffffff : xbytes), 0x00020000};
+  const bool pv = p.prev.mean != nullptr;
+  const int combo = tid / NSUB, sub = tid - combo * NSUB;
+  const int vb = combo / 3, wb = combo - (combo / 3) * 3;
+
+#pragma unroll
+  for (int h = 0; h < MR; ++h) {
+    __syncthreads();  // every wave is done with the main loop's buffers / the last half
+    if (MR == 1 || mi == h) {
+#pragma unroll
+      for (int rb = 0; rb < MR; ++rb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc_to_img(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
+    }
+    if (h == 0)  // A^T[w][v] (broadcast LDS reads in the contraction)
+      for (int i = tid; i < kSpbAt; i += 512) {
+        const int w = i / 20, v = i - w * 20;
+        At[i] = v < V ? p.sA[v * V + w] : 0.f;
+      }
+    asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
+    for (int rr = wave; rr < 64; rr += 8) {
+      const int c = r0 + h * 64 + rr;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned voff = (c < C && coff[k] != kOOB) ? ((unsigned)(c * cT) + coff[k]) * 4u : kOOB;
+        const unsigned m0v = (unsigned)reinterpret_cast<uintptr_t>(Ximg + rr * P + k * 64);
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+            "buffer_load_dword %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(m0v), "v"(voff), "s"(rsx)
+            : "memory");
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
+      const int rl = tid >> 3, fg = tid & 7;
+      const int c = r0 + h * 64 + rl;
+      const bool rok = c < C;
+      const float mu = rok ? p.mean1[c] : 0.f, is = rok ? p.invstd1[c] : 0.f;
+      const float a = is * (rok ? p.g1[c] : 0.f), be = rok ? p.b1[c] : 0.f;
+      const float pmu = pv && rok ? p.prev.mean[c] : 0.f, pis = pv && rok ? p.prev.invstd[c] : 1.f;
+      const float pa = pv && rok ? pis * p.prev.g[c] : 1.f, pb = pv && rok ? p.prev.b[c] : 0.f;
+      double sv[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int f = fg; f < nvf; f += 8) {
+        const float *hr = Himg + rl * P + f * V;
+        float *xr = Ximg + rl * P + f * V;
+        float hv[V];
+#pragma unroll
+        for (int i = 0; i < V / 2; ++i) {
+          const float2 a2 = *reinterpret_cast<const float2 *>(hr + 2 * i);
+          hv[2 * i] = a2.x;
+          hv[2 * i + 1] = a2.y;
+        }
+        float *dst = (p.out && rok) ? p.out + ((int64_t)n * C + c) * cT +
+                                          (int64_t)(p.s_out * (m0 + f) + p.p_out) * V
+                                    : nullptr;
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int i = 0; i < V / 2; ++i) {  // joints w = 2i, 2i + 1
+          float d[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float *ac = At + (2 * i + e) * 20;
+            float acc1 = 0.f;
+#pragma unroll
+            for (int v4 = 0; v4 < 20; v4 += 4) {
+              const float4 q = *reinterpret_cast<const float4 *>(ac + v4);
+              acc1 = fmaf(hv[v4], q.x, acc1);
+              acc1 = fmaf(hv[v4 + 1], q.y, acc1);
+              if (v4 + 2 < V) acc1 = fmaf(hv[v4 + 2], q.z, acc1);
+              if (v4 + 3 < V) acc1 = fmaf(hv[v4 + 3], q.w, acc1);
+            }
+            d[e] = acc1;
+          }
+          const float2 x2 = *reinterpret_cast<const float2 *>(xr + 2 * i);
+          float xs[2] = {x2.x, x2.y};
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            float xx = xs[e], uh = 0.f;
+            bool pm = false;
+            if (pv) {  // the previous block's output x = ReLU(BN2(U)) as its output pass formed it
+              const float t = (xx - pmu) * pa + pb;
+              uh = (xx - pmu) * pis;
+              pm = t > 0.f;
+              xx = pm ? t : 0.f;
+            }
+            const float bn = (xx - mu) * a + be;
+            s0 += d[e];
+            s1 = fmaf(d[e], (xx - mu) * is, s1);
+            if (pm) {
+              s2 += d[e];
+              s3 = fmaf(d[e], uh, s3);
+            }
+            xs[e] = rok ? bn : 0.f;
+          }
+          *reinterpret_cast<float2 *>(xr + 2 * i) = make_float2(xs[0], xs[1]);
+          if (dst) *reinterpret_cast<float2 *>(dst + 2 * i) = make_float2(d[0], d[1]);
+        }
+        sv[0] += s0;
+        sv[1] += s1;
+        sv[2] += s2;
+        sv[3] += s3;
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv[i] += __shfl_xor(sv[i], o, 64);
+      if (fg == 0 && rok) {
+        atomicAdd(p.sd + c, sv[0]);
+        atomicAdd(p.sdn + c, sv[1]);
+        if (pv) {
+          atomicAdd(p.prev.s1 + c, sv[2]);
+          atomicAdd(p.prev.s2 + c, sv[3]);
+        }
+      }
+    }
+    __syncthreads();  // BN1(x) and H images complete
+    // dA partials over this half's (row, frame) pairs: thread = (v block, w block,
+    // 1 / 56 of the pairs), then the partials meet in LDS (over the H image) and
+    // each entry is summed over its 56 threads in a fixed order
+    float dacc[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) dacc[i] = 0.f;
+    if (combo < 9) {
+      for (int q = sub; q < 64 * FT; q += NSUB) {
+        const int rr = q / FT, f = q - rr * FT;
+        if (f >= nvf) continue;
+        const float *hr = Himg + rr * P + f * V + vb * 6;
+        const float *xr = Ximg + rr * P + f * V + wb * 6;
+        float hv[6], xv[6];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const float2 a2 = *reinterpret_cast<const float2 *>(hr + 2 * i);
+          const float2 b2 = *reinterpret_cast<const float2 *>(xr + 2 * i);
+          hv[2 * i] = a2.x;
+          hv[2 * i + 1] = a2.y;
+          xv[2 * i] = b2.x;
+          xv[2 * i + 1] = b2.y;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+          for (int j = 0; j < 6; ++j) dacc[i * 6 + j] = fmaf(hv[i], xv[j], dacc[i * 6 + j]);
+      }
+    }
+    __syncthreads();  // the images are read
+    constexpr int PP = 37;  // partial pitch (odd: conflict-free column reads)
+    float *part = smem;
+    if (combo < 9) {
+#pragma unroll
+      for (int i = 0; i < 36; ++i) part[(combo * NSUB + sub) * PP + i] = dacc[i];
+    }
+    __syncthreads();
+    if (tid < V * V) {
+      const int v = tid / V, w = tid - (tid / V) * V;
+      const int cb = (v / 6) * 3 + w / 6, i = (v % 6) * 6 + (w % 6);
+      float sum = 0.f;
+      for (int k = 0; k < NSUB; ++k) sum += part[(cb * NSUB + k) * PP + i];
+      atomicAdd(p.dA + tid, sum);
+    }
+  }
+}
+
 // IB (NPL = 1 only): the input is stored in bf16 (p.in_bf16; a template switch so
 // the staging code of the fp32-input kernels is unchanged)
-template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false>
+// SPB (V = 18, NPL >= 2): the fused SpatialConv backward epilogue (spb_epilogue)
+template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false, bool SPB = false>
 __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
   using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -547,6 +763,11 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
     return;
   }
+  if constexpr (SPB) {
+    static_assert(V == 18 && SIN == 1 && NPL >= 2, "the folded block's data gradient");
+    spb_epilogue<MR>(p, acc, smem, n, r0, m0, mi, nj0);
+    return;
+  }
   if (p.s_out == 1) {
     // row-major epilogue through LDS: every wave writes its two tiles, then all
     // 512 threads store whole 16-byte row pieces (device_common.h)
@@ -655,6 +876,14 @@ static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
   if (p.V != V || p.s_in != SIN) return false;
   constexpr int TG = NQ == 9 ? 3 : NQ;
   constexpr int lds = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>::LDS;
+  if constexpr (V == 18 && SIN == 1 && NPL >= 2) {
+    if (p.spb) {  // the folded block's data gradient with the SpatialConv backward
+      constexpr int lds_spb = lds > kSpbLds ? lds : kSpbLds;
+      hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL, false, true>), dim3(nblk), dim3(512),
+                         lds_spb, s, p);
+      return true;
+    }
+  }
   if constexpr (NPL == 1) {
     if (p.in_bf16) {
       hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL, true>), dim3(nblk), dim3(512), lds, s,
@@ -725,6 +954,9 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
   if (!conv_x3_supported(p) || !p.wpk) return hipErrorInvalidValue;
   if (p.f16x2 && (!p.amax_in || !p.amax_w)) return hipErrorInvalidValue;
+  if (p.spb && (p.V != 18 || p.s_in != 1 || p.FT != kTileCols / 18 || !p.sx || !p.sA ||
+                !p.mean1 || !p.invstd1 || !p.g1 || !p.b1 || !p.sd || !p.sdn || !p.dA))
+    return hipErrorInvalidValue;
   return launch_conv_planes(p, p.f16x2 ? 2 : 3, s);
 }
 

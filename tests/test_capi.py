@@ -120,6 +120,7 @@ def test_block_plan_pins_the_paths(pkg, lib):
     plan = lambda **kw: hl.block_plan(_desc(pkg, **kw))  # noqa: E731
     p = plan(flags=4)  # cfg2 L1-type block (64 -> 64)
     assert p & hl.PLAN_FOLD and p & hl.PLAN_TCONV_SPLIT and p & hl.PLAN_TWGRAD_SPLIT, p
+    assert p & hl.PLAN_SP_BWD_FUSED, p  # the SpatialConv backward in the data gradient
     assert plan(flags=4, C_in=128, C_out=256, stride=2, T=150, T_out=75) & hl.PLAN_FOLD
     assert not plan(flags=4, C_in=3) & hl.PLAN_FOLD          # C_in < 16
     p = plan(flags=5)                                        # residual: never folded

@@ -99,6 +99,9 @@ def test_f32x3_block_random(pkg, case):
             # the folded block (W' inside the temporal conv's weights): the plan
             # says so, and the forward left Wc = Wt W' in the (opaque) Z buffer
             assert plan & pkg.hip_lib.PLAN_FOLD, plan
+            # ... and its SpatialConv backward runs inside the data gradient
+            # (H never in HBM): dA / dx / BN1 gradients are gated above
+            assert plan & pkg.hip_lib.PLAN_SP_BWD_FUSED, plan
             _assert_fold_ran(pkg, arrays, x)
         else:
             # spatial dW' = dZ G^T on the split products (k_wgrad_sp<.., X3>)
