@@ -65,6 +65,7 @@ __device__ __forceinline__ floatx16 mfma_x(bf16x8_t a, bf16x8_t b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 // fp16 operands carried in the same 16-byte fragment registers (NPL = 2)
 __device__ __forceinline__ floatx16 mfma_h(bf16x8_t a, bf16x8_t b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a),
@@ -260,7 +261,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
         for (int j = 0; j < 2; ++j)
           acc_to_img(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
     }
-    if (h == 0)  // A^T[w][v] (broadcast LDS reads in the contraction)
+    if (h == 0)  // A^T[w][v] (broadcast 16-byte LDS reads in the contraction)
       for (int i = tid; i < kSpbAt; i += 512) {
         const int w = i / 20, v = i - w * 20;
         At[i] = v < V ? p.sA[v * V + w] : 0.f;
@@ -310,7 +311,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
         for (int i = 0; i < V / 2; ++i) {  // joints w = 2i, 2i + 1
           float d[2];
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
+          for (int e = 0; e < 2; ++e) {  // dxhat[w] = sum_v H[v] A[v][w] (A^T rows: 16-byte reads)
             const float *ac = At + (2 * i + e) * 20;
             float acc1 = 0.f;
 #pragma unroll
@@ -369,29 +370,30 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     // dA partials over this half's (row, frame) pairs: thread = (v block, w block,
     // 1 / 56 of the pairs), then the partials meet in LDS (over the H image) and
     // each entry is summed over its 56 threads in a fixed order
-    float dacc[36];
+    f2v dacc[18];  // (v, w pair) of this thread's 6 x 6 block
 #pragma unroll
-    for (int i = 0; i < 36; ++i) dacc[i] = 0.f;
+    for (int i = 0; i < 18; ++i) dacc[i] = (f2v){0.f, 0.f};
     if (combo < 9) {
       for (int q = sub; q < 64 * FT; q += NSUB) {
         const int rr = q / FT, f = q - rr * FT;
         if (f >= nvf) continue;
         const float *hr = Himg + rr * P + f * V + vb * 6;
         const float *xr = Ximg + rr * P + f * V + wb * 6;
-        float hv[6], xv[6];
+        float hv[6];
+        f2v xv[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           const float2 a2 = *reinterpret_cast<const float2 *>(hr + 2 * i);
           const float2 b2 = *reinterpret_cast<const float2 *>(xr + 2 * i);
           hv[2 * i] = a2.x;
           hv[2 * i + 1] = a2.y;
-          xv[2 * i] = b2.x;
-          xv[2 * i + 1] = b2.y;
+          xv[i] = (f2v){b2.x, b2.y};
         }
 #pragma unroll
         for (int i = 0; i < 6; ++i)
 #pragma unroll
-          for (int j = 0; j < 6; ++j) dacc[i * 6 + j] = fmaf(hv[i], xv[j], dacc[i * 6 + j]);
+          for (int j = 0; j < 3; ++j)
+            dacc[i * 3 + j] = __builtin_elementwise_fma((f2v){hv[i], hv[i]}, xv[j], dacc[i * 3 + j]);
       }
     }
     __syncthreads();  // the images are read
@@ -399,7 +401,10 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     float *part = smem;
     if (combo < 9) {
 #pragma unroll
-      for (int i = 0; i < 36; ++i) part[(combo * NSUB + sub) * PP + i] = dacc[i];
+      for (int i = 0; i < 18; ++i) {
+        part[(combo * NSUB + sub) * PP + 2 * i] = dacc[i].x;
+        part[(combo * NSUB + sub) * PP + 2 * i + 1] = dacc[i].y;
+      }
     }
     __syncthreads();
     if (tid < V * V) {
