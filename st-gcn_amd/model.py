@@ -58,9 +58,11 @@ class STGCNStack(nn.Module):
 
     def forward_nctv(self, x):
         # same as self.conv(x), with cross-block fusion (network.StackChain)
-        chain = StackChain() if self.training else None
+        chain = StackChain(defer_counts=True) if self.training else None
         for blk in self.conv:
             x = blk(x, chain=chain)
+        if chain is not None:
+            chain.flush_counts()
         # global average pool over (T, V) (lightning_model.py:105): a mean over
         # the contiguous T*V axis; ROCm's avg_pool2d with a (T, V) window is a
         # slow generic kernel (1.7 ms at N=128), the reduction is ~20 us.
@@ -76,9 +78,11 @@ class STGCNStack(nn.Module):
         NCTV, labels int64 (N) -> (mean cross-entropy loss, logits); the same
         arithmetic as F.cross_entropy(self.forward_nctv(x), labels)
         (lightning_model.py:105-107, :202)."""
-        chain = StackChain() if self.training else None
+        chain = StackChain(defer_counts=True) if self.training else None
         for blk in self.conv:
             x = blk(x, chain=chain)
+        if chain is not None:
+            chain.flush_counts()
         return StgcnHeadFn.apply(x, self.fc_layer.weight, self.fc_layer.bias, labels)
 
 

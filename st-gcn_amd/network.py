@@ -25,12 +25,26 @@ class StackChain:
     code, eval mode) breaks the chain and both blocks fall back to their own
     passes: results are the same either way."""
 
-    def __init__(self):
+    def __init__(self, defer_counts=False):
+        """defer_counts: the caller (model.STGCNStack) applies the blocks'
+        num_batches_tracked increments itself with ``flush_counts``."""
+        self.defer_counts = defer_counts
+        self.counters = []
         self.reset()
 
     def reset(self):
         self.y, self.y_version, self.y_stats, self.link, self.g2b2 = None, None, None, None, None
         self.u_stats = None
+
+    def count_batch(self, *counters):
+        """BatchNorm num_batches_tracked increments of the chained blocks, applied
+        by ``flush_counts`` in one multi-tensor launch instead of two per block."""
+        self.counters.extend(counters)
+
+    def flush_counts(self):
+        if self.counters:
+            torch._foreach_add_(self.counters, 1)
+            self.counters = []
 
 
 class SpatialConv(nn.Module):
@@ -116,7 +130,9 @@ class SpatialTemporalConv(nn.Module):
         if bn1.momentum is None or bn2.momentum is None:
             raise NotImplementedError("BatchNorm momentum=None (cumulative average)")
         training = self.training
-        if training:
+        if training and chain is not None and chain.defer_counts:  # (chain.flush_counts)
+            chain.count_batch(bn1.num_batches_tracked, bn2.num_batches_tracked)
+        elif training:
             bn1.num_batches_tracked.add_(1)
             bn2.num_batches_tracked.add_(1)
         sc = self.spatialConv
