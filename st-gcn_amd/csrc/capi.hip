@@ -599,7 +599,8 @@ size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d) {
 size_t stgcn_keep_g_bytes(const stgcn_desc_t *d) {
   if (stgcn_check_desc(d) != STGCN_OK) return 0;
   if (fused_sp(d)) return sp_keep_g_bytes(d->N, d->C_in, d->T, d->V, d->K);
-  return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V;
+  // (f16x2: + one word after G, its max |G| for the backward's weight gradient)
+  return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V + (f16x2(d) ? 256 : 0);
 }
 
 size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d) {
@@ -659,7 +660,8 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
                                (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s));
   } else {
   float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
-  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s));
+  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s,
+                            f16x2(d) ? L.amax : nullptr));  // (f16x2: max |G| on the way)
   Gfold = G;
   if (!fold) {
     ConvGemmParams p = conv_base(d, L.wpk);
@@ -715,12 +717,13 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
       float *Wc = fold_wc_in_z(d) ? a->Z : L.Wc;  // (kept for the backward)
       HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, s));
       HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT, s));
-      if (f16x2(d)) {  // the fp16 splits' operand scales: max |G|, max |Wc|
-        HIP_TRY(launch_absmax(Gfold, (int64_t)N * C * T * V, L.amax, s));
+      if (f16x2(d)) {  // the fp16 splits' operand scales: max |G| (gather), max |Wc|
         HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
         p.f16x2 = 1;
         p.amax_in = L.amax;
         p.amax_w = L.amax + 1;
+        if (a->G)  // (the kept G carries its bound to the backward)
+          p.amax_keep = reinterpret_cast<unsigned *>(a->G + (size_t)N * C * T * V);
       }
       p.in = Gfold;
       p.w = Wc;
@@ -801,7 +804,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     if (cols_sums(d)) {
       HIP_TRY(launch_bn_relu_bwd_apply_cols(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
                                             L.dU, L.sdu, N, R, To * V, d->training, drop, s,
-                                            du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs));
+                                            du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs,
+                                            f16x2(d) ? L.amax : nullptr));  // (f16x2: max |dU|)
       HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.fpart, L.ftq,
                              s));
     } else {
@@ -856,10 +860,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
       HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
     }
-    if (f16x2(d)) {  // the fp16 splits' operand scales: max |dU|, max |Wc|
-      HIP_TRY(launch_absmax(L.dU, (int64_t)N * R * To * V, L.amax, s));
+    if (f16x2(d))  // the fp16 splits' operand scales: max |dU| (from the apply pass), max |Wc|
       HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
-    }
     {
       ConvGemmParams p = conv_base(d, L.wpk);
       p.in = L.dU;
@@ -917,18 +919,19 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
         }
       }
     }
-    const float *G = a->G;  // kept fp32 G, else recomputed
+    const float *G = a->G;  // kept fp32 G (f16x2: its max |G| follows it), else recomputed
+    const unsigned *amax_g = G ? reinterpret_cast<const unsigned *>(G + (size_t)N * C * T * V)
+                               : L.amax + 2;
     if (!G) {
       HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K,
-                                res, s));
+                                res, s, f16x2(d) ? L.amax + 2 : nullptr));
       G = L.G;
     }
     WgradParams w = make_wgrad_taps(d, L.dU, G, L.slab, C);
-    if (f16x2(d) && w.bf16 == 3) {  // (max |dU| from the data gradient's scale above)
-      HIP_TRY(launch_absmax(G, (int64_t)N * C * T * V, L.amax + 2, s));
+    if (f16x2(d) && w.bf16 == 3) {  // max |dU| (apply pass), max |G|
       w.f16x2 = 1;
       w.amax_p = L.amax;
-      w.amax_q = L.amax + 2;
+      w.amax_q = amax_g;
     }
     HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_fold_grads(L.slab, w.S, a->Wt, a->W, L.bZ, L.ftq, R, C, V, L.dWc, L.fpart,

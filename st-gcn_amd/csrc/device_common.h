@@ -27,6 +27,15 @@ __device__ __forceinline__ float wave_sumf(float v) {
   return v;
 }
 
+// amax[0] = max(amax[0], wave max of m) (m >= 0; float bits order as unsigned):
+// the operand bound of the fp16-split GEMMs (f16x2), folded into a producer.
+// Every lane of the wave must call it.
+__device__ __forceinline__ void wave_amax(float m, unsigned *amax) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(unsigned, m));
+}
+
 // Block (NT threads) reduction of two doubles, then one fp64 atomic each.
 // `red` must hold 2*NT/64 doubles of LDS.
 template <int NT>

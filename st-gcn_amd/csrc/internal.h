@@ -80,6 +80,7 @@ struct ConvGemmParams {
   // device words holding max |in| / max |w| as float bits (f16x2_scale)
   int f16x2;
   const unsigned *amax_in, *amax_w;
+  unsigned *amax_keep;  // (or null) block 0 copies *amax_in there (the kept G's bound)
   // spb (the folded block's data gradient, V = 18, K = 1; kernels_x3.hip
   // spb_epilogue): the tile holds H = W'^T dZ (rows = input channels). Instead of
   // storing H the epilogue forms dxhat = H A (stored to out, null: not stored),
@@ -141,7 +142,8 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
                                          const double *sg, const double *sgu, float *dU,
                                          double *sdu, int N, int C, int L, int training,
                                          Dropout drop, hipStream_t s, int du_bf16,
-                                         const float *dy_coef, double *cs);
+                                         const float *dy_coef, double *cs,
+                                         unsigned *amax = nullptr);
 // bf16 path (kernels_bf16.hip): the reference's graphs (V = 18, 25, 50) with
 // the fp32 path's tile plan (FT = kTileCols / V); launch_conv_gemm dispatches here
 // when p.bf16 and conv_bf16_supported(p).
@@ -254,9 +256,12 @@ hipError_t launch_pack_w(const float *W, float *Wpk, int K, int R, int C, hipStr
 hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K, int R, int V,
                           hipStream_t s);
 // G = f(BN1(x)) A^T with f = identity, or ReLU when relu != 0 (residual block)
+// amax (or null): max |G| as float bits (atomicMax; zeroed by the caller), the
+// f16x2 operand bound of the folded temporal GEMMs
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
-                             int C, int T, int V, int K, int relu, hipStream_t s);
+                             int C, int T, int V, int K, int relu, hipStream_t s,
+                             unsigned *amax = nullptr);
 hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out,
                          hipStream_t s, int x_bf16 = 0);
 hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K,

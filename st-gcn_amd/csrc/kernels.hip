@@ -1660,8 +1660,9 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
     const float *__restrict__ dy, const float *__restrict__ U, const float *mean,
     const float *invstd, const float *g, const float *b, const double *sg, const double *sgu,
     float *__restrict__ dU, double *sdu, int N, int C, int L, double invM, Dropout drop,
-    int du_bf16, const float *dy_coef, double *__restrict__ cs) {
+    int du_bf16, const float *dy_coef, double *__restrict__ cs, unsigned *amax) {
   __shared__ double red[8];
+  float om = 0.f;  // max |dU| (f16x2 operand bound)
   const int c = blockIdx.x;
   const int i = (blockIdx.y * 256 + threadIdx.x) * VEC;
   const int nz = gridDim.z, per = (N + nz - 1) / nz;
@@ -1717,6 +1718,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
         o[j] = a * (gg - mg - uh * mgu);
         s += o[j];
         col[j] += o[j];
+        om = fmaxf(om, fabsf(o[j]));
       }
       if (du_bf16) {
         __bf16 *ob = reinterpret_cast<__bf16 *>(dU) + base + i;
@@ -1737,6 +1739,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
 #pragma unroll
     for (int j = 0; j < VEC; ++j) cs[((int64_t)blockIdx.z * C + c) * L + i + j] = col[j];
   }
+  if (amax) wave_amax(om, amax);
   block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
 }
 
@@ -1747,7 +1750,7 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
                                          const double *sg, const double *sgu, float *dU,
                                          double *sdu, int N, int C, int L, int training,
                                          Dropout drop, hipStream_t s, int du_bf16,
-                                         const float *dy_coef, double *cs) {
+                                         const float *dy_coef, double *cs, unsigned *amax) {
   const double invM = training ? 1.0 / ((double)N * L) : 0.0;
   // (whole-row vectors: every row start VEC-aligned needs L % VEC == 0)
   int vec = slice_vec(L, {dy, U, dU});
@@ -1755,7 +1758,7 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
 #define COLS_LAUNCH(VV)                                                                     \
   hipLaunchKernelGGL((k_bn_relu_bwd_apply_cols<VV>), dim3(C, (L + 256 * VV - 1) / (256 * VV), nz), \
                      dim3(256), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, sdu, N, C, L,  \
-                     invM, drop, du_bf16, dy_coef, cs)
+                     invM, drop, du_bf16, dy_coef, cs, amax)
   if (vec == 4)
     COLS_LAUNCH(4);
   else if (vec == 2)
@@ -1974,9 +1977,11 @@ constexpr int kGatherTC = 32;  // frames per gather block
 __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float *mean,
                                                     const float *invstd, const float *g,
                                                     const float *b, const float *A, float *G,
-                                                    int C, int T, int V, int K, int relu) {
+                                                    int C, int T, int V, int K, int relu,
+                                                    unsigned *amax) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *As = smem;                 // [K][V][V]
+  float gm = 0.f;
   float *xs = smem + K * V * V;     // [TC][V]
   const int n = blockIdx.y, t0 = blockIdx.x * kGatherTC;
   int tc = T - t0;
@@ -2002,8 +2007,10 @@ __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float 
       float s = 0.f;
       for (int w = 0; w < V; ++w) s = fmaf(ar[w], xr[w], s);
       G[(((int64_t)n * K + k) * C + ci) * L + (int64_t)(t0 + t) * V + v] = s;
+      gm = fmaxf(gm, fabsf(s));
     }
   }
+  if (amax) wave_amax(gm, amax);
 }
 
 // Joint-axis (V) kernels: rows padded to VP (multiple of 4) for 16-byte LDS reads.
@@ -2024,7 +2031,8 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
                                                  const float *__restrict__ g,
                                                  const float *__restrict__ b,
                                                  const float *__restrict__ A, float *G, int C,
-                                                 int T, int K, int64_t rows, int relu) {
+                                                 int T, int K, int64_t rows, int relu,
+                                                 unsigned *amax) {
   constexpr int VP = JointCfg<V>::VP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *As = smem;  // [K][V][VP]
@@ -2034,8 +2042,10 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
     As[i] = w < V ? A[kv * V + w] : 0.f;
   }
   __syncthreads();
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + tid;
-  if (r >= rows) return;
+  const int64_t r0 = (int64_t)blockIdx.x * blockDim.x + tid;
+  const bool live = r0 < rows;
+  const int64_t r = live ? r0 : rows - 1;  // (the last row again: every lane reaches wave_amax)
+  float gm = 0.f;
   const int64_t CT = (int64_t)C * T;
   const int64_t n = r / CT;
   const int rem = (int)(r - n * CT);
@@ -2062,9 +2072,11 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
         acc = fmaf(q.z, xv[w4 + 2], acc);
         acc = fmaf(q.w, xv[w4 + 3], acc);
       }
-      gout[v] = acc;
+      if (live) gout[v] = acc;
+      gm = fmaxf(gm, fabsf(acc));
     }
   }
+  if (amax) wave_amax(gm, amax);
 }
 
 // k_gather4: k_gather3 with the block's rows moved through LDS: the 256 rows
@@ -2080,9 +2092,11 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
                                                  const float *__restrict__ g,
                                                  const float *__restrict__ b,
                                                  const float *__restrict__ A, float *G, int C,
-                                                 int T, int K, int64_t rows, int relu) {
+                                                 int T, int K, int64_t rows, int relu,
+                                                 unsigned *amax) {
   constexpr int VP = JointCfg<V>::VP;
   constexpr int BF = 256 * V;  // floats of a block (a multiple of 256: V DMA rounds)
+  float gm = 0.f;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2129,9 +2143,13 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
     }
     __syncthreads();
     float *dst = G + ((n0 * K + k) * CT + rem0) * V;
-    for (int e = tid; e < BF / 4; e += 256)
-      *reinterpret_cast<float4 *>(dst + e * 4) = *reinterpret_cast<const float4 *>(os + e * 4);
+    for (int e = tid; e < BF / 4; e += 256) {
+      const float4 q = *reinterpret_cast<const float4 *>(os + e * 4);
+      *reinterpret_cast<float4 *>(dst + e * 4) = q;
+      gm = fmaxf(gm, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+    }
   }
+  if (amax) wave_amax(gm, amax);
 }
 
 // Flat-row spatial backward (the math: see k_spatial_dx). Per block:
@@ -3008,9 +3026,9 @@ static bool joint_fast(int V) { return V == 18 || V == 25 || V == 50; }
 
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
-                             int C, int T, int V, int K, int relu, hipStream_t s) {
+                             int C, int T, int V, int K, int relu, hipStream_t s, unsigned *amax) {
   constexpr bool joint3 = STGCN_AB_JOINT3 != 0;  // A/B builds only (ab_switches.h)
-  if (!joint3 && K > 1 && (V == 25 || V == 50) && ((uintptr_t)x & 15) == 0 &&
+  if (!joint3 && !amax && K > 1 && (V == 25 || V == 50) && ((uintptr_t)x & 15) == 0 &&
       ((uintptr_t)G & 15) == 0) {  // partitioned graphs: contraction on MFMA
     const int64_t rows = (int64_t)N * C * T;
     const bool done =
@@ -3026,11 +3044,11 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
     const int64_t rows = (int64_t)N * C * T;
     const dim3 grid4((unsigned)(rows / 256));
     if (V == 18)
-      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
+      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
     else if (V == 25)
-      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
+      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
     else
-      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
+      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
     return hipGetLastError();
   }
   if (joint_fast(V)) {
@@ -3039,16 +3057,16 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
     const size_t lds3 = sizeof(float) * (size_t)K * V * VP;
     const dim3 grid3((unsigned)((rows + 255) / 256));
     if (V == 18)
-      hipLaunchKernelGGL(k_gather3<18>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
+      hipLaunchKernelGGL(k_gather3<18>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
     else if (V == 25)
-      hipLaunchKernelGGL(k_gather3<25>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
+      hipLaunchKernelGGL(k_gather3<25>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
     else
-      hipLaunchKernelGGL(k_gather3<50>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu);
+      hipLaunchKernelGGL(k_gather3<50>, grid3, dim3(256), lds3, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
     return hipGetLastError();
   }
   const size_t lds = sizeof(float) * ((size_t)K * V * V + kGatherTC * V);
   hipLaunchKernelGGL(k_gather_fwd, dim3((T + kGatherTC - 1) / kGatherTC, N), dim3(256), lds, s, x,
-                     mean, invstd, g, b, A, G, C, T, V, K, relu);
+                     mean, invstd, g, b, A, G, C, T, V, K, relu, amax);
   return hipGetLastError();
 }
 

@@ -478,6 +478,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // NPL = 2: the window's power-of-two scale (f16x2_se of max |in|)
   const int in_se = NPL == 2 ? f16x2_se(p.amax_in) : 0;
   const float in_scale = pow2f(in_se);
+  if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid == 0) *p.amax_keep = *p.amax_in;
   auto load_img = [&](int chunk) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
     const int esz = inb ? 2 : 4;
