@@ -269,7 +269,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.SdZ = c.take<double>((size_t)R * d->V);
   L.s1 = c.take<double>(C);
   L.s2 = c.take<double>(C);
-  L.amax = c.take<unsigned>(4);  // f16x2: max |dU|, |Wc|, |G| (zeroed with the sums)
+  L.amax = c.take<unsigned>(3 * kAmaxWords);  // f16x2: max |dU|, |Wc|, |G| (zeroed with the sums)
   L.dbl_bytes = c.off;
   if (!residual(d)) {  // clip-chunk sums of dU -> Tq -> sum_{n,t} dZ (kernels_fold.hip)
     L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
@@ -335,7 +335,7 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
   L.q1 = c.take<double>(C);
   L.s2 = c.take<double>(R);
   L.q2 = c.take<double>(R);
-  L.amax = c.take<unsigned>(4);
+  L.amax = c.take<unsigned>(2 * kAmaxWords);  // f16x2: max |G|, |Wc|
   L.dbl_bytes = c.off;
   L.G = c.take<float>((size_t)d->N * K * C * nT(d));
   L.Wpk = c.take<float>((size_t)R * K * C);
@@ -600,7 +600,8 @@ size_t stgcn_keep_g_bytes(const stgcn_desc_t *d) {
   if (stgcn_check_desc(d) != STGCN_OK) return 0;
   if (fused_sp(d)) return sp_keep_g_bytes(d->N, d->C_in, d->T, d->V, d->K);
   // (f16x2: + one word after G, its max |G| for the backward's weight gradient)
-  return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V + (f16x2(d) ? 256 : 0);
+  return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V +
+         (f16x2(d) ? sizeof(unsigned) * kAmaxWords : 0);
 }
 
 size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d) {
@@ -718,10 +719,10 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
       HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, s));
       HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT, s));
       if (f16x2(d)) {  // the fp16 splits' operand scales: max |G| (gather), max |Wc|
-        HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
+        HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
         p.f16x2 = 1;
         p.amax_in = L.amax;
-        p.amax_w = L.amax + 1;
+        p.amax_w = L.amax + kAmaxWords;
         if (a->G)  // (the kept G carries its bound to the backward)
           p.amax_keep = reinterpret_cast<unsigned *>(a->G + (size_t)N * C * T * V);
       }
@@ -861,7 +862,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
     }
     if (f16x2(d))  // the fp16 splits' operand scales: max |dU| (from the apply pass), max |Wc|
-      HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + 1, s));
+      HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
     {
       ConvGemmParams p = conv_base(d, L.wpk);
       p.in = L.dU;
@@ -869,7 +870,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       if (f16x2(d)) {
         p.f16x2 = 1;
         p.amax_in = L.amax;
-        p.amax_w = L.amax + 1;
+        p.amax_w = L.amax + kAmaxWords;
       }
       if (fold_spb(d)) {  // dxhat -> dx; BN1 / chain sums and dA from the tile (H on chip)
         p.spb = 1;
@@ -921,10 +922,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     }
     const float *G = a->G;  // kept fp32 G (f16x2: its max |G| follows it), else recomputed
     const unsigned *amax_g = G ? reinterpret_cast<const unsigned *>(G + (size_t)N * C * T * V)
-                               : L.amax + 2;
+                               : L.amax + 2 * kAmaxWords;
     if (!G) {
       HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, L.G, N, C, T, V, K,
-                                res, s, f16x2(d) ? L.amax + 2 : nullptr));
+                                res, s, f16x2(d) ? L.amax + 2 * kAmaxWords : nullptr));
       G = L.G;
     }
     WgradParams w = make_wgrad_taps(d, L.dU, G, L.slab, C);
@@ -1205,7 +1206,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
   const int CZ = fold ? C : R;
   const double tflops = 2.0 * 9 * R * (double)CZ * To * V * N;
   float *wpk = c.take<float>(wpk_floats(d));
-  if (f16x2(d) && which <= 2) P.amax = c.take<unsigned>(4);
+  if (f16x2(d) && which <= 2) P.amax = c.take<unsigned>(2 * kAmaxWords);
   if (which == 0) {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * CZ * T * V);
@@ -1241,7 +1242,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     if (P.amax) {
       p.f16x2 = 1;
       p.amax_in = P.amax;
-      p.amax_w = P.amax + 1;
+      p.amax_w = P.amax + kAmaxWords;
       P.ax[0] = p.in;
       P.an[0] = (int64_t)N * C * T * V;
       P.ax[1] = p.w;
@@ -1269,7 +1270,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     if (P.amax) {
       p.f16x2 = 1;
       p.amax_in = P.amax;
-      p.amax_w = P.amax + 1;
+      p.amax_w = P.amax + kAmaxWords;
       P.ax[0] = p.in;
       P.an[0] = (int64_t)N * R * To * V;
       P.ax[1] = w;
@@ -1324,7 +1325,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     if (P.amax && w.bf16 == 3) {
       w.f16x2 = 1;
       w.amax_p = P.amax;
-      w.amax_q = P.amax + 1;
+      w.amax_q = P.amax + kAmaxWords;
       P.ax[0] = dU;
       P.an[0] = (int64_t)N * R * To * V;
       P.ax[1] = Z;
@@ -1476,9 +1477,9 @@ int stgcn_time_kernel(const stgcn_desc_t *d, int which, void *scratch, size_t sc
     return hipSuccess;
   };
   if (P.amax) {  // the f16x2 operand scales (not timed)
-    HIP_TRY(hipMemsetAsync(P.amax, 0, 4 * sizeof(unsigned), s));
+    HIP_TRY(hipMemsetAsync(P.amax, 0, 2 * kAmaxWords * sizeof(unsigned), s));
     for (int i = 0; i < 2; ++i)
-      if (P.ax[i]) HIP_TRY(launch_absmax(P.ax[i], P.an[i], P.amax + i, s));
+      if (P.ax[i]) HIP_TRY(launch_absmax(P.ax[i], P.an[i], P.amax + i * kAmaxWords, s));
   }
   HIP_TRY(launch());  // warm-up
   hipEvent_t e0, e1;

@@ -27,13 +27,36 @@ __device__ __forceinline__ float wave_sumf(float v) {
   return v;
 }
 
-// amax[0] = max(amax[0], wave max of m) (m >= 0; float bits order as unsigned):
-// the operand bound of the fp16-split GEMMs (f16x2), folded into a producer.
-// Every lane of the wave must call it.
-__device__ __forceinline__ void wave_amax(float m, unsigned *amax) {
+// Operand bounds of the fp16-split GEMMs (f16x2): max |x| as float bits
+// (non-negative floats order as unsigned integers) in kAmaxSlots words
+// kAmaxStride apart (one per 128-byte line), zeroed by the caller; producers
+// add one atomicMax per workgroup to slot blockIdx % kAmaxSlots (thousands of
+// workgroups on ONE word serialise in L2: 3.4 ms per cfg2 step measured),
+// readers take the max over the slots (amax_read).
+
+__device__ __forceinline__ unsigned amax_read(const unsigned *amax) {
+  unsigned m = 0;
+#pragma unroll 8
+  for (int i = 0; i < kAmaxSlots; ++i) m = max(m, amax[i * kAmaxStride]);
+  return m;
+}
+
+// Block (NT threads) max of m >= 0 into amax's slot of this workgroup; every
+// thread of the block must call it (one barrier).
+template <int NT>
+__device__ __forceinline__ void block_amax(float m, unsigned *amax) {
+  __shared__ float wmax[NT / 64];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(unsigned, m));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = wmax[0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) b = fmaxf(b, wmax[i]);
+    const unsigned blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    atomicMax(amax + (blk % kAmaxSlots) * kAmaxStride, __builtin_bit_cast(unsigned, b));
+  }
 }
 
 // Block (NT threads) reduction of two doubles, then one fp64 atomic each.

@@ -37,6 +37,10 @@ struct PrevBn {
   double *s1 = nullptr, *s2 = nullptr;
 };
 
+// f16x2 operand bounds: kAmaxSlots words kAmaxStride apart per bound
+// (device_common.h block_amax / amax_read)
+constexpr int kAmaxSlots = 64, kAmaxStride = 32, kAmaxWords = kAmaxSlots * kAmaxStride;
+
 constexpr int kTileRows = 64;   // output rows per workgroup (2 MFMA 32-row tiles)
 constexpr int kTileCols = 256;  // max (frames x V) columns per workgroup (8 MFMA 32-col tiles)
 

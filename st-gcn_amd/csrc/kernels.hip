@@ -1739,7 +1739,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
 #pragma unroll
     for (int j = 0; j < VEC; ++j) cs[((int64_t)blockIdx.z * C + c) * L + i + j] = col[j];
   }
-  if (amax) wave_amax(om, amax);
+  if (amax) block_amax<256>(om, amax);
   block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
 }
 
@@ -2010,7 +2010,7 @@ __global__ __launch_bounds__(256) void k_gather_fwd(const float *x, const float 
       gm = fmaxf(gm, fabsf(s));
     }
   }
-  if (amax) wave_amax(gm, amax);
+  if (amax) block_amax<256>(gm, amax);
 }
 
 // Joint-axis (V) kernels: rows padded to VP (multiple of 4) for 16-byte LDS reads.
@@ -2076,7 +2076,7 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
       gm = fmaxf(gm, fabsf(acc));
     }
   }
-  if (amax) wave_amax(gm, amax);
+  if (amax) block_amax<256>(gm, amax);
 }
 
 // k_gather4: k_gather3 with the block's rows moved through LDS: the 256 rows
@@ -2149,7 +2149,7 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
       gm = fmaxf(gm, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
     }
   }
-  if (amax) wave_amax(gm, amax);
+  if (amax) block_amax<256>(gm, amax);
 }
 
 // Flat-row spatial backward (the math: see k_spatial_dx). Per block:

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 
+#include "device_common.h"
 #include "internal.h"
 
 #define HIP_RET(expr)                  \
@@ -27,129 +28,189 @@
 
 namespace stgcn {
 
-// The fold's small GEMMs as single launches on the fp64 matrix cores
-// (v_mfma_f64_16x16x4_f64; operands float or double, converted exactly, fp64
-// products and accumulation in a fixed order, so the results are deterministic):
-//   out(m, n) = sum_{k < K} A(m, k) B(k, n) + sum_{k < K2} A2(m, k) B2(k, n)
-// Every operand index is a two-level mixed-radix map per dimension,
-//   idx(x) = (x / d) * s1 + (x % d) * s0,
-// so the nine taps ride in M or K of ONE GEMM (no per-tap launches and no
-// per-tap partial sums): e.g. Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i] is the
-// (9 R) x C x R GEMM with m = 9 o + q.
-// Block = 256 threads on a 64 x 64 output tile (wave = 32 x 32 = 2 x 2 MFMA
-// tiles), K in chunks of 16 staged as fp64 in LDS.
-struct Map {
-  int d = 1;
-  int64_t s1 = 0, s0 = 0;
-  __host__ __device__ int64_t operator()(int x) const {
-    return d == 1 ? (int64_t)x * s1 : (int64_t)(x / d) * s1 + (int64_t)(x % d) * s0;
-  }
-};
-struct Gemm64 {
-  const void *A, *B, *A2, *B2;
-  void *out;
-  int M, N, K, K2;
-  int a_dbl, b_dbl, a2_dbl, b2_dbl, o_dbl;
-  Map am, ak, bk, bn, a2m, a2k, b2k, b2n, om, on;
-};
+// The fold's small GEMMs on the fp64 matrix cores (v_mfma_f64_16x16x4_f64;
+// operands float or double converted exactly, fp64 products and accumulation
+// in a fixed order: deterministic). Two shapes cover them:
+//
+// k_fold_tapgemm: out[m][n][q] = sum_k A[m][k][q] B[k][n] (+ sum_v A2[q][m][v] B2[v][n])
+//   for all nine taps q in ONE block: the A rows are contiguous 9-tap runs
+//   (coalesced), the B tile is shared by the taps. Wc = Wt W', dWt = dWc W'^T
+//   (+ the Tq bZ bias term) and the bias products bq.
+// k_fold_koq: out[m][n] = sum_o sum_q A[o][m][q] B[o][n][q]: K = (o, q), split
+//   over o in slabs summed in a fixed order afterwards. dW' = sum_q Wt_q^T dWc_q
+//   and sum_{n,t} dZ = sum_q Wt_q^T Tq.
+// Tiles of 32 x 32 per block, wave = one 16 x 16 MFMA tile (per tap).
+typedef double double4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double ld_fd(const void *p, int dbl, int64_t i) {
   return dbl ? reinterpret_cast<const double *>(p)[i] : (double)reinterpret_cast<const float *>(p)[i];
 }
 
-typedef double double4v __attribute__((ext_vector_type(4)));
+struct TapGemm {
+  const void *A;
+  int a_dbl;
+  int64_t am, ak, aq;  // A[m am + k ak + q aq]
+  const float *B;
+  int64_t bk, bn;      // B[k bk + n bn]
+  const double *A2;    // (or null) A2[q a2q + m a2m + v], v < K2
+  int64_t a2q, a2m;
+  const float *B2;     // B2[v b2k + n b2n]
+  int64_t b2k, b2n;
+  void *out;
+  int o_dbl;
+  int64_t om, on, oq;  // out[m om + n on + q oq]
+  int M, N, K, K2;
+};
 
-__global__ __launch_bounds__(256) void k_gemm_f64(Gemm64 g) {
-  constexpr int KC = 16, TP = 64 + 1;  // chunk depth, LDS pitch (doubles)
-  __shared__ double As[KC][TP], Bs[KC][TP];
+__global__ __launch_bounds__(256) void k_fold_tapgemm(TapGemm g) {
+  constexpr int KC = 8;
+  __shared__ double As[KC][9][32], Bs[KC][32];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  const int wm = (w & 1) * 32, wn = (w >> 1) * 32;
-  double4v acc[2][2];
+  const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  double4v acc[9];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (double4v){0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < 9; ++q) acc[q] = (double4v){0.0, 0.0, 0.0, 0.0};
   const int Ktot = g.K + (g.A2 ? g.K2 : 0);
   for (int k0 = 0; k0 < Ktot; k0 += KC) {
     __syncthreads();  // the previous chunk's reads are done
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 9; ++r) {  // A: q fastest, then k, then m (9-tap runs)
       const int e = r * 256 + tid;
-      const int kk = e & (KC - 1), mm = e >> 4;  // A: 16 consecutive k of a row
-      const int k = k0 + kk, m = m0 + mm, n = n0 + mm;
-      double a = 0.0, b = 0.0;
-      if (k < g.K) {
-        if (m < g.M) a = ld_fd(g.A, g.a_dbl, g.am(m) + g.ak(k));
-        if (n < g.N) b = ld_fd(g.B, g.b_dbl, g.bk(k) + g.bn(n));
-      } else if (k < Ktot) {
-        const int k2 = k - g.K;
-        if (m < g.M) a = ld_fd(g.A2, g.a2_dbl, g.a2m(m) + g.a2k(k2));
-        if (n < g.N) b = ld_fd(g.B2, g.b2_dbl, g.b2k(k2) + g.b2n(n));
+      const int q = e % 9, t = e / 9, kk = t % KC, mm = t / KC;
+      const int k = k0 + kk, m = m0 + mm;
+      double v = 0.0;
+      if (m < g.M) {
+        if (k < g.K)
+          v = ld_fd(g.A, g.a_dbl, m * g.am + k * g.ak + q * g.aq);
+        else if (k < Ktot)
+          v = g.A2[q * g.a2q + m * g.a2m + (k - g.K)];
       }
-      As[kk][mm] = a;
-      Bs[kk][mm] = b;
+      As[kk][q][mm] = v;
+    }
+    {
+      const int kk = tid >> 5, nn = tid & 31, k = k0 + kk, n = n0 + nn;
+      double v = 0.0;
+      if (n < g.N) {
+        if (k < g.K)
+          v = g.B[k * g.bk + n * g.bn];
+        else if (k < Ktot)
+          v = g.B2[(k - g.K) * g.b2k + n * g.b2n];
+      }
+      Bs[kk][nn] = v;
     }
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < KC; ks += 4) {
       // A operand: lane l holds A[row l & 15][k l >> 4]; B: B[k l >> 4][col l & 15]
-      double a[2], b[2];
+      const double b = Bs[ks + (l >> 4)][wn + (l & 15)];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[ks + (l >> 4)][wm + i * 16 + (l & 15)];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[ks + (l >> 4)][wn + j * 16 + (l & 15)];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int q = 0; q < 9; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(As[ks + (l >> 4)][q][wm + (l & 15)], b,
+                                                      acc[q], 0, 0, 0);
     }
   }
   // C/D: col = lane & 15, row = (lane >> 4) + 4 * reg
+  const int n = n0 + wn + (l & 15);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + wm + (l >> 4) + 4 * r;
+    if (m >= g.M || n >= g.N) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm + i * 16 + (l >> 4) + 4 * r, n = n0 + wn + j * 16 + (l & 15);
-        if (m >= g.M || n >= g.N) continue;
-        const int64_t o = g.om(m) + g.on(n);
-        if (g.o_dbl)
-          reinterpret_cast<double *>(g.out)[o] = acc[i][j][r];
-        else
-          reinterpret_cast<float *>(g.out)[o] = (float)acc[i][j][r];
-      }
+    for (int q = 0; q < 9; ++q) {
+      const int64_t o = m * g.om + n * g.on + q * g.oq;
+      if (g.o_dbl)
+        reinterpret_cast<double *>(g.out)[o] = acc[q][r];
+      else
+        reinterpret_cast<float *>(g.out)[o] = (float)acc[q][r];
+    }
+  }
 }
 
-static hipError_t gemm64(const Gemm64 &g, hipStream_t s) {
-  hipLaunchKernelGGL(k_gemm_f64, dim3((g.N + 63) / 64, (g.M + 63) / 64), dim3(256), 0, s, g);
+static hipError_t tapgemm(const TapGemm &g, hipStream_t s) {
+  hipLaunchKernelGGL(k_fold_tapgemm, dim3((g.N + 31) / 32, (g.M + 31) / 32), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 
-static Map mp(int64_t s1) {
-  Map m;
-  m.s1 = s1;
-  return m;
-}
-static Map mp(int d, int64_t s1, int64_t s0) {
-  Map m;
-  m.d = d;
-  m.s1 = s1;
-  m.s0 = s0;
-  return m;
+struct KoqGemm {
+  const float *A;
+  int64_t a_o, a_m, a_q;  // A[o a_o + m a_m + q a_q]
+  const void *B;
+  int b_dbl;
+  int64_t b_o, b_n, b_q;  // B[o b_o + n b_n + q b_q]
+  double *part;           // [S][M][N] partial sums over o-slices
+  int M, N, O, per;       // o in [s per, min(O, (s + 1) per)) for split s = blockIdx.z
+};
+
+__global__ __launch_bounds__(256) void k_fold_koq(KoqGemm g) {
+  constexpr int KO = 4;  // o per chunk: 36 k = 9 MFMA k-steps
+  __shared__ double As[KO * 9][32], Bs[KO * 9][32];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int o_begin = blockIdx.z * g.per, o_end = min(g.O, o_begin + g.per);
+  double4v acc = {0.0, 0.0, 0.0, 0.0};
+  for (int o0 = o_begin; o0 < o_end; o0 += KO) {
+    __syncthreads();
+    for (int e = tid; e < KO * 9 * 32; e += 256) {  // q fastest, then m / n, then o
+      const int q = e % 9, t = e / 9, mm = t % 32, oo = t / 32;
+      const int o = o0 + oo, m = m0 + mm, n = n0 + mm;
+      const bool ok = o < o_end;
+      As[oo * 9 + q][mm] = ok && m < g.M ? (double)g.A[o * g.a_o + m * g.a_m + q * g.a_q] : 0.0;
+      Bs[oo * 9 + q][mm] =
+          ok && n < g.N ? ld_fd(g.B, g.b_dbl, o * g.b_o + n * g.b_n + q * g.b_q) : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < KO * 9; ks += 4)
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(As[ks + (l >> 4)][wm + (l & 15)],
+                                                 Bs[ks + (l >> 4)][wn + (l & 15)], acc, 0, 0, 0);
+  }
+  const int n = n0 + wn + (l & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int m = m0 + wm + (l >> 4) + 4 * r;
+    if (m < g.M && n < g.N) g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[r];
+  }
 }
 
-// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in);
-// one (9 R) x C x R GEMM, m = 9 o + q
+// dst[i] = sum_{z < Z} part[z * n + i] (fixed order), as float or double
+__global__ void k_sum_parts(const double *part, int Z, int64_t n, float *dstf, double *dstd) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double a = 0.0;
+  for (int z = 0; z < Z; ++z) a += part[(int64_t)z * n + i];
+  if (dstf) dstf[i] = (float)a;
+  else dstd[i] = a;
+}
+
+// slabs of the o-split: enough blocks to fill the chip, at least 8 o per slab
+static int koq_splits(int M, int N, int O) {
+  const int tiles = ((M + 31) / 32) * ((N + 31) / 32);
+  return std::max(1, std::min(std::min((256 + tiles - 1) / tiles, (O + 7) / 8), 9));
+}
+
+// part must hold koq_splits(M, N, O) * M * N doubles (the callers' fold part buffer
+// holds 9 R max(C, V) >= that); the result goes to dstf (float) or dstd
+static hipError_t koq(KoqGemm g, double *part, float *dstf, double *dstd, hipStream_t s) {
+  const int S = koq_splits(g.M, g.N, g.O);
+  g.per = (g.O + S - 1) / S;
+  g.part = part;
+  hipLaunchKernelGGL(k_fold_koq, dim3((g.N + 31) / 32, (g.M + 31) / 32, S), dim3(256), 0, s, g);
+  const int64_t n = (int64_t)g.M * g.N;
+  hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, S, n,
+                     dstf, dstd);
+  return hipGetLastError();
+}
+
+// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in)
 hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s) {
-  Gemm64 g{};
-  g.A = Wt; g.am = mp(9, (int64_t)R * 9, 1); g.ak = mp(9);
-  g.B = W; g.bk = mp(C); g.bn = mp(1);
-  g.out = Wc; g.om = mp(9, (int64_t)C * 9, 1); g.on = mp(9);
-  g.M = 9 * R; g.N = C; g.K = R;
-  return gemm64(g, s);
+  TapGemm g{};
+  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.aq = 1;
+  g.B = W; g.bk = C; g.bn = 1;
+  g.out = Wc; g.om = (int64_t)C * 9; g.on = 9; g.oq = 1;
+  g.M = R; g.N = C; g.K = R;
+  return tapgemm(g, s);
 }
 
 // Boundary frames of the folded block: output frames t < nb0 and t >= tb1 read
@@ -177,13 +238,13 @@ __global__ void k_fold_bias(const double *bq, const float *bt, int R, int V, int
 
 hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
                             int To, int st, double *bq, float *BT, hipStream_t s) {
-  // bq[q][o][v]: one (9 R) x V x R GEMM, m = q R + o
-  Gemm64 g{};
-  g.A = Wt; g.am = mp(R, 1, (int64_t)R * 9); g.ak = mp(9);
-  g.B = bZ; g.bk = mp(V); g.bn = mp(1);
-  g.out = bq; g.o_dbl = 1; g.om = mp(R, (int64_t)R * V, V); g.on = mp(1);
-  g.M = 9 * R; g.N = V; g.K = R;
-  HIP_RET(gemm64(g, s));
+  // bq[q][o][v] = sum_c Wt[o][c][q] bZ[c][v]
+  TapGemm g{};
+  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.aq = 1;
+  g.B = bZ; g.bk = V; g.bn = 1;
+  g.out = bq; g.o_dbl = 1; g.om = V; g.on = 1; g.oq = (int64_t)R * V;
+  g.M = R; g.N = V; g.K = R;
+  HIP_RET(tapgemm(g, s));
   const int64_t n = (int64_t)R * To * V;
   hipLaunchKernelGGL(k_fold_bias, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bq, bt, R, V,
                      T, To, st, BT);
@@ -288,9 +349,7 @@ __global__ __launch_bounds__(256) void k_absmax(const float *x, int64_t n, unsig
   } else {
     for (int64_t i = i0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __builtin_bit_cast(unsigned, m));
+  block_amax<256>(m, amax);
 }
 
 hipError_t launch_absmax(const float *x, int64_t n, unsigned *amax, hipStream_t s) {
@@ -310,50 +369,42 @@ __global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *d
 // The folded block's weight gradients from dWc (slab of the temporal weight
 // gradient over C_in channels) and Tq:
 //   dWt[o][c][q] = sum_i dWc[o][i][q] W'[c][i] + sum_v Tq[q][o][v] bZ[c][v]
-//                  ((9 R) x R GEMM over K = C_in, plus the K2 = V bias term)
-//   dW'[c][i]    = sum_{(o,q)} Wt[o][c][q] dWc[o][i][q]   (R x C GEMM over K = 9 R)
-// (part: unused, kept for the caller's workspace layout)
+//   dW'[c][i]    = sum_{(o,q)} Wt[o][c][q] dWc[o][i][q]
+// part: 9 R max(C, V) doubles (the o-split slabs of dW')
 hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
                              const float *bZ, const double *Tq, int R, int C, int V,
                              double *dWc, double *part, float *dWt, float *dW, hipStream_t s) {
-  (void)part;
   const int64_t n = (int64_t)R * C * 9;
   hipLaunchKernelGGL(k_slab_reduce_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slab,
                      S, n, dWc);
   {
-    Gemm64 g{};
-    g.A = dWc; g.a_dbl = 1; g.am = mp(9, (int64_t)C * 9, 1); g.ak = mp(9);
-    g.B = W; g.bk = mp(1); g.bn = mp(C);
-    g.A2 = Tq; g.a2_dbl = 1; g.a2m = mp(9, V, (int64_t)R * V); g.a2k = mp(1);
-    g.B2 = bZ; g.b2k = mp(1); g.b2n = mp(V);
+    TapGemm g{};
+    g.A = dWc; g.a_dbl = 1; g.am = (int64_t)C * 9; g.ak = 9; g.aq = 1;
+    g.B = W; g.bk = 1; g.bn = C;
+    g.A2 = Tq; g.a2q = (int64_t)R * V; g.a2m = V;
+    g.B2 = bZ; g.b2k = 1; g.b2n = V;
     g.K2 = V;
-    g.out = dWt; g.om = mp(9, (int64_t)R * 9, 1); g.on = mp(9);
-    g.M = 9 * R; g.N = R; g.K = C;
-    HIP_RET(gemm64(g, s));
+    g.out = dWt; g.om = (int64_t)R * 9; g.on = 9; g.oq = 1;
+    g.M = R; g.N = R; g.K = C;
+    HIP_RET(tapgemm(g, s));
   }
-  {
-    Gemm64 g{};
-    g.A = Wt; g.am = mp(9); g.ak = mp(9, (int64_t)R * 9, 1);
-    g.B = dWc; g.b_dbl = 1; g.bk = mp(9, (int64_t)C * 9, 1); g.bn = mp(9);
-    g.out = dW; g.om = mp(C); g.on = mp(1);
-    g.M = R; g.N = C; g.K = 9 * R;
-    HIP_RET(gemm64(g, s));
-  }
-  return hipGetLastError();
+  KoqGemm g{};
+  g.A = Wt; g.a_o = (int64_t)R * 9; g.a_m = 9; g.a_q = 1;
+  g.B = dWc; g.b_dbl = 1; g.b_o = (int64_t)C * 9; g.b_n = 9; g.b_q = 1;
+  g.M = R; g.N = C; g.O = R;
+  return koq(g, part, dW, nullptr, s);
 }
 
 // SdZ[c][v] = sum_q sum_o Wt[o][c][q] Tq[q][o][v]  (= sum_{n,t} dZ[c,t,v]; Wt is
-// the temporal weight [R][C][9] with C = its input channels, the Z channels):
-// one C x V GEMM over K = 9 R (k = 9 o + q). (part: unused)
+// the temporal weight [R][C][9] with C = its input channels, the Z channels);
+// part: 9 R max(C, V) doubles
 hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
                            double *SdZ, hipStream_t s) {
-  (void)part;
-  Gemm64 g{};
-  g.A = Wt; g.am = mp(9); g.ak = mp(9, (int64_t)C * 9, 1);
-  g.B = Tq; g.b_dbl = 1; g.bk = mp(9, V, (int64_t)R * V); g.bn = mp(1);
-  g.out = SdZ; g.o_dbl = 1; g.om = mp(V); g.on = mp(1);
-  g.M = C; g.N = V; g.K = 9 * R;
-  return gemm64(g, s);
+  KoqGemm g{};
+  g.A = Wt; g.a_o = (int64_t)C * 9; g.a_m = 9; g.a_q = 1;
+  g.B = Tq; g.b_dbl = 1; g.b_o = V; g.b_n = 1; g.b_q = (int64_t)R * V;
+  g.M = C; g.N = V; g.O = R;
+  return koq(g, part, nullptr, SdZ, s);
 }
 
 }  // namespace stgcn

@@ -112,7 +112,7 @@ __device__ __forceinline__ void splith2(float a, float b, unsigned &h, unsigned 
 // exponent is clamped to +-100 (0 / denormal / inf maxima). Returns the scale's
 // exponent (scale = 2^se).
 __device__ __forceinline__ int f16x2_se(const unsigned *amax) {
-  const int e = (int)((amax ? *amax : 0x3f800000u) >> 23) & 0xff;
+  const int e = (int)((amax ? amax_read(amax) : 0x3f800000u) >> 23) & 0xff;
   const int se = e == 0 ? 0 : 140 - e;
   return se < -100 ? -100 : (se > 100 ? 100 : se);
 }
@@ -478,7 +478,8 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // NPL = 2: the window's power-of-two scale (f16x2_se of max |in|)
   const int in_se = NPL == 2 ? f16x2_se(p.amax_in) : 0;
   const float in_scale = pow2f(in_se);
-  if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid == 0) *p.amax_keep = *p.amax_in;
+  if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid < kAmaxSlots)  // (slot 0: the bound)
+    p.amax_keep[tid * kAmaxStride] = tid == 0 ? amax_read(p.amax_in) : 0u;
   auto load_img = [&](int chunk) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
     const int esz = inb ? 2 : 4;

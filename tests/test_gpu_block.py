@@ -71,7 +71,7 @@ def _compare(got, want, residual=False, tol=TOL, floor=None):
         if k == "grad.temporalConv.bias" and not residual:
             err = float(np.abs(gv - wv).max())
             if err > ATOL_ZERO:
-                bad.append((k, err))
+                bad.append((k, err, ATOL_ZERO))
             continue
         err = rel_to_max(gv, wv)
         lim = max(tol, 2.0 * floor.get(k, 0.0)) if floor else tol
