@@ -322,9 +322,10 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
                 npl = 2 if f16 and fold else 3  # operand planes: fp16 (h, l) or bf16 (h, m, l)
                 spb = "true" if fold else "false"  # the fused SpatialConv backward epilogue
+                # (the data gradient stays on the 3-way splits: capi.hip f16x2_dgrad)
                 sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false,false>",
-                       1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false,{spb}>" if s == 1 else
-                           f"k_conv_x3<5|4,{V},1,1,{npl},false,{spb}>"),
+                       1: (f"k_conv_x3<9,3,{V},1,{mr},3,false,{spb}>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,3,false,{spb}>"),
                        2: f"k_wgrad_x3<{V},{s},{npl}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:

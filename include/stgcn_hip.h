@@ -78,12 +78,14 @@ extern "C" {
                             * OPAQUE (it carries Wc from stgcn_block_fwd to
                             * stgcn_block_bwd). Exclusive with STGCN_F_BF16. */
 #define STGCN_F_F16X2 8    /* ABI 6, with STGCN_F_F32X3 only: the folded block's temporal
-                            * GEMMs (forward, data-grad, weight-grad) as 2-way fp16 splits
+                            * conv forward and weight-grad GEMMs as 2-way fp16 splits
                             * (x s = h + l, 22 significant bits, three partial products,
                             * fp32 accumulate) of operands scaled by powers of two s from
                             * their max |x| (so h <= 2^14 and no element underflows
                             * relative to the tensor's maximum); the result is scaled back
-                            * exactly. Same fp32 gate as STGCN_F_F32X3, half its MFMAs. */
+                            * exactly. Same fp32 gate as STGCN_F_F32X3, half its MFMAs.
+                            * The data gradient keeps the 3-way bf16 splits (its output
+                            * feeds the cancellation-heavy BN1 backward sums). */
 
 enum {
   STGCN_OK = 0,

@@ -125,6 +125,13 @@ bool fold_spb(const stgcn_desc_t *d) { return fold_w(d) && STGCN_AB_SPB_PAIR == 
 // The folded block's temporal GEMMs on 2-way fp16 splits (STGCN_F_F16X2; k_conv_x3 /
 // k_wgrad_x3 with NPL = 2), operand scales from max |x| words (launch_absmax)
 bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
+// ... except the data gradient, which stays on the 3-way bf16 splits: its output
+// H feeds the BN1 backward sums (sum dxhat over N T V elements of a zero-mean
+// dU: heavy cancellation), where the 2^-22 operand representation measured
+// 2.5x the fp32 reference's own error on the BN1 bias gradient at N = 32,
+// T = 300 (the 2^-24 of the 3-way splits stays within it). STGCN_AB_F16X2_DGRAD
+// build: the fp16 splits there too (A/B only).
+bool f16x2_dgrad(const stgcn_desc_t *d) { return f16x2(d) && STGCN_AB_F16X2_DGRAD != 0; }
 
 // sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
 // sums written by the ReLU + BN2 backward apply, k_fold_tq, one small GEMM with
@@ -861,13 +868,13 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
       HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
     }
-    if (f16x2(d))  // the fp16 splits' operand scales: max |dU| (from the apply pass), max |Wc|
+    if (f16x2_dgrad(d))  // the fp16 splits' operand scales: max |dU| (apply pass), max |Wc|
       HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
     {
       ConvGemmParams p = conv_base(d, L.wpk);
       p.in = L.dU;
       p.out = L.H;
-      if (f16x2(d)) {
+      if (f16x2_dgrad(d)) {
         p.f16x2 = 1;
         p.amax_in = L.amax;
         p.amax_w = L.amax + kAmaxWords;
@@ -1267,7 +1274,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
     p.T_src = To;
     p.T_dst = T;
     p.s_in = 1;
-    if (P.amax) {
+    if (P.amax && f16x2_dgrad(d)) {
       p.f16x2 = 1;
       p.amax_in = P.amax;
       p.amax_w = P.amax + kAmaxWords;

@@ -1,6 +1,7 @@
 """GPU parity of the fp32 block with STGCN_F_F16X2 (``gemm="f16x2"``): the
-folded block's temporal GEMMs (forward, data-grad incl. the stride-2 phases,
-weight-grad; st-gcn_amd/csrc/kernels_x3.hip NPL = 2) as 2-way fp16 splits of
+folded block's temporal conv forward and weight-grad GEMMs
+(st-gcn_amd/csrc/kernels_x3.hip NPL = 2; the data gradient keeps the 3-way
+bf16 splits, capi.hip f16x2_dgrad) as 2-way fp16 splits of
 operands scaled by powers of two from their max |x| (x s = h + l, 22
 significant bits; three partial products hh, hl, lh; fp32 accumulate).
 
@@ -38,7 +39,7 @@ def _plan(pkg, x, C_out, stride, K=1):
 @pytest.mark.parametrize("case", [
     # C_in, C_out, stride, V, K, N, T
     (64, 64, 1, 18, 1, 4, 64),      # cfg2 L1-L3 shape (64-row tiles)
-    (64, 128, 2, 18, 1, 3, 37),     # stride 2: the data-grad phases (NQ = 5 / 4), odd T
+    (64, 128, 2, 18, 1, 3, 37),     # stride 2: the strided forward / weight-grad, odd T
     (128, 128, 1, 18, 1, 2, 40),    # 128-row tiles (MR = 2)
     (128, 256, 2, 18, 1, 2, 30),    # 128-row tiles, stride-2 forward, 8 chunks
     (256, 256, 1, 18, 1, 2, 19),    # 16 chunks, ragged T
