@@ -281,7 +281,7 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   if (!residual(d)) {  // clip-chunk sums of dU -> Tq -> sum_{n,t} dZ (kernels_fold.hip)
     L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
     L.ftq = c.take<double>((size_t)9 * R * d->V);
-    L.fpart = c.take<double>(std::max((size_t)9 * R * std::max(C, d->V),
+    L.fpart = c.take<double>(std::max(fold_part_doubles(R, C, d->V),
                                       (size_t)R * apply_cols_chunks(d->N) *
                                           fold_tot_blocks(d->T_out) * d->V));
   }
@@ -331,6 +331,7 @@ struct FwdLayout {
   float *Rp;  // residual projection output (N, C_out, T_out, V)
   float *Wc, *BT;  // the folded block: composite weights, per-frame bias table
   double *bq;      // ... and its per-tap bias products
+  double *fpart;   // ... and the split-K slabs of its small GEMMs
   size_t dbl_bytes, total;
 };
 
@@ -353,6 +354,7 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
     L.Wc = c.take<float>((size_t)R * C * 9);
     L.BT = c.take<float>((size_t)R * nTo(d));
     L.bq = c.take<double>((size_t)9 * R * d->V);
+    L.fpart = c.take<double>(fold_part_doubles(R, C, d->V));
   }
   L.total = c.off;
   return L;
@@ -723,8 +725,9 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.R = R;
     if (fold) {  // U = sum_q Wc_q G[s t + q - 4] + BT[o, t, v]  (kernels_fold.hip)
       float *Wc = fold_wc_in_z(d) ? a->Z : L.Wc;  // (kept for the backward)
-      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, s));
-      HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT, s));
+      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, L.fpart, s));
+      HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT,
+                               L.fpart, s));
       if (f16x2(d)) {  // the fp16 splits' operand scales: max |G| (gather), max |Wc|
         HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
         p.f16x2 = 1;
@@ -860,7 +863,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     // over G gives dWc, and dWt, dW', sum_{n,t} dZ follow from dWc and the dU sums.
     const float *Wc = a->Z;  // (left there by the forward)
     if (!fold_wc_in_z(d)) {
-      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, s));
+      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, L.fpart, s));
       Wc = L.Wc;
     }
     HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));

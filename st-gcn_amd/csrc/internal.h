@@ -127,9 +127,12 @@ hipError_t launch_absmax(const float *x, int64_t n, unsigned *amax, hipStream_t 
 // The folded block (kernels_fold.hip; capi.hip fold_w): composite weights
 // Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i], the per-frame bias table, the dU
 // sums (total, boundary frames, per tap Tq) and the weight gradients from dWc.
-hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s);
+// (part: fold_part_doubles(R, C, V) doubles of split-K slabs for the small GEMMs)
+size_t fold_part_doubles(int R, int C, int V);
+hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, double *part,
+                         hipStream_t s);
 hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
-                            int To, int st, double *bq, float *BT, hipStream_t s);
+                            int To, int st, double *bq, float *BT, double *part, hipStream_t s);
 int fold_tot_blocks(int To);
 hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
                           double *part, double *Tq, hipStream_t s);

@@ -60,46 +60,55 @@ struct TapGemm {
   int o_dbl;
   int64_t om, on, oq;  // out[m om + n on + q oq]
   int M, N, K, K2;
+  double *part;        // [S][M][N][9] split-K partials (summed by k_tap_sum)
+  int kper;            // k per split (a multiple of the chunk)
 };
 
+// One block = 32 x 32 outputs x 9 taps over the k range of split blockIdx.z;
+// the next chunk's operands are loaded into registers while this chunk's MFMAs run.
 __global__ __launch_bounds__(256) void k_fold_tapgemm(TapGemm g) {
   constexpr int KC = 8;
   __shared__ double As[KC][9][32], Bs[KC][32];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
   const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int Ktot = g.K + (g.A2 ? g.K2 : 0);
+  const int kb = blockIdx.z * g.kper, ke = min(Ktot, kb + g.kper);
   double4v acc[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) acc[q] = (double4v){0.0, 0.0, 0.0, 0.0};
-  const int Ktot = g.K + (g.A2 ? g.K2 : 0);
-  for (int k0 = 0; k0 < Ktot; k0 += KC) {
-    __syncthreads();  // the previous chunk's reads are done
+  double ra[9], rb;
+  auto load = [&](int k0) {
 #pragma unroll
     for (int r = 0; r < 9; ++r) {  // A: q fastest, then k, then m (9-tap runs)
       const int e = r * 256 + tid;
       const int q = e % 9, t = e / 9, kk = t % KC, mm = t / KC;
       const int k = k0 + kk, m = m0 + mm;
       double v = 0.0;
-      if (m < g.M) {
+      if (m < g.M && k < ke) {
         if (k < g.K)
           v = ld_fd(g.A, g.a_dbl, m * g.am + k * g.ak + q * g.aq);
-        else if (k < Ktot)
+        else
           v = g.A2[q * g.a2q + m * g.a2m + (k - g.K)];
       }
-      As[kk][q][mm] = v;
+      ra[r] = v;
     }
-    {
-      const int kk = tid >> 5, nn = tid & 31, k = k0 + kk, n = n0 + nn;
-      double v = 0.0;
-      if (n < g.N) {
-        if (k < g.K)
-          v = g.B[k * g.bk + n * g.bn];
-        else if (k < Ktot)
-          v = g.B2[(k - g.K) * g.b2k + n * g.b2n];
-      }
-      Bs[kk][nn] = v;
+    const int kk = tid >> 5, nn = tid & 31, k = k0 + kk, n = n0 + nn;
+    rb = 0.0;
+    if (n < g.N && k < ke) rb = k < g.K ? g.B[k * g.bk + n * g.bn] : g.B2[(k - g.K) * g.b2k + n * g.b2n];
+  };
+  if (kb < ke) load(kb);
+  for (int k0 = kb; k0 < ke; k0 += KC) {
+    __syncthreads();  // the previous chunk's reads are done
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const int e = r * 256 + tid;
+      const int q = e % 9, t = e / 9;
+      As[t % KC][q][t / KC] = ra[r];
     }
+    Bs[tid >> 5][tid & 31] = rb;
     __syncthreads();
+    if (k0 + KC < ke) load(k0 + KC);  // in flight under this chunk's MFMAs
 #pragma unroll
     for (int ks = 0; ks < KC; ks += 4) {
       // A operand: lane l holds A[row l & 15][k l >> 4]; B: B[k l >> 4][col l & 15]
@@ -116,19 +125,40 @@ __global__ __launch_bounds__(256) void k_fold_tapgemm(TapGemm g) {
   for (int r = 0; r < 4; ++r) {
     const int m = m0 + wm + (l >> 4) + 4 * r;
     if (m >= g.M || n >= g.N) continue;
+    double *dst = g.part + (((int64_t)blockIdx.z * g.M + m) * g.N + n) * 9;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) {
-      const int64_t o = m * g.om + n * g.on + q * g.oq;
-      if (g.o_dbl)
-        reinterpret_cast<double *>(g.out)[o] = acc[q][r];
-      else
-        reinterpret_cast<float *>(g.out)[o] = (float)acc[q][r];
-    }
+    for (int q = 0; q < 9; ++q) dst[q] = acc[q][r];
   }
 }
 
-static hipError_t tapgemm(const TapGemm &g, hipStream_t s) {
-  hipLaunchKernelGGL(k_fold_tapgemm, dim3((g.N + 31) / 32, (g.M + 31) / 32), dim3(256), 0, s, g);
+// out[m om + n on + q oq] = sum_s part[s][m][n][q] (fixed order), float or double
+__global__ void k_tap_sum(TapGemm g, int S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)g.M * g.N * 9;
+  if (i >= tot) return;
+  const int q = (int)(i % 9);
+  const int64_t mn = i / 9;
+  const int n = (int)(mn % g.N), m = (int)(mn / g.N);
+  double a = 0.0;
+  for (int z = 0; z < S; ++z) a += g.part[(int64_t)z * tot + i];
+  const int64_t o = m * g.om + n * g.on + q * g.oq;
+  if (g.o_dbl)
+    reinterpret_cast<double *>(g.out)[o] = a;
+  else
+    reinterpret_cast<float *>(g.out)[o] = (float)a;
+}
+
+// split-K over <= 4 slabs so the grid fills the chip (part: 4 * 9 * M * N doubles)
+static hipError_t tapgemm(TapGemm g, double *part, hipStream_t s) {
+  const int tiles = ((g.M + 31) / 32) * ((g.N + 31) / 32);
+  const int Ktot = g.K + (g.A2 ? g.K2 : 0);
+  const int chunks = (Ktot + 7) / 8;
+  const int S = std::max(1, std::min(std::min(4, (256 + tiles - 1) / tiles), chunks));
+  g.kper = (chunks + S - 1) / S * 8;
+  g.part = part;
+  hipLaunchKernelGGL(k_fold_tapgemm, dim3((g.N + 31) / 32, (g.M + 31) / 32, S), dim3(256), 0, s, g);
+  const int64_t tot = (int64_t)g.M * g.N * 9;
+  hipLaunchKernelGGL(k_tap_sum, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, g, S);
   return hipGetLastError();
 }
 
@@ -150,17 +180,33 @@ __global__ __launch_bounds__(256) void k_fold_koq(KoqGemm g) {
   const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
   const int o_begin = blockIdx.z * g.per, o_end = min(g.O, o_begin + g.per);
   double4v acc = {0.0, 0.0, 0.0, 0.0};
-  for (int o0 = o_begin; o0 < o_end; o0 += KO) {
-    __syncthreads();
-    for (int e = tid; e < KO * 9 * 32; e += 256) {  // q fastest, then m / n, then o
+  constexpr int NE = (KO * 9 * 32 + 255) / 256;  // elements per thread and operand
+  double ra[NE], rb[NE];
+  auto load = [&](int o0) {  // q fastest, then m / n, then o
+#pragma unroll
+    for (int r = 0; r < NE; ++r) {
+      const int e = r * 256 + tid;
       const int q = e % 9, t = e / 9, mm = t % 32, oo = t / 32;
       const int o = o0 + oo, m = m0 + mm, n = n0 + mm;
-      const bool ok = o < o_end;
-      As[oo * 9 + q][mm] = ok && m < g.M ? (double)g.A[o * g.a_o + m * g.a_m + q * g.a_q] : 0.0;
-      Bs[oo * 9 + q][mm] =
-          ok && n < g.N ? ld_fd(g.B, g.b_dbl, o * g.b_o + n * g.b_n + q * g.b_q) : 0.0;
+      const bool ok = e < KO * 9 * 32 && o < o_end;
+      ra[r] = ok && m < g.M ? (double)g.A[o * g.a_o + m * g.a_m + q * g.a_q] : 0.0;
+      rb[r] = ok && n < g.N ? ld_fd(g.B, g.b_dbl, o * g.b_o + n * g.b_n + q * g.b_q) : 0.0;
+    }
+  };
+  if (o_begin < o_end) load(o_begin);
+  for (int o0 = o_begin; o0 < o_end; o0 += KO) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NE; ++r) {
+      const int e = r * 256 + tid;
+      if (e < KO * 9 * 32) {
+        const int q = e % 9, t = e / 9, mm = t % 32, oo = t / 32;
+        As[oo * 9 + q][mm] = ra[r];
+        Bs[oo * 9 + q][mm] = rb[r];
+      }
     }
     __syncthreads();
+    if (o0 + KO < o_end) load(o0 + KO);  // in flight under this chunk's MFMAs
 #pragma unroll
     for (int ks = 0; ks < KO * 9; ks += 4)
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(As[ks + (l >> 4)][wm + (l & 15)],
@@ -184,6 +230,10 @@ __global__ void k_sum_parts(const double *part, int Z, int64_t n, float *dstf, d
   else dstd[i] = a;
 }
 
+size_t fold_part_doubles(int R, int C, int V) {
+  return (size_t)36 * R * std::max(std::max(R, C), V);
+}
+
 // slabs of the o-split: enough blocks to fill the chip, at least 8 o per slab
 static int koq_splits(int M, int N, int O) {
   const int tiles = ((M + 31) / 32) * ((N + 31) / 32);
@@ -204,13 +254,14 @@ static hipError_t koq(KoqGemm g, double *part, float *dstf, double *dstd, hipStr
 }
 
 // Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in)
-hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, hipStream_t s) {
+hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, double *part,
+                         hipStream_t s) {
   TapGemm g{};
   g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.aq = 1;
   g.B = W; g.bk = C; g.bn = 1;
   g.out = Wc; g.om = (int64_t)C * 9; g.on = 9; g.oq = 1;
   g.M = R; g.N = C; g.K = R;
-  return tapgemm(g, s);
+  return tapgemm(g, part, s);
 }
 
 // Boundary frames of the folded block: output frames t < nb0 and t >= tb1 read
@@ -237,14 +288,14 @@ __global__ void k_fold_bias(const double *bq, const float *bt, int R, int V, int
 }
 
 hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
-                            int To, int st, double *bq, float *BT, hipStream_t s) {
+                            int To, int st, double *bq, float *BT, double *part, hipStream_t s) {
   // bq[q][o][v] = sum_c Wt[o][c][q] bZ[c][v]
   TapGemm g{};
   g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.aq = 1;
   g.B = bZ; g.bk = V; g.bn = 1;
   g.out = bq; g.o_dbl = 1; g.om = V; g.on = 1; g.oq = (int64_t)R * V;
   g.M = R; g.N = V; g.K = R;
-  HIP_RET(tapgemm(g, s));
+  HIP_RET(tapgemm(g, part, s));
   const int64_t n = (int64_t)R * To * V;
   hipLaunchKernelGGL(k_fold_bias, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bq, bt, R, V,
                      T, To, st, BT);
@@ -370,7 +421,7 @@ __global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *d
 // gradient over C_in channels) and Tq:
 //   dWt[o][c][q] = sum_i dWc[o][i][q] W'[c][i] + sum_v Tq[q][o][v] bZ[c][v]
 //   dW'[c][i]    = sum_{(o,q)} Wt[o][c][q] dWc[o][i][q]
-// part: 9 R max(C, V) doubles (the o-split slabs of dW')
+// part: fold_part_doubles(R, C, V) doubles (split-K slabs)
 hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
                              const float *bZ, const double *Tq, int R, int C, int V,
                              double *dWc, double *part, float *dWt, float *dW, hipStream_t s) {
@@ -386,7 +437,7 @@ hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const fl
     g.K2 = V;
     g.out = dWt; g.om = (int64_t)R * 9; g.on = 9; g.oq = 1;
     g.M = R; g.N = R; g.K = C;
-    HIP_RET(tapgemm(g, s));
+    HIP_RET(tapgemm(g, part, s));
   }
   KoqGemm g{};
   g.A = Wt; g.a_o = (int64_t)R * 9; g.a_m = 9; g.a_q = 1;
@@ -397,7 +448,7 @@ hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const fl
 
 // SdZ[c][v] = sum_q sum_o Wt[o][c][q] Tq[q][o][v]  (= sum_{n,t} dZ[c,t,v]; Wt is
 // the temporal weight [R][C][9] with C = its input channels, the Z channels);
-// part: 9 R max(C, V) doubles
+// part: fold_part_doubles(R, C, V) doubles
 hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
                            double *SdZ, hipStream_t s) {
   KoqGemm g{};
