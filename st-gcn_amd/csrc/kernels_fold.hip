@@ -68,7 +68,9 @@ struct TapGemm {
 // the next chunk's operands are loaded into registers while this chunk's MFMAs run.
 __global__ __launch_bounds__(256) void k_fold_tapgemm(TapGemm g) {
   constexpr int KC = 8;
-  __shared__ double As[KC][9][32], Bs[KC][32];
+  // (rows of 33: the staging writes walk q fastest, 33 doubles apart, so
+  // consecutive lanes hit different banks; 32 would put all nine taps on one)
+  __shared__ double As[KC][9][33], Bs[KC][32];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
   const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
@@ -174,7 +176,7 @@ struct KoqGemm {
 
 __global__ __launch_bounds__(256) void k_fold_koq(KoqGemm g) {
   constexpr int KO = 4;  // o per chunk: 36 k = 9 MFMA k-steps
-  __shared__ double As[KO * 9][32], Bs[KO * 9][32];
+  __shared__ double As[KO * 9][33], Bs[KO * 9][33];  // (33: conflict-free staging writes)
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
   const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
