@@ -259,7 +259,8 @@ struct BwdLayout {
   float *Wpk;  // W' = [W_0 | ... | W_{K-1}] (C_out, K*C_in) for the stacked H GEMM
   float *Rg;  // residual projection data-grad (N, C_in, T, V)
   // the folded block: dU summed over clips, per-tap sums Tq, dWc, partials, Wc, bZ
-  double *fcs, *ftq, *dWc, *fpart;
+  double *fcs, *ftq, *fpart, *f64scr, *SdH;
+  float *dWc, *fscr;  // the fold GEMMs' operand re-layouts (kernels_fold.hip)
   float *Wc, *bZ;
   size_t dbl_bytes, total;
 };
@@ -281,12 +282,15 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   if (!residual(d)) {  // clip-chunk sums of dU -> Tq -> sum_{n,t} dZ (kernels_fold.hip)
     L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
     L.ftq = c.take<double>((size_t)9 * R * d->V);
-    L.fpart = c.take<double>(std::max(fold_part_doubles(R, C, d->V),
-                                      (size_t)R * apply_cols_chunks(d->N) *
-                                          fold_tot_blocks(d->T_out) * d->V));
+    L.f64scr = c.take<double>(fold_sdz_scratch_doubles(R, C, d->V));
+    L.fpart = c.take<double>((size_t)R * apply_cols_chunks(d->N) * fold_tot_blocks(d->T_out) *
+                             d->V);
   }
   if (fold_w(d)) {
-    L.dWc = c.take<double>((size_t)R * C * 9);
+    L.dWc = c.take<float>(fold_dwc_floats(R, C));
+    L.fscr = c.take<float>(std::max(fold_bwd_scratch_floats(R, C),
+                                    fold_fwd_scratch_floats(R, C, d->V)));
+    L.SdH = c.take<double>((size_t)C * d->V);
     L.Wc = c.take<float>((size_t)R * C * 9);
     L.bZ = c.take<float>((size_t)R * d->V);
   }
@@ -331,7 +335,7 @@ struct FwdLayout {
   float *Rp;  // residual projection output (N, C_out, T_out, V)
   float *Wc, *BT;  // the folded block: composite weights, per-frame bias table
   double *bq;      // ... and its per-tap bias products
-  double *fpart;   // ... and the split-K slabs of its small GEMMs
+  float *fscr;     // ... and its GEMM operand re-layouts
   size_t dbl_bytes, total;
 };
 
@@ -354,7 +358,7 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
     L.Wc = c.take<float>((size_t)R * C * 9);
     L.BT = c.take<float>((size_t)R * nTo(d));
     L.bq = c.take<double>((size_t)9 * R * d->V);
-    L.fpart = c.take<double>(fold_part_doubles(R, C, d->V));
+    L.fscr = c.take<float>(fold_fwd_scratch_floats(R, C, d->V));
   }
   L.total = c.off;
   return L;
@@ -725,9 +729,8 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.R = R;
     if (fold) {  // U = sum_q Wc_q G[s t + q - 4] + BT[o, t, v]  (kernels_fold.hip)
       float *Wc = fold_wc_in_z(d) ? a->Z : L.Wc;  // (kept for the backward)
-      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, Wc, L.fpart, s));
-      HIP_TRY(launch_fold_bias(a->Wt, a->bWt, L.biasZ, R, V, T, To, d->stride, L.bq, L.BT,
-                               L.fpart, s));
+      HIP_TRY(launch_fold_fwd(a->Wt, a->W, a->bWt, L.biasZ, R, C, V, T, To, d->stride, Wc, L.bq,
+                              L.BT, L.fscr, s));
       if (f16x2(d)) {  // the fp16 splits' operand scales: max |G| (gather), max |Wc|
         HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
         p.f16x2 = 1;
@@ -863,13 +866,16 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     // over G gives dWc, and dWt, dW', sum_{n,t} dZ follow from dWc and the dU sums.
     const float *Wc = a->Z;  // (left there by the forward)
     if (!fold_wc_in_z(d)) {
-      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, L.fpart, s));
+      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, L.fscr, s));
       Wc = L.Wc;
     }
     HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));
-    if (fold_spb(d)) {  // dbW and the bias part of dA first: the data gradient adds to dA
-      HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
+    HIP_TRY(launch_fold_prep_bwd(a->Wt, a->W, R, C, L.fscr, s));
+    if (fold_spb(d)) {  // dbW and the bias part of dA first: the data gradient adds to dA;
+      // BN1's sd from the dU sums (fp64, exact against the cancellation in sum dxhat)
+      HIP_TRY(launch_fold_sdz(L.f64scr, a->Wt, Wc, L.ftq, R, C, V, L.SdZ, L.SdH, s));
       HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
+      HIP_TRY(launch_fold_sd(L.SdH, a->A, C, V, L.sd, s));
     }
     if (f16x2_dgrad(d))  // the fp16 splits' operand scales: max |dU| (apply pass), max |Wc|
       HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
@@ -893,6 +899,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
         p.b1 = a->b1;
         if (defer) p.prev = pvb;
         p.sd = L.sd;
+        p.sd_given = 1;
         p.sdn = L.sdn;
         p.dA = a->dA;
       }
@@ -945,7 +952,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       w.amax_q = amax_g;
     }
     HIP_TRY(launch_wgrad_taps(w, s));
-    HIP_TRY(launch_fold_grads(L.slab, w.S, a->Wt, a->W, L.bZ, L.ftq, R, C, V, L.dWc, L.fpart,
+    HIP_TRY(launch_fold_grads(L.slab, w.S, L.fscr, L.bZ, L.ftq, R, C, V, L.dWc,
                               a->dWt, a->dW, s));
   } else {
   // Temporal conv data-gradient: dZ = conv^T(dU)
@@ -1046,7 +1053,8 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   // non-residual block (dZ = conv^T(dU)); the residual block's dZ passes BN2
   // (the fused folded backward did both before its data gradient)
   if (!fold_spb(d)) {
-    if (cols_sums(d)) HIP_TRY(launch_fold_sdz(a->Wt, L.ftq, R, R, V, L.fpart, L.SdZ, s));
+    if (cols_sums(d))
+      HIP_TRY(launch_fold_sdz(L.f64scr, a->Wt, nullptr, L.ftq, R, C, V, L.SdZ, nullptr, s));
     HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
   }
   if (fold_spb(d)) {

@@ -92,6 +92,7 @@ struct ConvGemmParams {
   // s1 / s2 over the previous block's U read from sx) and dA += H^T BN1(x):
   // the SpatialConv backward never round-trips H through HBM.
   int spb;
+  int sd_given;  // sd already holds sum dxhat (launch_fold_sd): the epilogue adds only sdn
   const float *sx, *sA, *mean1, *invstd1, *g1, *b1;
   PrevBn prev;
   double *sd, *sdn;
@@ -127,20 +128,31 @@ hipError_t launch_absmax(const float *x, int64_t n, unsigned *amax, hipStream_t 
 // The folded block (kernels_fold.hip; capi.hip fold_w): composite weights
 // Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i], the per-frame bias table, the dU
 // sums (total, boundary frames, per tap Tq) and the weight gradients from dWc.
-// (part: fold_part_doubles(R, C, V) doubles of split-K slabs for the small GEMMs)
-size_t fold_part_doubles(int R, int C, int V);
-hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, double *part,
+// (scratch: fold_fwd_scratch_floats / fold_bwd_scratch_floats of padded
+// operand re-layouts; dwc: fold_dwc_floats)
+size_t fold_fwd_scratch_floats(int R, int C, int V);
+size_t fold_bwd_scratch_floats(int R, int C);
+size_t fold_sdz_scratch_doubles(int R, int C, int V);
+size_t fold_dwc_floats(int R, int C);
+hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, float *scratch,
                          hipStream_t s);
-hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
-                            int To, int st, double *bq, float *BT, double *part, hipStream_t s);
+hipError_t launch_fold_fwd(const float *Wt, const float *W, const float *bt, const float *bZ, int R,
+                           int C, int V, int T, int To, int st, float *Wc, double *bq, float *BT,
+                           float *scratch, hipStream_t s);
+hipError_t launch_fold_prep_bwd(const float *Wt, const float *W, int R, int C, float *scratch,
+                                hipStream_t s);
 int fold_tot_blocks(int To);
 hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
                           double *part, double *Tq, hipStream_t s);
-hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
-                           double *SdZ, hipStream_t s);
-hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
-                             const float *bZ, const double *Tq, int R, int C, int V,
-                             double *dWc, double *part, float *dWt, float *dW, hipStream_t s);
+// SdZ = sum_{n,t} dZ and (Wc, SdH non-null) SdH = sum_{n,t} H from Tq, fp64
+hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
+                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s);
+// BN1's sd (db1) of the folded block from SdH: sd[c] = sum_v SdH[c][v] rowsum(A)[v]
+hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, double *sd,
+                          hipStream_t s);
+hipError_t launch_fold_grads(const float *slab, int S, const float *scratch, const float *bZ,
+                             const double *Tq, int R, int C, int V, float *dwc, float *dWt,
+                             float *dW, hipStream_t s);
 // k_bn_relu_bwd_apply that also writes the clip-chunk sums of dU,
 // cs[z][C][L] for z < apply_cols_chunks(N) (kernels.hip)
 int apply_cols_chunks(int N);

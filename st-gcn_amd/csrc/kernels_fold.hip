@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <initializer_list>
 
 #include "device_common.h"
 #include "internal.h"
@@ -28,242 +29,295 @@
 
 namespace stgcn {
 
-// The fold's small GEMMs on the fp64 matrix cores (v_mfma_f64_16x16x4_f64;
-// operands float or double converted exactly, fp64 products and accumulation
-// in a fixed order: deterministic). Two shapes cover them:
+// The fold's small GEMMs on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: a
+// k-ordered fp32 fma chain per output, fixed order: deterministic).
 //
-// k_fold_tapgemm: out[m][n][q] = sum_k A[m][k][q] B[k][n] (+ sum_v A2[q][m][v] B2[v][n])
-//   for all nine taps q in ONE block: the A rows are contiguous 9-tap runs
-//   (coalesced), the B tile is shared by the taps. Wc = Wt W', dWt = dWc W'^T
-//   (+ the Tq bZ bias term) and the bias products bq.
-// k_fold_koq: out[m][n] = sum_o sum_q A[o][m][q] B[o][n][q]: K = (o, q), split
-//   over o in slabs summed in a fixed order afterwards. dW' = sum_q Wt_q^T dWc_q
-//   and sum_{n,t} dZ = sum_q Wt_q^T Tq.
-// Tiles of 32 x 32 per block, wave = one 16 x 16 MFMA tile (per tap).
+// Operands are first re-laid by k_fold_tr as fp32 [plane q][row][k] with k
+// contiguous and rows and k zero-padded to multiples of 32, so the GEMM's inner
+// loop is pure loads + MFMAs: lane l (row l & 31, k-half l >> 5) loads eight
+// consecutive k (32 bytes) per operand for eight MFMAs, no conversions, no
+// bounds selects. The small GEMMs are bound by operand traffic from L2, not by
+// the matrix rate: a 32 x 32 fp32 tile per wave moves 4x fewer bytes per flop
+// than a 16 x 16 fp64 one (measured 2-4x faster per launch).
+//
+// k_fold_gemm: block = nine waves = the nine taps q of one 32 x 32 output tile;
+// each wave streams its whole K range (L2-resident operands) with the next
+// 16-k group's loads in flight (no LDS staging, no split-K partials). Two kinds:
+//   TAP: out[q](m, n) = sum_k A[q](m, k) B[q](n, k) + sum_v A2(q, m, v) B2(n, v)
+//        (each wave writes its tap): Wc = Wt W', the bias products bq,
+//        dWt = dWc W'^T + Tq bZ (the short A2 / B2 term read directly)
+//   RED: out(m, n) = sum_q sum_k A[q](m, k) B[q](n, k) (the nine waves' tiles
+//        summed in LDS in tap order, in fp64): dW' = sum_q Wt_q^T dWc_q and
+//        sum_{n,t} dZ = sum_q Wt_q^T Tq.
+// Up to three jobs share a launch (blockIdx.x runs over their tiles).
+typedef float float16v __attribute__((ext_vector_type(16)));
+typedef float float8v __attribute__((ext_vector_type(8)));
 typedef double double4v __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ double ld_fd(const void *p, int dbl, int64_t i) {
-  return dbl ? reinterpret_cast<const double *>(p)[i] : (double)reinterpret_cast<const float *>(p)[i];
-}
+__host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
 
-struct TapGemm {
-  const void *A;
-  int a_dbl;
-  int64_t am, ak, aq;  // A[m am + k ak + q aq]
-  const float *B;
-  int64_t bk, bn;      // B[k bk + n bn]
-  const double *A2;    // (or null) A2[q a2q + m a2m + v], v < K2
-  int64_t a2q, a2m;
-  const float *B2;     // B2[v b2k + n b2n]
-  int64_t b2k, b2n;
+struct FoldJob {
+  const float *A, *B;  // A[q aq + m am + k], B[q bq + n bn + k] (padded re-layouts)
+  int64_t aq, am, bq, bn;
+  const double *A2;    // TAP only (or null): A2[q a2q + m a2m + v] B2[n b2n + v], v < K2
+  const float *B2;
+  int64_t a2q, a2m, b2n;
   void *out;
-  int o_dbl;
-  int64_t om, on, oq;  // out[m om + n on + q oq]
+  int64_t oq, om, on;  // out[q oq + m om + n on] (RED: q = 0)
+  int o_dbl, red;
   int M, N, K, K2;
-  double *part;        // [S][M][N][9] split-K partials (summed by k_tap_sum)
-  int kper;            // k per split (a multiple of the chunk)
 };
 
-// One block = 32 x 32 outputs x 9 taps over the k range of split blockIdx.z;
-// the next chunk's operands are loaded into registers while this chunk's MFMAs run.
-__global__ __launch_bounds__(256) void k_fold_tapgemm(TapGemm g) {
-  constexpr int KC = 8;
-  // (rows of 33: the staging writes walk q fastest, 33 doubles apart, so
-  // consecutive lanes hit different banks; 32 would put all nine taps on one)
-  __shared__ double As[KC][9][33], Bs[KC][32];
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
-  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
-  const int Ktot = g.K + (g.A2 ? g.K2 : 0);
-  const int kb = blockIdx.z * g.kper, ke = min(Ktot, kb + g.kper);
-  double4v acc[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) acc[q] = (double4v){0.0, 0.0, 0.0, 0.0};
-  double ra[9], rb;
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {  // A: q fastest, then k, then m (9-tap runs)
-      const int e = r * 256 + tid;
-      const int q = e % 9, t = e / 9, kk = t % KC, mm = t / KC;
-      const int k = k0 + kk, m = m0 + mm;
-      double v = 0.0;
-      if (m < g.M && k < ke) {
-        if (k < g.K)
-          v = ld_fd(g.A, g.a_dbl, m * g.am + k * g.ak + q * g.aq);
-        else
-          v = g.A2[q * g.a2q + m * g.a2m + (k - g.K)];
+struct FoldJobs {
+  FoldJob j[3];
+  int n;
+  int tile0[4];  // first tile of job i; tile0[n] = the grid
+};
+
+__global__ __launch_bounds__(576) void k_fold_gemm(FoldJobs js) {
+  __shared__ float red[9][32 * 33];
+  const int tile = blockIdx.x;
+  int ji = 0;
+  while (ji + 1 < js.n && tile >= js.tile0[ji + 1]) ++ji;
+  const FoldJob &g = js.j[ji];
+  const int t = tile - js.tile0[ji], ntn = (g.N + 31) >> 5;
+  const int m0 = (t / ntn) * 32, n0 = (t % ntn) * 32;
+  const int q = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
+  float16v acc = {};
+  {
+    // lane: k = 16 i + 8 h + j for MFMA j of group i (the pair k, k + 8 per MFMA)
+    const float *pa = g.A + q * g.aq + (int64_t)(m0 + r32) * g.am + 8 * h;
+    const float *pb = g.B + q * g.bq + (int64_t)(n0 + r32) * g.bn + 8 * h;
+    const int ng = (g.K + 15) >> 4;
+    float8v a = *reinterpret_cast<const float8v *>(pa);
+    float8v b = *reinterpret_cast<const float8v *>(pb);
+    for (int i = 0; i < ng; ++i) {
+      float8v an = a, bn = b;
+      if (i + 1 < ng) {
+        an = *reinterpret_cast<const float8v *>(pa + 16 * (i + 1));
+        bn = *reinterpret_cast<const float8v *>(pb + 16 * (i + 1));
       }
-      ra[r] = v;
-    }
-    const int kk = tid >> 5, nn = tid & 31, k = k0 + kk, n = n0 + nn;
-    rb = 0.0;
-    if (n < g.N && k < ke) rb = k < g.K ? g.B[k * g.bk + n * g.bn] : g.B2[(k - g.K) * g.b2k + n * g.b2n];
-  };
-  if (kb < ke) load(kb);
-  for (int k0 = kb; k0 < ke; k0 += KC) {
-    __syncthreads();  // the previous chunk's reads are done
 #pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      const int e = r * 256 + tid;
-      const int q = e % 9, t = e / 9;
-      As[t % KC][q][t / KC] = ra[r];
-    }
-    Bs[tid >> 5][tid & 31] = rb;
-    __syncthreads();
-    if (k0 + KC < ke) load(k0 + KC);  // in flight under this chunk's MFMAs
-#pragma unroll
-    for (int ks = 0; ks < KC; ks += 4) {
-      // A operand: lane l holds A[row l & 15][k l >> 4]; B: B[k l >> 4][col l & 15]
-      const double b = Bs[ks + (l >> 4)][wn + (l & 15)];
-#pragma unroll
-      for (int q = 0; q < 9; ++q)
-        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(As[ks + (l >> 4)][q][wm + (l & 15)], b,
-                                                      acc[q], 0, 0, 0);
+      for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+      a = an;
+      b = bn;
     }
   }
-  // C/D: col = lane & 15, row = (lane >> 4) + 4 * reg
-  const int n = n0 + wn + (l & 15);
+  if (g.A2) {  // (short: K2 = V; bounds-checked direct reads)
+    const int m = m0 + r32, n = n0 + r32;
+    const bool ok_m = m < g.M, ok_n = n < g.N;
+    const double *a2 = g.A2 + q * g.a2q + (int64_t)min(m, g.M - 1) * g.a2m;
+    const float *b2 = g.B2 + (int64_t)min(n, g.N - 1) * g.b2n;
+    for (int k0 = 0; k0 < g.K2; k0 += 2) {
+      const int k = k0 + h, kc = min(k, g.K2 - 1);
+      const float x = (float)a2[kc], y = b2[kc];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(k < g.K2 && ok_m ? x : 0.f,
+                                                 k < g.K2 && ok_n ? y : 0.f, acc, 0, 0, 0);
+    }
+  }
+  // C/D: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+  if (!g.red) {
+    const int nn = n0 + r32;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int m = m0 + wm + (l >> 4) + 4 * r;
-    if (m >= g.M || n >= g.N) continue;
-    double *dst = g.part + (((int64_t)blockIdx.z * g.M + m) * g.N + n) * 9;
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (mm >= g.M || nn >= g.N) continue;
+      const int64_t o = q * g.oq + mm * g.om + nn * g.on;
+      if (g.o_dbl)
+        reinterpret_cast<double *>(g.out)[o] = acc[r];
+      else
+        reinterpret_cast<float *>(g.out)[o] = acc[r];
+    }
+    return;
+  }
 #pragma unroll
-    for (int q = 0; q < 9; ++q) dst[q] = acc[q][r];
+  for (int r = 0; r < 16; ++r) red[q][((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + r32] = acc[r];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 1024; e += 576) {
+    const int rr = e >> 5, cc = e & 31;
+    const int mm = m0 + rr, nn = n0 + cc;
+    if (mm >= g.M || nn >= g.N) continue;
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) s += red[w][rr * 33 + cc];
+    const int64_t o = mm * g.om + nn * g.on;
+    if (g.o_dbl)
+      reinterpret_cast<double *>(g.out)[o] = s;
+    else
+      reinterpret_cast<float *>(g.out)[o] = (float)s;
   }
 }
 
-// out[m om + n on + q oq] = sum_s part[s][m][n][q] (fixed order), float or double
-__global__ void k_tap_sum(TapGemm g, int S) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t tot = (int64_t)g.M * g.N * 9;
-  if (i >= tot) return;
-  const int q = (int)(i % 9);
-  const int64_t mn = i / 9;
-  const int n = (int)(mn % g.N), m = (int)(mn / g.N);
-  double a = 0.0;
-  for (int z = 0; z < S; ++z) a += g.part[(int64_t)z * tot + i];
-  const int64_t o = m * g.om + n * g.on + q * g.oq;
-  if (g.o_dbl)
-    reinterpret_cast<double *>(g.out)[o] = a;
+static hipError_t fold_gemm(std::initializer_list<FoldJob> jobs, hipStream_t s) {
+  FoldJobs js{};
+  js.n = 0;
+  int tiles = 0;
+  for (const FoldJob &g : jobs) {
+    if (js.n == 3 || g.M <= 0 || g.N <= 0) return hipErrorInvalidValue;
+    js.j[js.n] = g;
+    js.tile0[js.n++] = tiles;
+    tiles += ((g.M + 31) / 32) * ((g.N + 31) / 32);
+  }
+  js.tile0[js.n] = tiles;
+  hipLaunchKernelGGL(k_fold_gemm, dim3(tiles), dim3(576), 0, s, js);
+  return hipGetLastError();
+}
+
+// k_fold_tr: the padded fp32 re-layouts. A job reads src(q, o, i) =
+// sum_{k < S} src[k sstride + q sq + o so + i si] (slabs summed in order in
+// fp64, then rounded to fp32; q < nq,
+// nq = 9 or 1) and writes outQ[q][o][i] (rows O -> Op = pad32(O), row stride
+// Ip = pad32(I)) and / or outT[q][i][o] (rows Ip, row stride Op), zeros in the
+// padding. Tile = OT o-rows x 16 i x nq taps, one element per thread (576
+// threads; OT = 4 for nq = 9, 36 for nq = 1); up to three jobs per launch.
+struct TrJob {
+  const void *src;
+  int s_dbl, S, nq, q_inner;  // q_inner: sq == 1 (the element order q, i, o)
+  int64_t sstride, sq, so, si;
+  int O, I;
+  void *outQ, *outT;
+  int o_dbl;    // outputs fp64 (else fp32)
+  int tiles_i;  // tiles along i (pad32(I) / 16)
+};
+
+struct TrJobs {
+  TrJob j[3];
+  int n;
+  int tile0[4];
+};
+
+__global__ __launch_bounds__(576) void k_fold_tr(TrJobs js) {
+  __shared__ double tile[36 * 16 + 4];
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  int ji = 0;
+  while (ji + 1 < js.n && blk >= js.tile0[ji + 1]) ++ji;
+  const TrJob &g = js.j[ji];
+  const int t = blk - js.tile0[ji];
+  const int nq = g.nq, OT = nq == 9 ? 4 : 36;
+  const int o0 = (t / g.tiles_i) * OT, i0 = (t % g.tiles_i) * 16;
+  const int Op = pad32(g.O), Ip = pad32(g.I);
+  // element e = tid: (oo, ii, q) with the source's innermost index fastest
+  int oo, ii, q;
+  if (nq == 1) {
+    oo = tid >> 4; ii = tid & 15; q = 0;
+  } else if (g.q_inner) {
+    oo = tid / 144; const int r = tid - oo * 144; ii = r / 9; q = r - ii * 9;
+  } else {
+    oo = tid / 144; const int r = tid - oo * 144; q = r >> 4; ii = r & 15;
+  }
+  const int o = o0 + oo, i = i0 + ii;
+  double v = 0.0;
+  if (o < g.O && i < g.I) {
+    const int64_t at = q * g.sq + o * g.so + i * g.si;
+    if (g.s_dbl) {
+      v = reinterpret_cast<const double *>(g.src)[at];
+    } else {
+      const float *p = reinterpret_cast<const float *>(g.src) + at;
+      int k = 0;
+      for (; k + 4 <= g.S; k += 4) {  // (four loads in flight, summed in slab order)
+        const float a0 = p[k * g.sstride], a1 = p[(k + 1) * g.sstride],
+                    a2 = p[(k + 2) * g.sstride], a3 = p[(k + 3) * g.sstride];
+        v += a0;
+        v += a1;
+        v += a2;
+        v += a3;
+      }
+      for (; k < g.S; ++k) v += p[k * g.sstride];
+    }
+  }
+  const int slot = (q * OT + oo) * 16 + ii;  // tile[q][oo][ii]
+  tile[slot + slot / 16 / 8] = v;           // (a pad word every 8 rows)
+  __syncthreads();
+  if (g.outQ) {  // [q][o][i]: runs of 16 i; the thread's own element order
+    const int sq2 = tid / (OT * 16), a = (tid >> 4) % OT, b = tid & 15;
+    const int s2 = (sq2 * OT + a) * 16 + b;
+    const int64_t at = ((int64_t)sq2 * Op + o0 + a) * Ip + i0 + b;
+    if (o0 + a < Op) {
+      if (g.o_dbl)
+        reinterpret_cast<double *>(g.outQ)[at] = tile[s2 + s2 / 16 / 8];
+      else
+        reinterpret_cast<float *>(g.outQ)[at] = (float)tile[s2 + s2 / 16 / 8];
+    }
+  }
+  if (g.outT) {  // [q][i][o]: runs of OT o
+    const int sq2 = tid / (OT * 16), a = (tid / OT) & 15, b = tid % OT;
+    const int s2 = (sq2 * OT + b) * 16 + a;
+    const int64_t at = ((int64_t)sq2 * Ip + i0 + a) * Op + o0 + b;
+    if (o0 + b < Op) {
+      if (g.o_dbl)
+        reinterpret_cast<double *>(g.outT)[at] = tile[s2 + s2 / 16 / 8];
+      else
+        reinterpret_cast<float *>(g.outT)[at] = (float)tile[s2 + s2 / 16 / 8];
+    }
+  }
+}
+
+static TrJob tr_job(const void *src, int s_dbl, int S, int64_t sstride, int nq, int64_t sq,
+                    int64_t so, int64_t si, int O, int I, float *outQ, float *outT,
+                    double *outQd = nullptr, double *outTd = nullptr) {
+  TrJob g{};
+  g.src = src; g.s_dbl = s_dbl; g.S = S; g.sstride = sstride;
+  g.nq = nq; g.sq = sq; g.so = so; g.si = si; g.q_inner = sq == 1;
+  g.O = O; g.I = I; g.outQ = outQ; g.outT = outT;
+  if (outQd || outTd) {
+    g.o_dbl = 1;
+    g.outQ = outQd;
+    g.outT = outTd;
+  }
+  g.tiles_i = pad32(I) / 16;
+  return g;
+}
+
+static hipError_t fold_tr(std::initializer_list<TrJob> jobs, hipStream_t s) {
+  TrJobs js{};
+  int tiles = 0;
+  for (const TrJob &g : jobs) {
+    if (js.n == 3 || (g.nq != 1 && g.nq != 9) || g.O <= 0 || g.I <= 0) return hipErrorInvalidValue;
+    js.j[js.n] = g;
+    js.tile0[js.n++] = tiles;
+    const int OT = g.nq == 9 ? 4 : 36;
+    tiles += g.tiles_i * ((pad32(g.O) + OT - 1) / OT);
+  }
+  js.tile0[js.n] = tiles;
+  hipLaunchKernelGGL(k_fold_tr, dim3(tiles), dim3(576), 0, s, js);
+  return hipGetLastError();
+}
+
+// Wt [R][R][9] (o, c, q) as the A operand WtQ[q][o][c] of Wc and bq; W' [R][C]
+// (c, i) as W'T[i][c]; bZ [R][V] (c, v) as bZT[v][c]
+size_t fold_fwd_scratch_floats(int R, int C, int V) {
+  const int Rp = pad32(R);
+  return (size_t)Rp * (9 * Rp + pad32(C) + pad32(V));
+}
+
+// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]  and  bq[q][o][v] = sum_c Wt[o][c][q] bZ[c][v]
+static hipError_t fold_fwd_gemms(const float *Wt, const float *W, const float *bZ, int R, int C,
+                                 int V, float *Wc, double *bq, float *scratch, hipStream_t s) {
+  const int Rp = pad32(R), Cp = pad32(C);
+  float *wtq = scratch, *wT = wtq + (size_t)9 * Rp * Rp, *bzT = wT + (size_t)Cp * Rp;
+  const TrJob ja = tr_job(Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, wtq, nullptr);
+  const TrJob jb = tr_job(W, 0, 1, 0, 1, 0, C, 1, R, C, nullptr, wT);
+  if (bq)
+    HIP_RET(fold_tr({ja, jb, tr_job(bZ, 0, 1, 0, 1, 0, V, 1, R, V, nullptr, bzT)}, s));
   else
-    reinterpret_cast<float *>(g.out)[o] = (float)a;
+    HIP_RET(fold_tr({ja, jb}, s));
+  FoldJob w{};
+  w.A = wtq; w.aq = (int64_t)Rp * Rp; w.am = Rp;
+  w.B = wT; w.bn = Rp;
+  w.out = Wc; w.oq = 1; w.om = (int64_t)C * 9; w.on = 9;
+  w.M = R; w.N = C; w.K = R;
+  if (!bq) return fold_gemm({w}, s);
+  FoldJob b{};
+  b.A = wtq; b.aq = (int64_t)Rp * Rp; b.am = Rp;
+  b.B = bzT; b.bn = Rp;
+  b.out = bq; b.o_dbl = 1; b.oq = (int64_t)R * V; b.om = V; b.on = 1;
+  b.M = R; b.N = V; b.K = R;
+  return fold_gemm({w, b}, s);
 }
 
-// split-K over <= 4 slabs so the grid fills the chip (part: 4 * 9 * M * N doubles)
-static hipError_t tapgemm(TapGemm g, double *part, hipStream_t s) {
-  const int tiles = ((g.M + 31) / 32) * ((g.N + 31) / 32);
-  const int Ktot = g.K + (g.A2 ? g.K2 : 0);
-  const int chunks = (Ktot + 7) / 8;
-  const int S = std::max(1, std::min(std::min(4, (256 + tiles - 1) / tiles), chunks));
-  g.kper = (chunks + S - 1) / S * 8;
-  g.part = part;
-  hipLaunchKernelGGL(k_fold_tapgemm, dim3((g.N + 31) / 32, (g.M + 31) / 32, S), dim3(256), 0, s, g);
-  const int64_t tot = (int64_t)g.M * g.N * 9;
-  hipLaunchKernelGGL(k_tap_sum, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, g, S);
-  return hipGetLastError();
-}
-
-struct KoqGemm {
-  const float *A;
-  int64_t a_o, a_m, a_q;  // A[o a_o + m a_m + q a_q]
-  const void *B;
-  int b_dbl;
-  int64_t b_o, b_n, b_q;  // B[o b_o + n b_n + q b_q]
-  double *part;           // [S][M][N] partial sums over o-slices
-  int M, N, O, per;       // o in [s per, min(O, (s + 1) per)) for split s = blockIdx.z
-};
-
-__global__ __launch_bounds__(256) void k_fold_koq(KoqGemm g) {
-  constexpr int KO = 4;  // o per chunk: 36 k = 9 MFMA k-steps
-  __shared__ double As[KO * 9][33], Bs[KO * 9][33];  // (33: conflict-free staging writes)
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int wm = (w & 1) * 16, wn = (w >> 1) * 16;
-  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
-  const int o_begin = blockIdx.z * g.per, o_end = min(g.O, o_begin + g.per);
-  double4v acc = {0.0, 0.0, 0.0, 0.0};
-  constexpr int NE = (KO * 9 * 32 + 255) / 256;  // elements per thread and operand
-  double ra[NE], rb[NE];
-  auto load = [&](int o0) {  // q fastest, then m / n, then o
-#pragma unroll
-    for (int r = 0; r < NE; ++r) {
-      const int e = r * 256 + tid;
-      const int q = e % 9, t = e / 9, mm = t % 32, oo = t / 32;
-      const int o = o0 + oo, m = m0 + mm, n = n0 + mm;
-      const bool ok = e < KO * 9 * 32 && o < o_end;
-      ra[r] = ok && m < g.M ? (double)g.A[o * g.a_o + m * g.a_m + q * g.a_q] : 0.0;
-      rb[r] = ok && n < g.N ? ld_fd(g.B, g.b_dbl, o * g.b_o + n * g.b_n + q * g.b_q) : 0.0;
-    }
-  };
-  if (o_begin < o_end) load(o_begin);
-  for (int o0 = o_begin; o0 < o_end; o0 += KO) {
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < NE; ++r) {
-      const int e = r * 256 + tid;
-      if (e < KO * 9 * 32) {
-        const int q = e % 9, t = e / 9, mm = t % 32, oo = t / 32;
-        As[oo * 9 + q][mm] = ra[r];
-        Bs[oo * 9 + q][mm] = rb[r];
-      }
-    }
-    __syncthreads();
-    if (o0 + KO < o_end) load(o0 + KO);  // in flight under this chunk's MFMAs
-#pragma unroll
-    for (int ks = 0; ks < KO * 9; ks += 4)
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(As[ks + (l >> 4)][wm + (l & 15)],
-                                                 Bs[ks + (l >> 4)][wn + (l & 15)], acc, 0, 0, 0);
-  }
-  const int n = n0 + wn + (l & 15);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int m = m0 + wm + (l >> 4) + 4 * r;
-    if (m < g.M && n < g.N) g.part[((int64_t)blockIdx.z * g.M + m) * g.N + n] = acc[r];
-  }
-}
-
-// dst[i] = sum_{z < Z} part[z * n + i] (fixed order), as float or double
-__global__ void k_sum_parts(const double *part, int Z, int64_t n, float *dstf, double *dstd) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double a = 0.0;
-  for (int z = 0; z < Z; ++z) a += part[(int64_t)z * n + i];
-  if (dstf) dstf[i] = (float)a;
-  else dstd[i] = a;
-}
-
-size_t fold_part_doubles(int R, int C, int V) {
-  return (size_t)36 * R * std::max(std::max(R, C), V);
-}
-
-// slabs of the o-split: enough blocks to fill the chip, at least 8 o per slab
-static int koq_splits(int M, int N, int O) {
-  const int tiles = ((M + 31) / 32) * ((N + 31) / 32);
-  return std::max(1, std::min(std::min((256 + tiles - 1) / tiles, (O + 7) / 8), 9));
-}
-
-// part must hold koq_splits(M, N, O) * M * N doubles (the callers' fold part buffer
-// holds 9 R max(C, V) >= that); the result goes to dstf (float) or dstd
-static hipError_t koq(KoqGemm g, double *part, float *dstf, double *dstd, hipStream_t s) {
-  const int S = koq_splits(g.M, g.N, g.O);
-  g.per = (g.O + S - 1) / S;
-  g.part = part;
-  hipLaunchKernelGGL(k_fold_koq, dim3((g.N + 31) / 32, (g.M + 31) / 32, S), dim3(256), 0, s, g);
-  const int64_t n = (int64_t)g.M * g.N;
-  hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, S, n,
-                     dstf, dstd);
-  return hipGetLastError();
-}
-
-// Wc[o][i][q] = sum_c Wt[o][c][q] W'[c][i]   (W' = SpatialConv.W, C_out x C_in)
-hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, double *part,
+hipError_t launch_fold_w(const float *Wt, const float *W, int R, int C, float *Wc, float *scratch,
                          hipStream_t s) {
-  TapGemm g{};
-  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.aq = 1;
-  g.B = W; g.bk = C; g.bn = 1;
-  g.out = Wc; g.om = (int64_t)C * 9; g.on = 9; g.oq = 1;
-  g.M = R; g.N = C; g.K = R;
-  return tapgemm(g, part, s);
+  return fold_fwd_gemms(Wt, W, nullptr, R, C, 0, Wc, nullptr, scratch, s);
 }
 
 // Boundary frames of the folded block: output frames t < nb0 and t >= tb1 read
@@ -274,34 +328,51 @@ __device__ __forceinline__ int fold_slot_frame(int slot, int nb0, int tb1) {
 
 // BT[o][t][v] = bt[o] + sum_{q: 0 <= s t + q - 4 < T} Bq[q][o][v],
 // Bq[q][o][v] = sum_c Wt[o][c][q] bZ[c][v] (small GEMM into `bq`, R * V * 9 doubles)
-__global__ void k_fold_bias(const double *bq, const float *bt, int R, int V, int T, int To, int st,
-                            float *BT) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)R * To * V) return;
-  const int v = (int)(idx % V);
-  const int64_t ot = idx / V;
-  const int t = (int)(ot % To), o = (int)(ot / To);
-  const int t0 = st * t - 4;
-  double a = bt[o];
+__global__ __launch_bounds__(256) void k_fold_bias(const double *bq, const float *bt, int R, int V,
+                                                   int T, int To, int st, float *BT) {
+  __shared__ double bs[9 * 256], full[256];  // (V <= 256, checked by the launcher)
+  const int o = blockIdx.x, tid = threadIdx.x;
+  for (int e = tid; e < 9 * V; e += 256) {
+    const int q = e / V, v = e - q * V;
+    bs[e] = bq[((int64_t)q * R + o) * V + v];
+  }
+  __syncthreads();
+  const double b0 = bt[o];
+  if (tid < V) {
+    double a = b0;
 #pragma unroll
-  for (int q = 0; q < 9; ++q)
-    if (t0 + q >= 0 && t0 + q < T) a += bq[((int64_t)q * R + o) * V + v];
-  BT[idx] = (float)a;
+    for (int q = 0; q < 9; ++q) a += bs[q * V + tid];
+    full[tid] = a;
+  }
+  __syncthreads();
+  float *dst = BT + (int64_t)o * To * V;
+  for (int tv = tid; tv < To * V; tv += 256) {
+    const int t = tv / V, v = tv - t * V, t0 = st * t - 4;
+    double a;
+    if (t0 >= 0 && t0 + 8 < T) {
+      a = full[v];  // (interior frame: all nine taps)
+    } else {
+      a = b0;
+      for (int q = 0; q < 9; ++q)
+        if (t0 + q >= 0 && t0 + q < T) a += bs[q * V + v];
+    }
+    dst[tv] = (float)a;
+  }
 }
 
-hipError_t launch_fold_bias(const float *Wt, const float *bt, const float *bZ, int R, int V, int T,
-                            int To, int st, double *bq, float *BT, double *part, hipStream_t s) {
-  // bq[q][o][v] = sum_c Wt[o][c][q] bZ[c][v]
-  TapGemm g{};
-  g.A = Wt; g.am = (int64_t)R * 9; g.ak = 9; g.aq = 1;
-  g.B = bZ; g.bk = V; g.bn = 1;
-  g.out = bq; g.o_dbl = 1; g.om = V; g.on = 1; g.oq = (int64_t)R * V;
-  g.M = R; g.N = V; g.K = R;
-  HIP_RET(tapgemm(g, part, s));
-  const int64_t n = (int64_t)R * To * V;
-  hipLaunchKernelGGL(k_fold_bias, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bq, bt, R, V,
-                     T, To, st, BT);
+static hipError_t fold_bias_frames(const double *bq, const float *bt, int R, int V, int T, int To,
+                                   int st, float *BT, hipStream_t s) {
+  if (V > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fold_bias, dim3(R), dim3(256), 0, s, bq, bt, R, V, T, To, st, BT);
   return hipGetLastError();
+}
+
+// the forward's fold in three launches: the re-layouts, {Wc, bq}, the table BT
+hipError_t launch_fold_fwd(const float *Wt, const float *W, const float *bt, const float *bZ, int R,
+                           int C, int V, int T, int To, int st, float *Wc, double *bq, float *BT,
+                           float *scratch, hipStream_t s) {
+  HIP_RET(fold_fwd_gemms(Wt, W, bZ, R, C, V, Wc, bq, scratch, s));
+  return fold_bias_frames(bq, bt, R, V, T, To, st, BT, s);
 }
 
 // Tq[q][o][v] = sum_t cs[o][t][v] over the frames t whose tap q reads inside
@@ -411,53 +482,164 @@ hipError_t launch_absmax(const float *x, int64_t n, unsigned *amax, hipStream_t 
   return hipGetLastError();
 }
 
-__global__ void k_slab_reduce_f64(const float *slab, int S, int64_t n, double *dst) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  double a = 0.0;
-  for (int k = 0; k < S; ++k) a += slab[(int64_t)k * n + i];
-  dst[i] = a;
+// The backward's re-layouts (scratch: [WtT | W'c]): WtT[q][c][o] (A of dW': rows
+// c, k = o), W' [c][i] (B of dWt: rows c, k = i)
+size_t fold_bwd_scratch_floats(int R, int C) {
+  const int Rp = pad32(R);
+  return (size_t)Rp * (9 * Rp + pad32(C));
+}
+size_t fold_dwc_floats(int R, int C) { return (size_t)18 * pad32(R) * pad32(C); }
+
+hipError_t launch_fold_prep_bwd(const float *Wt, const float *W, int R, int C, float *scratch,
+                                hipStream_t s) {
+  const int Rp = pad32(R);
+  float *wtT = scratch, *wd = wtT + (size_t)9 * Rp * Rp;
+  return fold_tr({tr_job(Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, wtT),
+                  tr_job(W, 0, 1, 0, 1, 0, C, 1, R, C, wd, nullptr)},
+                 s);
 }
 
-// The folded block's weight gradients from dWc (slab of the temporal weight
-// gradient over C_in channels) and Tq:
+// The folded block's weight gradients from the slabs of dWc (the temporal weight
+// gradient over C_in channels, [S][o][i][q]) and Tq: the slab sum re-laid as
+// dWcQ[q][o][i] and dWcT[q][i][o], then one GEMM launch:
 //   dWt[o][c][q] = sum_i dWc[o][i][q] W'[c][i] + sum_v Tq[q][o][v] bZ[c][v]
 //   dW'[c][i]    = sum_{(o,q)} Wt[o][c][q] dWc[o][i][q]
-// part: fold_part_doubles(R, C, V) doubles (split-K slabs)
-hipError_t launch_fold_grads(const float *slab, int S, const float *Wt, const float *W,
-                             const float *bZ, const double *Tq, int R, int C, int V,
-                             double *dWc, double *part, float *dWt, float *dW, hipStream_t s) {
-  const int64_t n = (int64_t)R * C * 9;
-  hipLaunchKernelGGL(k_slab_reduce_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slab,
-                     S, n, dWc);
-  {
-    TapGemm g{};
-    g.A = dWc; g.a_dbl = 1; g.am = (int64_t)C * 9; g.ak = 9; g.aq = 1;
-    g.B = W; g.bk = 1; g.bn = C;
-    g.A2 = Tq; g.a2q = (int64_t)R * V; g.a2m = V;
-    g.B2 = bZ; g.b2k = 1; g.b2n = V;
-    g.K2 = V;
-    g.out = dWt; g.om = (int64_t)R * 9; g.on = 9; g.oq = 1;
-    g.M = R; g.N = R; g.K = C;
-    HIP_RET(tapgemm(g, part, s));
-  }
-  KoqGemm g{};
-  g.A = Wt; g.a_o = (int64_t)R * 9; g.a_m = 9; g.a_q = 1;
-  g.B = dWc; g.b_dbl = 1; g.b_o = (int64_t)C * 9; g.b_n = 9; g.b_q = 1;
-  g.M = R; g.N = C; g.O = R;
-  return koq(g, part, dW, nullptr, s);
+hipError_t launch_fold_grads(const float *slab, int S, const float *scratch, const float *bZ,
+                             const double *Tq, int R, int C, int V, float *dwc, float *dWt,
+                             float *dW, hipStream_t s) {
+  const int Rp = pad32(R), Cp = pad32(C);
+  const float *wtT = scratch, *wd = wtT + (size_t)9 * Rp * Rp;
+  float *dWcQ = dwc, *dWcT = dwc + (size_t)9 * Rp * Cp;
+  HIP_RET(fold_tr({tr_job(slab, 0, S, (int64_t)R * C * 9, 9, 1, (int64_t)C * 9, 9, R, C, dWcQ,
+                          dWcT)},
+                  s));
+  FoldJob a{};
+  a.A = dWcQ; a.aq = (int64_t)Rp * Cp; a.am = Cp;
+  a.B = wd; a.bn = Cp;
+  a.A2 = Tq; a.a2q = (int64_t)R * V; a.a2m = V;
+  a.B2 = bZ; a.b2n = V;
+  a.K2 = V;
+  a.out = dWt; a.oq = 1; a.om = (int64_t)R * 9; a.on = 9;
+  a.M = R; a.N = R; a.K = C;
+  FoldJob b{};
+  b.A = wtT; b.aq = (int64_t)Rp * Rp; b.am = Rp;
+  b.B = dWcT; b.bq = (int64_t)Cp * Rp; b.bn = Rp;
+  b.out = dW; b.om = C; b.on = 1; b.red = 1;
+  b.M = R; b.N = C; b.K = R;
+  return fold_gemm({a, b}, s);
 }
 
-// SdZ[c][v] = sum_q sum_o Wt[o][c][q] Tq[q][o][v]  (= sum_{n,t} dZ[c,t,v]; Wt is
-// the temporal weight [R][C][9] with C = its input channels, the Z channels);
-// part: fold_part_doubles(R, C, V) doubles
-hipError_t launch_fold_sdz(const float *Wt, const double *Tq, int R, int C, int V, double *part,
-                           double *SdZ, hipStream_t s) {
-  KoqGemm g{};
-  g.A = Wt; g.a_o = (int64_t)C * 9; g.a_m = 9; g.a_q = 1;
-  g.B = Tq; g.b_dbl = 1; g.b_o = V; g.b_n = 1; g.b_q = (int64_t)R * V;
-  g.M = C; g.N = V; g.O = R;
-  return koq(g, part, nullptr, SdZ, s);
+// The dU-sum reductions on the fp64 matrix cores (v_mfma_f64_16x16x4_f64, 16 x 16
+// tiles, nine waves = taps summed in LDS in tap order), from fp64 re-layouts:
+//   SdZ[c][v] = sum_q sum_o Wt[o][c][q] Tq[q][o][v]   (= sum_{n,t} dZ[c,t,v])
+//   SdH[c][v] = sum_q sum_o Wc[o][c][q] Tq[q][o][v]   (= sum_{n,t} H[c,t,v])
+// Both feed sums that nearly cancel (BN2 makes sum_{t,v} dU = 0 per channel, so
+// the bias gradients dbW, db1 are small against their terms): fp64 throughout.
+struct Red64Job {
+  const double *A, *B;  // A[q aq + m am + k], B[q bq + n bn + k] (k < K, padded to 16)
+  int64_t aq, am, bq, bn;
+  double *out;          // out[m om + n]
+  int64_t om;
+  int M, N, K;
+};
+
+struct Red64Jobs {
+  Red64Job j[2];
+  int n;
+  int tile0[3];
+};
+
+__global__ __launch_bounds__(576) void k_fold_red64(Red64Jobs js) {
+  __shared__ double red[9][16 * 17];
+  const int tile = blockIdx.x;
+  const int ji = (js.n > 1 && tile >= js.tile0[1]) ? 1 : 0;
+  const Red64Job &g = js.j[ji];
+  const int t = tile - js.tile0[ji], ntn = (g.N + 15) >> 4;
+  const int m0 = (t / ntn) * 16, n0 = (t % ntn) * 16;
+  const int q = threadIdx.x >> 6, l = threadIdx.x & 63, r16 = l & 15, kq = (l >> 4) * 4;
+  double4v acc = {0.0, 0.0, 0.0, 0.0};
+  const double *pa = g.A + q * g.aq + (int64_t)(m0 + r16) * g.am + kq;
+  const double *pb = g.B + q * g.bq + (int64_t)(n0 + r16) * g.bn + kq;
+  for (int k0 = 0; k0 < g.K; k0 += 16) {  // lane: k = k0 + 4 (l >> 4) + j for MFMA j
+    const double4v a = *reinterpret_cast<const double4v *>(pa + k0);
+    const double4v b = *reinterpret_cast<const double4v *>(pb + k0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j], b[j], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[q][((l >> 4) + 4 * r) * 17 + r16] = acc[r];
+  __syncthreads();
+  if (threadIdx.x >= 256) return;
+  const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int mm = m0 + rr, nn = n0 + cc;
+  if (mm >= g.M || nn >= g.N) return;
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < 9; ++w) s += red[w][rr * 17 + cc];
+  g.out[mm * g.om + nn] = s;
+}
+
+// doubles of launch_fold_sdz's scratch: WtT, WcT, TqT as fp64 [q][row][o]
+size_t fold_sdz_scratch_doubles(int R, int C, int V) {
+  return (size_t)9 * pad32(R) * (pad32(R) + pad32(C) + pad32(V));
+}
+
+// SdZ (and, with Wc, SdH); Wt [R][R][9], Wc [R][C][9] (o, c, q), Tq [9][R][V]
+hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
+                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s) {
+  const int Rp = pad32(R), Cp = pad32(C), Vp = pad32(V);
+  double *wtT = scratch, *wcT = wtT + (size_t)9 * Rp * Rp, *tqT = wcT + (size_t)9 * Cp * Rp;
+  const TrJob jt = tr_job(Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, nullptr, nullptr, wtT);
+  const TrJob jq = tr_job(Tq, 1, 1, 0, 9, (int64_t)R * V, V, 1, R, V, nullptr, nullptr, nullptr, tqT);
+  if (Wc)
+    HIP_RET(fold_tr({jt, jq, tr_job(Wc, 0, 1, 0, 9, 1, (int64_t)C * 9, 9, R, C, nullptr, nullptr,
+                                    nullptr, wcT)},
+                    s));
+  else
+    HIP_RET(fold_tr({jt, jq}, s));
+  Red64Jobs js{};
+  Red64Job z{};
+  z.A = wtT; z.aq = (int64_t)Rp * Rp; z.am = Rp;
+  z.B = tqT; z.bq = (int64_t)Vp * Rp; z.bn = Rp;
+  z.out = SdZ; z.om = V;
+  z.M = R; z.N = V; z.K = R;
+  js.j[0] = z;
+  js.n = 1;
+  const int tz = ((R + 15) / 16) * ((V + 15) / 16);
+  js.tile0[1] = tz;
+  int tiles = tz;
+  if (Wc && SdH) {
+    Red64Job h = z;
+    h.A = wcT; h.aq = (int64_t)Cp * Rp;
+    h.out = SdH;
+    h.M = C;
+    js.j[1] = h;
+    js.n = 2;
+    tiles += ((C + 15) / 16) * ((V + 15) / 16);
+  }
+  js.tile0[js.n] = tiles;
+  hipLaunchKernelGGL(k_fold_red64, dim3(tiles), dim3(576), 0, s, js);
+  return hipGetLastError();
+}
+
+// sum_{n,t,v} of the BN1-output gradient of the folded block (db1 = BN1's sd):
+// sd[c] = sum_v SdH[c][v] sum_w A[v][w]   (dxhat[c,t,w] = sum_v A[v][w] H[c,t,v])
+__global__ void k_fold_sd(const double *SdH, const float *A, int C, int V, double *sd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0;
+  for (int v = 0; v < V; ++v) {
+    double rs = 0.0;
+    for (int w = 0; w < V; ++w) rs += (double)A[v * V + w];
+    a += SdH[(int64_t)c * V + v] * rs;
+  }
+  sd[c] = a;
+}
+
+hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, double *sd,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_fold_sd, dim3((C + 63) / 64), dim3(64), 0, s, SdH, A, C, V, sd);
+  return hipGetLastError();
 }
 
 }  // namespace stgcn

@@ -358,7 +358,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
 #pragma unroll
         for (int i = 0; i < 4; ++i) sv[i] += __shfl_xor(sv[i], o, 64);
       if (fg == 0 && rok) {
-        atomicAdd(p.sd + c, sv[0]);
+        if (!p.sd_given) atomicAdd(p.sd + c, sv[0]);
         atomicAdd(p.sdn + c, sv[1]);
         if (pv) {
           atomicAdd(p.prev.s1 + c, sv[2]);

@@ -84,7 +84,8 @@ def test_f16x2_full_size_block(pkg):
 def test_f16x2_unfolded_blocks_keep_bf16x3(pkg):
     """Where the block does not fold (first block C_in = 3, residual, K = 3) the
     flag changes nothing: the plan has no F16X2 bit and the results are
-    bit-identical to the bf16x3 path."""
+    bit-identical to the bf16x3 path (the adjacency gradient up to the order of
+    its fp32 atomic partial sums, which differs from run to run)."""
     hl = pkg.hip_lib
     for case, residual in (((3, 64, 1, 18, 1, 2, 30), False), ((64, 64, 1, 18, 1, 2, 30), True)):
         arrays, x, g = _random_case(pkg, *case, residual=residual)
@@ -94,4 +95,7 @@ def test_f16x2_unfolded_blocks_keep_bf16x3(pkg):
         a = _run_hip(pkg, arrays, x, g, gemm="f16x2")
         b = _run_hip(pkg, arrays, x, g, gemm="f32x3")
         for k in a:
-            assert torch.equal(a[k], b[k]), k
+            if k == "grad.spatialConv.A":
+                torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6 * b[k].abs().max())
+            else:
+                assert torch.equal(a[k], b[k]), k
