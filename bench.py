@@ -322,10 +322,9 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
                 npl = 2 if f16 and fold else 3  # operand planes: fp16 (h, l) or bf16 (h, m, l)
                 spb = "true" if fold else "false"  # the fused SpatialConv backward epilogue
-                # (the data gradient stays on the 3-way splits: capi.hip f16x2_dgrad)
                 sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false,false>",
-                       1: (f"k_conv_x3<9,3,{V},1,{mr},3,false,{spb}>" if s == 1 else
-                           f"k_conv_x3<5|4,{V},1,1,3,false,{spb}>"),
+                       1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false,{spb}>" if s == 1 else
+                           f"k_conv_x3<5|4,{V},1,1,{npl},false,{spb}>"),
                        2: f"k_wgrad_x3<{V},{s},{npl}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
@@ -407,11 +406,13 @@ def main():
                     help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3", "f16x2"], default="bf16x3",
-                    help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma) or "
-                         "as exact 3-way bf16 operand splits (bf16x3; fp32 accuracy)")
+    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3", "f16x2"], default="f16x2",
+                    help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma), "
+                         "as exact 3-way bf16 operand splits (bf16x3) or, on the folded "
+                         "blocks, as 2-way fp16 splits of power-of-two-scaled operands "
+                         "(f16x2); all held to the fp32 parity gate")
     ap.add_argument("--no-alt", action="store_true",
-                    help="skip timing the exact fp32-MFMA path beside the bf16x3 default")
+                    help="skip timing the other fp32 GEMM modes beside the default")
     ap.add_argument("--no-repeats", dest="repeats", action="store_false",
                     help="skip the two extra timed windows (median of three)")
     ap.add_argument("--no-sweep", dest="sweep", action="store_false",
@@ -509,22 +510,27 @@ def main():
     gf_clip = pkg.flops_per_clip(cfg["C"], cfg["T"], cfg["V"], cfg["K"], cfg["classes"]) / 1e9
     progress(f"{args.config}: {clips:.1f} clips/s ({[round(r, 1) for r in runs]})")
 
-    # the exact fp32-MFMA path (every GEMM on v_mfma_f32_32x32x2_f32) timed
-    # beside the default bf16x3 path, same model and inputs (N=1 only)
+    # the other fp32 GEMM modes (exact fp32 MFMA: every GEMM on
+    # v_mfma_f32_32x32x2_f32; bf16x3) timed beside the default, same model and
+    # inputs (N=1 only)
     alt = None
-    if world == 1 and not cfg["bf16"] and cfg["f32_gemm"] != "mfma" and not args.no_alt:
-        for blk in model.conv:
-            blk.f32_gemm = "mfma"
-        for _ in range(2):
-            step()
-        torch.cuda.synchronize()
-        ta = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        dta = time.perf_counter() - ta
-        alt = {"f32_gemm": "mfma", "value": round(cfg["N"] * args.steps / dta, 2),
-               "ms_per_step": round(dta / args.steps * 1e3, 3)}
+    if world == 1 and not cfg["bf16"] and not args.no_alt:
+        alt = []
+        for mode in ("mfma", "bf16x3", "f16x2"):
+            if mode == cfg["f32_gemm"]:
+                continue
+            for blk in model.conv:
+                blk.f32_gemm = mode
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            dta = time.perf_counter() - ta
+            alt.append({"f32_gemm": mode, "value": round(cfg["N"] * args.steps / dta, 2),
+                        "ms_per_step": round(dta / args.steps * 1e3, 3)})
         for blk in model.conv:
             blk.f32_gemm = cfg["f32_gemm"]
 
@@ -568,7 +574,8 @@ def main():
                                         "3-way bf16 splits (6 MFMAs, fp32-gated parity); "
                                         "spatial GEMMs fp32 MFMA"
                                         if cfg["f32_gemm"] == "bf16x3" else
-                                        "fp32: folded temporal GEMMs as 2-way fp16 splits of "
+                                        "fp32: folded temporal GEMMs (fwd, data-grad, "
+                                        "weight-grad) as 2-way fp16 splits of "
                                         "power-of-two-scaled operands (3 MFMAs, fp32-gated "
                                         "parity), other temporal GEMMs 3-way bf16 splits"
                                         if cfg["f32_gemm"] == "f16x2" else "fp32 MFMA")},
@@ -578,7 +585,7 @@ def main():
             "loss": round(float(loss.item()), 5),
         }
         if alt is not None:
-            out["fp32_mfma_path"] = alt
+            out["alt_fp32_modes"] = alt
         if sweep is not None:
             out["batch_sweep_clips_s"] = sweep
         if not args.no_roofline:

@@ -78,7 +78,7 @@ extern "C" {
                             * OPAQUE (it carries Wc from stgcn_block_fwd to
                             * stgcn_block_bwd). Exclusive with STGCN_F_BF16. */
 #define STGCN_F_F16X2 8    /* ABI 6, with STGCN_F_F32X3 only: the folded block's temporal
-                            * conv forward and weight-grad GEMMs as 2-way fp16 splits
+                            * conv forward, data-grad and weight-grad GEMMs as 2-way fp16 splits
                             * (x s = h + l, 22 significant bits, three partial products,
                             * fp32 accumulate) of operands scaled by powers of two s from
                             * their max |x| (so h <= 2^14 and no element underflows

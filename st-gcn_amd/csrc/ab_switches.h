@@ -67,6 +67,6 @@
 #ifndef STGCN_AB_SPB_PAIR        // the folded block's H stored + k_spatial_bwd5 (no fused epilogue)
 #define STGCN_AB_SPB_PAIR 0
 #endif
-#ifndef STGCN_AB_F16X2_DGRAD     // STGCN_F_F16X2 on the folded data gradient too
-#define STGCN_AB_F16X2_DGRAD 0
+#ifndef STGCN_AB_F16X2_DGRAD     // 0: the folded data gradient on 3-way bf16 splits under STGCN_F_F16X2
+#define STGCN_AB_F16X2_DGRAD 1
 #endif

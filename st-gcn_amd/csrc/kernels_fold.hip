@@ -74,6 +74,51 @@ struct FoldJobs {
   int tile0[4];  // first tile of job i; tile0[n] = the grid
 };
 
+// One wave's K stream, fully unrolled for NG 16-k groups (straight-line code:
+// the compiler's load counters stay exact, so D groups are in flight; a
+// runtime-trip loop with conditional prefetches made it wait for every load
+// at the loop head). Lane: k = 16 i + 8 (l >> 5) + j for MFMA j of group i.
+template <int NG>
+__device__ __forceinline__ void f32_stream(const float *pa, const float *pb, float16v &acc) {
+  constexpr int D = NG < 4 ? NG : 4;
+  float8v a[D], b[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    a[d] = *reinterpret_cast<const float8v *>(pa + 16 * d);
+    b[d] = *reinterpret_cast<const float8v *>(pb + 16 * d);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // (keeps the prefetches ahead: the scheduler
+                                      // would sink them next to their MFMAs)
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int d = i % D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[d][j], b[d][j], acc, 0, 0, 0);
+    if (i + D < NG) {
+      a[d] = *reinterpret_cast<const float8v *>(pa + 16 * (i + D));
+      b[d] = *reinterpret_cast<const float8v *>(pb + 16 * (i + D));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void f32_stream_any(const float *pa, const float *pb, int ng,
+                                               float16v &acc) {
+  switch (ng) {
+    case 4: f32_stream<4>(pa, pb, acc); return;
+    case 8: f32_stream<8>(pa, pb, acc); return;
+    case 16: f32_stream<16>(pa, pb, acc); return;
+    default: break;
+  }
+  for (int i = 0; i < ng; i += 4) {  // (other K: chunks of up to four groups)
+    if (ng - i >= 4) {
+      f32_stream<4>(pa + 16 * i, pb + 16 * i, acc);
+    } else {
+      for (int k = i; k < ng; ++k) f32_stream<1>(pa + 16 * k, pb + 16 * k, acc);
+    }
+  }
+}
+
 __global__ __launch_bounds__(576) void k_fold_gemm(FoldJobs js) {
   __shared__ float red[9][32 * 33];
   const int tile = blockIdx.x;
@@ -85,23 +130,9 @@ __global__ __launch_bounds__(576) void k_fold_gemm(FoldJobs js) {
   const int q = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
   float16v acc = {};
   {
-    // lane: k = 16 i + 8 h + j for MFMA j of group i (the pair k, k + 8 per MFMA)
     const float *pa = g.A + q * g.aq + (int64_t)(m0 + r32) * g.am + 8 * h;
     const float *pb = g.B + q * g.bq + (int64_t)(n0 + r32) * g.bn + 8 * h;
-    const int ng = (g.K + 15) >> 4;
-    float8v a = *reinterpret_cast<const float8v *>(pa);
-    float8v b = *reinterpret_cast<const float8v *>(pb);
-    for (int i = 0; i < ng; ++i) {
-      float8v an = a, bn = b;
-      if (i + 1 < ng) {
-        an = *reinterpret_cast<const float8v *>(pa + 16 * (i + 1));
-        bn = *reinterpret_cast<const float8v *>(pb + 16 * (i + 1));
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
-      a = an;
-      b = bn;
-    }
+    f32_stream_any(pa, pb, (g.K + 15) >> 4, acc);
   }
   if (g.A2) {  // (short: K2 = V; bounds-checked direct reads)
     const int m = m0 + r32, n = n0 + r32;
@@ -549,6 +580,29 @@ struct Red64Jobs {
   int tile0[3];
 };
 
+template <int NG>
+__device__ __forceinline__ void f64_stream(const double *pa, const double *pb, double4v &acc) {
+  constexpr int D = NG < 4 ? NG : 4;
+  double4v a[D], b[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    a[d] = *reinterpret_cast<const double4v *>(pa + 16 * d);
+    b[d] = *reinterpret_cast<const double4v *>(pb + 16 * d);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int d = i % D;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[d][j], b[d][j], acc, 0, 0, 0);
+    if (i + D < NG) {
+      a[d] = *reinterpret_cast<const double4v *>(pa + 16 * (i + D));
+      b[d] = *reinterpret_cast<const double4v *>(pb + 16 * (i + D));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 __global__ __launch_bounds__(576) void k_fold_red64(Red64Jobs js) {
   __shared__ double red[9][16 * 17];
   const int tile = blockIdx.x;
@@ -560,11 +614,22 @@ __global__ __launch_bounds__(576) void k_fold_red64(Red64Jobs js) {
   double4v acc = {0.0, 0.0, 0.0, 0.0};
   const double *pa = g.A + q * g.aq + (int64_t)(m0 + r16) * g.am + kq;
   const double *pb = g.B + q * g.bq + (int64_t)(n0 + r16) * g.bn + kq;
-  for (int k0 = 0; k0 < g.K; k0 += 16) {  // lane: k = k0 + 4 (l >> 4) + j for MFMA j
-    const double4v a = *reinterpret_cast<const double4v *>(pa + k0);
-    const double4v b = *reinterpret_cast<const double4v *>(pb + k0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[j], b[j], acc, 0, 0, 0);
+  // lane: k = 16 i + 4 (l >> 4) + j for MFMA j of group i (straight-line streams)
+  const int ng = (g.K + 15) >> 4;
+  if (ng == 4) {
+    f64_stream<4>(pa, pb, acc);
+  } else if (ng == 8) {
+    f64_stream<8>(pa, pb, acc);
+  } else if (ng == 16) {
+    f64_stream<16>(pa, pb, acc);
+  } else {
+    for (int i = 0; i < ng; i += 4) {
+      if (ng - i >= 4) {
+        f64_stream<4>(pa + 16 * i, pb + 16 * i, acc);
+      } else {
+        for (int k = i; k < ng; ++k) f64_stream<1>(pa + 16 * k, pb + 16 * k, acc);
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[q][((l >> 4) + 4 * r) * 17 + r16] = acc[r];
@@ -624,21 +689,26 @@ hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, co
 
 // sum_{n,t,v} of the BN1-output gradient of the folded block (db1 = BN1's sd):
 // sd[c] = sum_v SdH[c][v] sum_w A[v][w]   (dxhat[c,t,w] = sum_v A[v][w] H[c,t,v])
-__global__ void k_fold_sd(const double *SdH, const float *A, int C, int V, double *sd) {
+__global__ __launch_bounds__(256) void k_fold_sd(const double *SdH, const float *A, int C, int V,
+                                                 double *sd) {
+  __shared__ double rs[256];  // (V <= 256)
+  for (int v = threadIdx.x; v < V; v += blockDim.x) {
+    double a = 0.0;
+    for (int w = 0; w < V; ++w) a += (double)A[v * V + w];
+    rs[v] = a;
+  }
+  __syncthreads();
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double a = 0.0;
-  for (int v = 0; v < V; ++v) {
-    double rs = 0.0;
-    for (int w = 0; w < V; ++w) rs += (double)A[v * V + w];
-    a += SdH[(int64_t)c * V + v] * rs;
-  }
+  for (int v = 0; v < V; ++v) a += SdH[(int64_t)c * V + v] * rs[v];
   sd[c] = a;
 }
 
 hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, double *sd,
                           hipStream_t s) {
-  hipLaunchKernelGGL(k_fold_sd, dim3((C + 63) / 64), dim3(64), 0, s, SdH, A, C, V, sd);
+  if (V > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fold_sd, dim3((C + 255) / 256), dim3(256), 0, s, SdH, A, C, V, sd);
   return hipGetLastError();
 }
 

@@ -1,9 +1,10 @@
 """GPU parity of the fp32 block with STGCN_F_F16X2 (``gemm="f16x2"``): the
-folded block's temporal conv forward and weight-grad GEMMs
-(st-gcn_amd/csrc/kernels_x3.hip NPL = 2; the data gradient keeps the 3-way
-bf16 splits, capi.hip f16x2_dgrad) as 2-way fp16 splits of
-operands scaled by powers of two from their max |x| (x s = h + l, 22
-significant bits; three partial products hh, hl, lh; fp32 accumulate).
+folded block's temporal conv forward, data-grad and weight-grad GEMMs
+(st-gcn_amd/csrc/kernels_x3.hip NPL = 2) as 2-way fp16 splits of operands
+scaled by powers of two from their max |x| (x s = h + l, 22 significant bits;
+three partial products hh, hl, lh; fp32 accumulate). BN1's sum of dxhat, which
+nearly cancels, comes from the fp64 dU sums (kernels_fold.hip k_fold_sd), not
+from the 22-bit data gradient.
 
 The mode claims fp32-GEMM accuracy, so it is held to the SAME gate as the fp32
 MFMA path and the bf16x3 path (test_gpu_block.py): rel-to-max

@@ -398,7 +398,14 @@ def test_stack_observed_intermediate_gradient(pkg, monkeypatch, observe):
         assert len(seen) == 2
         assert rel_to_max(seen[0].cpu().numpy(), seen[1].cpu().numpy()) < 1e-4
     for (k, a), b in zip(m1.named_parameters(), m2.parameters()):
-        assert rel_to_max(a.grad.cpu().numpy(), b.grad.cpu().numpy()) < 2e-2, k
+        if a.grad is None:  # (parameters the loss does not reach)
+            assert b.grad is None, k
+            continue
+        ga, gb = a.grad.cpu().numpy(), b.grad.cpu().numpy()
+        if k.endswith("temporalConv.bias"):  # (analytically zero: rounding noise on both sides)
+            assert np.abs(ga - gb).max() < 1e-6, k
+            continue
+        assert rel_to_max(ga, gb) < 2e-2, k
 
 
 def test_stack_bf16_cfg3_shape(pkg):
