@@ -125,12 +125,12 @@ bool fold_spb(const stgcn_desc_t *d) { return fold_w(d) && STGCN_AB_SPB_PAIR == 
 // The folded block's temporal GEMMs on 2-way fp16 splits (STGCN_F_F16X2; k_conv_x3 /
 // k_wgrad_x3 with NPL = 2), operand scales from max |x| words (launch_absmax)
 bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
-// ... except the data gradient, which stays on the 3-way bf16 splits: its output
-// H feeds the BN1 backward sums (sum dxhat over N T V elements of a zero-mean
-// dU: heavy cancellation), where the 2^-22 operand representation measured
-// 2.5x the fp32 reference's own error on the BN1 bias gradient at N = 32,
-// T = 300 (the 2^-24 of the 3-way splits stays within it). STGCN_AB_F16X2_DGRAD
-// build: the fp16 splits there too (A/B only).
+// ... the data gradient included: its output feeds BN1's sum of dxhat over N T V
+// elements of a zero-mean dU (heavy cancellation; the 2^-22 operand
+// representation measured 2.5x the fp32 reference's own error on the BN1 bias
+// gradient at N = 32, T = 300), which the folded block takes from the fp64 dU
+// sums instead (kernels_fold.hip k_fold_sd). STGCN_AB_F16X2_DGRAD=0 build: the
+// 3-way bf16 splits there (A/B only).
 bool f16x2_dgrad(const stgcn_desc_t *d) { return f16x2(d) && STGCN_AB_F16X2_DGRAD != 0; }
 
 // sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
@@ -247,7 +247,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
   if (bf16(d)) plan_wgrad_bf16(w);
   // k_wgrad_x3 where it covers the shape (its S x R x C x 9 slab fits the fp32
   // plan's: twice the tiles, half the splits)
-  if (f32x3(d)) plan_wgrad_x3(w);
+  if (f32x3(d)) plan_wgrad_x3(w, f16x2(d));
   return w;
 }
 

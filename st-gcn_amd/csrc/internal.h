@@ -119,6 +119,7 @@ struct WgradParams {
   // power-of-two-scaled P / Q; amax_p / amax_q: device max |P| / max |Q| bits
   int f16x2;
   const unsigned *amax_p, *amax_q;
+  int x3_mr;  // k_wgrad_x3 row tiles of 64 x_mr rows (2: with f16x2 only; set by plan_wgrad_x3)
 };
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p, hipStream_t s);
@@ -181,7 +182,7 @@ hipError_t launch_conv_b1(const ConvGemmParams &p, hipStream_t s);
 // Re-plans the temporal weight gradient (NQ = 9, stride 1, V = 18) for
 // k_wgrad_x3 (sets FT, tiles, S, bf16 = 3); false (w unchanged) otherwise.
 // launch_wgrad_taps dispatches to launch_wgrad_x3 when w.bf16 == 3.
-bool plan_wgrad_x3(WgradParams &w);
+bool plan_wgrad_x3(WgradParams &w, bool f16x2);
 hipError_t launch_wgrad_x3(const WgradParams &p, hipStream_t s);
 // Re-plans a weight gradient (NQ = 9 temporal taps or NQ = 1) for k_wgrad_bf16
 // (sets FT, n_mtiles, n_rtiles, n_jtiles, S, bf16 = 1) when the shape is

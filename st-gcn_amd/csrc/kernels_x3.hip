@@ -1006,8 +1006,9 @@ namespace stgcn {
 // into registers (4-joint groups, fp32 dwords) under this item's MFMAs, split
 // and written after them; one barrier per item.
 // ---------------------------------------------------------------------------
-template <int V, int SIN, int NPL = 3>
+template <int V, int SIN, int NPL = 3, int MR = 1>
 struct WgX3Geo {
+  static constexpr int ROWS = 64 * MR;  // output rows per tile (MR = 2: NPL = 2 only)
   static constexpr int Vp = (V + 3) & ~3;
   static constexpr int G4 = Vp / 4;
   static constexpr int FT = 4;
@@ -1019,7 +1020,7 @@ struct WgX3Geo {
   static constexpr int QP0 = QF * Vp;
   static constexpr int QPITCH = QP0 % 8 == 0 ? QP0 + 4 : QP0;
   static constexpr int CB = 32;
-  static constexpr int PPL = 64 * PPITCH * 2;  // bytes per P plane
+  static constexpr int PPL = ROWS * PPITCH * 2;  // bytes per P plane
   static constexpr int QPL = CB * QPITCH * 2;  // bytes per Q plane
   static constexpr int BUF = NPL * (PPL + QPL);
   // double-buffered where it fits (stride 1; NPL = 2: stride 2 too); else one
@@ -1028,7 +1029,7 @@ struct WgX3Geo {
   static constexpr int LDS = NBUF * BUF;
   static constexpr int PG = FT * G4;  // 4-joint groups per P row
   static constexpr int QG = QF * G4;  // ... per Q row
-  static constexpr int NGRP = 64 * PG + CB * QG;
+  static constexpr int NGRP = ROWS * PG + CB * QG;
   static constexpr int GPT = (NGRP + 511) / 512;
   static_assert(KP % 16 == 0 && PPITCH % 16 == 8 && QPITCH % 8 == 4, "conflict-free pitches");
   static_assert(PPL % 16 == 0 && QPL % 16 == 0, "plane alignment");
@@ -1037,10 +1038,15 @@ struct WgX3Geo {
 
 // NPL = 2: fp32 as 2-way fp16 splits of the power-of-two-scaled operands (P and
 // Q by the f16x2_se scales of p.amax_p / p.amax_q, undone on the slab values),
-// three products hh, hl, lh
-template <int V, int SIN, int NPL = 3>
+// three products hh, hl, lh. MR = 2 (NPL = 2, R % 128 == 0): 128-row tiles, each
+// wave two 32-row blocks sharing its Q fragments (half the Q image traffic per
+// flop: the kernel is bound by the L2 -> LDS staging, not the matrix rate), one
+// accumulator per block (the three products summed in one fp32 chain, small
+// ones first)
+template <int V, int SIN, int NPL = 3, int MR = 1>
 __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
-  using G = WgX3Geo<V, SIN, NPL>;
+  using G = WgX3Geo<V, SIN, NPL, MR>;
+  static_assert(MR == 1 || NPL == 2, "128-row tiles on the fp16 splits only");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int p_se = NPL == 2 ? f16x2_se(p.amax_p) : 0, q_se = NPL == 2 ? f16x2_se(p.amax_q) : 0;
   const float p_scale = pow2f(p_se), q_scale = pow2f(q_se);
@@ -1053,7 +1059,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
   bid /= p.n_jtiles;
   const int rt = bid % p.n_rtiles;
   const int split = bid / p.n_rtiles;
-  const int r0 = rt * 64, c0 = jt * G::CB;
+  const int r0 = rt * G::ROWS, c0 = jt * G::CB;
   const int mi = wave & 1, tq = wave >> 1;
   const int q0 = tq ? 1 + 2 * tq : 0;
   const int total = p.N * p.n_mtiles;
@@ -1067,8 +1073,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 #pragma unroll
   for (int k = 0; k < G::GPT; ++k) {
     int e = k * 512 + tid;
-    isq[k] = e >= 64 * G::PG;
-    if (isq[k]) e -= 64 * G::PG;
+    isq[k] = e >= G::ROWS * G::PG;
+    if (isq[k]) e -= G::ROWS * G::PG;
     const int per_row = isq[k] ? G::QG : G::PG;
     const int row = e / per_row, g = e - row * per_row;
     grow[k] = row;
@@ -1112,7 +1118,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       }
     }
   };
-  static_assert(V % 2 == 0 && (64 * G::PG) % 64 == 0, "pair loads, uniform P/Q waves");
+  static_assert(V % 2 == 0 && (G::ROWS * G::PG) % 64 == 0, "pair loads, uniform P/Q waves");
   // splits and writes staging groups [K0, K1) of the loaded item
   auto write_part = [&](char *buf, auto k0_c, auto k1_c) {
     constexpr int K0 = decltype(k0_c)::value, K1 = decltype(k1_c)::value;
@@ -1148,13 +1154,22 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 
   auto run = [&](auto nt_c) {
     constexpr int NT = decltype(nt_c)::value;
-    floatx16 acc[NT], acl[NT];
+    floatx16 acc[MR == 1 ? NT : 1], acl[MR == 1 ? NT : 1], acm[MR][MR == 2 ? NT : 1];
+    if constexpr (MR == 1) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = acl[t][i] = 0.f;
+        for (int i = 0; i < 16; ++i) acc[t][i] = acl[t][i] = 0.f;
+    } else {
+#pragma unroll
+      for (int mb = 0; mb < MR; ++mb)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acm[mb][t][i] = 0.f;
+    }
     struct Frag {
-      bf16x8_t a[NPL], b[NPL][NT];
+      bf16x8_t a[MR][NPL], b[NPL][NT];
     };
     auto ld = [&](const char *buf, int s, Frag &f) {
       const __bf16 *P = reinterpret_cast<const __bf16 *>(buf) + pa + 8 * s;
@@ -1164,7 +1179,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       const __bf16 *Q = reinterpret_cast<const __bf16 *>(buf + NPL * G::PPL) + qb;
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) {
-        f.a[pl] = *reinterpret_cast<const bf16x8_t *>(P + pl * (G::PPL / 2));
+#pragma unroll
+        for (int mb = 0; mb < MR; ++mb)
+          f.a[mb][pl] = *reinterpret_cast<const bf16x8_t *>(P + pl * (G::PPL / 2) + mb * 64 * G::PPITCH);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const __bf16 *Qp = Q + pl * (G::QPL / 2) + t * G::Vp;
@@ -1175,19 +1192,30 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       }
     };
     auto mm = [&](const Frag &f) {
+      if constexpr (MR == 2) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma_p<NPL>(f.a[0], f.b[0][t], acc[t]);
+        for (int mb = 0; mb < MR; ++mb)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_p<NPL>(f.a[0], f.b[1][t], acl[t]);
+          for (int t = 0; t < NT; ++t) {
+            acm[mb][t] = mfma_p<NPL>(f.a[mb][1], f.b[0][t], acm[mb][t]);
+            acm[mb][t] = mfma_p<NPL>(f.a[mb][0], f.b[1][t], acm[mb][t]);
+            acm[mb][t] = mfma_p<NPL>(f.a[mb][0], f.b[0][t], acm[mb][t]);
+          }
+        return;
+      }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acl[t] = mfma_p<NPL>(f.a[1], f.b[0][t], acl[t]);
+      for (int t = 0; t < NT; ++t) acc[t] = mfma_p<NPL>(f.a[0][0], f.b[0][t], acc[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_p<NPL>(f.a[0][0], f.b[1][t], acl[t]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acl[t] = mfma_p<NPL>(f.a[0][1], f.b[0][t], acl[t]);
       if constexpr (NPL == 3) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0], f.b[2 % NPL][t], acl[t]);
+        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0][0], f.b[2 % NPL][t], acl[t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[1], f.b[1][t], acl[t]);
+        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0][1], f.b[1][t], acl[t]);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[2 % NPL], f.b[0][t], acl[t]);
+        for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0][2 % NPL], f.b[0][t], acl[t]);
       }
     };
     for (int it = it0; it < it1; ++it) {
@@ -1232,15 +1260,20 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
     float *slab = p.slab + (int64_t)split * p.R * p.C * 9;
     const int c = c0 + lo;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int mb = 0; mb < MR; ++mb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-        if (r < p.R && c < p.C)
-          slab[((int64_t)r * p.C + c) * 9 + q0 + t] =
-              NPL == 2 ? (acc[t][i] + acl[t][i]) * pow2f(-p_se) * pow2f(-q_se)
-                       : acc[t][i] + acl[t][i];
-      }
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = r0 + mb * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          float v;
+          if constexpr (MR == 2)
+            v = acm[mb][t][i] * pow2f(-p_se) * pow2f(-q_se);
+          else
+            v = NPL == 2 ? (acc[t][i] + acl[t][i]) * pow2f(-p_se) * pow2f(-q_se)
+                         : acc[t][i] + acl[t][i];
+          if (r < p.R && c < p.C) slab[((int64_t)r * p.C + c) * 9 + q0 + t] = v;
+        }
   };
   if (it0 < it1) {
     load_item(it0);
@@ -1253,12 +1286,13 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
     run(std::integral_constant<int, 2>{});
 }
 
-bool plan_wgrad_x3(WgradParams &w) {
+bool plan_wgrad_x3(WgradParams &w, bool f16x2) {
   if (w.V != 18 || (w.s_in != 1 && w.s_in != 2) || w.NQ != 9 || w.off != -4 || w.C < 16)
     return false;
   w.FT = WgX3Geo<18, 1>::FT;
   w.n_mtiles = (w.M + w.FT - 1) / w.FT;
-  w.n_rtiles = (w.R + 63) / 64;
+  w.x3_mr = f16x2 && w.R % 128 == 0 ? 2 : 1;  // (128-row tiles: k_wgrad_x3<.., 2, 2>)
+  w.n_rtiles = (w.R + 64 * w.x3_mr - 1) / (64 * w.x3_mr);
   w.n_jtiles = (w.C + WgX3Geo<18, 1>::CB - 1) / WgX3Geo<18, 1>::CB;
   const int tiles = w.n_rtiles * w.n_jtiles;
   w.S = std::max(1, std::min((256 + tiles - 1) / tiles, w.N * w.n_mtiles));
@@ -1272,13 +1306,21 @@ hipError_t launch_wgrad_x3(const WgradParams &p0, hipStream_t s) {
   if (p0.f16x2) {  // 2-way fp16 splits (NPL = 2)
     if (!p0.amax_p || !p0.amax_q) return hipErrorInvalidValue;
     const WgradParams &p = p0;
-    if (p.s_in == 1)
+    if (p.x3_mr == 2 && p.R % 128 != 0) return hipErrorInvalidValue;
+    if (p.s_in == 1 && p.x3_mr == 2)
+      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2, 2>::LDS),
+                         s, p);
+    else if (p.s_in == 1)
       hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2>::LDS), s, p);
+    else if (p.x3_mr == 2)
+      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2, 2>::LDS),
+                         s, p);
     else
       hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2>::LDS), s, p);
     return hipGetLastError();
   }
   const WgradParams &p = p0;
+  if (p.x3_mr != 1) return hipErrorInvalidValue;  // (128-row tiles: fp16 splits only)
   if (p.s_in == 1) {
     constexpr int lds = WgX3Geo<18, 1>::LDS;
     hipLaunchKernelGGL((k_wgrad_x3<18, 1>), dim3(nblk), dim3(512), lds, s, p);
