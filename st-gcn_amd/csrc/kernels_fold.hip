@@ -29,18 +29,16 @@
 
 namespace stgcn {
 
-// The fold's small GEMMs on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: a
+// The fold's small GEMMs on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: a
 // k-ordered fp32 fma chain per output, fixed order: deterministic).
 //
 // Operands are first re-laid by k_fold_tr as fp32 [plane q][row][k] with k
 // contiguous and rows and k zero-padded to multiples of 32, so the GEMM's inner
-// loop is pure loads + MFMAs: lane l (row l & 31, k-half l >> 5) loads eight
-// consecutive k (32 bytes) per operand for eight MFMAs, no conversions, no
-// bounds selects. The small GEMMs are bound by operand traffic from L2, not by
-// the matrix rate: a 32 x 32 fp32 tile per wave moves 4x fewer bytes per flop
-// than a 16 x 16 fp64 one (measured 2-4x faster per launch).
+// loop is pure loads + MFMAs: lane l (row l & 15, k-quad l >> 4) loads four
+// consecutive k (16 bytes) per operand for four MFMAs, no conversions, no
+// bounds selects.
 //
-// k_fold_gemm: block = nine waves = the nine taps q of one 32 x 32 output tile;
+// k_fold_gemm: block = nine waves = the nine taps q of one 16 x 16 output tile;
 // each wave streams its whole K range (L2-resident operands) with the next
 // 16-k group's loads in flight (no LDS staging, no split-K partials). Two kinds:
 //   TAP: out[q](m, n) = sum_k A[q](m, k) B[q](n, k) + sum_v A2(q, m, v) B2(n, v)
@@ -52,6 +50,7 @@ namespace stgcn {
 // Up to three jobs share a launch (blockIdx.x runs over their tiles).
 typedef float float16v __attribute__((ext_vector_type(16)));
 typedef float float8v __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef double double4v __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline int pad32(int x) { return (x + 31) & ~31; }
@@ -75,35 +74,36 @@ struct FoldJobs {
 };
 
 // One wave's K stream, fully unrolled for NG 16-k groups (straight-line code:
-// the compiler's load counters stay exact, so D groups are in flight; a
-// runtime-trip loop with conditional prefetches made it wait for every load
-// at the loop head). Lane: k = 16 i + 8 (l >> 5) + j for MFMA j of group i.
+// the compiler's load counters stay exact; D groups in flight, pinned by
+// sched_barrier: the scheduler would otherwise sink each prefetch next to its
+// MFMAs). Lane: k = 16 i + 4 (l >> 4) + j for MFMA j of group i.
 template <int NG>
-__device__ __forceinline__ void f32_stream(const float *pa, const float *pb, float16v &acc) {
+__device__ __forceinline__ void f32_stream(const float *pa, const float *pb, floatx4 &acc) {
   constexpr int D = NG < 4 ? NG : 4;
-  float8v a[D], b[D];
+  float4 a[D], b[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    a[d] = *reinterpret_cast<const float8v *>(pa + 16 * d);
-    b[d] = *reinterpret_cast<const float8v *>(pb + 16 * d);
+    a[d] = *reinterpret_cast<const float4 *>(pa + 16 * d);
+    b[d] = *reinterpret_cast<const float4 *>(pb + 16 * d);
   }
-  __builtin_amdgcn_sched_barrier(0);  // (keeps the prefetches ahead: the scheduler
-                                      // would sink them next to their MFMAs)
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
     const int d = i % D;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[d][j], b[d][j], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d].x, b[d].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d].y, b[d].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d].z, b[d].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[d].w, b[d].w, acc, 0, 0, 0);
     if (i + D < NG) {
-      a[d] = *reinterpret_cast<const float8v *>(pa + 16 * (i + D));
-      b[d] = *reinterpret_cast<const float8v *>(pb + 16 * (i + D));
+      a[d] = *reinterpret_cast<const float4 *>(pa + 16 * (i + D));
+      b[d] = *reinterpret_cast<const float4 *>(pb + 16 * (i + D));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 __device__ __forceinline__ void f32_stream_any(const float *pa, const float *pb, int ng,
-                                               float16v &acc) {
+                                               floatx4 &acc) {
   switch (ng) {
     case 4: f32_stream<4>(pa, pb, acc); return;
     case 8: f32_stream<8>(pa, pb, acc); return;
@@ -119,39 +119,42 @@ __device__ __forceinline__ void f32_stream_any(const float *pa, const float *pb,
   }
 }
 
+// 16 x 16 output tiles (v_mfma_f32_16x16x4_f32, same rate as 32 x 32 x 2): a
+// block is one CU's worth of waves, so the tile count sets how many CUs work;
+// 32 x 32 tiles left three quarters of the chip idle on the 256-channel blocks
 __global__ __launch_bounds__(576) void k_fold_gemm(FoldJobs js) {
-  __shared__ float red[9][32 * 33];
+  __shared__ float red[9][16 * 17];
   const int tile = blockIdx.x;
   int ji = 0;
   while (ji + 1 < js.n && tile >= js.tile0[ji + 1]) ++ji;
   const FoldJob &g = js.j[ji];
-  const int t = tile - js.tile0[ji], ntn = (g.N + 31) >> 5;
-  const int m0 = (t / ntn) * 32, n0 = (t % ntn) * 32;
-  const int q = threadIdx.x >> 6, l = threadIdx.x & 63, r32 = l & 31, h = l >> 5;
-  float16v acc = {};
+  const int t = tile - js.tile0[ji], ntn = (g.N + 15) >> 4;
+  const int m0 = (t / ntn) * 16, n0 = (t % ntn) * 16;
+  const int q = threadIdx.x >> 6, l = threadIdx.x & 63, r16 = l & 15, kq = l >> 4;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   {
-    const float *pa = g.A + q * g.aq + (int64_t)(m0 + r32) * g.am + 8 * h;
-    const float *pb = g.B + q * g.bq + (int64_t)(n0 + r32) * g.bn + 8 * h;
+    const float *pa = g.A + q * g.aq + (int64_t)(m0 + r16) * g.am + 4 * kq;
+    const float *pb = g.B + q * g.bq + (int64_t)(n0 + r16) * g.bn + 4 * kq;
     f32_stream_any(pa, pb, (g.K + 15) >> 4, acc);
   }
   if (g.A2) {  // (short: K2 = V; bounds-checked direct reads)
-    const int m = m0 + r32, n = n0 + r32;
+    const int m = m0 + r16, n = n0 + r16;
     const bool ok_m = m < g.M, ok_n = n < g.N;
     const double *a2 = g.A2 + q * g.a2q + (int64_t)min(m, g.M - 1) * g.a2m;
     const float *b2 = g.B2 + (int64_t)min(n, g.N - 1) * g.b2n;
-    for (int k0 = 0; k0 < g.K2; k0 += 2) {
-      const int k = k0 + h, kc = min(k, g.K2 - 1);
+    for (int k0 = 0; k0 < g.K2; k0 += 4) {
+      const int k = k0 + kq, kc = min(k, g.K2 - 1);
       const float x = (float)a2[kc], y = b2[kc];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(k < g.K2 && ok_m ? x : 0.f,
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(k < g.K2 && ok_m ? x : 0.f,
                                                  k < g.K2 && ok_n ? y : 0.f, acc, 0, 0, 0);
     }
   }
-  // C/D: col = lane & 31, row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
+  // C/D: col = lane & 15, row = 4 (lane >> 4) + reg
   if (!g.red) {
-    const int nn = n0 + r32;
+    const int nn = n0 + r16;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    for (int r = 0; r < 4; ++r) {
+      const int mm = m0 + 4 * kq + r;
       if (mm >= g.M || nn >= g.N) continue;
       const int64_t o = q * g.oq + mm * g.om + nn * g.on;
       if (g.o_dbl)
@@ -162,21 +165,20 @@ __global__ __launch_bounds__(576) void k_fold_gemm(FoldJobs js) {
     return;
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r) red[q][((r & 3) + 8 * (r >> 2) + 4 * h) * 33 + r32] = acc[r];
+  for (int r = 0; r < 4; ++r) red[q][(4 * kq + r) * 17 + r16] = acc[r];
   __syncthreads();
-  for (int e = threadIdx.x; e < 1024; e += 576) {
-    const int rr = e >> 5, cc = e & 31;
-    const int mm = m0 + rr, nn = n0 + cc;
-    if (mm >= g.M || nn >= g.N) continue;
-    double s = 0.0;
+  if (threadIdx.x >= 256) return;
+  const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  const int mm = m0 + rr, nn = n0 + cc;
+  if (mm >= g.M || nn >= g.N) return;
+  double sum = 0.0;
 #pragma unroll
-    for (int w = 0; w < 9; ++w) s += red[w][rr * 33 + cc];
-    const int64_t o = mm * g.om + nn * g.on;
-    if (g.o_dbl)
-      reinterpret_cast<double *>(g.out)[o] = s;
-    else
-      reinterpret_cast<float *>(g.out)[o] = (float)s;
-  }
+  for (int w = 0; w < 9; ++w) sum += red[w][rr * 17 + cc];
+  const int64_t o = mm * g.om + nn * g.on;
+  if (g.o_dbl)
+    reinterpret_cast<double *>(g.out)[o] = sum;
+  else
+    reinterpret_cast<float *>(g.out)[o] = (float)sum;
 }
 
 static hipError_t fold_gemm(std::initializer_list<FoldJob> jobs, hipStream_t s) {
@@ -187,7 +189,7 @@ static hipError_t fold_gemm(std::initializer_list<FoldJob> jobs, hipStream_t s) 
     if (js.n == 3 || g.M <= 0 || g.N <= 0) return hipErrorInvalidValue;
     js.j[js.n] = g;
     js.tile0[js.n++] = tiles;
-    tiles += ((g.M + 31) / 32) * ((g.N + 31) / 32);
+    tiles += ((g.M + 15) / 16) * ((g.N + 15) / 16);
   }
   js.tile0[js.n] = tiles;
   hipLaunchKernelGGL(k_fold_gemm, dim3(tiles), dim3(576), 0, s, js);
