@@ -325,7 +325,8 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false,false>",
                        1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false,{spb}>" if s == 1 else
                            f"k_conv_x3<5|4,{V},1,1,{npl},false,{spb}>"),
-                       2: f"k_wgrad_x3<{V},{s},{npl}>" if V == 18 else f"k_wgrad_taps<{V},{s}>",
+                       2: (f"k_wgrad_x3<{V},{s},{npl},{2 if npl == 2 and co % 128 == 0 else 1}>"
+                           if V == 18 else f"k_wgrad_taps<{V},{s}>"),
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
