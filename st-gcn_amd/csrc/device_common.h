@@ -273,11 +273,12 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
 // ---------------------------------------------------------------------------
 constexpr int kEpiPitch = 260;  // floats: rows 4 words apart modulo 64 banks
 
+template <int PITCH = kEpiPitch>
 __device__ __forceinline__ void acc_to_img(float *img, const floatx16 &a, int row0, int col0) {
   const int lane = threadIdx.x & 63, hi = lane >> 5, lo = lane & 31;
 #pragma unroll
   for (int i = 0; i < 16; ++i)
-    img[(row0 + (i & 3) + 8 * (i >> 2) + 4 * hi) * kEpiPitch + col0 + lo] = a[i];
+    img[(row0 + (i & 3) + 8 * (i >> 2) + 4 * hi) * PITCH + col0 + lo] = a[i];
 }
 
 template <int V, int NCOLS, int NT, int ROWS = 64, bool OB = false>

@@ -221,13 +221,16 @@ struct ConvX3Geo {
 // ---------------------------------------------------------------------------
 constexpr int kSpbAt = 18 * 20;  // A transposed, rows padded to 20 (16-byte aligned)
 // H and x images of one 64-row half + A^T
-constexpr int kSpbLds = (2 * 64 * kEpiPitch + kSpbAt) * 4;
+// image pitch: 272 = 16 mod 64 banks puts the row pass's 64 lanes (8 rows x 8
+// frame groups, 8-byte reads) on distinct bank pairs (260: two-way)
+constexpr int kSpbPitch = 272;
+constexpr int kSpbLds = (2 * 64 * kSpbPitch + kSpbAt) * 4;
 
 template <int MR>
 __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
                                              float *smem, int n, int r0, int m0, int mi,
                                              int nj0) {
-  constexpr int V = 18, FT = kTileCols / V, NCOLS = FT * V, P = kEpiPitch;
+  constexpr int V = 18, FT = kTileCols / V, NCOLS = FT * V, P = kSpbPitch;
   constexpr int NSUB = 56;  // threads per (v block, w block) combination of dA
   float *const Himg = smem, *const Ximg = smem + 64 * P, *const At = smem + 2 * 64 * P;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -259,7 +262,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
       for (int rb = 0; rb < MR; ++rb)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc_to_img(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
+          acc_to_img<P>(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
     }
     if (h == 0)  // A^T[w][v] (broadcast 16-byte LDS reads in the contraction)
       for (int i = tid; i < kSpbAt; i += 512) {
