@@ -4,7 +4,7 @@
 # GRBM clock) over kbench with KB_X3=1. No tracing domains.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp KB_X3=1
+export TMPDIR=/tmp KB_X3=1 KB_F16=${KB_F16:-0}
 OUT=gpurun_out/pmcx_${TAG:-x}
 mkdir -p $OUT
 for pr in ${PAIRS:-2:1 0:1 0:5}; do
