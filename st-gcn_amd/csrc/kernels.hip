@@ -1486,36 +1486,41 @@ hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_
 }
 
 // y = ReLU(BN(U)); optionally (ysum != null) also the per-channel sum and sum
-// of squares of y (fp64): the next block's BN1 batch statistics.
+// of squares of y (fp64): the next block's BN1 batch statistics. A block
+// covers kBnRows clips of one channel (one block reduction and one set of
+// fp64 atomics per kBnRows rows: per-row blocks spent their time there).
+constexpr int kBnRows = 4;
 template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
                                                      const float *invstd, const float *g,
-                                                     const float *b, float *y, int C, int L,
-                                                     double *ysum, double *ysq, Dropout drop,
-                                                     double *yext) {
+                                                     const float *b, float *y, int N, int C,
+                                                     int L, double *ysum, double *ysq,
+                                                     Dropout drop, double *yext) {
   __shared__ double red[8];
-  const int c = blockIdx.x, n = blockIdx.y;
-  const int64_t base = ((int64_t)n * C + c) * L;
+  const int c = blockIdx.x, n0 = blockIdx.y * kBnRows, n1 = min(N, n0 + kBnRows);
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   double s = 0.0, q = 0.0, cnt = 0.0, su = 0.0, xu = 0.0;
-  for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
-    float v[VEC];
-    vld<VEC>(U + base + i, v);
+  for (int n = n0; n < n1; ++n) {
+    const int64_t base = ((int64_t)n * C + c) * L;
+    for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
+      float v[VEC];
+      vld<VEC>(U + base + i, v);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      const float uh = (v[j] - mu) * is;
-      const float t = (v[j] - mu) * a + be;
-      v[j] = t > 0.f ? t : 0.f;
-      if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
-      s += (double)v[j];
-      q += (double)v[j] * (double)v[j];
-      if (yext && t > 0.f) {
-        cnt += 1.0;
-        su += (double)uh;
-        xu += (double)v[j] * (double)uh;
+      for (int j = 0; j < VEC; ++j) {
+        const float uh = (v[j] - mu) * is;
+        const float t = (v[j] - mu) * a + be;
+        v[j] = t > 0.f ? t : 0.f;
+        if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
+        s += (double)v[j];
+        q += (double)v[j] * (double)v[j];
+        if (yext && t > 0.f) {
+          cnt += 1.0;
+          su += (double)uh;
+          xu += (double)v[j] * (double)uh;
+        }
       }
+      vst<VEC>(y + base + i, v);
     }
-    vst<VEC>(y + base + i, v);
   }
   if (ysum) block_sum2_atomic<256>(s, q, ysum + c, ysq + c, red);
   if (yext) {
@@ -1528,8 +1533,8 @@ hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *in
                               const float *g, const float *b, float *y, int N, int C, int L,
                               double *ysum, double *ysq, Dropout drop, hipStream_t s,
                               double *yext) {
-  STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, N), U, mean, invstd, g, b, y, C,
-                   L, ysum, ysq, drop, yext);
+  STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, (N + kBnRows - 1) / kBnRows), U,
+                   mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext);
   return hipGetLastError();
 }
 
