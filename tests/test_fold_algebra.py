@@ -6,7 +6,8 @@ conv (st_graphconv.py:41-43, :99):
     U[o,t]  = sum_q Wc_q G[s t + q - 4] + BT[o,t],   Wc_q = Wt_q W'
     dWt_q   = dWc_q W'^T + sum_v Tq[o,v] bZ[c,v],     dWc_q = sum dU G[s t + q - 4]^T
     dW'     = sum_q Wt_q^T dWc_q,    H = W'^T dZ = conv^T(dU; Wc),
-    sum_{n,t} dZ[c,v] = sum_q sum_o Wt[o,c,q] Tq[o,v]
+    sum_{n,t} dZ[c,v] = sum_q sum_o Wt[o,c,q] Tq[o,v],
+    sum_{n,t} H[c,v]  = sum_q sum_o Wc[o,c,q] Tq[o,v]   (BN1's sum of dxhat, k_fold_sd)
 
 Tq is built exactly as the kernels build it (k_fold_tq: the per-clip-summed
 dU with the boundary frames of fold_slots subtracted), BT as k_fold_bias.
@@ -101,3 +102,12 @@ def test_fold_matches_unfolded_block(N, C, R, T, V, st):
     np.testing.assert_allclose(H, G.grad.numpy(), rtol=1e-10, atol=1e-9)
     SdZ = np.einsum("ocq,qov->cv", Wtn, Tq)
     np.testing.assert_allclose(SdZ, Z.grad.sum(dim=(0, 2)).numpy(), rtol=1e-10, atol=1e-9)
+    # the analytic BN1 sum of the folded backward (k_fold_red64 + k_fold_sd):
+    # sum_{n,t} H[c,v] = sum_q sum_o Wc[o,c,q] Tq[q,o,v], and with
+    # dxhat[c,t,w] = sum_v A[v,w] H[c,t,v]: sum_{n,t,w} dxhat = sum_v SdH rowsum(A)
+    SdH = np.einsum("ocq,qov->cv", Wc, Tq)
+    np.testing.assert_allclose(SdH, H.sum(axis=(0, 2)), rtol=1e-10, atol=1e-9)
+    A = np.random.default_rng(N + T).uniform(0.0, 1.0, (V, V))
+    dxhat = np.einsum("vw,nctv->nctw", A, H)
+    np.testing.assert_allclose(SdH @ A.sum(axis=1), dxhat.sum(axis=(0, 2, 3)), rtol=1e-10,
+                               atol=1e-9)
