@@ -84,8 +84,11 @@ extern "C" {
                             * their max |x| (so h <= 2^14 and no element underflows
                             * relative to the tensor's maximum); the result is scaled back
                             * exactly. Same fp32 gate as STGCN_F_F32X3, half its MFMAs.
-                            * The data gradient keeps the 3-way bf16 splits (its output
-                            * feeds the cancellation-heavy BN1 backward sums). */
+                            * The data gradient runs on the fp16 splits too; BN1's
+                            * nearly cancelling sum of dxhat (its bias gradient) is
+                            * formed from the fp64 per-tap dU sums instead of from the
+                            * 22-bit data gradient. (The 3-way bf16 data gradient is an
+                            * A/B measurement build only: STGCN_AB_F16X2_DGRAD=0.) */
 
 enum {
   STGCN_OK = 0,
@@ -131,7 +134,10 @@ typedef struct stgcn_fwd_args {
   /* ABI 2, optional: keep the joint contraction G = f(BN1(x)) A^T for the
    * backward instead of recomputing it: stgcn_keep_g_bytes(d) bytes; fp32
    * (N, K*C_in, T, V), or, where the bf16 path's fused spatial kernel runs
-   * (STGCN_F_BF16, C_in >= 16), bf16 in frame tiles (ABI 4: opaque to the caller) */
+   * (STGCN_F_BF16, C_in >= 16), bf16 in frame tiles (ABI 4: opaque to the caller).
+   * Under STGCN_F_F16X2 the words after G carry its operand bound max |G| to
+   * the backward's weight gradient: a kept G is valid only for a backward with
+   * the SAME descriptor (flags included) as the forward that wrote it. */
   float *G;
   /* ABI 2, optional stack chaining (training): x_stats = [sum(C_in), sumsq(C_in)]
    * of x over (n,t,v) in fp64 (produced by the previous block's y_stats: the

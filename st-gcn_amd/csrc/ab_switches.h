@@ -1,7 +1,9 @@
 // Compile-time A/B alternates of the tuned kernel paths.
 //
 // The shipped library (build.py default) has exactly one path per
-// configuration: every switch below is 0. A measurement build turns one on with
+// configuration: every switch below is at its default (0, except
+// STGCN_AB_F16X2_DGRAD = 1: the folded data gradient on the fp16 splits under
+// STGCN_F_F16X2). A measurement build flips one with
 // a -D define (`build.py`: build(variant="name", defines=("STGCN_AB_UNFUSED_SP=1",)),
 // loaded as lib/libstgcn_hip_<variant>.so by scripts/), so no environment
 // variable can route the product library to an untested kernel.

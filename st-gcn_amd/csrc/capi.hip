@@ -110,12 +110,14 @@ bool fused_spb50(const stgcn_desc_t *d) { return fused_spb(d) && d->V == 50; }
 // (Wc_q = Wt_q W'), so the temporal conv reads G = BN1(x) A^T (C_in channels)
 // and Z / dZ are never formed; the backward's data gradient yields H directly.
 // fp32 split path (cfg2: V = 18, K = 1), non-residual blocks over >= 16 input
-// channels whose spatial backward is the unfused pair (STGCN_AB_NO_FOLD build:
-// the unfolded kernels, A/B only).
+// and output channels (the data gradient reduces over C_out: k_conv_x3 needs
+// >= 16 there, and only k_conv_x3 runs the fused SpatialConv backward epilogue)
+// whose spatial backward is the unfused pair (STGCN_AB_NO_FOLD build: the
+// unfolded kernels, A/B only).
 bool fold_w(const stgcn_desc_t *d) {
   constexpr bool off = STGCN_AB_NO_FOLD != 0;
-  return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->V == 18 &&
-         !fused_spb(d);
+  return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->C_out >= 16 &&
+         d->V == 18 && !fused_spb(d);
 }
 // The folded block's SpatialConv backward inside its data gradient (kernels_x3.hip
 // spb_epilogue): dxhat = H A, dA, the BN1 / chain sums from the tile while H is

@@ -490,6 +490,9 @@ static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t ld
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
   if (p0.bf16 == 3 && conv_x3_supported(p0)) return launch_conv_x3(p0, s);
+  // (the fused SpatialConv backward epilogue and the fp16 operand scales exist in
+  // k_conv_x3 only: any other kernel would ignore them and write H / wrong results)
+  if (p0.spb || p0.f16x2) return hipErrorInvalidValue;
   if (p0.bf16 == 1 && conv_b1_supported(p0)) return launch_conv_b1(p0, s);
   if (p0.bf16 == 1 && conv_bf16_supported(p0)) return launch_conv_bf16(p0, s);
   // (bf16-stored operands: only the kernels above read / write them)

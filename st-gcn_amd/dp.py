@@ -67,6 +67,12 @@ class GradAllReduce:
             self._flat.append(flat)
         self._install_views()
         self._sync = True
+        # observable overlap: (kind, index) in arrival order -- ("grad", i) when
+        # parameter i's gradient has been accumulated (i in model.parameters()
+        # order), ("launch", b) when bucket b's all-reduce is issued; reset by
+        # synchronize(), kept in ``last_trace``
+        self._index = {p: i for i, p in enumerate(params)}
+        self.trace, self.last_trace = [], []
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._handles += [p.register_hook(self._guard(p)) for p in params]
         self._reset()
@@ -80,7 +86,9 @@ class GradAllReduce:
             # bucket whose all-reduce never launched because one of its
             # parameters is unused -- would add into a buffer that is (or will
             # be) reduced for the first backward only
-            if self._sync and (self._work[bi] is not None or p in self._seen):
+            # (in flight: always, no_sync or not -- the buffer is being reduced;
+            # a repeated arrival counts only for a backward that reduces)
+            if self._work[bi] is not None or (self._sync and p in self._seen):
                 raise RuntimeError(
                     "GradAllReduce: a second backward before synchronize() would accumulate "
                     "into a bucket whose all-reduce is in flight; run the earlier "
@@ -121,6 +129,7 @@ class GradAllReduce:
         if p.grad is not v:  # not accumulated into the bucket: move it there
             v.copy_(p.grad)
             p.grad = v
+        self.trace.append(("grad", self._index[p]))
         if not self._sync:
             return
         self._seen.add(p)
@@ -130,6 +139,7 @@ class GradAllReduce:
             self._launch(bi)
 
     def _launch(self, bi):
+        self.trace.append(("launch", bi))
         self._work[bi] = dist.all_reduce(self._flat[bi], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True)
 
@@ -143,6 +153,7 @@ class GradAllReduce:
             self._work[bi].wait()
             self._flat[bi].div_(self.world)
         self._install_views()
+        self.last_trace, self.trace = self.trace, []
         self._reset()
 
     def remove(self):

@@ -64,6 +64,14 @@ def _worker(rank, world, port, out_q, T, bucket_bytes):
         loss = nn.functional.cross_entropy(model(xs[rank]), ys[rank])
         loss.backward()
         dp.synchronize()
+        # overlap (north star: the all-reduce runs beside the remaining backward):
+        # the first bucket's all-reduce is issued before block 0 -- whose backward
+        # runs last -- has produced any gradient
+        tr = dp.last_trace
+        blk0 = {i for i, k in enumerate(model.names) if k.startswith("conv.0.")}
+        first_launch = next(j for j, (k, _) in enumerate(tr) if k == "launch")
+        first_blk0 = next(j for j, (k, i) in enumerate(tr) if k == "grad" and i in blk0)
+        overlapped = first_launch < first_blk0
         got = [p.grad.clone() for p in model.ps]
         # expected: mean over shards of per-shard grads (computed locally)
         per = [_shard_grads(params, buffers, xs[r], ys[r]) for r in range(world)]
@@ -77,7 +85,7 @@ def _worker(rank, world, port, out_q, T, bucket_bytes):
         ref = flat.clone()
         dist.broadcast(ref, 0)
         same = torch.equal(ref, flat)
-        out_q.put((rank, worst, same, len(dp.buckets)))
+        out_q.put((rank, worst, same, len(dp.buckets), overlapped))
     finally:
         dist.destroy_process_group()
 
@@ -95,10 +103,11 @@ def test_dp_allreduce_matches_mean_of_shards(world, bucket_bytes):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, worst, same, nb in res:
+    for rank, worst, same, nb, overlapped in res:
         assert worst < 1e-5, (rank, worst)
         assert same, rank
         assert nb >= 2
+        assert overlapped, rank
 
 
 def _accum_worker(rank, world, port, out_q):
@@ -156,7 +165,21 @@ def _accum_worker(rank, world, port, out_q):
         dp.synchronize()
         want = mean_over_ranks(2)
         errs.append(max((p.grad - w).abs().max().item() for p, w in zip(model.parameters(), want)))
-        out_q.put((rank, max(errs), raised))
+        # a synced backward (all-reduces in flight), then a
+        # no_sync() backward before synchronize() -- it would add into buffers
+        # that are being reduced, so it raises too
+        dp.zero_grad()
+        model(xs[0, rank]).square().sum().backward()
+        raised2 = False
+        try:
+            with dp.no_sync():
+                model(xs[1, rank]).square().sum().backward()
+        except RuntimeError as e:
+            raised2 = "no_sync" in str(e)
+        dp.synchronize()
+        want = mean_over_ranks(0)
+        errs.append(max((p.grad - w).abs().max().item() for p, w in zip(model.parameters(), want)))
+        out_q.put((rank, max(errs), raised and raised2))
     finally:
         dist.destroy_process_group()
 

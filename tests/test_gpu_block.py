@@ -81,13 +81,19 @@ def _compare(got, want, residual=False, tol=TOL, floor=None):
     assert not bad, "; ".join(f"{k}: {e:.2e} > {l:.1e}" for k, e, l in bad)
 
 
+@pytest.mark.parametrize("gemm", ["fp32", "f32x3", "f16x2"])
 @pytest.mark.parametrize("fixture", block_fixtures())
-def test_block_matches_reference_fixture(pkg, fixture):
+def test_block_matches_reference_fixture(pkg, fixture, gemm):
+    """The reference's own block fixtures through every fp32 GEMM mode: exact
+    fp32 MFMA, the 3-way bf16 splits and the benched 2-way fp16 splits (the
+    latter two where the block's GEMMs take them; elsewhere the same kernels as
+    fp32), each at the fp32 gate against the fp64 oracle and within 5e-5 of the
+    reference's own fp32 outputs."""
     ref = load_npz(fixture)
     residual = bool(ref["meta"][7])
     x = torch.from_numpy(ref["x"])
     g = torch.from_numpy(ref["g"])
-    got = _run_hip(pkg, ref, x, g)
+    got = _run_hip(pkg, ref, x, g, gemm=gemm)
     want64, floor = _oracle(ref, got)
     _compare(got, want64, residual=residual, floor=floor)
     # and against the reference's own fp32 outputs (its rounding included)
@@ -398,7 +404,7 @@ def test_block_dropout_seed_reproducible(pkg):
                            _keep_mask(sa + 1, (2, 64, 30, 18), 0.5))
 
 
-@pytest.mark.parametrize("gemm", ["fp32", "f32x3"])
+@pytest.mark.parametrize("gemm", ["fp32", "f32x3", "f16x2"])
 def test_bench_size_block(pkg, gemm):
     """The cfg2 layer-1 block at the bench's exact per-GPU size (N = 128,
     T = 300, V = 18), fp32 MFMA and the benched bf16x3 split path, against the

@@ -82,6 +82,75 @@ def test_f16x2_full_size_block(pkg):
         assert torch.isfinite(v).all(), k
 
 
+def test_f16x2_l8_shape_block(pkg):
+    """The dominant kernel's shape (cfg2 L8 / L9: 256 -> 256, T = 75) at
+    N = 16: 16 channel chunks per tile (the longest reductions), 128-row tiles,
+    at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, 256, 256, 1, 18, 1, 16, 75, seed=11)
+    got = _check(pkg, arrays, x, g)
+    assert _plan(pkg, x, 256, 1) & pkg.hip_lib.PLAN_F16X2
+
+
+def _per_channel_err(got, want, axis):
+    """max over channels c of max|got[c] - want[c]| / max|want[c]| (channel = axis)"""
+    g = got.double().movedim(axis, 0).reshape(got.shape[axis], -1)
+    w = want.detach().double().movedim(axis, 0).reshape(want.shape[axis], -1)
+    return ((g - w).abs().amax(1) / w.abs().amax(1).clamp_min(1e-300))
+
+
+def test_f16x2_mixed_scale_per_channel(pkg):
+    """One input channel and one output channel's weights (its temporal conv
+    row and its SpatialConv row) at 1e-4 of the rest: a single power-of-two
+    scale per operand tensor must not cost the small channels their precision.
+    Gated PER CHANNEL (not rel-to-max over the tensor, which cannot see a small
+    channel): every channel of y, dx, dWt and dW' within max(1e-5, 2x the fp32
+    reference's own error for that channel) of the fp64 oracle."""
+    from oracle import ref_cpu
+    arrays, x, g = _random_case(pkg, 64, 128, 1, 18, 1, 2, 33, seed=4)
+    ci, co = 5, 17
+    x = x.clone()
+    x[:, ci] *= 1e-4
+    arrays["x"] = x.numpy()
+    for k in ("param.temporalConv.weight", "param.spatialConv.W.weight"):
+        w = arrays[k].copy()
+        w[co] *= 1e-4
+        arrays[k] = w
+    got = _run_hip(pkg, arrays, x, g, gemm="f16x2")
+    want, _ = _oracle(arrays, got)
+    ref32 = ref_cpu.block_step(arrays, dtype=torch.float32, relu_mask=got["y"] > 0)
+    bad = []
+    for k, axis in (("y", 1), ("grad.x", 1), ("grad.temporalConv.weight", 0),
+                    ("grad.spatialConv.W.weight", 0)):
+        e = _per_channel_err(got[k], want[k], axis)
+        f = _per_channel_err(ref32[k].detach(), want[k], axis)
+        lim = torch.clamp(2.0 * f, min=1e-5)
+        if (e > lim).any():
+            c = int(torch.argmax(e / lim))
+            bad.append(f"{k}[{c}]: {e[c]:.2e} > {lim[c]:.1e}")
+    assert not bad, "; ".join(bad)
+
+
+@pytest.mark.parametrize("gemm", ["f32x3", "f16x2"])
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T: >= 16 input channels, < 16 output channels
+    (16, 8, 1, 18, 1, 2, 9),
+    (32, 8, 2, 18, 1, 2, 21),
+])
+def test_narrow_output_blocks_not_folded(pkg, case, gemm):
+    """a block with C_out < 16 has a data gradient that reduces
+    over fewer than 16 channels, which the split kernel (and its fused
+    SpatialConv backward epilogue) does not run; such a block must not fold, and
+    runs the unfolded kernels at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, *case)
+    hl = pkg.hip_lib
+    d = pkg.fused.make_desc(tuple(x.shape), case[1], 1, case[2], 4, 1e-5, 0.1, True,
+                            **pkg.fused._gemm_flags(gemm))
+    assert not hl.block_plan(d) & hl.PLAN_FOLD
+    got = _run_hip(pkg, arrays, x, g, gemm=gemm)
+    want, floor = _oracle(arrays, got)
+    _compare(got, want, floor=floor)
+
+
 def test_f16x2_unfolded_blocks_keep_bf16x3(pkg):
     """Where the block does not fold (first block C_in = 3, residual, K = 3) the
     flag changes nothing: the plan has no F16X2 bit and the results are
