@@ -212,6 +212,16 @@ def joint_bwd_symbol(cfg, ci, t):
     return f"k_spatial_bwd3<{V}>"
 
 
+def x3_planes(sym):
+    """Operand planes (NPL) of a split-kernel symbol: k_conv_x3<NQ,TG,V,SIN,MR,NPL,..>
+    (k_conv_x3<5|4,V,SIN,MR,NPL,..> for the stride-2 data-gradient pair),
+    k_wgrad_x3<V,SIN,NPL,MR[,QBN]>."""
+    args = [a.strip() for a in sym[sym.index("<") + 1:sym.rindex(">")].split(",")]
+    if sym.startswith("k_wgrad_x3"):
+        return int(args[2])
+    return int(args[4] if args[0] == "5|4" else args[5])
+
+
 def kernel_roofline(pkg, device, cfg, iters=10):
     """Per-kernel timing with HIP events on the launch stream (the library's
     stgcn_time_kernel entry point, same launch parameters as the block), over
@@ -265,7 +275,10 @@ def kernel_roofline(pkg, device, cfg, iters=10):
             # the folded block (capi.hip fold_w: fp32 split path, K = 1, V = 18,
             # C_in >= 16): no spatial / H GEMM, the temporal GEMMs read G (C_in
             # channels) in place of Z, and the data gradient writes H (C_in)
-            fold = x3 and K == 1 and V == 18 and ci >= 16
+            fold = x3 and K == 1 and V == 18 and ci >= 16 and co >= 16
+            # (f16x2 fold without G, PLAN_FOLD_NO_G: the forward GEMM reads x and the
+            # weight gradient x against dU A -- the same bytes as G / dU)
+            bna = bool(hl.block_plan(d) & hl.PLAN_FOLD_NO_G)
             CZ = ci if fold else co
             # (the folded block's data gradient carries the SpatialConv backward:
             # it reads x and writes dxhat instead of writing H)
@@ -322,11 +335,12 @@ def kernel_roofline(pkg, device, cfg, iters=10):
                 mr = 2 if co % 128 == 0 else 1  # 128-row tiles for the 9-tap launches
                 npl = 2 if f16 and fold else 3  # operand planes: fp16 (h, l) or bf16 (h, m, l)
                 spb = "true" if fold else "false"  # the fused SpatialConv backward epilogue
-                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false,false>",
+                nb = ",true" if bna else ""  # (the BNA / QBN template instances)
+                sym = {0: f"k_conv_x3<9,3,{V},{s},{mr},{npl},false,false{nb}>",
                        1: (f"k_conv_x3<9,3,{V},1,{mr},{npl},false,{spb}>" if s == 1 else
                            f"k_conv_x3<5|4,{V},1,1,{npl},false,{spb}>"),
-                       2: (f"k_wgrad_x3<{V},{s},{npl},{2 if npl == 2 and co % 128 == 0 else 1}>"
-                           if V == 18 else f"k_wgrad_taps<{V},{s}>"),
+                       2: (f"k_wgrad_x3<{V},{s},{npl},{2 if npl == 2 and co % 128 == 0 else 1}"
+                           f"{nb}>" if V == 18 else f"k_wgrad_taps<{V},{s}>"),
                        3: f"k_tconv<1,8,{V},1>"}[which]
             else:
                 sym = {0: f"k_tconv<9,2,{V},{s}>",
@@ -603,8 +617,7 @@ def main():
             # the products per fp32 product (6 for bf16 x3, 3 for the fp16 x2 planes)
             split = sym.startswith("k_conv_x3") or sym.startswith("k_wgrad_x3")
             fpeak = (MFMA_BF16_PEAK_TFLOPS if cfg["bf16"] else
-                     (F16X2_PEAK_TFLOPS if sym.rstrip(">").split(",")[-3 if sym.startswith(
-                         "k_conv_x3") else -1].strip() == "2" else X3_PEAK_TFLOPS) if split
+                     (F16X2_PEAK_TFLOPS if x3_planes(sym) == 2 else X3_PEAK_TFLOPS) if split
                      else MFMA_F32_PEAK_TFLOPS)
             # the roof that bounds the kernel's algorithmic work: MFMA or HBM
             # (the bf16 GEMMs over fp32 activations at 64-128 channels sit

@@ -51,7 +51,11 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 6
+#define STGCN_ABI_VERSION 7
+
+/* ABI 7: words of max |y| after the 5 * C sums of a y_stats block */
+#define STGCN_STATS_AMAX_WORDS 2048
+#define STGCN_Y_STATS_BYTES(C) (8 * 5 * (size_t)(C) + 4 * (size_t)STGCN_STATS_AMAX_WORDS)
 
 /* stgcn_desc_t.flags */
 #define STGCN_F_RESIDUAL 1 /* full pre-activation residual block (st_graphconv.py:60-82) */
@@ -148,6 +152,10 @@ typedef struct stgcn_fwd_args {
    * (the next block's deferred-dx chain, stgcn_bwd_args_t.x_stats). */
   const double *x_stats;
   double *y_stats;
+  /* ABI 7: x_stats / y_stats blocks are STGCN_Y_STATS_BYTES(C) bytes: the 5 * C
+   * doubles above, then STGCN_STATS_AMAX_WORDS uint32 words that receive max |y|
+   * (as float bits, the largest word wins): the operand bound of the next block's
+   * fp16-split GEMMs, which read y itself (STGCN_PLAN_FOLD_NO_G). */
   /* ABI 2, optional fused dropout on y (training only; st_graphconv.py:53-58,
    * :107-109): element e of y is kept iff splitmix64(seed + e * 0x9E3779B97F4A7C15)
    * >> 32 >= dropout_p * 2^32, then scaled by 1/(1 - dropout_p). 0: no dropout. */
@@ -256,6 +264,11 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
 #define STGCN_PLAN_TCONV_SPLIT 32  /* temporal conv forward on the split pipeline         */
 #define STGCN_PLAN_TWGRAD_SPLIT 64 /* temporal weight gradient on the split kernel        */
 #define STGCN_PLAN_F16X2 128       /* the folded GEMMs on 2-way fp16 splits (STGCN_F_F16X2) */
+#define STGCN_PLAN_FOLD_NO_G 256   /* ABI 7, with F16X2: G = BN1(x) A^T is never formed: the
+                                    * forward GEMM reads x (BN1 in its loader, the joint
+                                    * contraction in its epilogue), the weight gradient reads
+                                    * x against dU A; the kept-G buffer (stgcn_keep_g_bytes)
+                                    * then carries only max |x| to the backward          */
 int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan);
 
 /* Measurement (bench.py roofline): time one of the block's GEMM kernels,

@@ -50,6 +50,12 @@ namespace {
   } while (0)
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+// bytes of a y_stats / x_stats block (ABI 7): 5 * C doubles of sums, then the
+// max |y| words (block_amax slots)
+size_t y_stats_bytes(int C) {
+  return sizeof(double) * 5 * C + sizeof(unsigned) * STGCN_STATS_AMAX_WORDS;
+}
+static_assert(STGCN_STATS_AMAX_WORDS == kAmaxWords, "ABI 7: the amax block of y_stats");
 
 // Frames per conv tile: as many whole frames as fit 256 columns.
 int conv_ft(int V) { return std::max(1, kTileCols / V); }
@@ -134,6 +140,25 @@ bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
 // sums instead (kernels_fold.hip k_fold_sd). STGCN_AB_F16X2_DGRAD=0 build: the
 // 3-way bf16 splits there (A/B only).
 bool f16x2_dgrad(const stgcn_desc_t *d) { return f16x2(d) && STGCN_AB_F16X2_DGRAD != 0; }
+// ... and G never formed (north star N1; kernels_x3.hip bna_contract): the
+// forward GEMM reads x, applies BN1 in its window loader and the joint
+// contraction with A in its epilogue (U = A U' + BT), the weight gradient reads
+// x (BN1 at staging) against dU A (written by the ReLU + BN2 backward apply
+// pass), so the gather kernel and G's HBM round trips are gone
+// (STGCN_AB_FOLD_G=1 build: G formed by k_gather4 and read by both GEMMs, A/B only)
+bool fold_bna(const stgcn_desc_t *d) {
+  constexpr bool off = STGCN_AB_FOLD_G != 0;
+  if (off || !f16x2(d)) return false;
+  ConvGemmParams p{};
+  p.V = d->V;
+  p.FT = conv_ft(d->V);
+  p.NQ = 9;
+  p.C = d->C_in;
+  p.R = d->C_out;
+  p.s_in = d->stride;
+  p.s_out = 1;
+  return conv_x3_bna_supported(p);
+}
 
 // sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
 // sums written by the ReLU + BN2 backward apply, k_fold_tq, one small GEMM with
@@ -279,7 +304,8 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.SdZ = c.take<double>((size_t)R * d->V);
   L.s1 = c.take<double>(C);
   L.s2 = c.take<double>(C);
-  L.amax = c.take<unsigned>(3 * kAmaxWords);  // f16x2: max |dU|, |Wc|, |G| (zeroed with the sums)
+  // f16x2: max |dU|, |Wc|, |G| (bna: |dU A|), |x| (bna without a kept bound); zeroed with the sums
+  L.amax = c.take<unsigned>(4 * kAmaxWords);
   L.dbl_bytes = c.off;
   if (!residual(d)) {  // clip-chunk sums of dU -> Tq -> sum_{n,t} dZ (kernels_fold.hip)
     L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
@@ -520,7 +546,7 @@ static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
   p.relu_out = 1;
   p.drop = make_dropout(d, a->dropout_p, a->seed);
   if (d->training && a->y_stats) {  // next block's BN1 statistics from the epilogue
-    HIP_TRY(hipMemsetAsync(a->y_stats, 0, sizeof(double) * 2 * R, s));
+    HIP_TRY(hipMemsetAsync(a->y_stats, 0, y_stats_bytes(R), s));
     p.stat_sum = a->y_stats;
     p.stat_sq = a->y_stats + R;
   }
@@ -541,6 +567,9 @@ static int residual_fwd_tail(const stgcn_desc_t *d, const stgcn_fwd_args_t *a,
   p.T_dst = To;
   conv_tiles(p);
   HIP_TRY(launch_conv_gemm(p, s));
+  if (d->training && a->y_stats)  // (ABI 7: max y after the sums, the next block's bound)
+    HIP_TRY(launch_absmax(a->y, (int64_t)N * R * To * V,
+                          reinterpret_cast<unsigned *>(a->y_stats + 5 * R), s));
   return STGCN_OK;
 }
 
@@ -602,6 +631,7 @@ int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan) {
     if (w.bf16 == 3) f |= STGCN_PLAN_TWGRAD_SPLIT;
   }
   if (f16x2(d)) f |= STGCN_PLAN_F16X2;
+  if (fold_bna(d)) f |= STGCN_PLAN_FOLD_NO_G;
   *plan = f;
   return STGCN_OK;
 }
@@ -614,6 +644,8 @@ size_t stgcn_fwd_workspace_bytes(const stgcn_desc_t *d) {
 size_t stgcn_keep_g_bytes(const stgcn_desc_t *d) {
   if (stgcn_check_desc(d) != STGCN_OK) return 0;
   if (fused_sp(d)) return sp_keep_g_bytes(d->N, d->C_in, d->T, d->V, d->K);
+  // (no G: only the forward's max |x| for the backward's weight gradient)
+  if (fold_bna(d)) return sizeof(unsigned) * kAmaxWords;
   // (f16x2: + one word after G, its max |G| for the backward's weight gradient)
   return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V +
          (f16x2(d) ? sizeof(unsigned) * kAmaxWords : 0);
@@ -648,11 +680,16 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   // BN1 statistics of the block input (st_graphconv.py:98)
   // (the caller may hand over the previous block's y statistics: x_stats)
   const double *xs1 = L.s1, *xq1 = L.q1;
+  const bool bna = fold_bna(d);
+  const unsigned *xmax = L.amax;  // (bna: max |x|, the fp16 operand bound's input)
   if (d->training && a->x_stats) {
     xs1 = a->x_stats;
     xq1 = a->x_stats + C;
+    xmax = reinterpret_cast<const unsigned *>(a->x_stats + 5 * C);  // (ABI 7: after the sums)
   } else if (d->training) {
-    HIP_TRY(launch_bn_stats(a->x, N, C, T * V, L.s1, L.q1, s));
+    HIP_TRY(launch_bn_stats(a->x, N, C, T * V, L.s1, L.q1, s, bna ? L.amax : nullptr));
+  } else if (bna) {
+    HIP_TRY(launch_absmax(a->x, (int64_t)N * C * T * V, L.amax, s));
   }
   HIP_TRY(launch_bn_finalize(xs1, xq1, C, (int64_t)N * T * V, d->eps, d->momentum, d->training,
                              a->rm1, a->rv1, mean1, invstd1, s));
@@ -674,7 +711,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
                                a->Z, z_bf16(d) ? 1 : 0, reinterpret_cast<__bf16 *>(a->G),
                                (res && d->training) ? L.s2 : nullptr,
                                (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s));
-  } else {
+  } else if (!bna) {
   float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
   HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s,
                             f16x2(d) ? L.amax : nullptr));  // (f16x2: max |G| on the way)
@@ -742,6 +779,18 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
           p.amax_keep = reinterpret_cast<unsigned *>(a->G + (size_t)N * C * T * V);
       }
       p.in = Gfold;
+      if (bna) {  // x in, BN1 in the loader, A in the epilogue (G never formed)
+        p.in = a->x;
+        p.bna = 1;
+        p.amax_in = xmax;
+        p.sA = a->A;
+        p.mean1 = mean1;
+        p.invstd1 = invstd1;
+        p.g1 = a->g1;
+        p.b1 = a->b1;
+        // (the kept "G" buffer holds only max |x|, for the backward's weight gradient)
+        p.amax_keep = a->G ? reinterpret_cast<unsigned *>(a->G) : nullptr;
+      }
       p.w = Wc;
       p.bias_r = nullptr;
       p.res = L.BT;
@@ -767,11 +816,13 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
   const Dropout ydrop = make_dropout(d, a->dropout_p, a->seed);
   // (ABI 5: y_stats holds 5 * C_out sums; the last three -- over the ReLU mask --
-  // feed the next block's deferred-dx chain, meaningless under dropout)
-  if (ys) HIP_TRY(hipMemsetAsync(ys, 0, sizeof(double) * 5 * R, s));
+  // feed the next block's deferred-dx chain, meaningless under dropout; ABI 7:
+  // then max y in STGCN_STATS_AMAX_WORDS words, the next block's operand bound)
+  if (ys) HIP_TRY(hipMemsetAsync(ys, 0, y_stats_bytes(R), s));
   HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
                              ys ? ys + R : nullptr, ydrop, s,
-                             (ys && !ydrop.thresh) ? ys + 2 * R : nullptr));
+                             (ys && !ydrop.thresh) ? ys + 2 * R : nullptr,
+                             ys ? reinterpret_cast<unsigned *>(ys + 5 * R) : nullptr));
   return STGCN_OK;
 }
 
@@ -817,7 +868,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     }
     // (with the clip-chunk sums of dU: sum_{n,t} dZ follows from them per tap,
     // no pass over dZ)
-    if (cols_sums(d)) {
+    if (cols_sums(d) && fold_bna(d)) {  // + dU A (the weight gradient's P) in dZ's buffer
+      HIP_TRY(launch_bn_relu_bwd_apply_fr(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
+                                          L.dU, L.dZ, L.sdu, N, R, To, V, d->training, drop,
+                                          a->dy_coef, L.fcs, L.amax, L.amax + 2 * kAmaxWords,
+                                          a->A, s));
+      HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.fpart, L.ftq,
+                             s));
+    } else if (cols_sums(d)) {
       HIP_TRY(launch_bn_relu_bwd_apply_cols(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
                                             L.dU, L.sdu, N, R, To * V, d->training, drop, s,
                                             du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs,
@@ -939,6 +997,25 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
         }
       }
     }
+    if (fold_bna(d)) {  // dWc = sum (dU A) BN1(x): Q = x with BN1 at staging, P = dU A
+      const unsigned *xmax = reinterpret_cast<const unsigned *>(a->G);  // (the forward's max |x|)
+      if (!xmax) {
+        HIP_TRY(launch_absmax(a->x, (int64_t)N * C * T * V, L.amax + 3 * kAmaxWords, s));
+        xmax = L.amax + 3 * kAmaxWords;
+      }
+      WgradParams w = make_wgrad_taps(d, L.dZ, a->x, L.slab, C);
+      if (w.bf16 != 3) return fail(STGCN_E_HIP, "bna weight gradient: no split plan");
+      w.f16x2 = 1;
+      w.amax_p = L.amax + 2 * kAmaxWords;
+      w.amax_q = xmax;
+      w.q_mean = mean1;
+      w.q_invstd = invstd1;
+      w.q_g = a->g1;
+      w.q_b = a->b1;
+      HIP_TRY(launch_wgrad_taps(w, s));
+      HIP_TRY(launch_fold_grads(L.slab, w.S, L.fscr, L.bZ, L.ftq, R, C, V, L.dWc, a->dWt, a->dW,
+                                s));
+    } else {
     const float *G = a->G;  // kept fp32 G (f16x2: its max |G| follows it), else recomputed
     const unsigned *amax_g = G ? reinterpret_cast<const unsigned *>(G + (size_t)N * C * T * V)
                                : L.amax + 2 * kAmaxWords;
@@ -956,6 +1033,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_fold_grads(L.slab, w.S, L.fscr, L.bZ, L.ftq, R, C, V, L.dWc,
                               a->dWt, a->dW, s));
+    }
   } else {
   // Temporal conv data-gradient: dZ = conv^T(dU)
   {
@@ -1268,9 +1346,19 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       P.ax[1] = p.w;
       P.an[1] = (int64_t)R * C * 9;
     }
+    if (fold_bna(d)) {  // x in: BN1 in the loader, the joint contraction in the epilogue
+      p.bna = 1;
+      p.sA = c.take<float>((size_t)V * V);
+      float *st = c.take<float>((size_t)4 * C);
+      p.mean1 = st;
+      p.invstd1 = st + C;
+      p.g1 = st + 2 * C;
+      p.b1 = st + 3 * C;
+    }
     conv_tiles(p);
     P.cp[P.ncp++] = p;
-    P.flops = tflops;
+    // (bna: + the joint contraction 2 K C_out T V^2 of the spatial forward, now here)
+    P.flops = tflops + (fold_bna(d) ? 2.0 * K * R * (double)To * V * V * N : 0.0);
   } else if (which == 1) {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * R * To * V);
@@ -1350,6 +1438,13 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       P.an[0] = (int64_t)N * R * To * V;
       P.ax[1] = Z;
       P.an[1] = (int64_t)N * CZ * T * V;
+      if (fold_bna(d)) {  // P = dU A, Q = x with BN1 at staging
+        float *st = c.take<float>((size_t)4 * C);
+        w.q_mean = st;
+        w.q_invstd = st + C;
+        w.q_g = st + 2 * C;
+        w.q_b = st + 3 * C;
+      }
     }
     P.wp = w;
     P.wgrad = true;

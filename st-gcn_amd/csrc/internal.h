@@ -97,6 +97,11 @@ struct ConvGemmParams {
   PrevBn prev;
   double *sd, *sdn;
   float *dA;
+  // bna (with f16x2, V = 18, the folded block's forward; kernels_x3.hip): in[] is
+  // the block input x, BN1 (mean1, invstd1, g1, b1) is applied in the window
+  // loader and the joint contraction with sA in the epilogue -- G is never formed;
+  // amax_in holds max |x| (the fp16 operand bound is formed in the kernel)
+  int bna;
 };
 
 // Weight-gradient GEMM with split-K partial slabs:
@@ -119,6 +124,10 @@ struct WgradParams {
   // power-of-two-scaled P / Q; amax_p / amax_q: device max |P| / max |Q| bits
   int f16x2;
   const unsigned *amax_p, *amax_q;
+  // (f16x2 only) Q is the block input x of the folded block: BN1 (q_mean,
+  // q_invstd, q_g, q_b) is applied while staging Q (0 in padded frames), amax_q
+  // holds max |x|; P is dU contracted with A (dU A), so the product is dWc
+  const float *q_mean, *q_invstd, *q_g, *q_b;
   int x3_mr;  // k_wgrad_x3 row tiles of 64 x_mr rows (2: with f16x2 only; set by plan_wgrad_x3)
 };
 
@@ -164,6 +173,15 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
                                          Dropout drop, hipStream_t s, int du_bf16,
                                          const float *dy_coef, double *cs,
                                          unsigned *amax = nullptr);
+// ... frame-wise (V = 18), also writing dUA = dU A (the folded block without G,
+// capi.hip fold_bna) and the fp16 operand bounds max |dU| (amax), max |dUA| (amaxa)
+hipError_t launch_bn_relu_bwd_apply_fr(const float *dy, const float *U, const float *mean,
+                                       const float *invstd, const float *g, const float *b,
+                                       const double *sg, const double *sgu, float *dU, float *dUA,
+                                       double *sdu, int N, int C, int To, int V, int training,
+                                       Dropout drop, const float *dy_coef, double *cs,
+                                       unsigned *amax, unsigned *amaxa, const float *A,
+                                       hipStream_t s);
 // bf16 path (kernels_bf16.hip): the reference's graphs (V = 18, 25, 50) with
 // the fp32 path's tile plan (FT = kTileCols / V); launch_conv_gemm dispatches here
 // when p.bf16 and conv_bf16_supported(p).
@@ -174,6 +192,8 @@ hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s);
 // data-grad (NQ = 9, 5, 4) for V = 18, 25 over >= 16 channels; launch_conv_gemm
 // dispatches here when p.bf16 == 3 and conv_x3_supported(p).
 bool conv_x3_supported(const ConvGemmParams &p);
+// the bna forward's extra LDS (BN1 table of C channels + A rows) fits
+bool conv_x3_bna_supported(const ConvGemmParams &p);
 size_t conv_x3_wpk_bytes(const ConvGemmParams &p);
 hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s);
 // bf16 temporal-conv GEMMs on the one-plane k_conv_x3 pipeline (kernels_x3.hip)
@@ -216,8 +236,9 @@ hipError_t launch_slab_reduce(const float *slab, int S, int64_t n, float *dst, i
                               int R, int K, int C, hipStream_t s);
 
 // BatchNorm helpers (fp64 accumulation of per-channel sums).
+// (amax, or null: max |x| as float bits, device_common.h block_amax)
 hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, double *sq,
-                           hipStream_t s);
+                           hipStream_t s, unsigned *amax = nullptr);
 hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M,
                               float eps, float momentum, int training, float *rm, float *rv,
                               float *mean_out, float *invstd_out, hipStream_t s);
@@ -225,10 +246,11 @@ hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_
 // yext (or null, 3*C: [cnt | su | xu]): with the ReLU mask m = y > 0 and
 // uhat = (U - mean) * invstd, cnt += sum m, su += sum m * uhat, xu += sum y * uhat
 // (the deferred-dx chain's forward sums)
+// ymax (or null): max y as float bits (block_amax): the next block's operand bound
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
                               double *ysum, double *ysq, Dropout drop, hipStream_t s,
-                              double *yext = nullptr);
+                              double *yext = nullptr, unsigned *ymax = nullptr);
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b,
                                      int N, int C, int L, double *sg, double *sgu, Dropout drop,

@@ -1433,13 +1433,16 @@ static int slice_vec(int L, std::initializer_list<const void *> ptrs) {
       hipLaunchKernelGGL((kern<1>), grid, dim3(256), 0, s, __VA_ARGS__); \
   } while (0)
 
+// (amax, or null: max |x| as float bits, device_common.h block_amax -- the
+// fp16 operand bound of the folded block's GEMMs that read x, capi.hip fold_bna)
 template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_stats(const float *x, int C, int L, double *sum,
-                                                  double *sq) {
+                                                  double *sq, unsigned *amax) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const float *src = x + ((int64_t)n * C + c) * L;
   double s = 0.0, q = 0.0;
+  float m = 0.f;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float v[VEC];
     vld<VEC>(src + i, v);
@@ -1447,14 +1450,16 @@ __global__ __launch_bounds__(256) void k_bn_stats(const float *x, int C, int L, 
     for (int j = 0; j < VEC; ++j) {
       s += (double)v[j];
       q += (double)v[j] * (double)v[j];
+      m = fmaxf(m, fabsf(v[j]));
     }
   }
+  if (amax) block_amax<256>(m, amax);
   block_sum2_atomic<256>(s, q, sum + c, sq + c, red);
 }
 
 hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, double *sq,
-                           hipStream_t s) {
-  STGCN_VEC_LAUNCH(k_bn_stats, slice_vec(L, {x}), dim3(C, N), x, C, L, sum, sq);
+                           hipStream_t s, unsigned *amax) {
+  STGCN_VEC_LAUNCH(k_bn_stats, slice_vec(L, {x}), dim3(C, N), x, C, L, sum, sq, amax);
   return hipGetLastError();
 }
 
@@ -1498,11 +1503,13 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
                                                      const float *invstd, const float *g,
                                                      const float *b, float *y, int N, int C,
                                                      int L, double *ysum, double *ysq,
-                                                     Dropout drop, double *yext) {
+                                                     Dropout drop, double *yext,
+                                                     unsigned *ymax) {
   __shared__ double red[8];
   const int c = blockIdx.x, n0 = blockIdx.y * kBnRows, n1 = min(N, n0 + kBnRows);
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   double s = 0.0, q = 0.0, cnt = 0.0, su = 0.0, xu = 0.0;
+  float ym = 0.f;  // max y (y >= 0): the next block's fp16 operand bound
   for (int n = n0; n < n1; ++n) {
     const int64_t base = ((int64_t)n * C + c) * L;
     for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
@@ -1516,6 +1523,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
         if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
         s += (double)v[j];
         q += (double)v[j] * (double)v[j];
+        ym = fmaxf(ym, v[j]);
         if (yext && t > 0.f) {
           cnt += 1.0;
           su += (double)uh;
@@ -1530,14 +1538,15 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
     block_sum2_atomic<256>(cnt, su, yext + c, yext + C + c, red);
     block_sum2_atomic<256>(xu, 0.0, yext + 2 * C + c, nullptr, red);
   }
+  if (ymax) block_amax<256>(ym, ymax);
 }
 
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
                               double *ysum, double *ysq, Dropout drop, hipStream_t s,
-                              double *yext) {
+                              double *yext, unsigned *ymax) {
   STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, (N + kBnRows - 1) / kBnRows), U,
-                   mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext);
+                   mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext, ymax);
   return hipGetLastError();
 }
 
@@ -1752,6 +1761,105 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
 }
 
 int apply_cols_chunks(int N) { return std::min(N, 4); }
+
+// k_bn_relu_bwd_apply_cols for the folded block without G (capi.hip fold_bna):
+// thread = one frame (V joints) of channel c over the clips of chunk z. Besides
+// dU and its clip-chunk sums it writes the weight gradient's P operand
+//   dUA[n,c,t,w] = sum_v dU[n,c,t,v] A[v][w]   (fp32 fma in v order)
+// and the fp16 operand bounds max |dU| (amax) and max |dUA| (amaxa).
+template <int V>
+__global__ __launch_bounds__(128) void k_bn_relu_bwd_apply_fr(
+    const float *__restrict__ dy, const float *__restrict__ U, const float *mean,
+    const float *invstd, const float *g, const float *b, const double *sg, const double *sgu,
+    float *__restrict__ dU, float *__restrict__ dUA, double *sdu, int N, int C, int To,
+    double invM, Dropout drop, const float *dy_coef, double *__restrict__ cs, unsigned *amax,
+    unsigned *amaxa, const float *A) {
+  static_assert(V % 2 == 0, "frames of whole float2");
+  __shared__ float As[V * V];
+  __shared__ double red[4];
+  for (int i = threadIdx.x; i < V * V; i += blockDim.x) As[i] = A[i];
+  __syncthreads();
+  float om = 0.f, oma = 0.f;
+  const int c = blockIdx.x;
+  const int t = blockIdx.y * 128 + threadIdx.x;
+  const int L = To * V;
+  const int nz = gridDim.z, per = (N + nz - 1) / nz;
+  const int n0 = blockIdx.z * per, n1 = min(N, n0 + per);
+  const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
+  const float mg = (float)(sg[c] * invM), mgu = (float)(sgu[c] * invM);
+  float ca = 0.f, cmd = 0.f, cmu = 0.f, cis = 0.f, cmdn = 0.f;
+  if (dy_coef) {
+    ca = dy_coef[c];
+    cmd = dy_coef[C + c];
+    cmu = dy_coef[2 * C + c];
+    cis = dy_coef[3 * C + c];
+    cmdn = dy_coef[4 * C + c];
+  }
+  double s = 0.0, col[V] = {};
+  if (t < To) {
+    for (int n = n0; n < n1; ++n) {
+      const int64_t base = ((int64_t)n * C + c) * L + (int64_t)t * V;
+      float u[V], d[V], o[V], oa[V];
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        const float2 uu = *reinterpret_cast<const float2 *>(U + base + 2 * i);
+        const float2 dd = *reinterpret_cast<const float2 *>(dy + base + 2 * i);
+        u[2 * i] = uu.x;
+        u[2 * i + 1] = uu.y;
+        d[2 * i] = dd.x;
+        d[2 * i + 1] = dd.y;
+      }
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (dy_coef) {
+          const float tt = (u[j] - mu) * a + be;
+          const float yv = tt > 0.f ? tt : 0.f;
+          d[j] = ca * (d[j] - cmd - (yv - cmu) * cis * cmdn);
+        }
+        if (drop.thresh) d[j] = dropout_keep(drop, base + j) ? d[j] * drop.scale : 0.f;
+        const float uh = (u[j] - mu) * is;
+        const float gg = (u[j] - mu) * a + be > 0.f ? d[j] : 0.f;
+        o[j] = a * (gg - mg - uh * mgu);
+        s += o[j];
+        col[j] += o[j];
+        om = fmaxf(om, fabsf(o[j]));
+      }
+#pragma unroll
+      for (int w = 0; w < V; ++w) oa[w] = o[0] * As[w];
+#pragma unroll
+      for (int v = 1; v < V; ++v)
+#pragma unroll
+        for (int w = 0; w < V; ++w) oa[w] = fmaf(o[v], As[v * V + w], oa[w]);
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        *reinterpret_cast<float2 *>(dU + base + 2 * i) = make_float2(o[2 * i], o[2 * i + 1]);
+        *reinterpret_cast<float2 *>(dUA + base + 2 * i) = make_float2(oa[2 * i], oa[2 * i + 1]);
+        oma = fmaxf(oma, fmaxf(fabsf(oa[2 * i]), fabsf(oa[2 * i + 1])));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) cs[((int64_t)blockIdx.z * C + c) * L + (int64_t)t * V + j] = col[j];
+  }
+  block_amax<128>(om, amax);
+  __syncthreads();  // (block_amax's LDS words are reused by the second call)
+  block_amax<128>(oma, amaxa);
+  block_sum2_atomic<128>(s, 0.0, sdu + c, nullptr, red);
+}
+
+hipError_t launch_bn_relu_bwd_apply_fr(const float *dy, const float *U, const float *mean,
+                                       const float *invstd, const float *g, const float *b,
+                                       const double *sg, const double *sgu, float *dU, float *dUA,
+                                       double *sdu, int N, int C, int To, int V, int training,
+                                       Dropout drop, const float *dy_coef, double *cs,
+                                       unsigned *amax, unsigned *amaxa, const float *A,
+                                       hipStream_t s) {
+  if (V != 18 || !amax || !amaxa || !A) return hipErrorInvalidValue;
+  const double invM = training ? 1.0 / ((double)N * To * V) : 0.0;
+  hipLaunchKernelGGL((k_bn_relu_bwd_apply_fr<18>), dim3(C, (To + 127) / 128, apply_cols_chunks(N)),
+                     dim3(128), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, dUA, sdu, N, C, To,
+                     invM, drop, dy_coef, cs, amax, amaxa, A);
+  return hipGetLastError();
+}
 
 hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const float *mean,
                                          const float *invstd, const float *g, const float *b,

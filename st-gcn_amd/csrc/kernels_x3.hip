@@ -420,12 +420,111 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
   }
 }
 
+// ---------------------------------------------------------------------------
+// The folded block's forward without G (capi.hip fold_bna; north star N1: the
+// SpatialConv joint contraction inside the temporal conv kernel). With one
+// adjacency partition the joint contraction commutes with the folded conv's
+// channel and tap mixing (st_graphconv.py:99, :148-150):
+//   U[o,t,v] = sum_q sum_c Wc[o,c,q] G[c,t',v] + BT[o,t,v]
+//            = sum_w A[v][w] U'[o,t,w] + BT[o,t,v],
+//   U'[o,t,w] = sum_q sum_c Wc[o,c,q] xhat[c,t',w],   xhat = BN1(x) (0 in padded frames),
+// so the window loader reads x and applies BN1 per channel (a [mu | a | be] table
+// in LDS) before the fp16 split, and the epilogue contracts each (row, frame) of
+// the tile with A (rows of A in LDS, 18 fp32 fma per output, fixed order) before
+// the bias table, the BN2 statistics and the stores: G never exists.
+// fp16 operand bound: |xhat| <= max_c |a_c| (M + |mu_c|) + |be_c|, M = max |x|.
+// ---------------------------------------------------------------------------
+constexpr int kBnaAr = 18 * 20;  // A[v][w], rows padded to 20 floats
+
+__host__ __device__ constexpr int bna_cpad(int C) { return (C + 15) & ~15; }
+// (+ 8 floats: block_max_all's scratch)
+__host__ __device__ constexpr int bna_extra_bytes(int C) { return (3 * bna_cpad(C) + kBnaAr + 8) * 4; }
+
+__device__ __forceinline__ int f16x2_se_bits(unsigned bits) {
+  const int e = (int)(bits >> 23) & 0xff;
+  const int se = e == 0 ? 0 : 140 - e;
+  return se < -100 ? -100 : (se > 100 ? 100 : se);
+}
+
+// Block-wide max of m >= 0 (NT threads; red: NT / 64 floats of LDS); every
+// thread gets the result (two barriers)
+template <int NT>
+__device__ __forceinline__ float block_max_all(float m, float *red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float b = red[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) b = fmaxf(b, red[i]);
+  __syncthreads();
+  return b;
+}
+
+// |BN1(x)| bound of channel c (0 past C): |a| (M + |mu|) + |be|
+__device__ __forceinline__ float bn1_bound(const ConvGemmParams &p, int c, float M, float &mu,
+                                           float &a, float &be) {
+  mu = a = be = 0.f;
+  if (c >= p.C) return 0.f;
+  mu = p.mean1[c];
+  a = p.invstd1[c] * p.g1[c];
+  be = p.b1[c];
+  return fabsf(a) * (M + fabsf(mu)) + fabsf(be);
+}
+
+// The tile's output rows x frames in the row-major LDS image (acc_to_img),
+// each (row, frame) replaced by its joint contraction with A: out[v] =
+// sum_w A[v][w] in[w] (fp32 fma in w order). ar: A rows padded to 20.
+template <int ROWS>
+__device__ __forceinline__ void bna_contract(float *img, const float *ar) {
+  constexpr int V = 18, FT = kTileCols / V, NPAIR = ROWS * FT, S = (NPAIR + 511) / 512;
+  float in[S][V];
+  int base[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int q = threadIdx.x + 512 * s, r = q % ROWS, f = q / ROWS;
+    base[s] = q < NPAIR ? r * kEpiPitch + f * V : -1;
+    const float *src = img + (base[s] >= 0 ? base[s] : 0);
+#pragma unroll
+    for (int i = 0; i < V / 2; ++i) {
+      const float2 t = *reinterpret_cast<const float2 *>(src + 2 * i);
+      in[s][2 * i] = t.x;
+      in[s][2 * i + 1] = t.y;
+    }
+  }
+  // one row of A live at a time (a rolled loop: unrolled, the compiler hoists
+  // every row's LDS reads and spills); each output written in place as formed
+#pragma unroll 1
+  for (int v = 0; v < V; ++v) {
+    float av[20];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const float4 t = *reinterpret_cast<const float4 *>(ar + v * 20 + 4 * i);
+      av[4 * i] = t.x;
+      av[4 * i + 1] = t.y;
+      av[4 * i + 2] = t.z;
+      av[4 * i + 3] = t.w;
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      float o = av[0] * in[s][0];
+#pragma unroll
+      for (int w = 1; w < V; ++w) o = fmaf(av[w], in[s][w], o);
+      if (base[s] >= 0) img[base[s] + v] = o;
+    }
+  }
+}
+
 // IB (NPL = 1 only): the input is stored in bf16 (p.in_bf16; a template switch so
 // the staging code of the fp32-input kernels is unchanged)
 // SPB (V = 18, NPL >= 2): the fused SpatialConv backward epilogue (spb_epilogue)
-template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false, bool SPB = false>
+// BNA (V = 18, NPL = 2): the folded forward from x (BN1 in the loader, A in the
+// epilogue; see bna_contract)
+template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false, bool SPB = false,
+          bool BNA = false>
 __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
   using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>;
+  static_assert(!BNA || (V == 18 && NPL == 2 && !SPB), "bna: the folded fp16-split forward");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   char *const wbuf0 = lds, *const win0 = lds + G::NWB * G::WST;
@@ -459,7 +558,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   }
   // window staging items (octet o, position pp), dealt over all 8 waves
   unsigned voff[G::IPT];
-  int loff[G::IPT];
+  int loff[G::IPT], ioct[G::IPT];
 #pragma unroll
   for (int k = 0; k < G::IPT; ++k) {
     const int e = k * 512 + tid;
@@ -468,6 +567,28 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     const bool ok = e < G::NIT && g >= 0 && g < cstride;
     voff[k] = ok ? (unsigned)(o * 8 * cstride + g) * 4u : kOOB;
     loff[k] = e < G::NIT ? (pp * G::SLOTS + o) * 16 : -1;
+    ioct[k] = o;
+  }
+  // BNA: the BN1 table [mu | a | be] (Cp entries each) and the rows of A past
+  // the kernel's own LDS plan, and the fp16 operand bound of BN1(x)
+  const int Cp = nchunks * G::CK;
+  float *const btab = smem + G::LDS / 4, *const arow = btab + 3 * Cp;
+  float bna_bound = 0.f;
+  if constexpr (BNA) {
+    const float M = __builtin_bit_cast(float, amax_read(p.amax_in));
+    float bm = 0.f;
+    for (int c = tid; c < Cp; c += 512) {
+      float mu, a, be;
+      bm = fmaxf(bm, bn1_bound(p, c, M, mu, a, be));
+      btab[c] = mu;
+      btab[Cp + c] = a;
+      btab[2 * Cp + c] = be;
+    }
+    for (int i = tid; i < kBnaAr; i += 512) {
+      const int v = i / 20, w = i - v * 20;
+      arow[i] = w < 18 ? p.sA[v * 18 + w] : 0.f;
+    }
+    bna_bound = block_max_all<512>(bm, arow + kBnaAr);  // (scratch past A; barriers inside)
   }
   float st[G::IPT][8];
   // Window loads as inline asm too (the compiler neither waits for them nor
@@ -479,7 +600,8 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   static_assert(!IB || NPL == 1, "bf16 input: one-plane kernels");
   constexpr bool inb = IB;
   // NPL = 2: the window's power-of-two scale (f16x2_se of max |in|)
-  const int in_se = NPL == 2 ? f16x2_se(p.amax_in) : 0;
+  const int in_se = BNA ? f16x2_se_bits(__builtin_bit_cast(unsigned, bna_bound))
+                        : (NPL == 2 ? f16x2_se(p.amax_in) : 0);
   const float in_scale = pow2f(in_se);
   if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid < kAmaxSlots)  // (slot 0: the bound)
     p.amax_keep[tid * kAmaxStride] = tid == 0 ? amax_read(p.amax_in) : 0u;
@@ -513,7 +635,9 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
                        : "memory");
     }
   };
-  auto write_img = [&](char *win) {
+  auto write_img = [&](char *win, int chunk) {
+    // (BNA: chunk nchunks is the pipeline's zero tail, never read: any table row)
+    const int cch = min(chunk, nchunks - 1) * G::CK;
 #pragma unroll
     for (int k = 0; k < G::IPT; ++k)
       if (NPL == 1 && loff[k] >= 0) {  // bf16 operands: one rounded plane
@@ -533,11 +657,30 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
       } else if (NPL == 2 && loff[k] >= 0) {  // fp16 (h, l) planes of the scaled input
         const float sc = in_scale;
+        float xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = st[k][j];
+        if constexpr (BNA) {  // BN1 of the item's 8 channels; 0 in the padded frames
+          const float *tb = btab + cch + ioct[k] * 8;
+          float mu[8], a[8], be[8];
+#pragma unroll
+          for (int h4 = 0; h4 < 2; ++h4) {
+            const float4 m4 = *reinterpret_cast<const float4 *>(tb + 4 * h4);
+            const float4 a4 = *reinterpret_cast<const float4 *>(tb + Cp + 4 * h4);
+            const float4 b4 = *reinterpret_cast<const float4 *>(tb + 2 * Cp + 4 * h4);
+            mu[4 * h4] = m4.x; mu[4 * h4 + 1] = m4.y; mu[4 * h4 + 2] = m4.z; mu[4 * h4 + 3] = m4.w;
+            a[4 * h4] = a4.x; a[4 * h4 + 1] = a4.y; a[4 * h4 + 2] = a4.z; a[4 * h4 + 3] = a4.w;
+            be[4 * h4] = b4.x; be[4 * h4 + 1] = b4.y; be[4 * h4 + 2] = b4.z; be[4 * h4 + 3] = b4.w;
+          }
+          const bool live = voff[k] != kOOB;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xv[j] = live ? (xv[j] - mu[j]) * a[j] + be[j] : 0.f;
+        }
         uint4 h, l;
-        splith2(st[k][0] * sc, st[k][1] * sc, h.x, l.x);
-        splith2(st[k][2] * sc, st[k][3] * sc, h.y, l.y);
-        splith2(st[k][4] * sc, st[k][5] * sc, h.z, l.z);
-        splith2(st[k][6] * sc, st[k][7] * sc, h.w, l.w);
+        splith2(xv[0] * sc, xv[1] * sc, h.x, l.x);
+        splith2(xv[2] * sc, xv[3] * sc, h.y, l.y);
+        splith2(xv[4] * sc, xv[5] * sc, h.z, l.z);
+        splith2(xv[6] * sc, xv[7] * sc, h.w, l.w);
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
         *reinterpret_cast<uint4 *>(win + loff[k] + 32) = l;
       } else if (loff[k] >= 0) {
@@ -635,7 +778,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     if (d < nsteps) dma_w(d, d);
   load_img(0);
   wait_img<0>(st);
-  write_img(win0);
+  write_img(win0, 0);
   for (int c = 0; c < nchunks; ++c) {
     const char *win = win0 + (G::NWIN == 2 ? (c & 1) * G::IMG : 0);
 #pragma unroll
@@ -757,7 +900,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         wait_img<(G::NG - 1) * G::DPWMIN>(st);
         if (G::NWIN == 1)  // single window: every wave is done reading chunk c's
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        write_img(win0 + (G::NWIN == 2 ? ((c + 1) & 1) * G::IMG : 0));
+        write_img(win0 + (G::NWIN == 2 ? ((c + 1) & 1) * G::IMG : 0), c + 1);
       }
     }
   }
@@ -788,6 +931,10 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
       for (int j = 0; j < 2; ++j)
         acc_to_img(smem, acc[rb * 2 + j], mi * 32 * MR + rb * 32, (nj0 + j) * 32);
     __syncthreads();
+    if constexpr (BNA) {  // U' -> U = A U' per (row, frame), in place
+      bna_contract<G::ROWS>(smem, arow);
+      __syncthreads();
+    }
     // (one-plane bf16 path: the output may be stored in bf16, p.out_bf16 -- the
     // data gradient dZ of capi.hip dz_bf16)
     conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS, NPL == 1>(
@@ -868,6 +1015,13 @@ bool conv_x3_supported(const ConvGemmParams &p) {
   return p.s_in == 1 && (p.NQ == 9 || p.NQ == 5 || p.NQ == 4);
 }
 
+bool conv_x3_bna_supported(const ConvGemmParams &p) {
+  if (p.V != 18 || p.NQ != 9 || p.s_out != 1 || p.spb || !conv_x3_supported(p)) return false;
+  // the largest plan of the forward instances (128-row tiles, stride 2) + the table
+  constexpr int lds = ConvX3Geo<9, 3, 18, 2, 2, 2>::LDS;
+  return lds + bna_extra_bytes(p.C) <= 160 * 1024;
+}
+
 size_t conv_x3_wpk_bytes(const ConvGemmParams &p) {
   return (size_t)p.n_rtiles * ((p.C + 15) / 16) * 3 * p.NQ * 16 * 64 * 2;
 }
@@ -891,6 +1045,15 @@ static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
       constexpr int lds_spb = lds > kSpbLds ? lds : kSpbLds;
       hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL, false, true>), dim3(nblk), dim3(512),
                          lds_spb, s, p);
+      return true;
+    }
+  }
+  if constexpr (V == 18 && NPL == 2 && NQ == 9) {
+    if (p.bna) {  // the folded forward from x (BN1 in the loader, A in the epilogue)
+      const int lds_bna = lds + bna_extra_bytes(p.C);
+      if (lds_bna > 160 * 1024) return false;
+      hipLaunchKernelGGL((k_conv_x3<NQ, TG, V, SIN, MR, NPL, false, false, true>), dim3(nblk),
+                         dim3(512), lds_bna, s, p);
       return true;
     }
   }
@@ -966,6 +1129,9 @@ hipError_t launch_conv_x3(const ConvGemmParams &p, hipStream_t s) {
   if (p.f16x2 && (!p.amax_in || !p.amax_w)) return hipErrorInvalidValue;
   if (p.spb && (p.V != 18 || p.s_in != 1 || p.FT != kTileCols / 18 || !p.sx || !p.sA ||
                 !p.mean1 || !p.invstd1 || !p.g1 || !p.b1 || !p.sd || !p.sdn || !p.dA))
+    return hipErrorInvalidValue;
+  if (p.bna && (!p.f16x2 || !conv_x3_bna_supported(p) || !p.sA || !p.mean1 || !p.invstd1 ||
+                !p.g1 || !p.b1))
     return hipErrorInvalidValue;
   return launch_conv_planes(p, p.f16x2 ? 2 : 3, s);
 }
@@ -1046,13 +1212,17 @@ struct WgX3Geo {
 // flop: the kernel is bound by the L2 -> LDS staging, not the matrix rate), one
 // accumulator per block (the three products summed in one fp32 chain, small
 // ones first)
-template <int V, int SIN, int NPL = 3, int MR = 1>
+// QBN (NPL = 2, the folded block without G, capi.hip fold_bna): Q is the block
+// input x and BN1 is applied while staging it (a [mu, a, be] row per channel of
+// the tile in LDS past the plan; 0 in padded frames), P is dU A, so
+//   sum_{t,w} (dU A)[o,t,w] BN1(x)[c,t',w] = sum_{t,v} dU[o,t,v] G[c,t',v] = dWc;
+// Q's fp16 bound is |BN1(x)| <= max_c |a_c| (M + |mu_c|) + |be_c|, M = max |x|.
+template <int V, int SIN, int NPL = 3, int MR = 1, bool QBN = false>
 __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
   using G = WgX3Geo<V, SIN, NPL, MR>;
   static_assert(MR == 1 || NPL == 2, "128-row tiles on the fp16 splits only");
+  static_assert(!QBN || NPL == 2, "BN1 staging: the fp16 splits");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int p_se = NPL == 2 ? f16x2_se(p.amax_p) : 0, q_se = NPL == 2 ? f16x2_se(p.amax_q) : 0;
-  const float p_scale = pow2f(p_se), q_scale = pow2f(q_se);
   char *lds = reinterpret_cast<char *>(smem);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1063,6 +1233,26 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
   const int rt = bid % p.n_rtiles;
   const int split = bid / p.n_rtiles;
   const int r0 = rt * G::ROWS, c0 = jt * G::CB;
+  float *const qtab = smem + G::LDS / 4;  // QBN: [CB][4] = (mu, a, be, 0) of channels c0..
+  int q_se = NPL == 2 ? f16x2_se(p.amax_q) : 0;
+  if constexpr (QBN) {
+    const float M = __builtin_bit_cast(float, amax_read(p.amax_q));
+    float bm = 0.f;
+    for (int c = tid; c < p.C; c += 512) {
+      const float a = p.q_invstd[c] * p.q_g[c];
+      bm = fmaxf(bm, fabsf(a) * (M + fabsf(p.q_mean[c])) + fabsf(p.q_b[c]));
+    }
+    if (tid < G::CB) {
+      const int c = c0 + tid;
+      const bool ok = c < p.C;
+      *reinterpret_cast<float4 *>(qtab + 4 * tid) =
+          make_float4(ok ? p.q_mean[c] : 0.f, ok ? p.q_invstd[c] * p.q_g[c] : 0.f,
+                      ok ? p.q_b[c] : 0.f, 0.f);
+    }
+    q_se = f16x2_se_bits(__builtin_bit_cast(unsigned, block_max_all<512>(bm, qtab + 4 * G::CB)));
+  }
+  const int p_se = NPL == 2 ? f16x2_se(p.amax_p) : 0;
+  const float p_scale = pow2f(p_se), q_scale = pow2f(q_se);
   const int mi = wave & 1, tq = wave >> 1;
   const int q0 = tq ? 1 + 2 * tq : 0;
   const int total = p.N * p.n_mtiles;
@@ -1090,7 +1280,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
                      : (row * G::PPITCH + gfr[k] * G::Vp + gv0[k]) * 2;
   }
   float st[G::GPT][4];
+  unsigned qval = 0;  // QBN: bit 2k + j = pair j of staging group k lies inside the clip
   auto load_item = [&](int item) {
+    if constexpr (QBN) qval = 0;
     const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * G::FT;
     const __amdgpu_buffer_rsrc_t rp = make_rsrc(p.P + (int64_t)n * p.p_bstride, p.p_bstride);
     const __amdgpu_buffer_rsrc_t rq = make_rsrc(p.Q + (int64_t)n * p.q_bstride, p.q_bstride);
@@ -1115,6 +1307,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const unsigned off = gv0[k] + 2 * j < V ? base + 8u * j : kOOB;
+        if constexpr (QBN) qval |= (base != kOOB && gv0[k] + 2 * j < V) ? 1u << (2 * k + j) : 0u;
         const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
         st[k][2 * j] = __builtin_bit_cast(float, (unsigned)v2[0]);
         st[k][2 * j + 1] = __builtin_bit_cast(float, (unsigned)v2[1]);
@@ -1132,9 +1325,18 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         const int pl = isq[k] ? G::QPL : G::PPL;
         if constexpr (NPL == 2) {
           const float sc = isq[k] ? q_scale : p_scale;
+          float xv[4] = {st[k][0], st[k][1], st[k][2], st[k][3]};
+          if constexpr (QBN) {
+            if (isq[k]) {  // BN1(x) of the group's channel; 0 outside the clip
+              const float4 t = *reinterpret_cast<const float4 *>(qtab + 4 * grow[k]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                xv[e] = (qval >> (2 * k + e / 2)) & 1u ? (xv[e] - t.x) * t.y + t.z : 0.f;
+            }
+          }
           uint2 h, l;
-          splith2(st[k][0] * sc, st[k][1] * sc, h.x, l.x);
-          splith2(st[k][2] * sc, st[k][3] * sc, h.y, l.y);
+          splith2(xv[0] * sc, xv[1] * sc, h.x, l.x);
+          splith2(xv[2] * sc, xv[3] * sc, h.y, l.y);
           *reinterpret_cast<uint2 *>(dst) = h;
           *reinterpret_cast<uint2 *>(dst + pl) = l;
         } else {
@@ -1306,6 +1508,25 @@ bool plan_wgrad_x3(WgradParams &w, bool f16x2) {
 hipError_t launch_wgrad_x3(const WgradParams &p0, hipStream_t s) {
   if (p0.bf16 != 3 || p0.V != 18 || (p0.s_in != 1 && p0.s_in != 2)) return hipErrorInvalidValue;
   const int nblk = p0.n_rtiles * p0.n_jtiles * p0.S;
+  if (p0.f16x2 && p0.q_mean) {  // 2-way fp16 splits, Q = x with BN1 at staging (QBN)
+    const WgradParams &p = p0;
+    if (!p.amax_p || !p.amax_q || !p.q_invstd || !p.q_g || !p.q_b) return hipErrorInvalidValue;
+    if (p.x3_mr == 2 && p.R % 128 != 0) return hipErrorInvalidValue;
+    constexpr int ex = (4 * 32 + 8) * 4;  // the Q channel table + block_max_all's scratch
+    if (p.s_in == 1 && p.x3_mr == 2)
+      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 2, true>), dim3(nblk), dim3(512),
+                         (WgX3Geo<18, 1, 2, 2>::LDS + ex), s, p);
+    else if (p.s_in == 1)
+      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 1, true>), dim3(nblk), dim3(512),
+                         (WgX3Geo<18, 1, 2>::LDS + ex), s, p);
+    else if (p.x3_mr == 2)
+      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 2, true>), dim3(nblk), dim3(512),
+                         (WgX3Geo<18, 2, 2, 2>::LDS + ex), s, p);
+    else
+      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 1, true>), dim3(nblk), dim3(512),
+                         (WgX3Geo<18, 2, 2>::LDS + ex), s, p);
+    return hipGetLastError();
+  }
   if (p0.f16x2) {  // 2-way fp16 splits (NPL = 2)
     if (!p0.amax_p || !p0.amax_q) return hipErrorInvalidValue;
     const WgradParams &p = p0;

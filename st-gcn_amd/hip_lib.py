@@ -21,7 +21,7 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
     import sys
     print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
-ABI_VERSION = 6
+ABI_VERSION = 7
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -29,6 +29,14 @@ F_F16X2 = 8     # ABI 6, with F_F32X3: the folded GEMMs as 2-way fp16 splits (sc
 # stgcn_block_plan bits (ABI 6)
 PLAN_FOLD, PLAN_SP_FWD_FUSED, PLAN_SP_BWD_FUSED, PLAN_ACT_BF16 = 1, 2, 4, 8
 PLAN_WSP_SPLIT, PLAN_TCONV_SPLIT, PLAN_TWGRAD_SPLIT, PLAN_F16X2 = 16, 32, 64, 128
+PLAN_FOLD_NO_G = 256
+# ABI 7: a y_stats / x_stats block: 5 * C doubles, then STATS_AMAX_WORDS uint32 (max |y|)
+STATS_AMAX_WORDS = 2048
+
+
+def y_stats_doubles(C):
+    """float64 elements of a y_stats block of C channels (STGCN_Y_STATS_BYTES / 8)"""
+    return 5 * C + STATS_AMAX_WORDS // 2
 
 _c_int = ctypes.c_int32
 _c_float = ctypes.c_float

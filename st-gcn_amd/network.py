@@ -12,6 +12,7 @@ forward raises.
 import torch
 import torch.nn as nn
 
+from . import hip_lib
 from .fused import ChainCtx, Link, SpatialConvFn, StgcnBlockFn, StgcnResBlockFn
 
 
@@ -147,9 +148,11 @@ class SpatialTemporalConv(nn.Module):
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:
             # not with dropout on that output, nor for the residual block)
-            # (y_stats: [sum | sumsq | cnt | su | xu] per output channel, ABI 5)
-            cc = ChainCtx(y_stats=torch.empty(5 * self.temporalConv.out_channels,
-                                              device=x.device, dtype=torch.float64),
+            # (y_stats: [sum | sumsq | cnt | su | xu] per output channel, ABI 5, then
+            # the max |y| words, ABI 7)
+            cc = ChainCtx(y_stats=torch.empty(
+                              hip_lib.y_stats_doubles(self.temporalConv.out_channels),
+                              device=x.device, dtype=torch.float64),
                           out_link=None if (self.residual or drop > 0) else Link())
             if chain.y is not None and x is chain.y and x._version == chain.y_version:
                 cc.x_stats = chain.y_stats

@@ -54,6 +54,7 @@ def test_f16x2_block_random(pkg, case):
     plan = _plan(pkg, x, C_out, stride)
     hl = pkg.hip_lib
     assert plan & hl.PLAN_FOLD and plan & hl.PLAN_F16X2, plan
+    assert plan & hl.PLAN_FOLD_NO_G, plan  # (N1: G is never formed)
     ref = _run_hip(pkg, arrays, x, g, gemm="f32x3")
     assert not torch.equal(got["y"], ref["y"]), "fp16-split forward did not run"
     assert not torch.equal(got["grad.temporalConv.weight"], ref["grad.temporalConv.weight"])
@@ -80,6 +81,15 @@ def test_f16x2_full_size_block(pkg):
     got = _check(pkg, arrays, x, g)
     for k, v in got.items():
         assert torch.isfinite(v).all(), k
+
+
+def test_f16x2_backward_without_kept_bound(pkg, monkeypatch):
+    """A caller that keeps nothing between forward and backward (stgcn_fwd_args_t
+    .G null): the backward forms max |x| itself (one pass over x) for the
+    weight gradient's operand scale; same fp32 gate."""
+    monkeypatch.setattr(pkg.fused, "_keep_g", lambda ctx, x, desc: None)
+    arrays, x, g = _random_case(pkg, 64, 128, 2, 18, 1, 2, 29, seed=6)
+    _check(pkg, arrays, x, g)
 
 
 def test_f16x2_l8_shape_block(pkg):
