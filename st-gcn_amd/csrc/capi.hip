@@ -1438,13 +1438,14 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       P.an[0] = (int64_t)N * R * To * V;
       P.ax[1] = Z;
       P.an[1] = (int64_t)N * CZ * T * V;
-      if (fold_bna(d)) {  // P = dU A, Q = x with BN1 at staging
-        float *st = c.take<float>((size_t)4 * C);
-        w.q_mean = st;
-        w.q_invstd = st + C;
-        w.q_g = st + 2 * C;
-        w.q_b = st + 3 * C;
-      }
+    }
+    if (fold_bna(d) && w.bf16 == 3) {  // P = dU A, Q = x with BN1 at staging
+      // (taken whether or not scratch is given: the size query must match)
+      float *st = c.take<float>((size_t)4 * C);
+      w.q_mean = st;
+      w.q_invstd = st + C;
+      w.q_g = st + 2 * C;
+      w.q_b = st + 3 * C;
     }
     P.wp = w;
     P.wgrad = true;
