@@ -1762,27 +1762,34 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
 
 int apply_cols_chunks(int N) { return std::min(N, 4); }
 
-// k_bn_relu_bwd_apply_cols for the folded block without G (capi.hip fold_bna):
-// thread = one frame (V joints) of channel c over the clips of chunk z. Besides
-// dU and its clip-chunk sums it writes the weight gradient's P operand
-//   dUA[n,c,t,w] = sum_v dU[n,c,t,v] A[v][w]   (fp32 fma in v order)
-// and the fp16 operand bounds max |dU| (amax) and max |dUA| (amaxa).
+// k_bn_relu_bwd_apply_cols for the folded block without G (capi.hip fold_bna).
+// Block = (channel c, a tile of FR = 28 frames, clip chunk z), 256 threads; per
+// clip of the chunk:
+//   1. thread i < 252 takes joints 2i, 2i + 1 of the tile's 504 positions (fp32
+//      pairs, coalesced): dU as k_bn_relu_bwd_apply_cols forms it, stored, its
+//      clip-chunk sums in registers, and dU into an LDS row (double-buffered);
+//   2. thread i forms dUA at positions e = i, i + 256 (< 504), frame e / V,
+//      joint w = e % V:  dUA[n,c,t,w] = sum_v dU[n,c,t,v] A[v][w]  (fp32 fma in v
+//      order, its two columns of A in registers), stored as coalesced words:
+// the weight gradient's P operand. Also the fp16 operand bounds max |dU|
+// (amax) and max |dUA| (amaxa). One barrier per clip.
+constexpr int kFrTile = 28;
 template <int V>
-__global__ __launch_bounds__(128) void k_bn_relu_bwd_apply_fr(
+__global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_fr(
     const float *__restrict__ dy, const float *__restrict__ U, const float *mean,
     const float *invstd, const float *g, const float *b, const double *sg, const double *sgu,
     float *__restrict__ dU, float *__restrict__ dUA, double *sdu, int N, int C, int To,
     double invM, Dropout drop, const float *dy_coef, double *__restrict__ cs, unsigned *amax,
     unsigned *amaxa, const float *A) {
-  static_assert(V % 2 == 0, "frames of whole float2");
-  __shared__ float As[V * V];
-  __shared__ double red[4];
-  for (int i = threadIdx.x; i < V * V; i += blockDim.x) As[i] = A[i];
-  __syncthreads();
-  float om = 0.f, oma = 0.f;
+  static_assert(V % 2 == 0, "whole pairs per frame");
+  constexpr int NP = kFrTile * V;  // positions of a tile
+  static_assert(NP / 2 <= 256 && NP <= 512, "one pair per thread, two outputs per thread");
+  __shared__ float ob[2][NP];
+  __shared__ double red[8];
+  const int tid = threadIdx.x;
   const int c = blockIdx.x;
-  const int t = blockIdx.y * 128 + threadIdx.x;
-  const int L = To * V;
+  const int f0 = blockIdx.y * kFrTile, nf = min(kFrTile, To - f0);
+  const int L = To * V, np = nf * V;
   const int nz = gridDim.z, per = (N + nz - 1) / nz;
   const int n0 = blockIdx.z * per, n1 = min(N, n0 + per);
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
@@ -1795,55 +1802,72 @@ __global__ __launch_bounds__(128) void k_bn_relu_bwd_apply_fr(
     cis = dy_coef[3 * C + c];
     cmdn = dy_coef[4 * C + c];
   }
-  double s = 0.0, col[V] = {};
-  if (t < To) {
-    for (int n = n0; n < n1; ++n) {
-      const int64_t base = ((int64_t)n * C + c) * L + (int64_t)t * V;
-      float u[V], d[V], o[V], oa[V];
+  // this thread's two output positions of dUA and their columns of A
+  const int e0 = tid, e1 = tid + 256;
+  const int w0 = e0 % V, w1 = e1 % V, fr0 = e0 / V, fr1 = e1 / V;
+  float a0[V], a1[V];
 #pragma unroll
-      for (int i = 0; i < V / 2; ++i) {
-        const float2 uu = *reinterpret_cast<const float2 *>(U + base + 2 * i);
-        const float2 dd = *reinterpret_cast<const float2 *>(dy + base + 2 * i);
-        u[2 * i] = uu.x;
-        u[2 * i + 1] = uu.y;
-        d[2 * i] = dd.x;
-        d[2 * i + 1] = dd.y;
-      }
+  for (int v = 0; v < V; ++v) {
+    a0[v] = A[v * V + w0];
+    a1[v] = A[v * V + w1];
+  }
+  const int pp = 2 * tid;  // this thread's pair of phase 1
+  const bool pok = pp < np;
+  float om = 0.f, oma = 0.f;
+  double s = 0.0, col0 = 0.0, col1 = 0.0;
+  for (int n = n0; n < n1; ++n) {
+    const int64_t base = ((int64_t)n * C + c) * L + (int64_t)f0 * V;
+    float *obn = ob[(n - n0) & 1];
+    if (pok) {
+      const float2 uu = *reinterpret_cast<const float2 *>(U + base + pp);
+      const float2 dd = *reinterpret_cast<const float2 *>(dy + base + pp);
+      float u[2] = {uu.x, uu.y}, d[2] = {dd.x, dd.y}, o[2];
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
+      for (int j = 0; j < 2; ++j) {
         if (dy_coef) {
           const float tt = (u[j] - mu) * a + be;
           const float yv = tt > 0.f ? tt : 0.f;
           d[j] = ca * (d[j] - cmd - (yv - cmu) * cis * cmdn);
         }
-        if (drop.thresh) d[j] = dropout_keep(drop, base + j) ? d[j] * drop.scale : 0.f;
+        if (drop.thresh) d[j] = dropout_keep(drop, base + pp + j) ? d[j] * drop.scale : 0.f;
         const float uh = (u[j] - mu) * is;
         const float gg = (u[j] - mu) * a + be > 0.f ? d[j] : 0.f;
         o[j] = a * (gg - mg - uh * mgu);
         s += o[j];
-        col[j] += o[j];
         om = fmaxf(om, fabsf(o[j]));
       }
-#pragma unroll
-      for (int w = 0; w < V; ++w) oa[w] = o[0] * As[w];
-#pragma unroll
-      for (int v = 1; v < V; ++v)
-#pragma unroll
-        for (int w = 0; w < V; ++w) oa[w] = fmaf(o[v], As[v * V + w], oa[w]);
-#pragma unroll
-      for (int i = 0; i < V / 2; ++i) {
-        *reinterpret_cast<float2 *>(dU + base + 2 * i) = make_float2(o[2 * i], o[2 * i + 1]);
-        *reinterpret_cast<float2 *>(dUA + base + 2 * i) = make_float2(oa[2 * i], oa[2 * i + 1]);
-        oma = fmaxf(oma, fmaxf(fabsf(oa[2 * i]), fabsf(oa[2 * i + 1])));
-      }
+      col0 += o[0];
+      col1 += o[1];
+      *reinterpret_cast<float2 *>(dU + base + pp) = make_float2(o[0], o[1]);
+      *reinterpret_cast<float2 *>(obn + pp) = make_float2(o[0], o[1]);
     }
+    __syncthreads();  // (double buffer: the other row is free since the last barrier)
+    if (e0 < np) {
+      const float *r = obn + fr0 * V;
+      float t = r[0] * a0[0];
 #pragma unroll
-    for (int j = 0; j < V; ++j) cs[((int64_t)blockIdx.z * C + c) * L + (int64_t)t * V + j] = col[j];
+      for (int v = 1; v < V; ++v) t = fmaf(r[v], a0[v], t);
+      dUA[base + e0] = t;
+      oma = fmaxf(oma, fabsf(t));
+    }
+    if (e1 < np) {
+      const float *r = obn + fr1 * V;
+      float t = r[0] * a1[0];
+#pragma unroll
+      for (int v = 1; v < V; ++v) t = fmaf(r[v], a1[v], t);
+      dUA[base + e1] = t;
+      oma = fmaxf(oma, fabsf(t));
+    }
   }
-  block_amax<128>(om, amax);
+  if (pok) {
+    double *dst = cs + ((int64_t)blockIdx.z * C + c) * L + (int64_t)f0 * V + pp;
+    dst[0] = col0;
+    dst[1] = col1;
+  }
+  block_amax<256>(om, amax);
   __syncthreads();  // (block_amax's LDS words are reused by the second call)
-  block_amax<128>(oma, amaxa);
-  block_sum2_atomic<128>(s, 0.0, sdu + c, nullptr, red);
+  block_amax<256>(oma, amaxa);
+  block_sum2_atomic<256>(s, 0.0, sdu + c, nullptr, red);
 }
 
 hipError_t launch_bn_relu_bwd_apply_fr(const float *dy, const float *U, const float *mean,
@@ -1855,33 +1879,10 @@ hipError_t launch_bn_relu_bwd_apply_fr(const float *dy, const float *U, const fl
                                        hipStream_t s) {
   if (V != 18 || !amax || !amaxa || !A) return hipErrorInvalidValue;
   const double invM = training ? 1.0 / ((double)N * To * V) : 0.0;
-  hipLaunchKernelGGL((k_bn_relu_bwd_apply_fr<18>), dim3(C, (To + 127) / 128, apply_cols_chunks(N)),
-                     dim3(128), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, dUA, sdu, N, C, To,
-                     invM, drop, dy_coef, cs, amax, amaxa, A);
-  return hipGetLastError();
-}
-
-hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const float *mean,
-                                         const float *invstd, const float *g, const float *b,
-                                         const double *sg, const double *sgu, float *dU,
-                                         double *sdu, int N, int C, int L, int training,
-                                         Dropout drop, hipStream_t s, int du_bf16,
-                                         const float *dy_coef, double *cs, unsigned *amax) {
-  const double invM = training ? 1.0 / ((double)N * L) : 0.0;
-  // (whole-row vectors: every row start VEC-aligned needs L % VEC == 0)
-  int vec = slice_vec(L, {dy, U, dU});
-  const int nz = apply_cols_chunks(N);
-#define COLS_LAUNCH(VV)                                                                     \
-  hipLaunchKernelGGL((k_bn_relu_bwd_apply_cols<VV>), dim3(C, (L + 256 * VV - 1) / (256 * VV), nz), \
-                     dim3(256), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, sdu, N, C, L,  \
-                     invM, drop, du_bf16, dy_coef, cs, amax)
-  if (vec == 4)
-    COLS_LAUNCH(4);
-  else if (vec == 2)
-    COLS_LAUNCH(2);
-  else
-    COLS_LAUNCH(1);
-#undef COLS_LAUNCH
+  hipLaunchKernelGGL((k_bn_relu_bwd_apply_fr<18>),
+                     dim3(C, (To + kFrTile - 1) / kFrTile, apply_cols_chunks(N)), dim3(256), 0, s,
+                     dy, U, mean, invstd, g, b, sg, sgu, dU, dUA, sdu, N, C, To, invM, drop, dy_coef,
+                     cs, amax, amaxa, A);
   return hipGetLastError();
 }
 

@@ -492,9 +492,9 @@ __device__ __forceinline__ void bna_contract(float *img, const float *ar) {
       in[s][2 * i + 1] = t.y;
     }
   }
-  // one row of A live at a time (a rolled loop: unrolled, the compiler hoists
-  // every row's LDS reads and spills); each output written in place as formed
-#pragma unroll 1
+  // a few rows of A live at a time (fully unrolled, the compiler hoists every
+  // row's LDS reads and spills); each output written in place as formed
+#pragma unroll 3
   for (int v = 0; v < V; ++v) {
     float av[20];
 #pragma unroll
@@ -1233,7 +1233,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
   const int rt = bid % p.n_rtiles;
   const int split = bid / p.n_rtiles;
   const int r0 = rt * G::ROWS, c0 = jt * G::CB;
-  float *const qtab = smem + G::LDS / 4;  // QBN: [CB][4] = (mu, a, be, 0) of channels c0..
+  // QBN: [CB + 1][4] = (mu, a, be, 0) of channels c0.., then the identity (0, 1, 0)
+  // that P's groups use (the transform runs branch-free on every group)
+  float *const qtab = smem + G::LDS / 4;
   int q_se = NPL == 2 ? f16x2_se(p.amax_q) : 0;
   if constexpr (QBN) {
     const float M = __builtin_bit_cast(float, amax_read(p.amax_q));
@@ -1242,14 +1244,16 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       const float a = p.q_invstd[c] * p.q_g[c];
       bm = fmaxf(bm, fabsf(a) * (M + fabsf(p.q_mean[c])) + fabsf(p.q_b[c]));
     }
-    if (tid < G::CB) {
+    if (tid <= G::CB) {
       const int c = c0 + tid;
-      const bool ok = c < p.C;
+      const bool ok = tid < G::CB && c < p.C;
       *reinterpret_cast<float4 *>(qtab + 4 * tid) =
-          make_float4(ok ? p.q_mean[c] : 0.f, ok ? p.q_invstd[c] * p.q_g[c] : 0.f,
-                      ok ? p.q_b[c] : 0.f, 0.f);
+          tid == G::CB ? make_float4(0.f, 1.f, 0.f, 0.f)
+                       : make_float4(ok ? p.q_mean[c] : 0.f, ok ? p.q_invstd[c] * p.q_g[c] : 0.f,
+                                     ok ? p.q_b[c] : 0.f, 0.f);
     }
-    q_se = f16x2_se_bits(__builtin_bit_cast(unsigned, block_max_all<512>(bm, qtab + 4 * G::CB)));
+    q_se = f16x2_se_bits(
+        __builtin_bit_cast(unsigned, block_max_all<512>(bm, qtab + 4 * (G::CB + 1))));
   }
   const int p_se = NPL == 2 ? f16x2_se(p.amax_p) : 0;
   const float p_scale = pow2f(p_se), q_scale = pow2f(q_se);
@@ -1307,7 +1311,8 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const unsigned off = gv0[k] + 2 * j < V ? base + 8u * j : kOOB;
-        if constexpr (QBN) qval |= (base != kOOB && gv0[k] + 2 * j < V) ? 1u << (2 * k + j) : 0u;
+        if constexpr (QBN)  // (P's groups: always live; their zeros pass the identity)
+          qval |= (!q_k || (base != kOOB && gv0[k] + 2 * j < V)) ? 1u << (2 * k + j) : 0u;
         const auto v2 = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
         st[k][2 * j] = __builtin_bit_cast(float, (unsigned)v2[0]);
         st[k][2 * j + 1] = __builtin_bit_cast(float, (unsigned)v2[1]);
@@ -1326,13 +1331,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         if constexpr (NPL == 2) {
           const float sc = isq[k] ? q_scale : p_scale;
           float xv[4] = {st[k][0], st[k][1], st[k][2], st[k][3]};
-          if constexpr (QBN) {
-            if (isq[k]) {  // BN1(x) of the group's channel; 0 outside the clip
-              const float4 t = *reinterpret_cast<const float4 *>(qtab + 4 * grow[k]);
+          if constexpr (QBN) {  // BN1(x) of a Q group's channel, 0 outside the clip;
+            // P's groups take the identity entry (no branch around the LDS read)
+            const float4 t = *reinterpret_cast<const float4 *>(qtab + 4 * (isq[k] ? grow[k] : G::CB));
 #pragma unroll
-              for (int e = 0; e < 4; ++e)
-                xv[e] = (qval >> (2 * k + e / 2)) & 1u ? (xv[e] - t.x) * t.y + t.z : 0.f;
-            }
+            for (int e = 0; e < 4; ++e)
+              xv[e] = (qval >> (2 * k + e / 2)) & 1u ? (xv[e] - t.x) * t.y + t.z : 0.f;
           }
           uint2 h, l;
           splith2(xv[0] * sc, xv[1] * sc, h.x, l.x);
@@ -1512,7 +1516,7 @@ hipError_t launch_wgrad_x3(const WgradParams &p0, hipStream_t s) {
     const WgradParams &p = p0;
     if (!p.amax_p || !p.amax_q || !p.q_invstd || !p.q_g || !p.q_b) return hipErrorInvalidValue;
     if (p.x3_mr == 2 && p.R % 128 != 0) return hipErrorInvalidValue;
-    constexpr int ex = (4 * 32 + 8) * 4;  // the Q channel table + block_max_all's scratch
+    constexpr int ex = (4 * 33 + 8) * 4;  // the Q channel table + block_max_all's scratch
     if (p.s_in == 1 && p.x3_mr == 2)
       hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 2, true>), dim3(nblk), dim3(512),
                          (WgX3Geo<18, 1, 2, 2>::LDS + ex), s, p);
