@@ -1886,6 +1886,30 @@ hipError_t launch_bn_relu_bwd_apply_fr(const float *dy, const float *U, const fl
   return hipGetLastError();
 }
 
+hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const float *mean,
+                                         const float *invstd, const float *g, const float *b,
+                                         const double *sg, const double *sgu, float *dU,
+                                         double *sdu, int N, int C, int L, int training,
+                                         Dropout drop, hipStream_t s, int du_bf16,
+                                         const float *dy_coef, double *cs, unsigned *amax) {
+  const double invM = training ? 1.0 / ((double)N * L) : 0.0;
+  // (whole-row vectors: every row start VEC-aligned needs L % VEC == 0)
+  int vec = slice_vec(L, {dy, U, dU});
+  const int nz = apply_cols_chunks(N);
+#define COLS_LAUNCH(VV)                                                                     \
+  hipLaunchKernelGGL((k_bn_relu_bwd_apply_cols<VV>), dim3(C, (L + 256 * VV - 1) / (256 * VV), nz), \
+                     dim3(256), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, sdu, N, C, L,  \
+                     invM, drop, du_bf16, dy_coef, cs, amax)
+  if (vec == 4)
+    COLS_LAUNCH(4);
+  else if (vec == 2)
+    COLS_LAUNCH(2);
+  else
+    COLS_LAUNCH(1);
+#undef COLS_LAUNCH
+  return hipGetLastError();
+}
+
 // The deferred-dx chain's per-channel finalize (see internal.h): with
 // a = invstd1 g1, md = sd / M, mdn = sdn / M the next-to-be-applied dx is
 //   dx = a (dxhat - md - (x - mu1) invstd1 mdn)
