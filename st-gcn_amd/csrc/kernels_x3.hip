@@ -1285,7 +1285,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
   }
   float st[G::GPT][4];
   unsigned qval = 0;  // QBN: bit 2k + j = pair j of staging group k lies inside the clip
-  auto load_item = [&](int item) {
+  auto load_item = [&](int item) __attribute__((always_inline)) {
     if constexpr (QBN) qval = 0;
     const int n = item / p.n_mtiles, m0 = (item - n * p.n_mtiles) * G::FT;
     const __amdgpu_buffer_rsrc_t rp = make_rsrc(p.P + (int64_t)n * p.p_bstride, p.p_bstride);
@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
   };
   static_assert(V % 2 == 0 && (G::ROWS * G::PG) % 64 == 0, "pair loads, uniform P/Q waves");
   // splits and writes staging groups [K0, K1) of the loaded item
-  auto write_part = [&](char *buf, auto k0_c, auto k1_c) {
+  auto write_part = [&](char *buf, auto k0_c, auto k1_c) __attribute__((always_inline)) {
     constexpr int K0 = decltype(k0_c)::value, K1 = decltype(k1_c)::value;
 #pragma unroll
     for (int k = K0; k < K1; ++k)
@@ -1331,12 +1331,14 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         if constexpr (NPL == 2) {
           const float sc = isq[k] ? q_scale : p_scale;
           float xv[4] = {st[k][0], st[k][1], st[k][2], st[k][3]};
-          if constexpr (QBN) {  // BN1(x) of a Q group's channel, 0 outside the clip;
-            // P's groups take the identity entry (no branch around the LDS read)
-            const float4 t = *reinterpret_cast<const float4 *>(qtab + 4 * (isq[k] ? grow[k] : G::CB));
+          if constexpr (QBN) {  // BN1(x) of a Q group's channel, 0 outside the clip
+            // (the P / Q split of the groups falls on wave boundaries: a scalar branch)
+            if (__builtin_amdgcn_readfirstlane((int)isq[k]) != 0) {
+              const float4 t = *reinterpret_cast<const float4 *>(qtab + 4 * grow[k]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              xv[e] = (qval >> (2 * k + e / 2)) & 1u ? (xv[e] - t.x) * t.y + t.z : 0.f;
+              for (int e = 0; e < 4; ++e)
+                xv[e] = (qval >> (2 * k + e / 2)) & 1u ? (xv[e] - t.x) * t.y + t.z : 0.f;
+            }
           }
           uint2 h, l;
           splith2(xv[0] * sc, xv[1] * sc, h.x, l.x);
@@ -1353,15 +1355,26 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         }
       }
   };
-  auto write_item = [&](char *buf) {
-    write_part(buf, std::integral_constant<int, 0>{}, std::integral_constant<int, G::GPT>{});
+  auto write_item = [&](char *buf) __attribute__((always_inline)) {
+    // (in parts of three groups: one loop over all of them is not unrolled at every
+    // instance -- the staging registers then go to scratch memory)
+    using std::integral_constant;
+    constexpr int Q = G::GPT;
+    static_assert(Q <= 12, "write_item parts");
+    write_part(buf, integral_constant<int, 0>{}, integral_constant<int, (Q < 3 ? Q : 3)>{});
+    if constexpr (Q > 3)
+      write_part(buf, integral_constant<int, 3>{}, integral_constant<int, (Q < 6 ? Q : 6)>{});
+    if constexpr (Q > 6)
+      write_part(buf, integral_constant<int, 6>{}, integral_constant<int, (Q < 9 ? Q : 9)>{});
+    if constexpr (Q > 9)
+      write_part(buf, integral_constant<int, 9>{}, integral_constant<int, Q>{});
   };
 
   // lane bases (elements) of the A (P) and B (Q) fragments in plane 0
   const int pa = (mi * 32 + lo) * G::PPITCH + hi * G::HF * G::Vp;
   const int qb = lo * G::QPITCH + hi * SIN * G::HF * G::Vp + q0 * G::Vp;
 
-  auto run = [&](auto nt_c) {
+  auto run = [&](auto nt_c) __attribute__((always_inline)) {
     constexpr int NT = decltype(nt_c)::value;
     floatx16 acc[MR == 1 ? NT : 1], acl[MR == 1 ? NT : 1], acm[MR][MR == 2 ? NT : 1];
     if constexpr (MR == 1) {
@@ -1380,7 +1393,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
     struct Frag {
       bf16x8_t a[MR][NPL], b[NPL][NT];
     };
-    auto ld = [&](const char *buf, int s, Frag &f) {
+    auto ld = [&](const char *buf, int s, Frag &f) __attribute__((always_inline)) {
       const __bf16 *P = reinterpret_cast<const __bf16 *>(buf) + pa + 8 * s;
       const int ga = 2 * s, gb = 2 * s + 1;
       const int oa = SIN * (ga / G::G4) * G::Vp + (ga % G::G4) * 4;
@@ -1400,7 +1413,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         }
       }
     };
-    auto mm = [&](const Frag &f) {
+    auto mm = [&](const Frag &f) __attribute__((always_inline)) {
       if constexpr (MR == 2) {
 #pragma unroll
         for (int mb = 0; mb < MR; ++mb)
