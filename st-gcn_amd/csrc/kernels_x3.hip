@@ -53,6 +53,9 @@
 #ifndef STGCN_X3_EXP  // timing experiments only (bits skip work; results wrong)
 #define STGCN_X3_EXP 0
 #endif
+#ifndef STGCN_BNA_EXP  // bna timing experiments only (results wrong): bit 1 no epilogue
+#define STGCN_BNA_EXP 0  // contraction, 2 no loader BN1, 4 no table / bound setup
+#endif
 
 namespace stgcn {
 
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   const int Cp = nchunks * G::CK;
   float *const btab = smem + G::LDS / 4, *const arow = btab + 3 * Cp;
   float bna_bound = 0.f;
-  if constexpr (BNA) {
+  if constexpr (BNA && !(STGCN_BNA_EXP & 4)) {
     const float M = __builtin_bit_cast(float, amax_read(p.amax_in));
     float bm = 0.f;
     for (int c = tid; c < Cp; c += 512) {
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         float xv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) xv[j] = st[k][j];
-        if constexpr (BNA) {  // BN1 of the item's 8 channels; 0 in the padded frames
+        if constexpr (BNA && !(STGCN_BNA_EXP & 2)) {  // BN1 of the item's 8 channels; 0 in padded frames
           const float *tb = btab + cch + ioct[k] * 8;
           float mu[8], a[8], be[8];
 #pragma unroll
@@ -931,7 +934,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
       for (int j = 0; j < 2; ++j)
         acc_to_img(smem, acc[rb * 2 + j], mi * 32 * MR + rb * 32, (nj0 + j) * 32);
     __syncthreads();
-    if constexpr (BNA) {  // U' -> U = A U' per (row, frame), in place
+    if constexpr (BNA && !(STGCN_BNA_EXP & 1)) {  // U' -> U = A U' per (row, frame), in place
       bna_contract<G::ROWS>(smem, arow);
       __syncthreads();
     }
