@@ -29,12 +29,14 @@ def main(path, steps=10):
     print(f"steps {steps}: wall {(t1 - t0) / 1e6 / steps:.3f} ms/step, GPU busy "
           f"{busy / 1e6 / steps:.3f} ms/step ({busy / (t1 - t0):.4f}), "
           f"{len(seg) / steps:.0f} launches/step")
-    agg = defaultdict(float)
+    agg, cnt = defaultdict(float), defaultdict(int)
     for r in seg:
-        agg[r["Kernel_Name"].split("(")[0][:60]] += (
-            int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 / steps
-    for k, v in sorted(agg.items(), key=lambda x: -x[1])[:25]:
-        print(f"{v:8.3f} ms/step  {k}")
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        k = name.split("(")[0][:60]
+        agg[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 / steps
+        cnt[k] += 1
+    for k, v in sorted(agg.items(), key=lambda x: -x[1])[:40]:
+        print(f"{v:8.3f} ms/step  {cnt[k] / steps:5.1f}x  {k}")
 
 
 if __name__ == "__main__":

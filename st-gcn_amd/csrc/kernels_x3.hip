@@ -481,18 +481,27 @@ __device__ __forceinline__ float bn1_bound(const ConvGemmParams &p, int c, float
 template <int ROWS>
 __device__ __forceinline__ void bna_contract(float *img, const float *ar) {
   constexpr int V = 18, FT = kTileCols / V, NPAIR = ROWS * FT, S = (NPAIR + 511) / 512;
-  float in[S][V];
+  static_assert(S % 2 == 0, "pairs of (row, frame) items per packed fma");
+  constexpr int S2 = S / 2;
+  // items s and s + S2 of this thread side by side in one float2 (v_pk_fma_f32:
+  // two outputs per instruction)
+  f2v in[S2][V];
   int base[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int q = threadIdx.x + 512 * s, r = q % ROWS, f = q / ROWS;
     base[s] = q < NPAIR ? r * kEpiPitch + f * V : -1;
-    const float *src = img + (base[s] >= 0 ? base[s] : 0);
+  }
+#pragma unroll
+  for (int s = 0; s < S2; ++s) {
+    const float *s0 = img + (base[s] >= 0 ? base[s] : 0);
+    const float *s1 = img + (base[s + S2] >= 0 ? base[s + S2] : 0);
 #pragma unroll
     for (int i = 0; i < V / 2; ++i) {
-      const float2 t = *reinterpret_cast<const float2 *>(src + 2 * i);
-      in[s][2 * i] = t.x;
-      in[s][2 * i + 1] = t.y;
+      const float2 t0 = *reinterpret_cast<const float2 *>(s0 + 2 * i);
+      const float2 t1 = *reinterpret_cast<const float2 *>(s1 + 2 * i);
+      in[s][2 * i] = (f2v){t0.x, t1.x};
+      in[s][2 * i + 1] = (f2v){t0.y, t1.y};
     }
   }
   // a few rows of A live at a time (fully unrolled, the compiler hoists every
@@ -509,11 +518,12 @@ __device__ __forceinline__ void bna_contract(float *img, const float *ar) {
       av[4 * i + 3] = t.w;
     }
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      float o = av[0] * in[s][0];
+    for (int s = 0; s < S2; ++s) {
+      f2v o = (f2v){av[0], av[0]} * in[s][0];
 #pragma unroll
-      for (int w = 1; w < V; ++w) o = fmaf(av[w], in[s][w], o);
-      if (base[s] >= 0) img[base[s] + v] = o;
+      for (int w = 1; w < V; ++w) o = __builtin_elementwise_fma((f2v){av[w], av[w]}, in[s][w], o);
+      if (base[s] >= 0) img[base[s] + v] = o.x;
+      if (base[s + S2] >= 0) img[base[s + S2] + v] = o.y;
     }
   }
 }
@@ -528,6 +538,7 @@ template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false, bool
 __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
   using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>;
   static_assert(!BNA || (V == 18 && NPL == 2 && !SPB), "bna: the folded fp16-split forward");
+  static_assert(kBnaAr <= 512, "one A element per thread");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
   char *const wbuf0 = lds, *const win0 = lds + G::NWB * G::WST;
@@ -576,22 +587,17 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // the kernel's own LDS plan, and the fp16 operand bound of BN1(x)
   const int Cp = nchunks * G::CK;
   float *const btab = smem + G::LDS / 4, *const arow = btab + 3 * Cp;
-  float bna_bound = 0.f;
+  // (loaded here into registers, written to LDS after the prologue's DMA is
+  // issued, so the two latencies overlap; Cp <= 512 and kBnaAr <= 512: one
+  // channel and one A element per thread)
+  float t_mu = 0.f, t_a = 0.f, t_be = 0.f, t_ar = 0.f, t_bm = 0.f;
   if constexpr (BNA && !(STGCN_BNA_EXP & 4)) {
     const float M = __builtin_bit_cast(float, amax_read(p.amax_in));
-    float bm = 0.f;
-    for (int c = tid; c < Cp; c += 512) {
-      float mu, a, be;
-      bm = fmaxf(bm, bn1_bound(p, c, M, mu, a, be));
-      btab[c] = mu;
-      btab[Cp + c] = a;
-      btab[2 * Cp + c] = be;
+    if (tid < Cp) t_bm = bn1_bound(p, tid, M, t_mu, t_a, t_be);
+    if (tid < kBnaAr) {
+      const int v = tid / 20, w = tid - v * 20;
+      t_ar = w < 18 ? p.sA[v * 18 + w] : 0.f;
     }
-    for (int i = tid; i < kBnaAr; i += 512) {
-      const int v = i / 20, w = i - v * 20;
-      arow[i] = w < 18 ? p.sA[v * 18 + w] : 0.f;
-    }
-    bna_bound = block_max_all<512>(bm, arow + kBnaAr);  // (scratch past A; barriers inside)
   }
   float st[G::IPT][8];
   // Window loads as inline asm too (the compiler neither waits for them nor
@@ -603,9 +609,8 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   static_assert(!IB || NPL == 1, "bf16 input: one-plane kernels");
   constexpr bool inb = IB;
   // NPL = 2: the window's power-of-two scale (f16x2_se of max |in|)
-  const int in_se = BNA ? f16x2_se_bits(__builtin_bit_cast(unsigned, bna_bound))
-                        : (NPL == 2 ? f16x2_se(p.amax_in) : 0);
-  const float in_scale = pow2f(in_se);
+  int in_se = NPL == 2 && !BNA ? f16x2_se(p.amax_in) : 0;  // (BNA: after the table)
+  float in_scale = pow2f(in_se);
   if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid < kAmaxSlots)  // (slot 0: the bound)
     p.amax_keep[tid * kAmaxStride] = tid == 0 ? amax_read(p.amax_in) : 0u;
   auto load_img = [&](int chunk) {
@@ -780,6 +785,17 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   for (int d = 0; d < G::PD; ++d)
     if (d < nsteps) dma_w(d, d);
   load_img(0);
+  if constexpr (BNA && !(STGCN_BNA_EXP & 4)) {  // the BN1 table, A's rows, the operand bound
+    if (tid < Cp) {
+      btab[tid] = t_mu;
+      btab[Cp + tid] = t_a;
+      btab[2 * Cp + tid] = t_be;
+    }
+    if (tid < kBnaAr) arow[tid] = t_ar;
+    const float bound = block_max_all<512>(t_bm, arow + kBnaAr);  // (barriers inside)
+    in_se = f16x2_se_bits(__builtin_bit_cast(unsigned, bound));
+    in_scale = pow2f(in_se);
+  }
   wait_img<0>(st);
   write_img(win0, 0);
   for (int c = 0; c < nchunks; ++c) {
@@ -1020,6 +1036,7 @@ bool conv_x3_supported(const ConvGemmParams &p) {
 
 bool conv_x3_bna_supported(const ConvGemmParams &p) {
   if (p.V != 18 || p.NQ != 9 || p.s_out != 1 || p.spb || !conv_x3_supported(p)) return false;
+  if (bna_cpad(p.C) > 512) return false;  // (the kernel sets one table channel per thread)
   // the largest plan of the forward instances (128-row tiles, stride 2) + the table
   constexpr int lds = ConvX3Geo<9, 3, 18, 2, 2, 2>::LDS;
   return lds + bna_extra_bytes(p.C) <= 160 * 1024;
