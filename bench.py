@@ -241,10 +241,11 @@ def kernel_roofline(pkg, device, cfg, iters=10):
     V4 = cfg["V"] * 4
     for li, (ci, co, t, s) in enumerate(stack_layers(cfg)):
         progress(f"kernel timing: layer {li}")
-        x3 = cfg.get("f32_gemm") in ("bf16x3", "f16x2") and not cfg["bf16"]
-        f16 = cfg.get("f32_gemm") == "f16x2" and not cfg["bf16"]
+        x3 = cfg.get("f32_gemm") in ("bf16x3", "f16x2", "f16x2-nog") and not cfg["bf16"]
+        f16 = cfg.get("f32_gemm") in ("f16x2", "f16x2-nog") and not cfg["bf16"]
         d = pkg.fused.make_desc((cfg["N"], ci, t, cfg["V"]), co, cfg["K"], s, 4, 1e-5, 0.1, True,
-                                bf16=cfg["bf16"], f32x3=x3 and not f16, f16x2=f16)
+                                bf16=cfg["bf16"], f32x3=x3 and not f16, f16x2=f16,
+                                no_g=cfg.get("f32_gemm") == "f16x2-nog" and not cfg["bf16"])
         for which in range(7):
             nbytes = lib.stgcn_time_kernel_bytes(ctypes.byref(d), which)
             if nbytes == 0:  # 5 / 6 where the spatial backward is one fused kernel
@@ -421,7 +422,7 @@ def main():
                     help="BASELINE.json workload (default cfg2, the headline metric)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3", "f16x2"], default="f16x2",
+    ap.add_argument("--f32-gemm", choices=["mfma", "bf16x3", "f16x2", "f16x2-nog"], default="f16x2",
                     help="fp32 configs: temporal-conv GEMMs on the fp32 matrix cores (mfma), "
                          "as exact 3-way bf16 operand splits (bf16x3) or, on the folded "
                          "blocks, as 2-way fp16 splits of power-of-two-scaled operands "

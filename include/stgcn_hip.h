@@ -94,6 +94,16 @@ extern "C" {
                             * 22-bit data gradient. (The 3-way bf16 data gradient is an
                             * A/B measurement build only: STGCN_AB_F16X2_DGRAD=0.) */
 
+#define STGCN_F_NO_G 16    /* ABI 7, with STGCN_F_F16X2 only (memory-lean folded block):
+                            * G = BN1(x) A^T is never formed or kept -- the forward GEMM
+                            * reads x (BN1 in its loader, the joint contraction in its
+                            * epilogue), the weight gradient reads x against dU A formed
+                            * by the ReLU + BN2 backward pass -- so the N*C_in*T*V*4-byte
+                            * G buffer is not kept between forward and backward
+                            * (stgcn_keep_g_bytes then returns only the bound words).
+                            * Same fp32 gate; measured slower than the G path on cfg2
+                            * (DESIGN.md), hence opt-in. */
+
 enum {
   STGCN_OK = 0,
   STGCN_E_INVALID = -1,     /* bad pointer / shape / parameter            */
@@ -112,7 +122,7 @@ typedef struct stgcn_desc {
   int32_t training;    /* 1: batch statistics + running-stat update          */
   int32_t need_dx;     /* backward: write dx (0 for the network's first block)*/
   int32_t flags;       /* STGCN_F_RESIDUAL | (STGCN_F_BF16 or STGCN_F_F32X3
-                        * [| STGCN_F_F16X2])                                  */
+                        * [| STGCN_F_F16X2 [| STGCN_F_NO_G]])                  */
 } stgcn_desc_t;
 
 /* Forward arguments. Saved tensors (Z, U, stats; residual: Z, Za, y, stats)

@@ -72,6 +72,3 @@
 #ifndef STGCN_AB_F16X2_DGRAD     // 0: the folded data gradient on 3-way bf16 splits under STGCN_F_F16X2
 #define STGCN_AB_F16X2_DGRAD 1
 #endif
-#ifndef STGCN_AB_FOLD_G           // the folded f16x2 block forms G (k_gather4) and both GEMMs read it
-#define STGCN_AB_FOLD_G 0
-#endif

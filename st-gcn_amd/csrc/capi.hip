@@ -145,10 +145,12 @@ bool f16x2_dgrad(const stgcn_desc_t *d) { return f16x2(d) && STGCN_AB_F16X2_DGRA
 // contraction with A in its epilogue (U = A U' + BT), the weight gradient reads
 // x (BN1 at staging) against dU A (written by the ReLU + BN2 backward apply
 // pass), so the gather kernel and G's HBM round trips are gone
-// (STGCN_AB_FOLD_G=1 build: G formed by k_gather4 and read by both GEMMs, A/B only)
+// Opt-in (STGCN_F_NO_G, the memory-lean mode: G is not kept between forward and
+// backward): measured 4% slower per cfg2 step than forming G once with k_gather4
+//  -- the joint contraction then runs on the VALU inside
+// latency-bound GEMM kernels instead of inside an HBM-bound pass.
 bool fold_bna(const stgcn_desc_t *d) {
-  constexpr bool off = STGCN_AB_FOLD_G != 0;
-  if (off || !f16x2(d)) return false;
+  if (!f16x2(d) || !(d->flags & STGCN_F_NO_G)) return false;
   ConvGemmParams p{};
   p.V = d->V;
   p.FT = conv_ft(d->V);
@@ -585,8 +587,11 @@ int stgcn_check_desc(const stgcn_desc_t *d) {
   if (!d) return fail(STGCN_E_INVALID, "null descriptor");
   if (d->N <= 0 || d->C_in <= 0 || d->C_out <= 0 || d->T <= 0 || d->V <= 0 || d->K <= 0)
     return fail(STGCN_E_INVALID, "non-positive dimension");
-  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16 | STGCN_F_F32X3 | STGCN_F_F16X2)) != 0)
+  if ((d->flags & ~(STGCN_F_RESIDUAL | STGCN_F_BF16 | STGCN_F_F32X3 | STGCN_F_F16X2 |
+                    STGCN_F_NO_G)) != 0)
     return fail(STGCN_E_UNSUPPORTED, "unknown flags");
+  if ((d->flags & STGCN_F_NO_G) && !(d->flags & STGCN_F_F16X2))
+    return fail(STGCN_E_INVALID, "STGCN_F_NO_G needs STGCN_F_F16X2");
   if ((d->flags & STGCN_F_BF16) && (d->flags & STGCN_F_F32X3))
     return fail(STGCN_E_INVALID, "STGCN_F_BF16 and STGCN_F_F32X3 are exclusive");
   if ((d->flags & STGCN_F_F16X2) && !(d->flags & STGCN_F_F32X3))

@@ -23,23 +23,26 @@ def _f32c(t, name):
 
 
 def make_desc(x_shape, C_out, K, stride, pad, eps, momentum, training, need_dx=1, gamma=9,
-              residual=False, bf16=False, f32x3=False, f16x2=False):
+              residual=False, bf16=False, f32x3=False, f16x2=False, no_g=False):
     N, C_in, T, V = x_shape
     T_out = (T + 2 * pad - gamma) // stride + 1
     flags = ((hip_lib.F_RESIDUAL if residual else 0) | (hip_lib.F_BF16 if bf16 else 0)
-             | (hip_lib.F_F32X3 if f32x3 or f16x2 else 0) | (hip_lib.F_F16X2 if f16x2 else 0))
+             | (hip_lib.F_F32X3 if f32x3 or f16x2 or no_g else 0)
+             | (hip_lib.F_F16X2 if f16x2 or no_g else 0) | (hip_lib.F_NO_G if no_g else 0))
     return hip_lib.Desc(N, C_in, C_out, T, T_out, V, K, gamma, stride, pad, eps, momentum,
                         int(training), int(need_dx), flags)
 
 
 def _gemm_flags(gemm):
     """Channel-GEMM arithmetic of a block: "fp32" (fp32 MFMA), "f32x3" (fp32 via
-    exact 3-way bf16 operand splits, STGCN_F_F32X3), "f16x2" (STGCN_F_F32X3 with
+    exact 3-way bf16 operand splits, STGCN_F_F32X3), "f16x2_nog" (f16x2 without G,
+    STGCN_F_NO_G: the memory-lean folded block), "f16x2" (STGCN_F_F32X3 with
     the folded GEMMs as 2-way fp16 splits of power-of-two-scaled operands,
     STGCN_F_F16X2), "bf16" (STGCN_F_BF16)."""
-    if gemm not in ("fp32", "f32x3", "f16x2", "bf16"):
+    if gemm not in ("fp32", "f32x3", "f16x2", "f16x2_nog", "bf16"):
         raise ValueError(f"unknown gemm mode {gemm!r}")
-    return {"bf16": gemm == "bf16", "f32x3": gemm == "f32x3", "f16x2": gemm == "f16x2"}
+    return {"bf16": gemm == "bf16", "f32x3": gemm == "f32x3", "f16x2": gemm == "f16x2",
+            "no_g": gemm == "f16x2_nog"}
 
 
 class Link:

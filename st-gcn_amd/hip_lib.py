@@ -26,6 +26,7 @@ F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
 F_F16X2 = 8     # ABI 6, with F_F32X3: the folded GEMMs as 2-way fp16 splits (scaled)
+F_NO_G = 16     # ABI 7, with F_F16X2: the folded block without G (memory-lean)
 # stgcn_block_plan bits (ABI 6)
 PLAN_FOLD, PLAN_SP_FWD_FUSED, PLAN_SP_BWD_FUSED, PLAN_ACT_BF16 = 1, 2, 4, 8
 PLAN_WSP_SPLIT, PLAN_TCONV_SPLIT, PLAN_TWGRAD_SPLIT, PLAN_F16X2 = 16, 32, 64, 128

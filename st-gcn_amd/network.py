@@ -88,14 +88,16 @@ class SpatialTemporalConv(nn.Module):
         super().__init__()
         if gemm_dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("gemm_dtype must be torch.float32 or torch.bfloat16")
-        if f32_gemm not in ("mfma", "bf16x3", "f16x2"):
-            raise ValueError("f32_gemm must be 'mfma', 'bf16x3' or 'f16x2'")
+        if f32_gemm not in ("mfma", "bf16x3", "f16x2", "f16x2-nog"):
+            raise ValueError("f32_gemm must be 'mfma', 'bf16x3', 'f16x2' or 'f16x2-nog'")
         # (not in the reference) how fp32 channel GEMMs run: "mfma" on the fp32
         # matrix cores, "bf16x3" as exact 3-way bf16 operand splits with six
         # partial products on the bf16 matrix cores (fp32-GEMM accuracy,
         # STGCN_F_F32X3; the stride-1 temporal conv forward and data-grad),
         # "f16x2" the same with the folded block's temporal GEMMs as 2-way fp16
-        # splits of power-of-two-scaled operands (three products, STGCN_F_F16X2)
+        # splits of power-of-two-scaled operands (three products, STGCN_F_F16X2),
+        # "f16x2-nog" that without the joint contraction G ever formed or kept
+        # (STGCN_F_NO_G: less activation memory, slower)
         self.f32_gemm = f32_gemm
         # (not in the reference) arithmetic of the channel GEMMs: bf16 rounds the
         # GEMM operands to bf16 on the bf16 matrix cores (fp32 accumulate; tensors,
@@ -142,8 +144,8 @@ class SpatialTemporalConv(nn.Module):
         if getattr(self, "gemm_dtype", torch.float32) == torch.bfloat16:
             gemm = "bf16"
         else:
-            gemm = {"bf16x3": "f32x3", "f16x2": "f16x2"}.get(getattr(self, "f32_gemm", "mfma"),
-                                                             "fp32")
+            gemm = {"bf16x3": "f32x3", "f16x2": "f16x2", "f16x2-nog": "f16x2_nog"}.get(
+                getattr(self, "f32_gemm", "mfma"), "fp32")
         cc = None
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:

@@ -48,7 +48,9 @@ def test_check_desc_accepts_north_star_shapes(pkg, lib):
                dict(flags=2, V=25, K=3), dict(flags=2, V=50, K=3, C_in=128, C_out=256, stride=2,
                                                T_out=150), dict(flags=3, V=18),
                # STGCN_F_F32X3 (fp32 via bf16 splits), plain and residual; + STGCN_F_F16X2
-               dict(flags=4), dict(flags=5, V=25, K=3), dict(flags=12)):
+               dict(flags=4), dict(flags=5, V=25, K=3), dict(flags=12),
+               # + STGCN_F_NO_G (ABI 7)
+               dict(flags=28)):
         d = _desc(pkg, **kw)
         assert lib.stgcn_check_desc(ctypes.byref(d)) == 0, kw
         assert lib.stgcn_fwd_workspace_bytes(ctypes.byref(d)) > 0
@@ -56,7 +58,7 @@ def test_check_desc_accepts_north_star_shapes(pkg, lib):
 
 
 @pytest.mark.parametrize("kw,code", [
-    (dict(flags=16), -2), (dict(flags=8), -1), (dict(flags=10), -1), (dict(flags=6), -1), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
+    (dict(flags=32), -2), (dict(flags=16), -1), (dict(flags=20), -1), (dict(flags=8), -1), (dict(flags=10), -1), (dict(flags=6), -1), (dict(gamma=7, pad=3, T_out=300), -2), (dict(stride=3, T_out=100), -2),
     (dict(T_out=299), -1), (dict(N=0), -1), (dict(V=300), -2)])
 def test_check_desc_rejects(pkg, lib, kw, code):
     d = _desc(pkg, **kw)

@@ -145,7 +145,7 @@ def _eval_case(pkg, case, residual, seed=0):
     # the benched f16x2 folded block without G: in eval mode its forward takes
     # max |x| from its own pass (no BN1 statistics pass runs)
     ((64, 64, 1, 18, 1, 3, 40), False, "f16"),
-    ((64, 128, 2, 18, 1, 2, 37), False, "f16"),
+    ((64, 128, 2, 18, 1, 2, 37), False, "f16n"),
 ])
 def test_block_eval_mode_backward(pkg, case, residual, gemm):
     """Eval mode with gradients (frozen BatchNorm statistics): the backward
@@ -160,7 +160,7 @@ def test_block_eval_mode_backward(pkg, case, residual, gemm):
         blk = pkg.SpatialTemporalConv(
             C_in, C_out, A, 9, stride, 4, dropout_rate=0.5, residual=residual,
             gemm_dtype=torch.bfloat16 if gemm == "bf16" else torch.float32,
-            f32_gemm={"x3": "bf16x3", "f16": "f16x2"}.get(gemm, "mfma"))
+            f32_gemm={"x3": "bf16x3", "f16": "f16x2", "f16n": "f16x2-nog"}.get(gemm, "mfma"))
     sd = {k: v for k, v in p.items()}
     sd.update({k: v for k, v in b.items()})
     blk.load_state_dict(sd)

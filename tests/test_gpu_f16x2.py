@@ -23,8 +23,13 @@ from test_gpu_block import _compare, _oracle, _random_case, _run_hip
 pytestmark = pytest.mark.gpu
 
 
-def _check(pkg, arrays, x, g, need_dx=True):
-    got = _run_hip(pkg, arrays, x, g, need_dx=need_dx, gemm="f16x2")
+# "f16x2_nog": the same GEMMs with G never formed (STGCN_F_NO_G; kernels_x3.hip
+# bna_contract, k_wgrad_x3 QBN), held to the same gate
+MODES = ["f16x2", "f16x2_nog"]
+
+
+def _check(pkg, arrays, x, g, need_dx=True, gemm="f16x2"):
+    got = _run_hip(pkg, arrays, x, g, need_dx=need_dx, gemm=gemm)
     want, floor = _oracle(arrays, got)
     if not need_dx:
         want.pop("grad.x")
@@ -32,9 +37,9 @@ def _check(pkg, arrays, x, g, need_dx=True):
     return got
 
 
-def _plan(pkg, x, C_out, stride, K=1):
+def _plan(pkg, x, C_out, stride, K=1, gemm="f16x2"):
     return pkg.hip_lib.block_plan(pkg.fused.make_desc(
-        tuple(x.shape), C_out, K, stride, 4, 1e-5, 0.1, True, f16x2=True))
+        tuple(x.shape), C_out, K, stride, 4, 1e-5, 0.1, True, **pkg.fused._gemm_flags(gemm)))
 
 
 @pytest.mark.parametrize("case", [
@@ -47,21 +52,24 @@ def _plan(pkg, x, C_out, stride, K=1):
     (24, 40, 1, 18, 1, 2, 23),      # partial channel chunk (24 = 16 + 8), partial rows
     (16, 16, 1, 18, 1, 2, 9),       # smallest folded block
 ])
-def test_f16x2_block_random(pkg, case):
+@pytest.mark.parametrize("gemm", MODES)
+def test_f16x2_block_random(pkg, case, gemm):
     arrays, x, g = _random_case(pkg, *case)
-    got = _check(pkg, arrays, x, g)
+    got = _check(pkg, arrays, x, g, gemm=gemm)
     C_in, C_out, stride = case[:3]
-    plan = _plan(pkg, x, C_out, stride)
+    plan = _plan(pkg, x, C_out, stride, gemm=gemm)
     hl = pkg.hip_lib
     assert plan & hl.PLAN_FOLD and plan & hl.PLAN_F16X2, plan
-    assert plan & hl.PLAN_FOLD_NO_G, plan  # (N1: G is never formed)
+    # (no G: the joint contraction inside the GEMMs)
+    assert bool(plan & hl.PLAN_FOLD_NO_G) == (gemm == "f16x2_nog"), plan
     ref = _run_hip(pkg, arrays, x, g, gemm="f32x3")
     assert not torch.equal(got["y"], ref["y"]), "fp16-split forward did not run"
     assert not torch.equal(got["grad.temporalConv.weight"], ref["grad.temporalConv.weight"])
 
 
+@pytest.mark.parametrize("gemm", MODES)
 @pytest.mark.parametrize("xs,gs", [(1e-6, 1e-4), (1e5, 1e2)])
-def test_f16x2_operand_scales(pkg, xs, gs):
+def test_f16x2_operand_scales(pkg, xs, gs, gemm):
     """Input (hence G: BN1 of a near-constant input is eps-dominated at 1e-6)
     and output gradient (hence dU) far from O(1): the power-of-two operand
     scales keep every GEMM at the fp32 gate. (The analytically-zero temporal
@@ -72,13 +80,14 @@ def test_f16x2_operand_scales(pkg, xs, gs):
     arrays["x"] = x.numpy()
     g = g * gs
     arrays["g"] = g.numpy()
-    _check(pkg, arrays, x, g)
+    _check(pkg, arrays, x, g, gemm=gemm)
 
 
-def test_f16x2_full_size_block(pkg):
+@pytest.mark.parametrize("gemm", MODES)
+def test_f16x2_full_size_block(pkg, gemm):
     """cfg2 L1-type shape at N = 32, T = 300 (the bench layer) at the fp32 gate."""
     arrays, x, g = _random_case(pkg, 64, 64, 1, 18, 1, 32, 300, seed=7)
-    got = _check(pkg, arrays, x, g)
+    got = _check(pkg, arrays, x, g, gemm=gemm)
     for k, v in got.items():
         assert torch.isfinite(v).all(), k
 
@@ -89,16 +98,17 @@ def test_f16x2_backward_without_kept_bound(pkg, monkeypatch):
     weight gradient's operand scale; same fp32 gate."""
     monkeypatch.setattr(pkg.fused, "_keep_g", lambda ctx, x, desc: None)
     arrays, x, g = _random_case(pkg, 64, 128, 2, 18, 1, 2, 29, seed=6)
-    _check(pkg, arrays, x, g)
+    _check(pkg, arrays, x, g, gemm="f16x2_nog")
 
 
-def test_f16x2_l8_shape_block(pkg):
+@pytest.mark.parametrize("gemm", MODES)
+def test_f16x2_l8_shape_block(pkg, gemm):
     """The dominant kernel's shape (cfg2 L8 / L9: 256 -> 256, T = 75) at
     N = 16: 16 channel chunks per tile (the longest reductions), 128-row tiles,
     at the fp32 gate."""
     arrays, x, g = _random_case(pkg, 256, 256, 1, 18, 1, 16, 75, seed=11)
-    got = _check(pkg, arrays, x, g)
-    assert _plan(pkg, x, 256, 1) & pkg.hip_lib.PLAN_F16X2
+    _check(pkg, arrays, x, g, gemm=gemm)
+    assert _plan(pkg, x, 256, 1, gemm=gemm) & pkg.hip_lib.PLAN_F16X2
 
 
 def _per_channel_err(got, want, axis):
@@ -108,7 +118,8 @@ def _per_channel_err(got, want, axis):
     return ((g - w).abs().amax(1) / w.abs().amax(1).clamp_min(1e-300))
 
 
-def test_f16x2_mixed_scale_per_channel(pkg):
+@pytest.mark.parametrize("gemm", MODES)
+def test_f16x2_mixed_scale_per_channel(pkg, gemm):
     """One input channel and one output channel's weights (its temporal conv
     row and its SpatialConv row) at 1e-4 of the rest: a single power-of-two
     scale per operand tensor must not cost the small channels their precision.
@@ -125,7 +136,7 @@ def test_f16x2_mixed_scale_per_channel(pkg):
         w = arrays[k].copy()
         w[co] *= 1e-4
         arrays[k] = w
-    got = _run_hip(pkg, arrays, x, g, gemm="f16x2")
+    got = _run_hip(pkg, arrays, x, g, gemm=gemm)
     want, _ = _oracle(arrays, got)
     ref32 = ref_cpu.block_step(arrays, dtype=torch.float32, relu_mask=got["y"] > 0)
     bad = []

@@ -470,7 +470,7 @@ def test_stack_bf16_cfg3_shape(pkg):
 
 # --- the exact benched configuration (round 2) --------------------------------
 
-@pytest.mark.parametrize("f32_gemm", ["bf16x3", "f16x2"])
+@pytest.mark.parametrize("f32_gemm", ["bf16x3", "f16x2", "f16x2-nog"])
 def test_stack_cfg1_benched_path_matches_reference(pkg, f32_gemm):
     """bench.py's step on the cfg1 golden case: STGCNStack(f32_gemm="bf16x3")
     (temporal GEMMs as exact bf16 splits) or "f16x2" (the folded blocks' GEMMs
@@ -510,7 +510,7 @@ def test_stack_cfg1_benched_path_matches_reference(pkg, f32_gemm):
 
 
 @pytest.mark.parametrize("residual,f32_gemm", [(False, "bf16x3"), (True, "bf16x3"),
-                                               (False, "f16x2")])
+                                               (False, "f16x2"), (False, "f16x2-nog")])
 def test_stack_chain_matches_unchained_bf16x3(pkg, residual, f32_gemm):
     """StackChain in the benched bf16x3 mode (at the bench's T = 300) gives the
     same results as the blocks run one by one, through the fused head."""
