@@ -171,6 +171,9 @@ typedef struct stgcn_fwd_args {
    * >> 32 >= dropout_p * 2^32, then scaled by 1/(1 - dropout_p). 0: no dropout. */
   float dropout_p;
   uint64_t seed;
+  /* ABI 7, optional (folded blocks): the block's stgcn_fold_prep buffer of this
+   * training step -- its weight-only operands are then not formed again */
+  const void *prep;
 } stgcn_fwd_args_t;
 
 /* Backward arguments: the gradients of every input of the forward. */
@@ -221,6 +224,8 @@ typedef struct stgcn_bwd_args {
   /* ABI 5, in: dy holds the next block's dxhat, to be combined as above with
    * these 5 * C_out coefficients (needs dy_sums; non-residual, no dropout) */
   const float *dy_coef;
+  /* ABI 7, optional: the same stgcn_fold_prep buffer as the forward's */
+  const void *prep;
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);
@@ -280,6 +285,22 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
                                     * x against dU A; the kept-G buffer (stgcn_keep_g_bytes)
                                     * then carries only max |x| to the backward          */
 int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan);
+
+/* ABI 7: the weight-only operands of a stack's folded blocks (STGCN_PLAN_FOLD),
+ * formed together once per training step (the weights change every optimizer
+ * step): bZ = bW rowsum(A), the composite weights Wc_q = Wt_q W', the per-frame
+ * bias table, max |Wc|, the packed split planes of the forward and data-gradient
+ * GEMMs and the backward's operand re-layouts -- a dozen launches for the whole
+ * stack instead of ~11 small launches per block. stgcn_fold_prep_bytes(d) is the
+ * block's buffer size (0: the block does not fold); the buffer is then passed as
+ * stgcn_fwd_args_t.prep / stgcn_bwd_args_t.prep of that block in the same step
+ * (same weights). Blocks whose size is 0 are skipped. */
+typedef struct stgcn_fold_weights {
+  const float *A, *W, *bW, *Wt, *bWt;   /* as in stgcn_fwd_args_t            */
+} stgcn_fold_weights_t;
+size_t stgcn_fold_prep_bytes(const stgcn_desc_t *d);
+int stgcn_fold_prep(int nblocks, const stgcn_desc_t *descs, const stgcn_fold_weights_t *weights,
+                    void *const *prep, void *stream);
 
 /* Measurement (bench.py roofline): time one of the block's GEMM kernels,
  * launched `iters` times with the exact parameters the block uses for this

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/stgcn_hip.h"
 #include "internal.h"
@@ -409,6 +410,83 @@ void conv_tiles(ConvGemmParams &p) {
   p.n_rtiles = (p.R + kTileRows - 1) / kTileRows;
 }
 
+// The weight operand fields of the folded block's temporal GEMMs (Wc [R][C][9])
+// -- everything the split-plane pack reads (conv_x3_pack_job): the forward
+// (R = C_out rows over C_in), and the data gradient's launch `ph` (flipped taps;
+// stride 2: phase 0 taps 8, 6, .., 0 and phase 1 taps 7, .., 1)
+ConvGemmParams fold_fwd_wparams(const stgcn_desc_t *d, const float *Wc) {
+  ConvGemmParams p = conv_base(d, nullptr);
+  p.w = Wc;
+  p.w_sr = (int64_t)d->C_in * 9;
+  p.w_sc = 9;
+  p.w_sq = 1;
+  p.C = d->C_in;
+  p.R = d->C_out;
+  p.NQ = 9;
+  p.s_in = d->stride;
+  p.s_out = 1;
+  return p;
+}
+ConvGemmParams fold_dgrad_wparams(const stgcn_desc_t *d, const float *Wc, int ph) {
+  ConvGemmParams p = conv_base(d, nullptr);
+  p.w_sr = 9;
+  p.w_sc = (int64_t)d->C_in * 9;
+  p.C = d->C_out;
+  p.R = d->C_in;
+  p.s_in = 1;
+  if (d->stride == 1) {
+    p.w = Wc + 8;
+    p.w_sq = -1;
+    p.NQ = 9;
+    p.s_out = 1;
+  } else {
+    p.w = Wc + (ph == 0 ? 8 : 7);
+    p.w_sq = -2;
+    p.NQ = ph == 0 ? 5 : 4;
+    p.s_out = 2;
+  }
+  return p;
+}
+int fold_fwd_npl(const stgcn_desc_t *d) { return f16x2(d) ? 2 : 3; }
+int fold_dgrad_npl(const stgcn_desc_t *d) { return f16x2_dgrad(d) ? 2 : 3; }
+
+// A folded block's stgcn_fold_prep buffer (ABI 7)
+struct PrepLayout {
+  float *bZ, *Wc, *BT, *fscr_f, *fscr_b;
+  double *bq, *f64;
+  unsigned *amax;  // max |Wc| (kAmaxWords, every slot written)
+  char *wpk_f, *wpk_d[2];
+  size_t total;
+};
+
+PrepLayout prep_layout(const stgcn_desc_t *d, const void *base) {
+  Carve c(const_cast<void *>(base));
+  PrepLayout P{};
+  const int R = d->C_out, C = d->C_in, V = d->V;
+  P.amax = c.take<unsigned>(kAmaxWords);
+  P.bq = c.take<double>((size_t)9 * R * V);
+  P.f64 = c.take<double>(fold_sdz_scratch_doubles(R, C, V));
+  P.bZ = c.take<float>((size_t)R * V);
+  P.Wc = c.take<float>((size_t)R * C * 9);
+  P.BT = c.take<float>((size_t)R * nTo(d));
+  P.fscr_f = c.take<float>(fold_fwd_scratch_floats(R, C, V));
+  P.fscr_b = c.take<float>(fold_bwd_scratch_floats(R, C));
+  P.wpk_f = c.take<char>(conv_x3_pack_bytes(fold_fwd_wparams(d, nullptr), fold_fwd_npl(d)));
+  for (int ph = 0; ph < (d->stride == 1 ? 1 : 2); ++ph)
+    P.wpk_d[ph] =
+        c.take<char>(conv_x3_pack_bytes(fold_dgrad_wparams(d, nullptr, ph), fold_dgrad_npl(d)));
+  P.total = c.off;
+  return P;
+}
+// (the block takes a prep buffer: folded, with split-plane forward and data gradient)
+bool prep_applies(const stgcn_desc_t *d) {
+  if (!fold_w(d)) return false;
+  if (!conv_x3_supported(fold_fwd_wparams(d, nullptr))) return false;
+  for (int ph = 0; ph < (d->stride == 1 ? 1 : 2); ++ph)
+    if (!conv_x3_supported(fold_dgrad_wparams(d, nullptr, ph))) return false;
+  return true;
+}
+
 // Activations stored in bf16 on the bf16 path's non-residual blocks: Z (the
 // SpatialConv output) and dU (the gradient at the temporal conv output). Every
 // reader of them rounds them to bf16 anyway -- Z: the temporal conv forward
@@ -656,6 +734,66 @@ size_t stgcn_keep_g_bytes(const stgcn_desc_t *d) {
          (f16x2(d) ? sizeof(unsigned) * kAmaxWords : 0);
 }
 
+size_t stgcn_fold_prep_bytes(const stgcn_desc_t *d) {
+  if (stgcn_check_desc(d) != STGCN_OK || !prep_applies(d)) return 0;
+  return prep_layout(d, nullptr).total;
+}
+
+int stgcn_fold_prep(int nblocks, const stgcn_desc_t *descs, const stgcn_fold_weights_t *weights,
+                    void *const *prep, void *stream) {
+  if (nblocks < 0 || (nblocks > 0 && (!descs || !weights || !prep)))
+    return fail(STGCN_E_INVALID, "null fold_prep argument");
+  std::vector<FoldPrepSpec> sp;
+  std::vector<PackJob> pk;
+  for (int i = 0; i < nblocks; ++i) {
+    const stgcn_desc_t *d = descs + i;
+    int rc = stgcn_check_desc(d);
+    if (rc) return rc;
+    if (!prep_applies(d)) continue;  // (stgcn_fold_prep_bytes == 0: not a folded block)
+    const stgcn_fold_weights_t &w = weights[i];
+    if (!prep[i] || !w.A || !w.W || !w.bW || !w.Wt || !w.bWt)
+      return fail(STGCN_E_INVALID, "null fold_prep weights / buffer of a folded block");
+    const PrepLayout P = prep_layout(d, prep[i]);
+    FoldPrepSpec b{};
+    b.A = w.A;
+    b.W = w.W;
+    b.bW = w.bW;
+    b.Wt = w.Wt;
+    b.bWt = w.bWt;
+    b.R = d->C_out;
+    b.C = d->C_in;
+    b.V = d->V;
+    b.T = d->T;
+    b.To = d->T_out;
+    b.stride = d->stride;
+    b.bZ = P.bZ;
+    b.Wc = P.Wc;
+    b.BT = P.BT;
+    b.fscr_f = P.fscr_f;
+    b.fscr_b = P.fscr_b;
+    b.bq = P.bq;
+    b.f64 = P.f64;
+    b.amax = P.amax;
+    sp.push_back(b);
+    // the split-plane packs of the forward and data-gradient GEMMs (with max |Wc|)
+    ConvGemmParams f = fold_fwd_wparams(d, P.Wc);
+    f.wpk = reinterpret_cast<float *>(P.wpk_f);
+    f.amax_w = P.amax;
+    pk.push_back(conv_x3_pack_job(f, fold_fwd_npl(d)));
+    for (int ph = 0; ph < (d->stride == 1 ? 1 : 2); ++ph) {
+      ConvGemmParams g = fold_dgrad_wparams(d, P.Wc, ph);
+      g.wpk = reinterpret_cast<float *>(P.wpk_d[ph]);
+      g.amax_w = P.amax;
+      pk.push_back(conv_x3_pack_job(g, fold_dgrad_npl(d)));
+    }
+  }
+  if (sp.empty()) return STGCN_OK;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(launch_fold_prep(sp.data(), (int)sp.size(), s));
+  HIP_TRY(launch_pack_jobs(pk.data(), (int)pk.size(), s));
+  return STGCN_OK;
+}
+
 size_t stgcn_bwd_workspace_bytes(const stgcn_desc_t *d) {
   if (stgcn_check_desc(d) != STGCN_OK) return 0;
   return bwd_layout(d, nullptr).total;
@@ -698,10 +836,13 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   }
   HIP_TRY(launch_bn_finalize(xs1, xq1, C, (int64_t)N * T * V, d->eps, d->momentum, d->training,
                              a->rm1, a->rv1, mean1, invstd1, s));
-  // Spatial graph conv (st_graphconv.py:139-152) in the form (1).
-  HIP_TRY(launch_bias_rv(a->A, a->bW, L.biasZ, K, R, V, s));
   // (the folded block: G only; W' rides on the temporal conv's weights)
   const bool fold = fold_w(d);
+  // (ABI 7: the folded block's weight-only operands from stgcn_fold_prep)
+  const bool pre = fold && a->prep && prep_applies(d);
+  const PrepLayout P = pre ? prep_layout(d, a->prep) : PrepLayout{};
+  // Spatial graph conv (st_graphconv.py:139-152) in the form (1).
+  if (!pre) HIP_TRY(launch_bias_rv(a->A, a->bW, L.biasZ, K, R, V, s));
   const float *Gfold = nullptr;
   const float *Wz = a->W;
   if (K > 1) {
@@ -773,17 +914,28 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.R = R;
     if (fold) {  // U = sum_q Wc_q G[s t + q - 4] + BT[o, t, v]  (kernels_fold.hip)
       float *Wc = fold_wc_in_z(d) ? a->Z : L.Wc;  // (kept for the backward)
-      HIP_TRY(launch_fold_fwd(a->Wt, a->W, a->bWt, L.biasZ, R, C, V, T, To, d->stride, Wc, L.bq,
-                              L.BT, L.fscr, s));
+      const float *BT = L.BT;
+      const unsigned *amax_wc = L.amax + kAmaxWords;
+      if (pre) {  // (formed for the whole stack by stgcn_fold_prep)
+        Wc = P.Wc;
+        BT = P.BT;
+        amax_wc = P.amax;
+        p.wpk = reinterpret_cast<float *>(P.wpk_f);
+        p.wpk_ready = 1;
+      } else {
+        HIP_TRY(launch_fold_fwd(a->Wt, a->W, a->bWt, L.biasZ, R, C, V, T, To, d->stride, Wc, L.bq,
+                                L.BT, L.fscr, s));
+        if (f16x2(d)) HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
+      }
       if (f16x2(d)) {  // the fp16 splits' operand scales: max |G| (gather), max |Wc|
-        HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
         p.f16x2 = 1;
         p.amax_in = L.amax;
-        p.amax_w = L.amax + kAmaxWords;
+        p.amax_w = amax_wc;
         if (a->G)  // (the kept G carries its bound to the backward)
           p.amax_keep = reinterpret_cast<unsigned *>(a->G + (size_t)N * C * T * V);
       }
       p.in = Gfold;
+      p.res = BT;
       if (bna) {  // x in, BN1 in the loader, A in the epilogue (G never formed)
         p.in = a->x;
         p.bna = 1;
@@ -798,7 +950,6 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
       }
       p.w = Wc;
       p.bias_r = nullptr;
-      p.res = L.BT;
       p.res_shared = 1;
       p.in_bstride = (int64_t)C * T * V;
       p.w_sr = (int64_t)C * 9;
@@ -929,20 +1080,34 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     // The folded block (kernels_fold.hip): Wc_q = Wt_q W'; the data gradient
     // with Wc gives H = W'^T dZ directly (C_in channels), the weight gradient
     // over G gives dWc, and dWt, dW', sum_{n,t} dZ follow from dWc and the dU sums.
+    // (ABI 7: the weight-only operands from stgcn_fold_prep, same step)
+    const bool pre = a->prep && prep_applies(d);
+    const PrepLayout P = pre ? prep_layout(d, a->prep) : PrepLayout{};
     const float *Wc = a->Z;  // (left there by the forward)
-    if (!fold_wc_in_z(d)) {
-      HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, L.fscr, s));
-      Wc = L.Wc;
+    const float *bZ = L.bZ, *fscr = L.fscr;
+    double *f64scr = L.f64scr;
+    const unsigned *amax_wc = L.amax + kAmaxWords;
+    if (pre) {
+      Wc = P.Wc;
+      bZ = P.bZ;
+      fscr = P.fscr_b;
+      f64scr = P.f64;
+      amax_wc = P.amax;
+    } else {
+      if (!fold_wc_in_z(d)) {
+        HIP_TRY(launch_fold_w(a->Wt, a->W, R, C, L.Wc, L.fscr, s));
+        Wc = L.Wc;
+      }
+      HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));
+      HIP_TRY(launch_fold_prep_bwd(a->Wt, a->W, R, C, L.fscr, s));
     }
-    HIP_TRY(launch_bias_rv(a->A, a->bW, L.bZ, K, R, V, s));
-    HIP_TRY(launch_fold_prep_bwd(a->Wt, a->W, R, C, L.fscr, s));
     if (fold_spb(d)) {  // dbW and the bias part of dA first: the data gradient adds to dA;
       // BN1's sd from the dU sums (fp64, exact against the cancellation in sum dxhat)
-      HIP_TRY(launch_fold_sdz(L.f64scr, a->Wt, Wc, L.ftq, R, C, V, L.SdZ, L.SdH, s));
+      HIP_TRY(launch_fold_sdz(f64scr, a->Wt, Wc, L.ftq, R, C, V, L.SdZ, L.SdH, s, pre));
       HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
       HIP_TRY(launch_fold_sd(L.SdH, a->A, C, V, L.sd, s));
     }
-    if (f16x2_dgrad(d))  // the fp16 splits' operand scales: max |dU| (apply pass), max |Wc|
+    if (f16x2_dgrad(d) && !pre)  // the fp16 splits' operand scales: max |dU| (apply pass), max |Wc|
       HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));
     {
       ConvGemmParams p = conv_base(d, L.wpk);
@@ -951,7 +1116,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       if (f16x2_dgrad(d)) {
         p.f16x2 = 1;
         p.amax_in = L.amax;
-        p.amax_w = L.amax + kAmaxWords;
+        p.amax_w = amax_wc;
       }
       if (fold_spb(d)) {  // dxhat -> dx; BN1 / chain sums and dA from the tile (H on chip)
         p.spb = 1;
@@ -985,6 +1150,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
         p.s_out = 1;
         p.p_out = 0;
         p.M = T;
+        if (pre) {
+          p.wpk = reinterpret_cast<float *>(P.wpk_d[0]);
+          p.wpk_ready = 1;
+        }
         conv_tiles(p);
         HIP_TRY(launch_conv_gemm(p, s));
       } else {
@@ -996,6 +1165,10 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
           p.s_out = 2;
           p.p_out = ph;
           p.M = ph == 0 ? (T + 1) / 2 : T / 2;
+          if (pre) {
+            p.wpk = reinterpret_cast<float *>(P.wpk_d[ph]);
+            p.wpk_ready = 1;
+          }
           if (p.M <= 0) continue;
           conv_tiles(p);
           HIP_TRY(launch_conv_gemm(p, s));
@@ -1018,8 +1191,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       w.q_g = a->g1;
       w.q_b = a->b1;
       HIP_TRY(launch_wgrad_taps(w, s));
-      HIP_TRY(launch_fold_grads(L.slab, w.S, L.fscr, L.bZ, L.ftq, R, C, V, L.dWc, a->dWt, a->dW,
-                                s));
+      HIP_TRY(launch_fold_grads(L.slab, w.S, fscr, bZ, L.ftq, R, C, V, L.dWc, a->dWt, a->dW, s));
     } else {
     const float *G = a->G;  // kept fp32 G (f16x2: its max |G| follows it), else recomputed
     const unsigned *amax_g = G ? reinterpret_cast<const unsigned *>(G + (size_t)N * C * T * V)
@@ -1036,8 +1208,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       w.amax_q = amax_g;
     }
     HIP_TRY(launch_wgrad_taps(w, s));
-    HIP_TRY(launch_fold_grads(L.slab, w.S, L.fscr, L.bZ, L.ftq, R, C, V, L.dWc,
-                              a->dWt, a->dW, s));
+    HIP_TRY(launch_fold_grads(L.slab, w.S, fscr, bZ, L.ftq, R, C, V, L.dWc, a->dWt, a->dW, s));
     }
   } else {
   // Temporal conv data-gradient: dZ = conv^T(dU)

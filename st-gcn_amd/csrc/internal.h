@@ -97,6 +97,8 @@ struct ConvGemmParams {
   PrevBn prev;
   double *sd, *sdn;
   float *dA;
+  // wpk already holds the packed split planes of w (stgcn_fold_prep): no pack launch
+  int wpk_ready;
   // bna (with f16x2, V = 18, the folded block's forward; kernels_x3.hip): in[] is
   // the block input x, BN1 (mean1, invstd1, g1, b1) is applied in the window
   // loader and the joint contraction with sA in the epilogue -- G is never formed;
@@ -155,11 +157,25 @@ int fold_tot_blocks(int To);
 hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
                           double *part, double *Tq, hipStream_t s);
 // SdZ = sum_{n,t} dZ and (Wc, SdH non-null) SdH = sum_{n,t} H from Tq, fp64
+// (pre: the scratch already holds the Wt / Wc re-layouts, launch_fold_prep)
 hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
-                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s);
+                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s,
+                           bool pre = false);
 // BN1's sd (db1) of the folded block from SdH: sd[c] = sum_v SdH[c][v] rowsum(A)[v]
 hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, double *sd,
                           hipStream_t s);
+// The weight-only operands of several folded blocks, formed together once per
+// training step (capi.hip stgcn_fold_prep): bZ = bW rowsum(A), Wc = Wt W', the
+// bias table BT, max |Wc|, and the re-layouts the backward's small GEMMs read
+// (fscr_b: launch_fold_prep_bwd's; f64: launch_fold_sdz's Wt / Wc parts)
+struct FoldPrepSpec {
+  const float *A, *W, *bW, *Wt, *bWt;
+  int R, C, V, T, To, stride;
+  float *bZ, *Wc, *BT, *fscr_f, *fscr_b;
+  double *bq, *f64;
+  unsigned *amax;
+};
+hipError_t launch_fold_prep(const FoldPrepSpec *specs, int n, hipStream_t s);
 hipError_t launch_fold_grads(const float *slab, int S, const float *scratch, const float *bZ,
                              const double *Tq, int R, int C, int V, float *dwc, float *dWt,
                              float *dW, hipStream_t s);
@@ -192,6 +208,20 @@ hipError_t launch_conv_bf16(const ConvGemmParams &p, hipStream_t s);
 // data-grad (NQ = 9, 5, 4) for V = 18, 25 over >= 16 channels; launch_conv_gemm
 // dispatches here when p.bf16 == 3 and conv_x3_supported(p).
 bool conv_x3_supported(const ConvGemmParams &p);
+// The weight pack of k_conv_x3 (split planes [row tile][chunk][tap group][plane]
+// [tap][octet][rows][8]) as a job, so several tensors pack in one launch
+// (stgcn_fold_prep); conv_x3_pack_bytes: its size (npl: 3 bf16 / 2 fp16 planes)
+constexpr int kPackJobs = 16;
+struct PackJob {
+  const float *w;
+  void *wpk;
+  int R, C, NQ, TG, nch, rows, npl;
+  int64_t w_sr, w_sc, w_sq, total;
+  const unsigned *amax_w;
+};
+PackJob conv_x3_pack_job(const ConvGemmParams &p, int npl);
+size_t conv_x3_pack_bytes(const ConvGemmParams &p, int npl);
+hipError_t launch_pack_jobs(const PackJob *jobs, int n, hipStream_t s);
 // the bna forward's extra LDS (BN1 table of C channels + A rows) fits
 bool conv_x3_bna_supported(const ConvGemmParams &p);
 size_t conv_x3_wpk_bytes(const ConvGemmParams &p);

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <initializer_list>
+#include <vector>
 
 #include "device_common.h"
 #include "internal.h"
@@ -67,10 +68,11 @@ struct FoldJob {
   int M, N, K, K2;
 };
 
+constexpr int kFoldJobs = 18;  // jobs per k_fold_gemm launch (the stack prep batches blocks)
 struct FoldJobs {
-  FoldJob j[3];
+  FoldJob j[kFoldJobs];
   int n;
-  int tile0[4];  // first tile of job i; tile0[n] = the grid
+  int tile0[kFoldJobs + 1];  // first tile of job i; tile0[n] = the grid
 };
 
 // One wave's K stream, fully unrolled for NG 16-k groups (straight-line code:
@@ -181,19 +183,27 @@ __global__ __launch_bounds__(576) void k_fold_gemm(FoldJobs js) {
     reinterpret_cast<float *>(g.out)[o] = (float)sum;
 }
 
-static hipError_t fold_gemm(std::initializer_list<FoldJob> jobs, hipStream_t s) {
-  FoldJobs js{};
-  js.n = 0;
-  int tiles = 0;
-  for (const FoldJob &g : jobs) {
-    if (js.n == 3 || g.M <= 0 || g.N <= 0) return hipErrorInvalidValue;
-    js.j[js.n] = g;
-    js.tile0[js.n++] = tiles;
-    tiles += ((g.M + 15) / 16) * ((g.N + 15) / 16);
+// (any number of jobs: kFoldJobs per launch)
+static hipError_t fold_gemm_v(const FoldJob *jobs, int n, hipStream_t s) {
+  for (int i0 = 0; i0 < n; i0 += kFoldJobs) {
+    FoldJobs js{};
+    js.n = 0;
+    int tiles = 0;
+    for (int i = i0; i < std::min(n, i0 + kFoldJobs); ++i) {
+      const FoldJob &g = jobs[i];
+      if (g.M <= 0 || g.N <= 0) return hipErrorInvalidValue;
+      js.j[js.n] = g;
+      js.tile0[js.n++] = tiles;
+      tiles += ((g.M + 15) / 16) * ((g.N + 15) / 16);
+    }
+    js.tile0[js.n] = tiles;
+    hipLaunchKernelGGL(k_fold_gemm, dim3(tiles), dim3(576), 0, s, js);
   }
-  js.tile0[js.n] = tiles;
-  hipLaunchKernelGGL(k_fold_gemm, dim3(tiles), dim3(576), 0, s, js);
   return hipGetLastError();
+}
+
+static hipError_t fold_gemm(std::initializer_list<FoldJob> jobs, hipStream_t s) {
+  return fold_gemm_v(jobs.begin(), (int)jobs.size(), s);
 }
 
 // k_fold_tr: the padded fp32 re-layouts. A job reads src(q, o, i) =
@@ -213,10 +223,11 @@ struct TrJob {
   int tiles_i;  // tiles along i (pad32(I) / 16)
 };
 
+constexpr int kTrJobs = 16;  // jobs per k_fold_tr launch
 struct TrJobs {
-  TrJob j[3];
+  TrJob j[kTrJobs];
   int n;
-  int tile0[4];
+  int tile0[kTrJobs + 1];
 };
 
 __global__ __launch_bounds__(576) void k_fold_tr(TrJobs js) {
@@ -301,19 +312,27 @@ static TrJob tr_job(const void *src, int s_dbl, int S, int64_t sstride, int nq, 
   return g;
 }
 
-static hipError_t fold_tr(std::initializer_list<TrJob> jobs, hipStream_t s) {
-  TrJobs js{};
-  int tiles = 0;
-  for (const TrJob &g : jobs) {
-    if (js.n == 3 || (g.nq != 1 && g.nq != 9) || g.O <= 0 || g.I <= 0) return hipErrorInvalidValue;
-    js.j[js.n] = g;
-    js.tile0[js.n++] = tiles;
-    const int OT = g.nq == 9 ? 4 : 36;
-    tiles += g.tiles_i * ((pad32(g.O) + OT - 1) / OT);
+// (any number of jobs: kTrJobs per launch)
+static hipError_t fold_tr_v(const TrJob *jobs, int n, hipStream_t s) {
+  for (int i0 = 0; i0 < n; i0 += kTrJobs) {
+    TrJobs js{};
+    int tiles = 0;
+    for (int i = i0; i < std::min(n, i0 + kTrJobs); ++i) {
+      const TrJob &g = jobs[i];
+      if ((g.nq != 1 && g.nq != 9) || g.O <= 0 || g.I <= 0) return hipErrorInvalidValue;
+      js.j[js.n] = g;
+      js.tile0[js.n++] = tiles;
+      const int OT = g.nq == 9 ? 4 : 36;
+      tiles += g.tiles_i * ((pad32(g.O) + OT - 1) / OT);
+    }
+    js.tile0[js.n] = tiles;
+    hipLaunchKernelGGL(k_fold_tr, dim3(tiles), dim3(576), 0, s, js);
   }
-  js.tile0[js.n] = tiles;
-  hipLaunchKernelGGL(k_fold_tr, dim3(tiles), dim3(576), 0, s, js);
   return hipGetLastError();
+}
+
+static hipError_t fold_tr(std::initializer_list<TrJob> jobs, hipStream_t s) {
+  return fold_tr_v(jobs.begin(), (int)jobs.size(), s);
 }
 
 // Wt [R][R][9] (o, c, q) as the A operand WtQ[q][o][c] of Wc and bq; W' [R][C]
@@ -653,12 +672,14 @@ size_t fold_sdz_scratch_doubles(int R, int C, int V) {
 
 // SdZ (and, with Wc, SdH); Wt [R][R][9], Wc [R][C][9] (o, c, q), Tq [9][R][V]
 hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
-                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s) {
+                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s, bool pre) {
   const int Rp = pad32(R), Cp = pad32(C), Vp = pad32(V);
   double *wtT = scratch, *wcT = wtT + (size_t)9 * Rp * Rp, *tqT = wcT + (size_t)9 * Cp * Rp;
   const TrJob jt = tr_job(Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, nullptr, nullptr, wtT);
   const TrJob jq = tr_job(Tq, 1, 1, 0, 9, (int64_t)R * V, V, 1, R, V, nullptr, nullptr, nullptr, tqT);
-  if (Wc)
+  if (pre)  // (the weight re-layouts were formed by launch_fold_prep)
+    HIP_RET(fold_tr({jq}, s));
+  else if (Wc)
     HIP_RET(fold_tr({jt, jq, tr_job(Wc, 0, 1, 0, 9, 1, (int64_t)C * 9, 9, R, C, nullptr, nullptr,
                                     nullptr, wcT)},
                     s));
@@ -711,6 +732,184 @@ hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, doubl
                           hipStream_t s) {
   if (V > 256) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_fold_sd, dim3((C + 255) / 256), dim3(256), 0, s, SdH, A, C, V, sd);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// stgcn_fold_prep (capi.hip): the weight-only operands of every folded block of
+// a stack in a dozen launches per training step instead of ~11 small launches
+// per block in each block's forward and backward. Every job is the one the
+// block would run itself (same kernels, same operand layouts, same order of
+// arithmetic), batched over the blocks by job tables in the kernel arguments.
+// ---------------------------------------------------------------------------
+constexpr int kPrepJobs = 16;
+
+struct BiasRvJob {
+  const float *A, *bW;
+  float *out;
+  int R, V, blk0;  // first block of the job
+};
+struct BiasRvJobs {
+  BiasRvJob j[kPrepJobs];
+  int n, blk1;  // blk1 = total blocks
+};
+
+// bZ[co][v] = bW[co] rowsum(A)[v] (K = 1: the folded block), as k_bias_rv
+__global__ void k_bias_rv_multi(BiasRvJobs js) {
+  int k = 0;
+  while (k + 1 < js.n && (int)blockIdx.x >= js.j[k + 1].blk0) ++k;
+  const BiasRvJob &q = js.j[k];
+  const int idx = ((int)blockIdx.x - q.blk0) * blockDim.x + threadIdx.x;
+  if (idx >= q.R * q.V) return;
+  const int co = idx / q.V, v = idx - co * q.V;
+  double ra = 0.0;
+  for (int w = 0; w < q.V; ++w) ra += q.A[(int64_t)v * q.V + w];
+  q.out[idx] = (float)((double)q.bW[co] * ra);
+}
+
+struct BiasJob {
+  const double *bq;
+  const float *bt;
+  float *BT;
+  int R, V, T, To, st, blk0;
+};
+struct BiasJobs {
+  BiasJob j[kPrepJobs];
+  int n;
+};
+
+// k_fold_bias over several blocks (block = one output channel of one job)
+__global__ __launch_bounds__(256) void k_fold_bias_multi(BiasJobs js) {
+  int k = 0;
+  while (k + 1 < js.n && (int)blockIdx.x >= js.j[k + 1].blk0) ++k;
+  const BiasJob &q = js.j[k];
+  __shared__ double bs[9 * 256], full[256];
+  const int o = (int)blockIdx.x - q.blk0, tid = threadIdx.x, V = q.V, R = q.R;
+  for (int e = tid; e < 9 * V; e += 256) {
+    const int qq = e / V, v = e - qq * V;
+    bs[e] = q.bq[((int64_t)qq * R + o) * V + v];
+  }
+  __syncthreads();
+  const double b0 = q.bt[o];
+  if (tid < V) {
+    double a = b0;
+#pragma unroll
+    for (int qq = 0; qq < 9; ++qq) a += bs[qq * V + tid];
+    full[tid] = a;
+  }
+  __syncthreads();
+  float *dst = q.BT + (int64_t)o * q.To * V;
+  for (int tv = tid; tv < q.To * V; tv += 256) {
+    const int t = tv / V, v = tv - t * V, t0 = q.st * t - 4;
+    double a;
+    if (t0 >= 0 && t0 + 8 < q.T) {
+      a = full[v];
+    } else {
+      a = b0;
+      for (int qq = 0; qq < 9; ++qq)
+        if (t0 + qq >= 0 && t0 + qq < q.T) a += bs[qq * V + v];
+    }
+    dst[tv] = (float)a;
+  }
+}
+
+struct AmaxJob {
+  const float *x;
+  int64_t n;
+  unsigned *amax;
+};
+struct AmaxJobs {
+  AmaxJob j[kPrepJobs];
+  int n;
+};
+
+// max |x| of each job into its kAmaxSlots words: job = blockIdx.y, the job's
+// kAmaxSlots workgroups each store their own slot (no atomics: nothing to zero)
+__global__ __launch_bounds__(256) void k_absmax_multi(AmaxJobs js) {
+  const AmaxJob &q = js.j[blockIdx.y];
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < q.n; i += (int64_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf(q.x[i]));
+  __shared__ float wmax[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    q.amax[blockIdx.x * kAmaxStride] =
+        __builtin_bit_cast(unsigned, fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+}
+
+hipError_t launch_fold_prep(const FoldPrepSpec *sp, int n, hipStream_t s) {
+  for (int i = 0; i < n; ++i)
+    if (sp[i].V > 256 || sp[i].V <= 0 || sp[i].R <= 0 || sp[i].C <= 0) return hipErrorInvalidValue;
+  // 1. bZ of every block
+  for (int i0 = 0; i0 < n; i0 += kPrepJobs) {
+    BiasRvJobs js{};
+    int blk = 0;
+    for (int i = i0; i < std::min(n, i0 + kPrepJobs); ++i) {
+      js.j[js.n] = {sp[i].A, sp[i].bW, sp[i].bZ, sp[i].R, sp[i].V, blk};
+      blk += (sp[i].R * sp[i].V + 255) / 256;
+      ++js.n;
+    }
+    js.blk1 = blk;
+    hipLaunchKernelGGL(k_bias_rv_multi, dim3(blk), dim3(256), 0, s, js);
+  }
+  // 2. the re-layouts of Wt, W', bZ: the forward's fold GEMM operands
+  //    (fold_fwd_gemms), the backward's (launch_fold_prep_bwd) and the fp64 Wt of
+  //    launch_fold_sdz
+  std::vector<TrJob> tr;
+  std::vector<FoldJob> fg;
+  for (int i = 0; i < n; ++i) {
+    const FoldPrepSpec &b = sp[i];
+    const int R = b.R, C = b.C, V = b.V, Rp = pad32(R), Cp = pad32(C);
+    float *wtq = b.fscr_f, *wT = wtq + (size_t)9 * Rp * Rp, *bzT = wT + (size_t)Cp * Rp;
+    tr.push_back(tr_job(b.Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, wtq, nullptr));
+    tr.push_back(tr_job(b.W, 0, 1, 0, 1, 0, C, 1, R, C, nullptr, wT));
+    tr.push_back(tr_job(b.bZ, 0, 1, 0, 1, 0, V, 1, R, V, nullptr, bzT));
+    float *wtT = b.fscr_b, *wd = wtT + (size_t)9 * Rp * Rp;
+    tr.push_back(tr_job(b.Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, wtT));
+    tr.push_back(tr_job(b.W, 0, 1, 0, 1, 0, C, 1, R, C, wd, nullptr));
+    tr.push_back(tr_job(b.Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, nullptr, nullptr,
+                        b.f64));
+    FoldJob w{};
+    w.A = wtq; w.aq = (int64_t)Rp * Rp; w.am = Rp;
+    w.B = wT; w.bn = Rp;
+    w.out = b.Wc; w.oq = 1; w.om = (int64_t)C * 9; w.on = 9;
+    w.M = R; w.N = C; w.K = R;
+    FoldJob q{};
+    q.A = wtq; q.aq = (int64_t)Rp * Rp; q.am = Rp;
+    q.B = bzT; q.bn = Rp;
+    q.out = b.bq; q.o_dbl = 1; q.oq = (int64_t)R * V; q.om = V; q.on = 1;
+    q.M = R; q.N = V; q.K = R;
+    fg.push_back(w);
+    fg.push_back(q);
+  }
+  HIP_RET(fold_tr_v(tr.data(), (int)tr.size(), s));
+  // 3. Wc = Wt W' and the bias products bq (fold_fwd_gemms)
+  HIP_RET(fold_gemm_v(fg.data(), (int)fg.size(), s));
+  // 4. the per-frame bias tables, the fp64 Wc re-layout of launch_fold_sdz, max |Wc|
+  for (int i0 = 0; i0 < n; i0 += kPrepJobs) {
+    BiasJobs js{};
+    AmaxJobs am{};
+    int blk = 0;
+    for (int i = i0; i < std::min(n, i0 + kPrepJobs); ++i) {
+      js.j[js.n++] = {sp[i].bq, sp[i].bWt, sp[i].BT, sp[i].R, sp[i].V, sp[i].T, sp[i].To,
+                      sp[i].stride, blk};
+      blk += sp[i].R;
+      am.j[am.n++] = {sp[i].Wc, (int64_t)sp[i].R * sp[i].C * 9, sp[i].amax};
+    }
+    hipLaunchKernelGGL(k_fold_bias_multi, dim3(blk), dim3(256), 0, s, js);
+    hipLaunchKernelGGL(k_absmax_multi, dim3(kAmaxSlots, am.n), dim3(256), 0, s, am);
+  }
+  tr.clear();
+  for (int i = 0; i < n; ++i) {
+    const FoldPrepSpec &b = sp[i];
+    const int R = b.R, C = b.C, Rp = pad32(R);
+    tr.push_back(tr_job(b.Wc, 0, 1, 0, 9, 1, (int64_t)C * 9, 9, R, C, nullptr, nullptr, nullptr,
+                        b.f64 + (size_t)9 * Rp * Rp));
+  }
+  HIP_RET(fold_tr_v(tr.data(), (int)tr.size(), s));
   return hipGetLastError();
 }
 

@@ -1024,6 +1024,54 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
   wpk[idx] = pl == 0 ? h : (pl == 1 ? m : l);
 }
 
+// The pack of several weight tensors in one launch (stgcn_fold_prep: every
+// folded block's forward and data-gradient weights once per step): job i covers
+// flat indices [start[i], start[i + 1]) of the concatenated jobs.
+struct PackJobs {
+  PackJob j[kPackJobs];
+  int64_t start[kPackJobs + 1];
+  int n;
+};
+
+__global__ void k_pack_conv_w_x3_multi(PackJobs js) {
+  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= js.start[js.n]) return;
+  int k = 0;
+  while (k + 1 < js.n && gi >= js.start[k + 1]) ++k;
+  const PackJob &q = js.j[k];
+  const int64_t idx = gi - js.start[k];
+  const int jj = (int)(idx & 7);
+  int64_t t = idx >> 3;
+  const int rl = (int)(t % q.rows);
+  t /= q.rows;
+  const int o = (int)(t & 1);
+  t >>= 1;
+  const int qq = (int)(t % q.TG);
+  t /= q.TG;
+  const int pl = (int)(t % q.npl);
+  t /= q.npl;
+  const int NG = q.NQ / q.TG;
+  const int g = (int)(t % NG);
+  t /= NG;
+  const int ch = (int)(t % q.nch);
+  const int rt = (int)(t / q.nch);
+  const int r = rt * q.rows + rl, c = ch * 16 + o * 8 + jj, tap = g * q.TG + qq;
+  float v = 0.f;
+  if (r < q.R && c < q.C) v = q.w[(int64_t)r * q.w_sr + (int64_t)c * q.w_sc + (int64_t)tap * q.w_sq];
+  if (q.npl == 2) {
+    const float vs = v * pow2f(f16x2_se(q.amax_w));
+    const _Float16 h = (_Float16)vs;
+    const _Float16 l = (_Float16)(vs - (float)h);
+    reinterpret_cast<_Float16 *>(q.wpk)[idx] = pl == 0 ? h : l;
+    return;
+  }
+  const __bf16 h = (__bf16)v;
+  const float r1 = v - (float)h;
+  const __bf16 m = (__bf16)r1;
+  const __bf16 l = (__bf16)(r1 - (float)m);
+  reinterpret_cast<__bf16 *>(q.wpk)[idx] = pl == 0 ? h : (pl == 1 ? m : l);
+}
+
 static int x3_tg(int NQ) { return NQ == 9 ? 3 : NQ; }
 
 bool conv_x3_supported(const ConvGemmParams &p) {
@@ -1104,13 +1152,58 @@ static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
 
 // npl = 3: fp32 as exact 3-way splits (STGCN_F_F32X3); npl = 1: bf16 operands
 // (STGCN_F_BF16), the same pipeline with one plane and two workgroups per CU
+// The pack job of a launch_conv_planes call (same layout, same scales)
+static PackJob pack_job(const ConvGemmParams &p, int npl) {
+  const bool wide = npl >= 2 && x3_wide_rows(p);
+  const int rows = wide ? 128 : 64;
+  PackJob j{};
+  j.w = p.w;
+  j.wpk = p.wpk;
+  j.R = p.R;
+  j.C = p.C;
+  j.NQ = p.NQ;
+  j.TG = x3_tg(p.NQ);
+  j.nch = (p.C + 15) / 16;
+  j.rows = rows;
+  j.npl = npl;
+  j.w_sr = p.w_sr;
+  j.w_sc = p.w_sc;
+  j.w_sq = p.w_sq;
+  j.total = (int64_t)((p.R + rows - 1) / rows) * j.nch * npl * p.NQ * 2 * rows * 8;
+  j.amax_w = p.amax_w;
+  return j;
+}
+
+size_t conv_x3_pack_bytes(const ConvGemmParams &p, int npl) {
+  return (size_t)pack_job(p, npl).total * 2;
+}
+
+PackJob conv_x3_pack_job(const ConvGemmParams &p, int npl) { return pack_job(p, npl); }
+
+hipError_t launch_pack_jobs(const PackJob *jobs, int n, hipStream_t s) {
+  for (int i0 = 0; i0 < n; i0 += kPackJobs) {
+    PackJobs js{};
+    js.n = std::min(kPackJobs, n - i0);
+    js.start[0] = 0;
+    for (int k = 0; k < js.n; ++k) {
+      js.j[k] = jobs[i0 + k];
+      js.start[k + 1] = js.start[k] + js.j[k].total;
+    }
+    const int64_t tot = js.start[js.n];
+    if (tot > 0)
+      hipLaunchKernelGGL(k_pack_conv_w_x3_multi, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                         js);
+  }
+  return hipGetLastError();
+}
+
 static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStream_t s) {
   const bool wide = npl >= 2 && x3_wide_rows(p0);
   ConvGemmParams p = p0;
   const int rows = wide ? 128 : 64;
   p.n_rtiles = (p.R + rows - 1) / rows;
   const int nch = (p.C + 15) / 16;
-  {
+  if (!p.wpk_ready) {  // (else packed by stgcn_fold_prep, pack_job's layout)
     const int64_t total = (int64_t)p.n_rtiles * nch * npl * p.NQ * 2 * rows * 8;
     hipLaunchKernelGGL(k_pack_conv_w_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                        p.w, reinterpret_cast<__bf16 *>(p.wpk), p.R, p.C, p.NQ, x3_tg(p.NQ), nch,

@@ -76,8 +76,10 @@ class ChainCtx:
     and to the next one (``out_link``)."""
 
     def __init__(self, x_stats=None, y_stats=None, in_link=None, out_link=None, prev_g2=None,
-                 prev_b2=None, prev_U=None, prev_stats=None):
+                 prev_b2=None, prev_U=None, prev_stats=None, prep=None):
         self.x_stats, self.y_stats = x_stats, y_stats
+        # ABI 7: this block's stgcn_fold_prep buffer of the step (or None)
+        self.prep = prep
         self.in_link, self.out_link = in_link, out_link
         self.prev_g2, self.prev_b2 = prev_g2, prev_b2
         # the previous block's pre-BN2 tensor and [mean2 | invstd2] (ABI 4): read
@@ -85,6 +87,51 @@ class ChainCtx:
         self.prev_U, self.prev_stats = prev_U, prev_stats
         # this block's (U, [mean2 | invstd2]) for the next block's link
         self.U, self.stats2 = None, None
+
+
+class FoldPrep:
+    """The per-step weight preparation of a block stack's folded blocks (ABI 7
+    stgcn_fold_prep: every folded block's Wc, bias table, max |Wc|, packed
+    forward / data-gradient weights and backward re-layouts in about a dozen
+    launches for the whole stack, instead of ~11 small launches per block).
+    Buffers are cached per input shape and reused every step; a step's
+    forward and backward use the same weights, so they read the same buffers."""
+
+    def __init__(self):
+        self._bufs = {}
+
+    def run(self, blocks, x_shape, dev):
+        """blocks: the stack's SpatialTemporalConv modules in order; x_shape the
+        stack input (N, C, T, V). Returns one prep tensor (or None) per block."""
+        lib = hip_lib.lib()
+        N, C, T, V = x_shape
+        descs, weights, ptrs, out = [], [], [], []
+        for i, blk in enumerate(blocks):
+            sc, tc = blk.spatialConv, blk.temporalConv
+            gemm = blk.gemm_mode()
+            desc = make_desc((N, C, T, V), tc.out_channels, sc.A.shape[0], blk.stride, blk.pad,
+                             blk.batch_n.eps, blk.batch_n.momentum, True,
+                             residual=blk.residual, **_gemm_flags(gemm))
+            nbytes = lib.stgcn_fold_prep_bytes(ctypes.byref(desc))
+            buf = None
+            if nbytes:
+                key = (i, tuple(x_shape), gemm, nbytes)
+                buf = self._bufs.get(key)
+                if buf is None or buf.device != dev:
+                    buf = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+                    self._bufs[key] = buf
+                descs.append(desc)
+                weights.append(hip_lib.FoldWeights(*[hip_lib.ptr(t) for t in (
+                    sc.A, sc.W.weight, sc.W.bias, tc.weight, tc.bias)]))
+                ptrs.append(hip_lib.ptr(buf))
+            out.append(buf)
+            C, T = tc.out_channels, desc.T_out
+        if descs:
+            n = len(descs)
+            hip_lib.check(lib.stgcn_fold_prep(
+                n, (hip_lib.Desc * n)(*descs), (hip_lib.FoldWeights * n)(*weights),
+                (ctypes.c_void_p * n)(*ptrs), hip_lib.stream_handle(dev)))
+        return out
 
 
 def _observed(xref):
@@ -192,12 +239,15 @@ class StgcnBlockFn(torch.autograd.Function):
         G = _keep_g(ctx, x, desc)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
+        prep = cc.prep if cc is not None else None
         args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (
             x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats,
-            None, None, None, G, cc and cc.x_stats, cc and cc.y_stats)], drop, seed)
+            None, None, None, G, cc and cc.x_stats, cc and cc.y_stats)], drop, seed,
+            prep=hip_lib.ptr(prep))
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
+        ctx.prep = prep
         if cc is not None:
             cc.U, cc.stats2 = U, stats[2 * C_in:]
         ctx.cfg = (stride, pad, eps, momentum, training)
@@ -232,7 +282,7 @@ class StgcnBlockFn(torch.autograd.Function):
             prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst), x_stats=hip_lib.ptr(xst),
             dx_coef=hip_lib.ptr(dx_coef),
             dx_deferred=ctypes.addressof(deferred) if dx_coef is not None else None,
-            dy_coef=hip_lib.ptr(dy_coef))
+            dy_coef=hip_lib.ptr(dy_coef), prep=hip_lib.ptr(ctx.prep))
         hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes,
                                           hip_lib.stream_handle(x.device)))

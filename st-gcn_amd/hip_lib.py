@@ -59,7 +59,8 @@ class FwdArgs(ctypes.Structure):
         "Wr", "br", "Za",        # ABI 2: residual block
         "G",                     # ABI 2: optional kept joint contraction
         "x_stats", "y_stats")    # ABI 2: optional stack chaining
-    ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)]  # ABI 2: fused dropout
+    ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)  # ABI 2: fused dropout
+         ] + [("prep", _vp)]                                  # ABI 7: stgcn_fold_prep
 
 
 class BwdArgs(ctypes.Structure):
@@ -72,7 +73,12 @@ class BwdArgs(ctypes.Structure):
     ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)  # ABI 2: fused dropout
          ] + [("prev_U", _vp), ("prev_stats", _vp)  # ABI 4: chain conditioning fallback
               ] + [("x_stats", _vp), ("dx_coef", _vp), ("dx_deferred", _vp),  # ABI 5:
-                   ("dy_coef", _vp)]                                         # deferred dx
+                   ("dy_coef", _vp)                                          # deferred dx
+                   ] + [("prep", _vp)]                                       # ABI 7
+
+
+class FoldWeights(ctypes.Structure):  # ABI 7: stgcn_fold_prep
+    _fields_ = [(n, _vp) for n in ("A", "W", "bW", "Wt", "bWt")]
 
 
 class SpatialDesc(ctypes.Structure):  # ABI 4: SpatialConv on its own
@@ -96,7 +102,7 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
             "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
             "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes",
-            "stgcn_block_plan")
+            "stgcn_block_plan", "stgcn_fold_prep_bytes", "stgcn_fold_prep")
 
 _LIB = None
 
@@ -150,6 +156,11 @@ def load_library(path=LIB_PATH):
     lib.stgcn_spatial_bwd.restype = ctypes.c_int
     lib.stgcn_block_plan.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(ctypes.c_uint32)]
     lib.stgcn_block_plan.restype = ctypes.c_int
+    lib.stgcn_fold_prep_bytes.argtypes = [ctypes.POINTER(Desc)]
+    lib.stgcn_fold_prep_bytes.restype = ctypes.c_size_t
+    lib.stgcn_fold_prep.argtypes = [ctypes.c_int, ctypes.POINTER(Desc),
+                                    ctypes.POINTER(FoldWeights), ctypes.POINTER(_vp), _vp]
+    lib.stgcn_fold_prep.restype = ctypes.c_int
     if lib.stgcn_abi_version() != ABI_VERSION:
         raise RuntimeError("libstgcn_hip.so ABI version mismatch; rebuild it")
     return lib

@@ -8,6 +8,7 @@ import torch
 import torch.nn as nn
 
 from .graph import Strategy, get_normalized_adjacency_matrices
+from .fused import FoldPrep
 from .network import SpatialTemporalConv, StackChain
 from .train_ops import StgcnHeadFn
 
@@ -56,9 +57,21 @@ class STGCNStack(nn.Module):
         self.conv = nn.Sequential(*blocks).float()
         self.fc_layer = nn.Linear(256, nr_classes).float()
 
+    def _chain(self, x):
+        """The StackChain of a training forward, with the stack's folded blocks'
+        weight-only operands formed for this step (fused.FoldPrep, ABI 7)."""
+        if not self.training:
+            return None
+        chain = StackChain(defer_counts=True)
+        if x.is_cuda:
+            if getattr(self, "_fold_prep", None) is None:
+                self._fold_prep = FoldPrep()
+            chain.set_prep(self._fold_prep.run(list(self.conv), tuple(x.shape), x.device))
+        return chain
+
     def forward_nctv(self, x):
         # same as self.conv(x), with cross-block fusion (network.StackChain)
-        chain = StackChain(defer_counts=True) if self.training else None
+        chain = self._chain(x)
         for blk in self.conv:
             x = blk(x, chain=chain)
         if chain is not None:
@@ -78,7 +91,7 @@ class STGCNStack(nn.Module):
         NCTV, labels int64 (N) -> (mean cross-entropy loss, logits); the same
         arithmetic as F.cross_entropy(self.forward_nctv(x), labels)
         (lightning_model.py:105-107, :202)."""
-        chain = StackChain(defer_counts=True) if self.training else None
+        chain = self._chain(x)
         for blk in self.conv:
             x = blk(x, chain=chain)
         if chain is not None:

@@ -37,6 +37,15 @@ class StackChain:
         self.y, self.y_version, self.y_stats, self.link, self.g2b2 = None, None, None, None, None
         self.u_stats = None
 
+    def set_prep(self, preps):
+        """The stack's per-block stgcn_fold_prep buffers of this step (fused.FoldPrep),
+        handed to the blocks in order."""
+        self.preps = list(preps)
+
+    def next_prep(self):
+        preps = getattr(self, "preps", None)
+        return preps.pop(0) if preps else None
+
     def count_batch(self, *counters):
         """BatchNorm num_batches_tracked increments of the chained blocks, applied
         by ``flush_counts`` in one multi-tensor launch instead of two per block."""
@@ -127,6 +136,13 @@ class SpatialTemporalConv(nn.Module):
         self.stride = temporal_stride
         self.pad = temporal_padding
 
+    def gemm_mode(self):
+        """The channel-GEMM arithmetic of this block (fused._gemm_flags mode)."""
+        if getattr(self, "gemm_dtype", torch.float32) == torch.bfloat16:
+            return "bf16"
+        return {"bf16x3": "f32x3", "f16x2": "f16x2", "f16x2-nog": "f16x2_nog"}.get(
+            getattr(self, "f32_gemm", "mfma"), "fp32")
+
     def forward(self, f_in, chain=None):
         """``chain``: optional ``StackChain`` (not part of the reference API)."""
         bn1, bn2 = self.batch_n, self.batch_n_2
@@ -141,11 +157,7 @@ class SpatialTemporalConv(nn.Module):
         sc = self.spatialConv
         x = f_in.float()
         drop = self.dropout.p if (self.dropout is not None and training) else 0.0
-        if getattr(self, "gemm_dtype", torch.float32) == torch.bfloat16:
-            gemm = "bf16"
-        else:
-            gemm = {"bf16x3": "f32x3", "f16x2": "f16x2", "f16x2-nog": "f16x2_nog"}.get(
-                getattr(self, "f32_gemm", "mfma"), "fp32")
+        gemm = self.gemm_mode()
         cc = None
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:
@@ -155,6 +167,7 @@ class SpatialTemporalConv(nn.Module):
             cc = ChainCtx(y_stats=torch.empty(
                               hip_lib.y_stats_doubles(self.temporalConv.out_channels),
                               device=x.device, dtype=torch.float64),
+                          prep=chain.next_prep(),
                           out_link=None if (self.residual or drop > 0) else Link())
             if chain.y is not None and x is chain.y and x._version == chain.y_version:
                 cc.x_stats = chain.y_stats

@@ -139,3 +139,20 @@ def test_block_plan_pins_the_paths(pkg, lib):
     d = _desc(pkg, N=0)
     out = ctypes.c_uint32(7)
     assert lib.stgcn_block_plan(ctypes.byref(d), ctypes.byref(out)) == -1
+
+
+def test_fold_prep_sizes(pkg, lib):
+    """ABI 7 stgcn_fold_prep_bytes: a buffer for the folded split-path blocks
+    (K = 1, V = 18, fp32 via splits), none for blocks that do not fold (first
+    block C_in = 3, K = 3, residual, bf16, exact fp32 MFMA)."""
+    fl = pkg.hip_lib
+    folded = [dict(C_in=64, flags=12), dict(C_in=64, C_out=128, stride=2, T_out=150, flags=12),
+              dict(C_in=64, flags=4), dict(C_in=64, flags=28)]
+    for kw in folded:
+        assert lib.stgcn_fold_prep_bytes(ctypes.byref(_desc(pkg, **kw))) > 0, kw
+    for kw in (dict(C_in=3, flags=12), dict(V=25, K=3, flags=4), dict(C_in=64, flags=13),
+               dict(C_in=64, flags=2), dict(C_in=64, flags=0)):
+        assert lib.stgcn_fold_prep_bytes(ctypes.byref(_desc(pkg, **kw))) == 0, kw
+    # no blocks: nothing to do, no GPU touched
+    assert lib.stgcn_fold_prep(0, None, None, None, None) == 0
+

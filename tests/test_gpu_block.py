@@ -28,12 +28,37 @@ TOL_RUNNING = 1e-5
 DEV = "cuda:0"
 
 
-def _run_hip(pkg, arrays, x, g, need_dx=True, gemm="fp32"):
+def _fold_prep(pkg, cu, xshape, C_out, K, stride, gemm):
+    """ABI 7 stgcn_fold_prep of one folded block (as STGCNStack does per step)"""
+    import ctypes
+    hl = pkg.hip_lib
+    lib = hl.lib()
+    d = pkg.fused.make_desc(tuple(xshape), C_out, K, stride, 4, 1e-5, 0.1, True,
+                            **pkg.fused._gemm_flags(gemm))
+    nbytes = lib.stgcn_fold_prep_bytes(ctypes.byref(d))
+    assert nbytes > 0, "the block does not fold"
+    buf = torch.empty(nbytes, device=DEV, dtype=torch.uint8)
+    w = hl.FoldWeights(*[hl.ptr(cu[k]) for k in (
+        "spatialConv.A", "spatialConv.W.weight", "spatialConv.W.bias", "temporalConv.weight",
+        "temporalConv.bias")])
+    hl.check(lib.stgcn_fold_prep(1, (hl.Desc * 1)(d), (hl.FoldWeights * 1)(w),
+                                 (ctypes.c_void_p * 1)(hl.ptr(buf)), hl.stream_handle(DEV)))
+    return buf
+
+
+def _run_hip(pkg, arrays, x, g, need_dx=True, gemm="fp32", prep=False):
     """Fused block fwd+bwd on the GPU; returns the oracle-style result dict.
-    gemm: channel-GEMM arithmetic ("fp32", "f32x3", "bf16"; fused._gemm_flags)."""
+    gemm: channel-GEMM arithmetic ("fp32", "f32x3", "bf16"; fused._gemm_flags).
+    prep: the folded block's weight operands from stgcn_fold_prep (ABI 7)."""
     p, b = ref_cpu.block_params_from_arrays(arrays, dtype=torch.float32, requires_grad=False)
     stride, residual = int(arrays["meta"][2]), bool(arrays["meta"][7])
     cu = {k: v.to(DEV).contiguous().requires_grad_(True) for k, v in p.items()}
+    cc = None
+    if prep:
+        with torch.no_grad():
+            buf = _fold_prep(pkg, cu, x.shape, cu["temporalConv.weight"].shape[0],
+                             cu["spatialConv.A"].shape[0], stride, gemm)
+        cc = pkg.fused.ChainCtx(prep=buf)
     bu = {k: v.to(DEV).clone() for k, v in b.items() if "num_batches" not in k}
     xd = x.to(DEV).float().contiguous().requires_grad_(need_dx)
     common = (xd, cu["spatialConv.A"], cu["spatialConv.W.weight"], cu["spatialConv.W.bias"],
@@ -47,7 +72,7 @@ def _run_hip(pkg, arrays, x, g, need_dx=True, gemm="fp32"):
             stride, 4, 1e-5, 0.1, True, None, 0.0, gemm)
     else:
         y = pkg.fused.StgcnBlockFn.apply(*common, *running, stride, 4, 1e-5, 0.1, True,
-                                         None, 0.0, gemm)
+                                         cc, 0.0, gemm)
     y.backward(g.to(DEV).float())
     torch.cuda.synchronize()
     out = {"y": y.detach().cpu()}

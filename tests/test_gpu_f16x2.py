@@ -190,3 +190,27 @@ def test_f16x2_unfolded_blocks_keep_bf16x3(pkg):
                 torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6 * b[k].abs().max())
             else:
                 assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("gemm", ["f32x3", "f16x2", "f16x2_nog"])
+@pytest.mark.parametrize("case", [
+    (64, 64, 1, 18, 1, 2, 40),      # stride 1: one data-gradient launch
+    (64, 128, 2, 18, 1, 3, 37),     # stride 2: two data-gradient phases, odd T
+    (128, 256, 1, 18, 1, 2, 19),    # 128-row tiles
+])
+def test_fold_prep_matches_own_operands(pkg, case, gemm):
+    """ABI 7 stgcn_fold_prep (the stack's per-step weight operands in batched
+    launches) runs exactly the kernels and arithmetic the block runs on its own:
+    every output and gradient bit-identical (the adjacency gradient up to the
+    order of its fp32 atomic partial sums), and at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, *case)
+    a = _run_hip(pkg, arrays, x, g, gemm=gemm)
+    b = _run_hip(pkg, arrays, x, g, gemm=gemm, prep=True)
+    for k in a:
+        if k == "grad.spatialConv.A":
+            torch.testing.assert_close(b[k], a[k], rtol=1e-5, atol=1e-6 * a[k].abs().max())
+        else:
+            assert torch.equal(a[k], b[k]), k
+    want, floor = _oracle(arrays, b)
+    _compare(b, want, floor=floor)
+
