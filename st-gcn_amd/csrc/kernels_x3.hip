@@ -53,6 +53,9 @@
 #ifndef STGCN_X3_EXP  // timing experiments only (bits skip work; results wrong)
 #define STGCN_X3_EXP 0
 #endif
+#ifndef STGCN_SPB_EXP  // spb_epilogue timing experiments only (results wrong): bit 1 no dA
+#define STGCN_SPB_EXP 0  // partials / atomics, 2 no dxhat / BN1 pass, 4 no x DMA
+#endif
 #ifndef STGCN_BNA_EXP  // bna timing experiments only (results wrong): bit 1 no epilogue
 #define STGCN_BNA_EXP 0  // contraction, 2 no loader BN1, 4 no table / bound setup
 #endif
@@ -273,7 +276,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
         At[i] = v < V ? p.sA[v * V + w] : 0.f;
       }
     asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
-    for (int rr = wave; rr < 64; rr += 8) {
+    for (int rr = wave; rr < 64 && !(STGCN_SPB_EXP & 4); rr += 8) {
       const int c = r0 + h * 64 + rr;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -290,7 +293,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
+    if (!(STGCN_SPB_EXP & 2)) {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
       const int rl = tid >> 3, fg = tid & 7;
       const int c = r0 + h * 64 + rl;
       const bool rok = c < C;
@@ -379,6 +382,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     f2v dacc[18];  // (v, w pair) of this thread's 6 x 6 block
 #pragma unroll
     for (int i = 0; i < 18; ++i) dacc[i] = (f2v){0.f, 0.f};
+    if (STGCN_SPB_EXP & 1) continue;
     if (combo < 9) {
       for (int q = sub; q < 64 * FT; q += NSUB) {
         const int rr = q / FT, f = q - rr * FT;
