@@ -289,7 +289,7 @@ struct BwdLayout {
   float *Wpk;  // W' = [W_0 | ... | W_{K-1}] (C_out, K*C_in) for the stacked H GEMM
   float *Rg;  // residual projection data-grad (N, C_in, T, V)
   // the folded block: dU summed over clips, per-tap sums Tq, dWc, partials, Wc, bZ
-  double *fcs, *ftq, *fpart, *f64scr, *SdH;
+  double *fcs, *ftq, *f64scr, *SdH;
   float *dWc, *fscr;  // the fold GEMMs' operand re-layouts (kernels_fold.hip)
   float *Wc, *bZ;
   size_t dbl_bytes, total;
@@ -314,8 +314,6 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
     L.fcs = c.take<double>((size_t)apply_cols_chunks(d->N) * R * nTo(d));
     L.ftq = c.take<double>((size_t)9 * R * d->V);
     L.f64scr = c.take<double>(fold_sdz_scratch_doubles(R, C, d->V));
-    L.fpart = c.take<double>((size_t)R * apply_cols_chunks(d->N) * fold_tot_blocks(d->T_out) *
-                             d->V);
   }
   if (fold_w(d)) {
     L.dWc = c.take<float>(fold_dwc_floats(R, C));
@@ -1011,6 +1009,13 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   const float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
 
   HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
+  // (Tq's fp64 re-layout goes straight into launch_fold_sdz's scratch)
+  double *tqT = nullptr;
+  if (cols_sums(d))
+    tqT = fold_sdz_tq_slot(fold_spb(d) && a->prep && prep_applies(d)
+                               ? prep_layout(d, a->prep).f64
+                               : L.f64scr,
+                           R, C);
   if (!res) {
     // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias); the
     // reduction comes from the next block when it was chained (dy_sums)
@@ -1029,14 +1034,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                                           L.dU, L.dZ, L.sdu, N, R, To, V, d->training, drop,
                                           a->dy_coef, L.fcs, L.amax, L.amax + 2 * kAmaxWords,
                                           a->A, s));
-      HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.fpart, L.ftq,
+      HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.ftq, tqT,
                              s));
     } else if (cols_sums(d)) {
       HIP_TRY(launch_bn_relu_bwd_apply_cols(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
                                             L.dU, L.sdu, N, R, To * V, d->training, drop, s,
                                             du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs,
                                             f16x2(d) ? L.amax : nullptr));  // (f16x2: max |dU|)
-      HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.fpart, L.ftq,
+      HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.ftq, tqT,
                              s));
     } else {
       HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
@@ -1104,8 +1109,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     if (fold_spb(d)) {  // dbW and the bias part of dA first: the data gradient adds to dA;
       // BN1's sd from the dU sums (fp64, exact against the cancellation in sum dxhat)
       HIP_TRY(launch_fold_sdz(f64scr, a->Wt, Wc, L.ftq, R, C, V, L.SdZ, L.SdH, s, pre));
-      HIP_TRY(launch_spatial_small(L.SdZ, a->A, a->bW, K, R, V, a->dbW, a->dA, s));
-      HIP_TRY(launch_fold_sd(L.SdH, a->A, C, V, L.sd, s));
+      HIP_TRY(launch_fold_small_sd(L.SdZ, a->A, a->bW, R, V, a->dbW, a->dA, L.SdH, C, L.sd, s));
     }
     if (f16x2_dgrad(d) && !pre)  // the fp16 splits' operand scales: max |dU| (apply pass), max |Wc|
       HIP_TRY(launch_absmax(Wc, (int64_t)R * C * 9, L.amax + kAmaxWords, s));

@@ -92,7 +92,7 @@ struct ConvGemmParams {
   // s1 / s2 over the previous block's U read from sx) and dA += H^T BN1(x):
   // the SpatialConv backward never round-trips H through HBM.
   int spb;
-  int sd_given;  // sd already holds sum dxhat (launch_fold_sd): the epilogue adds only sdn
+  int sd_given;  // sd already holds sum dxhat (launch_fold_small_sd): the epilogue adds only sdn
   const float *sx, *sA, *mean1, *invstd1, *g1, *b1;
   PrevBn prev;
   double *sd, *sdn;
@@ -153,17 +153,21 @@ hipError_t launch_fold_fwd(const float *Wt, const float *W, const float *bt, con
                            float *scratch, hipStream_t s);
 hipError_t launch_fold_prep_bwd(const float *Wt, const float *W, int R, int C, float *scratch,
                                 hipStream_t s);
-int fold_tot_blocks(int To);
+// Tq (and, tqT non-null, its fp64 re-layout in launch_fold_sdz's scratch:
+// fold_sdz_tq_slot) from the clip-chunk sums
 hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
-                          double *part, double *Tq, hipStream_t s);
+                          double *Tq, double *tqT, hipStream_t s);
+double *fold_sdz_tq_slot(double *scratch, int R, int C);
 // SdZ = sum_{n,t} dZ and (Wc, SdH non-null) SdH = sum_{n,t} H from Tq, fp64
 // (pre: the scratch already holds the Wt / Wc re-layouts, launch_fold_prep)
 hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
                            int R, int C, int V, double *SdZ, double *SdH, hipStream_t s,
                            bool pre = false);
 // BN1's sd (db1) of the folded block from SdH: sd[c] = sum_v SdH[c][v] rowsum(A)[v]
-hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, double *sd,
-                          hipStream_t s);
+// launch_spatial_small (K = 1) and BN1's sd of the folded block (from SdH) in one launch
+hipError_t launch_fold_small_sd(const double *SdZ, const float *A, const float *bW, int R, int V,
+                                float *dbW, float *dA, const double *SdH, int C, double *sd,
+                                hipStream_t s);
 // The weight-only operands of several folded blocks, formed together once per
 // training step (capi.hip stgcn_fold_prep): bZ = bW rowsum(A), Wc = Wt W', the
 // bias table BT, max |Wc|, and the re-layouts the backward's small GEMMs read

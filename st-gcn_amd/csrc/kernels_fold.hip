@@ -430,43 +430,40 @@ hipError_t launch_fold_fwd(const float *Wt, const float *W, const float *bt, con
 // Tq[q][o][v] = sum_t cs[o][t][v] over the frames t whose tap q reads inside
 // [0, T) (all but a few boundary frames): the total minus those frames.
 // cs holds nz clip-chunk partials ([nz][R][To][V], k_bn_relu_bwd_apply_cols).
-// Two steps: k_fold_tot sums frame blocks of 16 (grid R x nz x blocks, one
-// partial per block and joint, fixed order), k_fold_tq adds the partials and
-// subtracts the boundary frames per tap.
-constexpr int kTotFrames = 16;
+// One launch, one block per output channel (R <= 512 blocks reading R nz To V
+// doubles: a few microseconds).
 
-__global__ __launch_bounds__(256) void k_fold_tot(const double *cs, int R, int V, int To,
-                                                  double *part) {
-  __shared__ double ts[256];
-  const int o = blockIdx.x, z = blockIdx.y, tb = blockIdx.z, tid = threadIdx.x;
-  const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
-  const double *c = cs + ((int64_t)z * R + o) * To * V;
-  double a = 0.0;
-  if (ph < PH)
-    for (int t = tb * kTotFrames + ph; t < min(To, (tb + 1) * kTotFrames); t += PH)
-      a += c[(int64_t)t * V + v];
-  ts[tid] = a;
-  __syncthreads();
-  if (tid >= V) return;
-  double tot = 0.0;
-  for (int p = 0; p < PH; ++p) tot += ts[p * V + tid];
-  part[(((int64_t)o * gridDim.y + z) * gridDim.z + tb) * V + tid] = tot;
-}
-
-// block = o; thread (phase ph, joint v): partial totals over the frame-block
-// partials k = ph, ph + PH, ..., and the boundary frame ph (< nsl) summed over
-// the clip chunks; LDS reduce; threads v < V form the nine taps
-__global__ __launch_bounds__(256) void k_fold_tq(const double *cs, const double *part, int np,
-                                                 int nz, int R, int V, int T, int To, int st,
-                                                 int nb0, int tb1, double *Tq) {
+// block = o; thread (phase ph, joint v): the total over the chunks' frames
+// t = ph, ph + PH, ... (in chunk order) and the boundary frame ph (< nsl) summed
+// over the clip chunks; LDS reduce; threads v < V form the nine taps. tqT (or
+// null): Tq also as the fp64 re-layout launch_fold_sdz reads ([q][Vp][Rp], zero
+// padded; blocks o >= R only write their padding column)
+__global__ __launch_bounds__(256) void k_fold_tq(const double *cs, int nz, int R, int V, int T,
+                                                 int To, int st, int nb0, int tb1, double *Tq,
+                                                 double *tqT) {
   __shared__ double ts[256], bs[8 * 256];  // (boundary slots x joints, V <= 256)
   const int o = blockIdx.x, tid = threadIdx.x;
+  const int Rp = pad32(R), Vp = pad32(V);
+  if (o >= R) {  // (tqT's zero padding columns)
+    for (int e = tid; e < 9 * Vp; e += 256) tqT[(int64_t)e * Rp + o] = 0.0;
+    return;
+  }
   const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
   const int nsl = nb0 + (To - tb1);
   const int64_t zs = (int64_t)R * To * V;
   double a = 0.0;
   if (ph < PH) {
-    for (int k = ph; k < np; k += PH) a += part[((int64_t)o * np + k) * V + v];
+    double a1 = 0.0;  // (two chains for the loads' latency)
+    for (int z = 0; z < nz; ++z) {
+      const double *c = cs + z * zs + (int64_t)o * To * V + v;
+      int t = ph;
+      for (; t + PH < To; t += 2 * PH) {
+        a += c[(int64_t)t * V];
+        a1 += c[(int64_t)(t + PH) * V];
+      }
+      if (t < To) a += c[(int64_t)t * V];
+    }
+    a += a1;
     for (int sl = ph; sl < nsl; sl += PH) {
       const int t = fold_slot_frame(sl, nb0, tb1);
       double b = 0.0;
@@ -476,6 +473,8 @@ __global__ __launch_bounds__(256) void k_fold_tq(const double *cs, const double 
   }
   ts[tid] = a;
   __syncthreads();
+  if (tqT && tid >= V && tid < Vp)  // (padding rows)
+    for (int q = 0; q < 9; ++q) tqT[((int64_t)q * Vp + tid) * Rp + o] = 0.0;
   if (tid >= V) return;
   double tot = 0.0;
   for (int p = 0; p < PH; ++p) tot += ts[p * V + tid];
@@ -486,6 +485,7 @@ __global__ __launch_bounds__(256) void k_fold_tq(const double *cs, const double 
       if (tt < 0 || tt >= T) r -= bs[sl * V + tid];
     }
     Tq[((int64_t)q * R + o) * V + tid] = r;
+    if (tqT) tqT[((int64_t)q * Vp + tid) * Rp + o] = r;
   }
 }
 
@@ -494,19 +494,20 @@ void fold_slots(int T, int To, int st, int &nb0, int &tb1) {
   tb1 = std::max(nb0, std::min(To, (T - 4 + st - 1) / st));  // frames with s t + 4 >= T
 }
 
-int fold_tot_blocks(int To) { return (To + kTotFrames - 1) / kTotFrames; }
-
-// part: R * nz * fold_tot_blocks(To) * V doubles
+// one launch (the frame totals are summed by the same blocks; one block per
+// output channel reads its nz * To * V sums)
 hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V, int st,
-                          double *part, double *Tq, hipStream_t s) {
+                          double *Tq, double *tqT, hipStream_t s) {
   if (V > 256) return hipErrorInvalidValue;  // (checked before any launch)
   int nb0, tb1;
   fold_slots(T, To, st, nb0, tb1);
-  const int ntb = fold_tot_blocks(To);
-  hipLaunchKernelGGL(k_fold_tot, dim3(R, nz, ntb), dim3(256), 0, s, cs, R, V, To, part);
-  hipLaunchKernelGGL(k_fold_tq, dim3(R), dim3(256), 0, s, cs, part, nz * ntb, nz, R, V, T, To, st,
-                     nb0, tb1, Tq);
+  hipLaunchKernelGGL(k_fold_tq, dim3(tqT ? pad32(R) : R), dim3(256), 0, s, cs, nz, R, V, T, To, st,
+                     nb0, tb1, Tq, tqT);
   return hipGetLastError();
+}
+
+double *fold_sdz_tq_slot(double *scratch, int R, int C) {
+  return scratch + (size_t)9 * pad32(R) * (pad32(R) + pad32(C));
 }
 
 // amax[0] = max(amax[0], max_i |x[i]|) as float bits (non-negative floats order
@@ -676,15 +677,16 @@ hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, co
   const int Rp = pad32(R), Cp = pad32(C), Vp = pad32(V);
   double *wtT = scratch, *wcT = wtT + (size_t)9 * Rp * Rp, *tqT = wcT + (size_t)9 * Cp * Rp;
   const TrJob jt = tr_job(Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, nullptr, nullptr, wtT);
-  const TrJob jq = tr_job(Tq, 1, 1, 0, 9, (int64_t)R * V, V, 1, R, V, nullptr, nullptr, nullptr, tqT);
-  if (pre)  // (the weight re-layouts were formed by launch_fold_prep)
-    HIP_RET(fold_tr({jq}, s));
-  else if (Wc)
-    HIP_RET(fold_tr({jt, jq, tr_job(Wc, 0, 1, 0, 9, 1, (int64_t)C * 9, 9, R, C, nullptr, nullptr,
-                                    nullptr, wcT)},
+  (void)Tq;  // (its re-layout tqT [q][Vp][Rp]: written by k_fold_tq, fold_sdz_tq_slot)
+  if (pre) {
+    // (the weight re-layouts were formed by launch_fold_prep)
+  } else if (Wc) {
+    HIP_RET(fold_tr({jt, tr_job(Wc, 0, 1, 0, 9, 1, (int64_t)C * 9, 9, R, C, nullptr, nullptr,
+                                nullptr, wcT)},
                     s));
-  else
-    HIP_RET(fold_tr({jt, jq}, s));
+  } else {
+    HIP_RET(fold_tr({jt}, s));
+  }
   Red64Jobs js{};
   Red64Job z{};
   z.A = wtT; z.aq = (int64_t)Rp * Rp; z.am = Rp;
@@ -710,30 +712,61 @@ hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, co
   return hipGetLastError();
 }
 
-// sum_{n,t,v} of the BN1-output gradient of the folded block (db1 = BN1's sd):
-// sd[c] = sum_v SdH[c][v] sum_w A[v][w]   (dxhat[c,t,w] = sum_v A[v][w] H[c,t,v])
-__global__ __launch_bounds__(256) void k_fold_sd(const double *SdH, const float *A, int C, int V,
-                                                 double *sd) {
-  __shared__ double rs[256];  // (V <= 256)
-  for (int v = threadIdx.x; v < V; v += blockDim.x) {
-    double a = 0.0;
-    for (int w = 0; w < V; ++w) a += (double)A[v * V + w];
-    rs[v] = a;
+// k_spatial_small (K = 1: dbW, the bias part of dA from SdZ) and BN1's sd of the
+// folded block (db1: sum_{n,t,v} of the BN1-output gradient,
+// sd[c] = sum_v SdH[c][v] sum_w A[v][w], since dxhat[c,t,w] = sum_v A[v][w] H[c,t,v])
+// in one launch: block 0 the first, blocks 1.. the second
+__global__ __launch_bounds__(256) void k_fold_small_sd(const double *SdZ, const float *A,
+                                                       const float *bW, int R, int V, float *dbW,
+                                                       float *dA, const double *SdH, int C,
+                                                       double *sd) {
+  __shared__ double rs[256], part[256];
+  const int tid = threadIdx.x;
+  for (int v = tid; v < V; v += 256) {
+    double ra = 0.0;
+    for (int w = 0; w < V; ++w) ra += (double)A[v * V + w];
+    rs[v] = ra;
   }
   __syncthreads();
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0.0;
-  for (int v = 0; v < V; ++v) a += SdH[(int64_t)c * V + v] * rs[v];
-  sd[c] = a;
+  if (blockIdx.x > 0) {  // sd
+    const int c = (blockIdx.x - 1) * blockDim.x + tid;
+    if (c >= C) return;
+    double a = 0.0;
+    for (int v = 0; v < V; ++v) a += SdH[(int64_t)c * V + v] * rs[v];
+    sd[c] = a;
+    return;
+  }
+  // k_spatial_small, K = 1
+  for (int co = tid; co < R; co += 256) {
+    double acc = 0.0;
+    for (int v = 0; v < V; ++v) acc += SdZ[co * V + v] * rs[v];
+    dbW[co] = (float)acc;
+  }
+  const int P = 256 / V;
+  const int v = tid % V, j = tid / V;
+  double acc = 0.0;
+  if (j < P)
+    for (int co = j; co < R; co += P) acc += (double)bW[co] * SdZ[co * V + v];
+  part[tid] = acc;
+  __syncthreads();
+  if (tid < V) {
+    double t = 0.0;
+    for (int jj = 0; jj < P; ++jj) t += part[jj * V + tid];
+    rs[tid] = t;  // (rowsums no longer needed: block 0 only)
+  }
+  __syncthreads();
+  for (int i = tid; i < V * V; i += 256) dA[i] = (float)rs[i / V];
 }
 
-hipError_t launch_fold_sd(const double *SdH, const float *A, int C, int V, double *sd,
-                          hipStream_t s) {
-  if (V > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_fold_sd, dim3((C + 255) / 256), dim3(256), 0, s, SdH, A, C, V, sd);
+hipError_t launch_fold_small_sd(const double *SdZ, const float *A, const float *bW, int R, int V,
+                                float *dbW, float *dA, const double *SdH, int C, double *sd,
+                                hipStream_t s) {
+  if (V > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_fold_small_sd, dim3(1 + (C + 255) / 256), dim3(256), 0, s, SdZ, A, bW, R, V,
+                     dbW, dA, SdH, C, sd);
   return hipGetLastError();
 }
+
 
 // ---------------------------------------------------------------------------
 // stgcn_fold_prep (capi.hip): the weight-only operands of every folded block of
