@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 7
+#define STGCN_ABI_VERSION 8
 
 /* ABI 7: words of max |y| after the 5 * C sums of a y_stats block */
 #define STGCN_STATS_AMAX_WORDS 2048
@@ -137,7 +137,8 @@ typedef struct stgcn_fwd_args {
   const float *A, *W, *bW, *Wt, *bWt;   /* SpatialConv.A / W ; temporalConv   */
   const float *g1, *b1, *g2, *b2;       /* batch_n / batch_n_2 affine         */
   float *rm1, *rv1, *rm2, *rv2;         /* running stats (updated if training)*/
-  float *y;                             /* out: N,C_out,T_out,V               */
+  float *y;                             /* out: N,C_out,T_out,V (ABI 8: may be
+                                         * null, see prev_U below)            */
   float *Z;                             /* saved: spatial output N,C_out,T,V
                                          * (fp32-sized; opaque under STGCN_F_BF16) */
   float *U;                             /* saved: temporal output N,C_out,T_out,V */
@@ -174,6 +175,16 @@ typedef struct stgcn_fwd_args {
   /* ABI 7, optional (folded blocks): the block's stgcn_fold_prep buffer of this
    * training step -- its weight-only operands are then not formed again */
   const void *prep;
+  /* ABI 8, optional stack chaining without the block output in HBM
+   * (STGCN_PLAN_X_FROM_U; training, with x_stats; non-residual previous block
+   * without dropout): the block input is x = ReLU(BN2_prev(prev_U)), formed
+   * where the block reads it, from the previous block's U, [mean2 | invstd2]
+   * (its stats + 2 * C_in_prev) and BN2 affine; x may then be null. The
+   * previous block's forward ran with y = null (a non-residual block without
+   * dropout, with y_stats: only the statistics of y are formed), and this
+   * block's backward is called with x = null, its kept G and the deferred-dx
+   * chain arguments (stgcn_bwd_args_t prev_*, x_stats, dx_coef, dx_deferred). */
+  const float *prev_U, *prev_stats, *prev_g2, *prev_b2;
 } stgcn_fwd_args_t;
 
 /* Backward arguments: the gradients of every input of the forward. */
@@ -226,6 +237,10 @@ typedef struct stgcn_bwd_args {
   const float *dy_coef;
   /* ABI 7, optional: the same stgcn_fold_prep buffer as the forward's */
   const void *prep;
+  /* ABI 8: x may be null when the forward took its input from prev_U
+   * (STGCN_PLAN_X_FROM_U); the call then needs the kept G and the deferred-dx
+   * arguments (prev_U, prev_stats, prev_g2, prev_b2, prev_sums, x_stats, dx_coef,
+   * dx_deferred) and fails with STGCN_E_INVALID where it could not defer. */
 } stgcn_bwd_args_t;
 
 int stgcn_abi_version(void);
@@ -284,6 +299,10 @@ int stgcn_spatial_bwd(const stgcn_spatial_desc_t *d, const float *dout, const fl
                                     * contraction in its epilogue), the weight gradient reads
                                     * x against dU A; the kept-G buffer (stgcn_keep_g_bytes)
                                     * then carries only max |x| to the backward          */
+#define STGCN_PLAN_X_FROM_U 512    /* ABI 8: the training forward can take its input as
+                                    * ReLU(BN2(U)) of the previous block
+                                    * (stgcn_fwd_args_t.prev_U): that block's y is never
+                                    * written                                             */
 int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan);
 
 /* ABI 7: the weight-only operands of a stack's folded blocks (STGCN_PLAN_FOLD),

@@ -1,7 +1,9 @@
-"""A/B variant library that differs from the default build only in
-kernels_spbwd.hip (-D defines): compiles that one source and links it with the
-default build's other objects (st-gcn_amd/build/default). Usage:
-  python scripts/build_spb_variant.py <name> DEFINE=VAL [...]  -> lib/libstgcn_hip_<name>.so"""
+"""A/B variant library that differs from the default build only in one source
+(kernels_spbwd.hip, or VARIANT_SRC=<file>) built with -D defines: compiles that
+one source and links it with the default build's other objects
+(st-gcn_amd/build/default). Usage:
+  [VARIANT_SRC=kernels_x3.hip] python scripts/build_spb_variant.py <name> DEFINE=VAL [...]
+  -> lib/libstgcn_hip_<name>.so"""
 import os
 import subprocess
 import sys
@@ -14,10 +16,11 @@ import build  # noqa: E402
 name, defs = sys.argv[1], sys.argv[2:]
 objdir = os.path.join(PKG, "build", name)
 os.makedirs(objdir, exist_ok=True)
-obj = os.path.join(objdir, "kernels_spbwd.hip.o")
+src = os.environ.get("VARIANT_SRC", "kernels_spbwd.hip")
+obj = os.path.join(objdir, src + ".o")
 subprocess.run([build.HIPCC, *build.FLAGS, *[f"-D{d}" for d in defs], "-c",
-                os.path.join(build.CSRC, "kernels_spbwd.hip"), "-o", obj], check=True)
-objs = [obj if s == "kernels_spbwd.hip" else os.path.join(PKG, "build", "default", s + ".o")
+                os.path.join(build.CSRC, src), "-o", obj], check=True)
+objs = [obj if s == src else os.path.join(PKG, "build", "default", s + ".o")
         for s in build.SOURCES]
 out = os.path.join(PKG, "lib", f"libstgcn_hip_{name}.so")
 subprocess.run([build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out],

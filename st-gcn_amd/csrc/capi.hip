@@ -162,6 +162,14 @@ bool fold_bna(const stgcn_desc_t *d) {
   p.s_out = 1;
   return conv_x3_bna_supported(p);
 }
+// ABI 8 (STGCN_PLAN_X_FROM_U): the training forward of a folded block that forms
+// G (k_gather4) can read its input as ReLU(BN2_prev(U_prev)) of the previous
+// block -- that block then writes only y's statistics, not y -- and its fused
+// backward (spb_epilogue, deferred dx) already reads U_prev in place of x
+bool x_from_u(const stgcn_desc_t *d) {
+  return d->training && fold_spb(d) && !fold_bna(d) && d->K == 1 &&
+         gather_prev_supported(d->C_in, d->T, d->V);
+}
 
 // sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
 // sums written by the ReLU + BN2 backward apply, k_fold_tq, one small GEMM with
@@ -713,6 +721,7 @@ int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan) {
   }
   if (f16x2(d)) f |= STGCN_PLAN_F16X2;
   if (fold_bna(d)) f |= STGCN_PLAN_FOLD_NO_G;
+  if (x_from_u(d)) f |= STGCN_PLAN_X_FROM_U;
   *plan = f;
   return STGCN_OK;
 }
@@ -802,13 +811,22 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
   const bool res = residual(d);
-  if (!a || !a->x || !a->A || !a->W || !a->bW || !a->Wt || !a->bWt || !a->g1 || !a->b1 ||
-      !a->g2 || !a->b2 || !a->y || !a->Z || (!res && !a->U) || !a->stats)
+  // ABI 8: x from the previous block's U (STGCN_PLAN_X_FROM_U); y null: statistics only
+  const bool xu = a && a->prev_U;
+  const bool ystats_only = a && !a->y && a->y_stats && d->training && !res && a->dropout_p == 0.f;
+  if (!a || (!a->x && !xu) || !a->A || !a->W || !a->bW || !a->Wt || !a->bWt || !a->g1 ||
+      !a->b1 || !a->g2 || !a->b2 || (!a->y && !ystats_only) || !a->Z || (!res && !a->U) ||
+      !a->stats)
     return fail(STGCN_E_INVALID, "null tensor argument");
   if (res && (!a->Za || (projection(d) && (!a->Wr || !a->br))))
     return fail(STGCN_E_INVALID, "residual block: null Za / projection weights");
   if (!a->rm1 || !a->rv1 || !a->rm2 || !a->rv2)
     return fail(STGCN_E_INVALID, "null running-stat buffer");
+  if (xu && (!x_from_u(d) || !a->x_stats || !a->prev_stats || !a->prev_g2 || !a->prev_b2 ||
+             ((uintptr_t)a->prev_U & 15) != 0))
+    return fail(STGCN_E_INVALID,
+                "prev_U input: needs STGCN_PLAN_X_FROM_U, x_stats, prev_stats / prev_g2 / "
+                "prev_b2 and a 16-byte aligned prev_U");
   const FwdLayout L = fwd_layout(d, workspace);
   if (!workspace || workspace_bytes < L.total)
     return fail(STGCN_E_INVALID, "workspace too small");
@@ -857,8 +875,16 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
                                (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s));
   } else if (!bna) {
   float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
-  HIP_TRY(launch_gather_fwd(a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C, T, V, K, res, s,
-                            f16x2(d) ? L.amax : nullptr));  // (f16x2: max |G| on the way)
+  PrevBn pv;  // (x = ReLU(BN2_prev(prev_U)) formed on load)
+  if (xu) {
+    pv.mean = a->prev_stats;
+    pv.invstd = a->prev_stats + C;
+    pv.g = a->prev_g2;
+    pv.b = a->prev_b2;
+  }
+  HIP_TRY(launch_gather_fwd(xu ? a->prev_U : a->x, mean1, invstd1, a->g1, a->b1, a->A, G, N, C,
+                            T, V, K, res, s, f16x2(d) ? L.amax : nullptr,  // (f16x2: max |G|)
+                            xu ? &pv : nullptr));
   Gfold = G;
   if (!fold) {
     ConvGemmParams p = conv_base(d, L.wpk);
@@ -971,7 +997,8 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   const Dropout ydrop = make_dropout(d, a->dropout_p, a->seed);
   // (ABI 5: y_stats holds 5 * C_out sums; the last three -- over the ReLU mask --
   // feed the next block's deferred-dx chain, meaningless under dropout; ABI 7:
-  // then max y in STGCN_STATS_AMAX_WORDS words, the next block's operand bound)
+  // then max y in STGCN_STATS_AMAX_WORDS words, the next block's operand bound;
+  // ABI 8, y null: only these -- k_bn_relu_stats)
   if (ys) HIP_TRY(hipMemsetAsync(ys, 0, y_stats_bytes(R), s));
   HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
                              ys ? ys + R : nullptr, ydrop, s,
@@ -985,7 +1012,12 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
   const bool res = residual(d);
-  if (!a || !a->dy || !a->x || !a->Z || (!res && !a->U) || !a->stats || !a->A || !a->W ||
+  // ABI 8: x null after a forward from prev_U -- the fused folded backward reads
+  // prev_U (deferred dx) and the kept G, nothing else reads x
+  const bool xnull = a && !a->x;
+  if (xnull && (res || !fold_spb(d) || fold_bna(d) || !a->G))
+    return fail(STGCN_E_INVALID, "x null: needs a folded block (STGCN_PLAN_X_FROM_U) and its kept G");
+  if (!a || !a->dy || (!a->x && !xnull) || !a->Z || (!res && !a->U) || !a->stats || !a->A || !a->W ||
       !a->bW || !a->Wt || !a->g1 || !a->b1 || !a->g2 || !a->b2 || !a->dA || !a->dW || !a->dbW ||
       !a->dWt || !a->dbWt || !a->dg1 || !a->db1 || !a->dg2 || !a->db2 || (d->need_dx && !a->dx))
     return fail(STGCN_E_INVALID, "null tensor argument");
@@ -1007,6 +1039,15 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   const int N = d->N, C = d->C_in, R = d->C_out, T = d->T, To = d->T_out, V = d->V, K = d->K;
   const float *mean1 = a->stats, *invstd1 = a->stats + C;
   const float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
+  // deferred dx (ABI 5; below)
+  const bool defer = d->need_dx && d->training && !res && a->prev_g2 && a->prev_b2 &&
+                     a->prev_sums && a->prev_U && a->prev_stats && a->x_stats && a->dx_coef &&
+                     a->dx_deferred &&
+                     (fused_spb(d) || fold_spb(d) || spatial_dx_prev_supported(N, C, T, V, K));
+  if (xnull && !defer)
+    return fail(STGCN_E_INVALID,
+                "x null: the backward must defer dx (prev_U, prev_stats, prev_g2 / prev_b2, "
+                "prev_sums, x_stats, dx_coef, dx_deferred)");
 
   HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
   // (Tq's fp64 re-layout goes straight into launch_fold_sdz's scratch)
@@ -1066,10 +1107,6 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   // x (PrevBn: x rebuilt, that block's mask / uhat sums), dx receives dxhat, and
   // launch_chain_coef forms dg1 / db1, the coefficients and the previous block's
   // ReLU+BN2 sums: dx never makes its own HBM round trip.
-  const bool defer = d->need_dx && d->training && !res && a->prev_g2 && a->prev_b2 &&
-                     a->prev_sums && a->prev_U && a->prev_stats && a->x_stats && a->dx_coef &&
-                     a->dx_deferred &&
-                     (fused_spb(d) || fold_spb(d) || spatial_dx_prev_supported(N, C, T, V, K));
   PrevBn pvb;
   if (defer) {
     pvb.mean = a->prev_stats;

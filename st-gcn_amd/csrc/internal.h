@@ -337,7 +337,10 @@ hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, int relu, hipStream_t s,
-                             unsigned *amax = nullptr);
+                             unsigned *amax = nullptr, const PrevBn *pv = nullptr);
+// pv (x = ReLU(BN2_prev(U)) from the previous block's U, ABI 8) runs on
+// k_gather4 only: K = 1, 16-byte aligned x / G and these shapes
+bool gather_prev_supported(int C, int T, int V);
 hipError_t launch_sum_nt(const float *X, int N, int C, int T, int V, double *out,
                          hipStream_t s, int x_bf16 = 0);
 hipError_t launch_spatial_small(const double *SdZ, const float *A, const float *bW, int K,

@@ -1497,14 +1497,15 @@ hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_
 // of squares of y (fp64): the next block's BN1 batch statistics. A block
 // covers kBnRows clips of one channel (one block reduction and one set of
 // fp64 atomics per kBnRows rows: per-row blocks spent their time there).
+// (y null, ABI 8: only the statistics -- the next block forms y itself from U,
+// STGCN_PLAN_X_FROM_U -- as k_bn_relu_stats, so traces tell the two apart)
 constexpr int kBnRows = 4;
-template <int VEC>
-__global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
-                                                     const float *invstd, const float *g,
-                                                     const float *b, float *y, int N, int C,
-                                                     int L, double *ysum, double *ysq,
-                                                     Dropout drop, double *yext,
-                                                     unsigned *ymax) {
+template <int VEC, bool WY>
+__device__ __forceinline__ void bn_relu_fwd_body(const float *U, const float *mean,
+                                                 const float *invstd, const float *g,
+                                                 const float *b, float *y, int N, int C, int L,
+                                                 double *ysum, double *ysq, Dropout drop,
+                                                 double *yext, unsigned *ymax) {
   __shared__ double red[8];
   const int c = blockIdx.x, n0 = blockIdx.y * kBnRows, n1 = min(N, n0 + kBnRows);
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
@@ -1530,7 +1531,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
           xu += (double)v[j] * (double)uh;
         }
       }
-      vst<VEC>(y + base + i, v);
+      if constexpr (WY) vst<VEC>(y + base + i, v);
     }
   }
   if (ysum) block_sum2_atomic<256>(s, q, ysum + c, ysq + c, red);
@@ -1541,10 +1542,36 @@ __global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float
   if (ymax) block_amax<256>(ym, ymax);
 }
 
+template <int VEC>
+__global__ __launch_bounds__(256) void k_bn_relu_fwd(const float *U, const float *mean,
+                                                     const float *invstd, const float *g,
+                                                     const float *b, float *y, int N, int C,
+                                                     int L, double *ysum, double *ysq,
+                                                     Dropout drop, double *yext,
+                                                     unsigned *ymax) {
+  bn_relu_fwd_body<VEC, true>(U, mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext, ymax);
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256) void k_bn_relu_stats(const float *U, const float *mean,
+                                                       const float *invstd, const float *g,
+                                                       const float *b, float *y, int N, int C,
+                                                       int L, double *ysum, double *ysq,
+                                                       Dropout drop, double *yext,
+                                                       unsigned *ymax) {
+  bn_relu_fwd_body<VEC, false>(U, mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext, ymax);
+}
+
 hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *invstd,
                               const float *g, const float *b, float *y, int N, int C, int L,
                               double *ysum, double *ysq, Dropout drop, hipStream_t s,
                               double *yext, unsigned *ymax) {
+  if (!y) {
+    if (!ysum) return hipErrorInvalidValue;  // (nothing to form)
+    STGCN_VEC_LAUNCH(k_bn_relu_stats, slice_vec(L, {U}), dim3(C, (N + kBnRows - 1) / kBnRows), U,
+                     mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext, ymax);
+    return hipGetLastError();
+  }
   STGCN_VEC_LAUNCH(k_bn_relu_fwd, slice_vec(L, {U, y}), dim3(C, (N + kBnRows - 1) / kBnRows), U,
                    mean, invstd, g, b, y, N, C, L, ysum, ysq, drop, yext, ymax);
   return hipGetLastError();
@@ -2226,6 +2253,8 @@ __global__ __launch_bounds__(256) void k_gather3(const float *__restrict__ x,
 // they arrive by 16-byte LDS-DMA, each thread contracts its row from LDS (A in
 // LDS), and the outputs leave through LDS as float4 stores. (A persistent,
 // double-buffered variant measured slower: fewer workgroups per CU.)
+// pv.mean non-null (ABI 8, STGCN_PLAN_X_FROM_U): x holds the previous block's U
+// and the input is ReLU(BN2_prev(U)), formed as k_bn_relu_fwd forms its y.
 template <int V>
 __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
                                                  const float *__restrict__ mean,
@@ -2234,7 +2263,7 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
                                                  const float *__restrict__ b,
                                                  const float *__restrict__ A, float *G, int C,
                                                  int T, int K, int64_t rows, int relu,
-                                                 unsigned *amax) {
+                                                 unsigned *amax, PrevBn pv) {
   constexpr int VP = JointCfg<V>::VP;
   constexpr int BF = 256 * V;  // floats of a block (a multiple of 256: V DMA rounds)
   float gm = 0.f;
@@ -2259,11 +2288,19 @@ __global__ __launch_bounds__(256) void k_gather4(const float *__restrict__ x,
   const int64_t n0 = r0 / CT, rem0 = r0 - n0 * CT;
   const int ci = (int)((rem0 + tid) / T);
   const float mu = mean[ci], a = invstd[ci] * g[ci], be = b[ci];
+  const bool prev = pv.mean != nullptr;
+  const float pmu = prev ? pv.mean[ci] : 0.f, pa = prev ? pv.invstd[ci] * pv.g[ci] : 0.f;
+  const float pbe = prev ? pv.b[ci] : 0.f;
   __syncthreads();
   float xv[VP];
 #pragma unroll
   for (int w = 0; w < VP; ++w) {
-    const float t = w < V ? (xs[tid * V + w] - mu) * a + be : 0.f;
+    float xx = w < V ? xs[tid * V + w] : 0.f;
+    if (prev) {
+      const float u = (xx - pmu) * pa + pbe;
+      xx = u > 0.f ? u : 0.f;
+    }
+    const float t = w < V ? (xx - mu) * a + be : 0.f;
     xv[w] = relu ? fmaxf(t, 0.f) : t;
   }
   for (int k = 0; k < K; ++k) {
@@ -3165,11 +3202,21 @@ static int bwd3_rows(int V, int K) {
 
 static bool joint_fast(int V) { return V == 18 || V == 25 || V == 50; }
 
+bool gather_prev_supported(int C, int T, int V) {
+  return STGCN_AB_JOINT3 == 0 && joint_fast(V) && ((int64_t)C * T) % 256 == 0 &&
+         sizeof(float) * ((size_t)2 * 256 * V + (size_t)V * ((V + 3) & ~3)) <= 160 * 1024;
+}
+
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
-                             int C, int T, int V, int K, int relu, hipStream_t s, unsigned *amax) {
+                             int C, int T, int V, int K, int relu, hipStream_t s, unsigned *amax,
+                             const PrevBn *pv) {
   constexpr bool joint3 = STGCN_AB_JOINT3 != 0;  // A/B builds only (ab_switches.h)
-  if (!joint3 && !amax && K > 1 && (V == 25 || V == 50) && ((uintptr_t)x & 15) == 0 &&
+  const PrevBn pvb = pv ? *pv : PrevBn{};
+  if (pv && (K != 1 || !gather_prev_supported(C, T, V) || ((uintptr_t)x & 15) != 0 ||
+             ((uintptr_t)G & 15) != 0))
+    return hipErrorInvalidValue;  // (x from U: k_gather4 only; checked by the caller first)
+  if (!pv && !joint3 && !amax && K > 1 && (V == 25 || V == 50) && ((uintptr_t)x & 15) == 0 &&
       ((uintptr_t)G & 15) == 0) {  // partitioned graphs: contraction on MFMA
     const int64_t rows = (int64_t)N * C * T;
     const bool done =
@@ -3185,11 +3232,11 @@ hipError_t launch_gather_fwd(const float *x, const float *mean, const float *inv
     const int64_t rows = (int64_t)N * C * T;
     const dim3 grid4((unsigned)(rows / 256));
     if (V == 18)
-      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
+      hipLaunchKernelGGL(k_gather4<18>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax, pvb);
     else if (V == 25)
-      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
+      hipLaunchKernelGGL(k_gather4<25>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax, pvb);
     else
-      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax);
+      hipLaunchKernelGGL(k_gather4<50>, grid4, dim3(256), lds4, s, x, mean, invstd, g, b, A, G, C, T, K, rows, relu, amax, pvb);
     return hipGetLastError();
   }
   if (joint_fast(V)) {

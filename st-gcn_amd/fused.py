@@ -87,6 +87,50 @@ class ChainCtx:
         self.prev_U, self.prev_stats = prev_U, prev_stats
         # this block's (U, [mean2 | invstd2]) for the next block's link
         self.U, self.stats2 = None, None
+        # ABI 8: this block's y is not written (the next block forms it from U);
+        # this block's input is the previous block's ReLU(BN2(prev_U)) (x unwritten)
+        self.y_lazy, self.x_from_u = False, False
+
+
+def stack_descs(blocks, x_shape, training=True):
+    """The training descriptors of a block stack's blocks (network.SpatialTemporalConv,
+    in order) for a stack input of shape x_shape (N, C, T, V)."""
+    N, C, T, V = x_shape
+    out = []
+    for blk in blocks:
+        sc, tc = blk.spatialConv, blk.temporalConv
+        desc = make_desc((N, C, T, V), tc.out_channels, sc.A.shape[0], blk.stride, blk.pad,
+                         blk.batch_n.eps, blk.batch_n.momentum, training,
+                         residual=blk.residual, **_gemm_flags(blk.gemm_mode()))
+        out.append(desc)
+        C, T = tc.out_channels, desc.T_out
+    return out
+
+
+def _hooked(m):
+    """Forward hooks that could see a block's output or input (module-level or global)."""
+    from torch.nn.modules import module as _mod
+    return bool(m._forward_hooks or m._forward_pre_hooks
+                or getattr(_mod, "_global_forward_hooks", None)
+                or getattr(_mod, "_global_forward_pre_hooks", None))
+
+
+def lazy_links(blocks, x_shape):
+    """Per block of a training stack: True when its output y can stay unwritten --
+    the next block reads the block's U and forms ReLU(BN2(U)) on load (ABI 8,
+    STGCN_PLAN_X_FROM_U). Needs a non-residual block without dropout feeding a
+    block with that plan, and no forward hooks that could observe y."""
+    descs = stack_descs(blocks, x_shape)
+    out = []
+    for i, blk in enumerate(blocks):
+        ok = False
+        if i + 1 < len(blocks):
+            nxt = blocks[i + 1]
+            drop = blk.dropout.p if blk.dropout is not None else 0.0
+            ok = (not blk.residual and drop == 0 and not _hooked(blk) and not _hooked(nxt)
+                  and bool(hip_lib.block_plan(descs[i + 1]) & hip_lib.PLAN_X_FROM_U))
+        out.append(ok)
+    return out
 
 
 class FoldPrep:
@@ -104,14 +148,10 @@ class FoldPrep:
         """blocks: the stack's SpatialTemporalConv modules in order; x_shape the
         stack input (N, C, T, V). Returns one prep tensor (or None) per block."""
         lib = hip_lib.lib()
-        N, C, T, V = x_shape
         descs, weights, ptrs, out = [], [], [], []
-        for i, blk in enumerate(blocks):
+        for i, (blk, desc) in enumerate(zip(blocks, stack_descs(blocks, x_shape))):
             sc, tc = blk.spatialConv, blk.temporalConv
             gemm = blk.gemm_mode()
-            desc = make_desc((N, C, T, V), tc.out_channels, sc.A.shape[0], blk.stride, blk.pad,
-                             blk.batch_n.eps, blk.batch_n.momentum, True,
-                             residual=blk.residual, **_gemm_flags(gemm))
             nbytes = lib.stgcn_fold_prep_bytes(ctypes.byref(desc))
             buf = None
             if nbytes:
@@ -125,7 +165,6 @@ class FoldPrep:
                     sc.A, sc.W.weight, sc.W.bias, tc.weight, tc.bias)]))
                 ptrs.append(hip_lib.ptr(buf))
             out.append(buf)
-            C, T = tc.out_channels, desc.T_out
         if descs:
             n = len(descs)
             hip_lib.check(lib.stgcn_fold_prep(
@@ -240,10 +279,19 @@ class StgcnBlockFn(torch.autograd.Function):
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         prep = cc.prep if cc is not None else None
+        # ABI 8: x never written (the previous block's ReLU(BN2(U)) formed on load);
+        # y not written (the next block does the same)
+        xu = cc is not None and cc.x_from_u
+        y_lazy = cc is not None and cc.y_lazy
         args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (
-            x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2, y, Z, U, stats,
+            None if xu else x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
+            None if y_lazy else y, Z, U, stats,
             None, None, None, G, cc and cc.x_stats, cc and cc.y_stats)], drop, seed,
             prep=hip_lib.ptr(prep))
+        if xu:
+            args.prev_U, args.prev_stats = hip_lib.ptr(cc.prev_U), hip_lib.ptr(cc.prev_stats)
+            args.prev_g2, args.prev_b2 = hip_lib.ptr(cc.prev_g2), hip_lib.ptr(cc.prev_b2)
+        ctx.x_lazy = xu
         hip_lib.check(lib.stgcn_block_fwd(ctypes.byref(desc), ctypes.byref(args),
                                           hip_lib.ptr(ws), nbytes, hip_lib.stream_handle(dev)))
         ctx.save_for_backward(x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G)
@@ -276,7 +324,7 @@ class StgcnBlockFn(torch.autograd.Function):
         nbytes = lib.stgcn_bwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=x.device, dtype=torch.uint8)
         args = _args(hip_lib.BwdArgs, [hip_lib.ptr(t) for t in (
-            dy, x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
+            dy, None if ctx.x_lazy else x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, dx,
             grads[0], grads[1], grads[2], grads[3], dbWt, dg1, db1, dg2, db2,
             None, None, None, None, None, G, dy_sums, pg2, pb2, psums)], *ctx.drop,
             prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst), x_stats=hip_lib.ptr(xst),

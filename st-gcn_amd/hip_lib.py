@@ -21,7 +21,7 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
     import sys
     print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
-ABI_VERSION = 7
+ABI_VERSION = 8
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -31,6 +31,7 @@ F_NO_G = 16     # ABI 7, with F_F16X2: the folded block without G (memory-lean)
 PLAN_FOLD, PLAN_SP_FWD_FUSED, PLAN_SP_BWD_FUSED, PLAN_ACT_BF16 = 1, 2, 4, 8
 PLAN_WSP_SPLIT, PLAN_TCONV_SPLIT, PLAN_TWGRAD_SPLIT, PLAN_F16X2 = 16, 32, 64, 128
 PLAN_FOLD_NO_G = 256
+PLAN_X_FROM_U = 512  # ABI 8: the input as ReLU(BN2(U)) of the previous block
 # ABI 7: a y_stats / x_stats block: 5 * C doubles, then STATS_AMAX_WORDS uint32 (max |y|)
 STATS_AMAX_WORDS = 2048
 
@@ -60,7 +61,8 @@ class FwdArgs(ctypes.Structure):
         "G",                     # ABI 2: optional kept joint contraction
         "x_stats", "y_stats")    # ABI 2: optional stack chaining
     ] + [("dropout_p", _c_float), ("seed", ctypes.c_uint64)  # ABI 2: fused dropout
-         ] + [("prep", _vp)]                                  # ABI 7: stgcn_fold_prep
+         ] + [("prep", _vp)                                   # ABI 7: stgcn_fold_prep
+              ] + [(n, _vp) for n in ("prev_U", "prev_stats", "prev_g2", "prev_b2")]  # ABI 8
 
 
 class BwdArgs(ctypes.Structure):

@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from .graph import Strategy, get_normalized_adjacency_matrices
-from .fused import FoldPrep
+from .fused import FoldPrep, lazy_links
 from .network import SpatialTemporalConv, StackChain
 from .train_ops import StgcnHeadFn
 
@@ -67,6 +67,10 @@ class STGCNStack(nn.Module):
             if getattr(self, "_fold_prep", None) is None:
                 self._fold_prep = FoldPrep()
             chain.set_prep(self._fold_prep.run(list(self.conv), tuple(x.shape), x.device))
+            # (ABI 8: block outputs that only the next block reads stay unwritten;
+            # self.lazy_links = False writes every one)
+            if getattr(self, "lazy_links", True):
+                chain.set_lazy(lazy_links(list(self.conv), tuple(x.shape)))
         return chain
 
     def forward_nctv(self, x):

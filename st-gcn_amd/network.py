@@ -36,6 +36,17 @@ class StackChain:
     def reset(self):
         self.y, self.y_version, self.y_stats, self.link, self.g2b2 = None, None, None, None, None
         self.u_stats = None
+        self.y_lazy = False  # self.y was not written (ABI 8): the next block reads U
+
+    def set_lazy(self, flags):
+        """Per block: its output goes to the next block as ReLU(BN2(U)) formed on
+        load, and is never written (ABI 8, STGCN_PLAN_X_FROM_U; model.STGCNStack
+        decides, knowing the next block)."""
+        self.lazy = list(flags)
+
+    def next_lazy(self):
+        lazy = getattr(self, "lazy", None)
+        return lazy.pop(0) if lazy else False
 
     def set_prep(self, preps):
         """The stack's per-block stgcn_fold_prep buffers of this step (fused.FoldPrep),
@@ -159,6 +170,12 @@ class SpatialTemporalConv(nn.Module):
         drop = self.dropout.p if (self.dropout is not None and training) else 0.0
         gemm = self.gemm_mode()
         cc = None
+        lazy = chain.next_lazy() if chain is not None else False
+        if chain is not None and chain.y_lazy and not (
+                training and x is chain.y and x._version == chain.y_version
+                and chain.link is not None):
+            raise RuntimeError("STGCNStack chain: a block output that was never written "
+                               "(formed by the next block from U) reached other code")
         if chain is not None and training:
             # (the backward link derives this block's ReLU mask from its output:
             # not with dropout on that output, nor for the residual block)
@@ -169,12 +186,14 @@ class SpatialTemporalConv(nn.Module):
                               device=x.device, dtype=torch.float64),
                           prep=chain.next_prep(),
                           out_link=None if (self.residual or drop > 0) else Link())
+            cc.y_lazy = bool(lazy) and cc.out_link is not None
             if chain.y is not None and x is chain.y and x._version == chain.y_version:
                 cc.x_stats = chain.y_stats
                 if chain.link is not None:
                     cc.in_link = chain.link
                     cc.prev_g2, cc.prev_b2 = chain.g2b2
                     cc.prev_U, cc.prev_stats = chain.u_stats
+                    cc.x_from_u = chain.y_lazy
         if self.residual:
             proj = self.apply_residual if isinstance(self.apply_residual, nn.Conv2d) else None
             y = StgcnResBlockFn.apply(
@@ -195,6 +214,7 @@ class SpatialTemporalConv(nn.Module):
                 chain.reset()
             else:
                 chain.y, chain.y_version, chain.y_stats = y, y._version, cc.y_stats
+                chain.y_lazy = cc.y_lazy
                 chain.link = cc.out_link
                 chain.g2b2 = None if self.residual else (bn2.weight, bn2.bias)
                 chain.u_stats = None if self.residual else (cc.U, cc.stats2)

@@ -629,3 +629,54 @@ def test_stack_bf16_multi_seed(pkg, V):
     worst = sorted(ratios.items(), key=lambda kv: -kv[1])[:5]
     print(f"V={V} worst mean err / ref-bf16 floor:", [(k, round(r, 2)) for k, r in worst])
     assert not bad, "; ".join(bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f32_gemm", ["f16x2", "bf16x3"])
+def test_stack_lazy_links_bit_identical(pkg, f32_gemm):
+    """ABI 8 (STGCN_PLAN_X_FROM_U): inside the training stack a block output that
+    only the next block reads is never written -- the block writes only y's
+    statistics (k_bn_relu_stats) and the next block's gather forms
+    ReLU(BN2(U)) from U as k_bn_relu_fwd would. The step must be bit-identical
+    to the stack that writes every output (loss, logits, every gradient, running
+    stats), and a forward hook on a block keeps that block's output (and its
+    input) written and exact."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    torch.manual_seed(3)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 400, A, f32_gemm=f32_gemm).cuda().train()
+        m2 = pkg.STGCNStack(3, 400, A, f32_gemm=f32_gemm).cuda().train()
+    m2.load_state_dict(m1.state_dict())
+    m2.lazy_links = False
+    x = torch.randn(4, 3, 300, 18, generator=torch.Generator().manual_seed(4)).cuda()
+    lab = torch.randint(0, 400, (4,), generator=torch.Generator().manual_seed(5)).cuda()
+    flags = pkg.fused.lazy_links(list(m1.conv), tuple(x.shape))
+    assert flags == [True] * 9 + [False], flags
+    seen = {}
+    hook = m1.conv[4].register_forward_hook(lambda m, i, o: seen.__setitem__("y4", o.clone()))
+    flags_h = pkg.fused.lazy_links(list(m1.conv), tuple(x.shape))
+    assert flags_h == [True] * 3 + [False, False] + [True] * 4 + [False], flags_h
+    hook.remove()
+    for step in range(2):
+        hooks = []
+        if step == 1:  # an observed output: written, and the same as the unlazy stack's
+            for m, key in ((m1, "y4"), (m2, "y4_ref")):
+                hooks.append(m.conv[4].register_forward_hook(
+                    lambda mod, i, o, key=key: seen.__setitem__(key, o.detach().clone())))
+        loss1, out1 = m1.forward_loss(x, lab)
+        loss2, out2 = m2.forward_loss(x, lab)
+        for h in hooks:
+            h.remove()
+        m1.zero_grad()
+        m2.zero_grad()
+        loss1.backward()
+        loss2.backward()
+        torch.cuda.synchronize()
+        assert torch.equal(out1, out2) and torch.equal(loss1, loss2), step
+        for (k, a), b in zip(m1.named_parameters(), m2.parameters()):
+            assert torch.equal(a.grad, b.grad), (step, k)
+        for (k, a), b in zip(m1.named_buffers(), m2.buffers()):
+            assert torch.equal(a, b), (step, k)
+        if step == 1:
+            assert torch.equal(seen["y4"], seen["y4_ref"])
