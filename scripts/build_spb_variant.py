@@ -2,8 +2,10 @@
 (kernels_spbwd.hip, or VARIANT_SRC=<file>) built with -D defines: compiles that
 one source and links it with the default build's other objects
 (st-gcn_amd/build/default). Usage:
-  [VARIANT_SRC=kernels_x3.hip] python scripts/build_spb_variant.py <name> DEFINE=VAL [...]
-  -> lib/libstgcn_hip_<name>.so"""
+  [VARIANT_SRC=kernels_x3.hip[,more.hip]] [VARIANT_CSRC=<dir>] \
+      python scripts/build_spb_variant.py <name> DEFINE=VAL [...]  -> lib/libstgcn_hip_<name>.so
+(VARIANT_CSRC: compile those sources from another source tree, e.g. an older
+commit's csrc exported with git archive, for same-box A/B of a change)"""
 import os
 import subprocess
 import sys
@@ -16,11 +18,12 @@ import build  # noqa: E402
 name, defs = sys.argv[1], sys.argv[2:]
 objdir = os.path.join(PKG, "build", name)
 os.makedirs(objdir, exist_ok=True)
-src = os.environ.get("VARIANT_SRC", "kernels_spbwd.hip")
-obj = os.path.join(objdir, src + ".o")
-subprocess.run([build.HIPCC, *build.FLAGS, *[f"-D{d}" for d in defs], "-c",
-                os.path.join(build.CSRC, src), "-o", obj], check=True)
-objs = [obj if s == src else os.path.join(PKG, "build", "default", s + ".o")
+srcs = os.environ.get("VARIANT_SRC", "kernels_spbwd.hip").split(",")
+csrc = os.environ.get("VARIANT_CSRC", build.CSRC)
+for src in srcs:
+    subprocess.run([build.HIPCC, *build.FLAGS, *[f"-D{d}" for d in defs], "-c",
+                    os.path.join(csrc, src), "-o", os.path.join(objdir, src + ".o")], check=True)
+objs = [os.path.join(objdir if s in srcs else os.path.join(PKG, "build", "default"), s + ".o")
         for s in build.SOURCES]
 out = os.path.join(PKG, "lib", f"libstgcn_hip_{name}.so")
 subprocess.run([build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out],

@@ -122,7 +122,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
 // there by coalesced loads instead of one scattered load per element).
 // OB: the kernel may write a bf16 output (p.out_bf16 read at run time; kept a
 // template switch so the fp32-only kernels' epilogue code is unchanged)
-template <int V, int NCOLS, bool BV_LDS = false, bool OB = false>
+// PF: the loads software-pipelined ahead of the stores (below; one-workgroup-
+// per-CU kernels only: +72 registers)
+template <int V, int NCOLS, bool BV_LDS = false, bool OB = false, bool PF = false>
 __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
                                                    int n, int r0, int m0, float *smem) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -167,21 +169,62 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
     ocol[j] = (p.s_out * m + p.p_out) * V + v;
   }
   const int rowb = r0 + mi * 32 + 4 * hi;
+  // The loads of a group of 4 accumulator registers (row bias, bias table,
+  // residual) are issued before the previous group's stores (software
+  // pipelined): vmcnt counts loads and stores in one in-order counter, so a load
+  // issued after a store can only be waited for together with that store
+  struct Pre {
+    float br[4], bv[16], rs[16];
+  };
+  auto prefetch = [&](int g, Pre &P) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = g * 4 + ii;
+      const int row = rowb + (i & 3) + 8 * (i >> 2);
+      const bool rok = row < p.R;
+      // (null bias pointers: uniform branches, so no load is issued for them --
+      // an OOB load still costs a trip through the memory pipeline and a wait)
+      P.br[ii] = 0.f;
+      if (p.bias_r)
+        P.br[ii] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rs_b, rok ? row * 4 : (int)kOOB, 0, 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = rok && cok[j];
+        P.bv[ii * 4 + j] = 0.f;
+        P.rs[ii * 4 + j] = 0.f;
+        if (!BV_LDS && p.bias_rv)
+          P.bv[ii * 4 + j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                           rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
+        if (p.res)
+          P.rs[ii * 4 + j] = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(
+                         rs_res, ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB, 0, 0));
+      }
+    }
+  };
   auto epilogue = [&](auto stats_c) {
     constexpr bool STATS = decltype(stats_c)::value;
     double *red = reinterpret_cast<double *>(smem);  // [4 waves][2 halves][32]
+    Pre pf[PF ? 2 : 1];
+    if constexpr (PF) prefetch(0, pf[0]);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {  // groups of 4 accumulator registers
+      if constexpr (PF)
+        if (g + 1 < 4) prefetch(g + 1, pf[(g + 1) & 1]);
+      const Pre &P = pf[PF ? (g & 1) : 0];
       double gv[8];                // [stat][register]: partials over this lane's 4 columns
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int i = g * 4 + ii;
         const int row = rowb + (i & 3) + 8 * (i >> 2);
         const bool rok = row < p.R;
-        // (null bias pointers: uniform branches, so no load is issued for them --
-        // an OOB load still costs a trip through the memory pipeline and a wait)
+        // (!PF: loads next to their use; null bias pointers are uniform branches,
+        // so no load is issued for them)
         float br = 0.f;
-        if (p.bias_r)
+        if constexpr (PF)
+          br = P.br[ii];
+        else if (p.bias_r)
           br = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(rs_b, rok ? row * 4 : (int)kOOB, 0, 0));
         double s = 0.0, sq = 0.0;
@@ -191,13 +234,16 @@ __device__ __forceinline__ void conv_tile_epilogue(const ConvGemmParams &p, floa
           float val = acc[j][i] + br;
           if constexpr (BV_LDS) {
             if (p.bias_rv && ok) val += sbv[(row - r0) * V + cv[j]];
-          } else {
-            if (p.bias_rv)
-              val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                   rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
+          } else if constexpr (PF) {
+            val += P.bv[ii * 4 + j];
+          } else if (p.bias_rv) {
+            val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 rs_bv, ok ? (row * V + cv[j]) * 4 : (int)kOOB, 0, 0));
           }
           const int off = ok ? (row * ostride + ocol[j]) * 4 : (int)kOOB;
-          if (p.res)
+          if constexpr (PF)
+            val += P.rs[ii * 4 + j];
+          else if (p.res)
             val += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_res, off, 0, 0));
           if (p.relu_out) val = fmaxf(val, 0.f);
           if (p.drop.thresh && ok)
@@ -281,7 +327,10 @@ __device__ __forceinline__ void acc_to_img(float *img, const floatx16 &a, int ro
     img[(row0 + (i & 3) + 8 * (i >> 2) + 4 * hi) * PITCH + col0 + lo] = a[i];
 }
 
-template <int V, int NCOLS, int NT, int ROWS = 64, bool OB = false>
+// PF: every residual / bias-table load hoisted ahead of the stores (below);
+// costs 4 PPT registers -- for one-workgroup-per-CU kernels only (at two per CU
+// the extra registers halved the occupancy: +37% on the bf16 k_conv_x3)
+template <int V, int NCOLS, int NT, int ROWS = 64, bool OB = false, bool PF = false>
 __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, const float *img,
                                                      float *sbv, int n, int r0, int m0) {
   constexpr int TPR = NT / ROWS;
@@ -311,6 +360,28 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
                       ? 4
                       : (((obase & 1) == 0 && (rbase & 1) == 0 && (ostride & 1) == 0) ? 2 : 1);
   double s = 0.0, sq = 0.0;
+  // The residual / bias-table pieces, all loaded before the first store: vmcnt
+  // counts stores and loads in one in-order counter, so a load issued after a
+  // store can only be waited for together with that store -- loads interleaved
+  // with the stores made every piece wait for the previous piece's store to
+  // complete (its full write latency, PPT times per tile)
+  float rq[PF ? PPT : 1][4];
+#pragma unroll
+  for (int k = 0; k < (PF ? PPT : 0); ++k) {
+    const int pc = q + k * TPR, c0 = pc * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rq[k][e] = 0.f;
+    if (res && rok && pc < NP) {
+      if (c0 + 3 < ncv && vec == 4) {
+        const float4 t = *reinterpret_cast<const float4 *>(res + c0);
+        rq[k][0] = t.x; rq[k][1] = t.y; rq[k][2] = t.z; rq[k][3] = t.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c0 + e < ncv) rq[k][e] = res[c0 + e];
+      }
+    }
+  }
 #pragma unroll
   for (int k = 0; k < PPT; ++k) {
     const int pc = q + k * TPR;
@@ -318,9 +389,12 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
     const int c0 = pc * 4;
     const float4 a = *reinterpret_cast<const float4 *>(img + r * kEpiPitch + c0);
     float v[4] = {a.x, a.y, a.z, a.w};
-    float rv[4] = {0.f, 0.f, 0.f, 0.f};
     const bool full = rok && c0 + 3 < ncv;
-    if (res && rok) {
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (PF) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rv[e] = rq[k][e];
+    } else if (res && rok) {
       if (full && vec == 4) {
         const float4 t = *reinterpret_cast<const float4 *>(res + c0);
         rv[0] = t.x; rv[1] = t.y; rv[2] = t.z; rv[3] = t.w;

@@ -168,18 +168,44 @@ __global__ __launch_bounds__(256, 2) void k_conv_gemm(ConvGemmParams p) {
   // per-lane partial BN statistics (fp64 over this lane's 4 columns), summed
   // across lanes and waves through LDS (the staging buffers are free now).
   double *red = reinterpret_cast<double *>(smem);  // [4 waves][16 regs][2][64 lanes]
+  // (every load ahead of the stores that follow it: vmcnt counts loads and
+  // stores in one in-order counter, so a load issued after a store is only
+  // waited for together with that store. Row biases first; bias-table and
+  // residual values one register ahead of their stores)
+  float brv[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+    brv[i] = (row < p.R && p.bias_r) ? p.bias_r[row] : 0.f;
+  }
+  const float *resN = p.res ? p.res + (p.res_shared ? 0 : (int64_t)n * p.out_bstride) : nullptr;
+  float pbv[2][4], prs[2][4];
+  auto pre = [&](int i, float (&bv)[4], float (&rs)[4]) {
+    const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bv[j] = 0.f;
+      rs[j] = 0.f;
+      if (row < p.R && cok[j]) {
+        if (p.bias_rv) bv[j] = p.bias_rv[row * V + cv[j]];
+        if (resN) rs[j] = resN[row * ostride + ocol[j]];
+      }
+    }
+  };
+  pre(0, pbv[0], prs[0]);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (i + 1 < 16) pre(i + 1, pbv[(i + 1) & 1], prs[(i + 1) & 1]);
+    const int row = r0 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
     const bool rok = row < p.R;
-    const float br = (rok && p.bias_r) ? p.bias_r[row] : 0.f;
+    const float br = brv[i];
     double s = 0.0, sq = 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (rok && cok[j]) {
         float val = acc[j][i] + br;
-        if (p.bias_rv) val += p.bias_rv[row * V + cv[j]];
-        if (p.res) val += p.res[(p.res_shared ? 0 : (int64_t)n * p.out_bstride) + row * ostride + ocol[j]];
+        if (p.bias_rv) val += pbv[i & 1][j];
+        if (p.res) val += prs[i & 1][j];
         if (p.relu_out) val = fmaxf(val, 0.f);
         if (p.drop.thresh)
           val = dropout_keep(p.drop, (uint64_t)n * p.out_bstride + row * ostride + ocol[j])

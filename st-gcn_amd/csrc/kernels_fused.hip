@@ -622,29 +622,45 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
                    : make_rsrc(p.out + (int64_t)n * p.out_bstride, p.out_bstride);
     const __amdgpu_buffer_rsrc_t rs_bv = make_rsrc(p.bias_rv, (int64_t)p.R * V);
     const int ostride = p.T_dst * V;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    // (bias-table loads one register group ahead of its stores: vmcnt counts loads
+    // and stores in one in-order counter, so a load issued after a store is only
+    // waited for together with that store -- one store latency per element)
+    constexpr int NGRP = 2 * G::MB;  // (column tile j, row block rb) groups of 16
+    auto bias16 = [&](int gidx, float (&bv)[16]) {
+      const int j = gidx / G::MB, rb = gidx % G::MB;
       const int col = (cj * 2 + j) * 32 + lo;
       const bool cok = col < pos_lim;
       const int v = col % V;
 #pragma unroll
-      for (int rb = 0; rb < G::MB; ++rb)
+      for (int i = 0; i < 16; ++i) {
+        const int row = mi * (ROWS / 2) + rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        const bool ok = cok && row < p.R;
+        bv[i] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rs_bv, ok ? (row * V + v) * 4 : (int)kOOB,
+                                                        0, 0));
+      }
+    };
+    float bvb[2][16];
+    bias16(0, bvb[0]);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = mi * (ROWS / 2) + rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
-          const bool ok = cok && row < p.R;
-          const float bv = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(rs_bv, ok ? (row * V + v) * 4 : (int)kOOB,
-                                                          0, 0));
-          const int e = row * ostride + m0 * V + col;
-          if (p.out_bf16)
-            __builtin_amdgcn_raw_buffer_store_b16(
-                __builtin_bit_cast(unsigned short, (__bf16)(acc[rb][j][i] + bv)), rs_o,
-                ok ? e * 2 : (int)kOOB, 0, 0);
-          else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, acc[rb][j][i] + bv),
-                                                  rs_o, ok ? e * 4 : (int)kOOB, 0, 0);
-        }
+    for (int gidx = 0; gidx < NGRP; ++gidx) {
+      if (gidx + 1 < NGRP) bias16(gidx + 1, bvb[(gidx + 1) & 1]);
+      const int j = gidx / G::MB, rb = gidx % G::MB;
+      const int col = (cj * 2 + j) * 32 + lo;
+      const bool cok = col < pos_lim;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = mi * (ROWS / 2) + rb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+        const bool ok = cok && row < p.R;
+        const float val = acc[rb][j][i] + bvb[gidx & 1][i];
+        const int e = row * ostride + m0 * V + col;
+        if (p.out_bf16)
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (__bf16)val),
+                                                rs_o, ok ? e * 2 : (int)kOOB, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs_o,
+                                                ok ? e * 4 : (int)kOOB, 0, 0);
+      }
     }
     return;
   } else {
@@ -656,7 +672,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
       for (int j = 0; j < 2; ++j)
         acc_to_img(smem, acc[rb][j], mi * (ROWS / 2) + rb * 32, (cj * 2 + j) * 32);
     __syncthreads();
-    conv_tile_store_rows<V, G::NCOLS, G::NT, ROWS, true>(p, smem, smem + ROWS * kEpiPitch, n, 0,
+    conv_tile_store_rows<V, G::NCOLS, G::NT, ROWS, true, true>(p, smem, smem + ROWS * kEpiPitch, n, 0,
                                                          m0);
   }
 }

@@ -54,8 +54,8 @@
 #define STGCN_X3_EXP 0
 #endif
 #ifndef STGCN_SPB_EXP  // spb_epilogue timing experiments only (results wrong): bit 1 no dA
-#define STGCN_SPB_EXP 0  // partials / atomics, 2 no dxhat / BN1 pass, 4 no x DMA
-#endif
+#define STGCN_SPB_EXP 0  // partials / atomics, 2 no dxhat / BN1 pass, 4 no x DMA, 8 no BN1 /
+#endif                   // chain sum atomics, 16 no dxhat stores, 32 no dA atomics
 #ifndef STGCN_BNA_EXP  // bna timing experiments only (results wrong): bit 1 no epilogue
 #define STGCN_BNA_EXP 0  // contraction, 2 no loader BN1, 4 no table / bound setup
 #endif
@@ -208,37 +208,44 @@ struct ConvX3Geo {
 // The folded block's SpatialConv backward fused into its data gradient's
 // epilogue (capi.hip fold_spb; the backward of st_graphconv.py:148-150 with
 // K = 1, V = 18 -- north star: the spatial and temporal halves in one kernel,
-// A pinned in LDS / scalar registers, H never in HBM). The tile's accumulators
-// hold H = sum_q Wc_q^T dU (rows = input channels c, columns = 14 frames x 18
+// A pinned in LDS / registers, H never in HBM). The tile's accumulators hold
+// H = sum_q Wc_q^T dU (rows = input channels c, columns = 14 frames x 18
 // joints; frame t = s_out m + p_out covers the stride-2 phases too). In halves
 // of 64 rows (MR = 2: the waves of row half h hand their accumulators over):
 //   1. H -> LDS image; the tile's x rows (deferred dx: the previous block's U)
 //      -> LDS by 4-byte LDS-DMA (column offsets per lane, OOB -> 0);
-//   2. thread (row, frame group): dxhat[w] = sum_v H[v] A[v][w] (A from scalar
-//      registers), x rebuilt as k_spatial_bwd5's row pass does (prev mode: ReLU(
-//      BN2_prev(U)), its mask and uhat), BN1(x) written back over x, the BN1
-//      sums sd += dxhat, sdn += dxhat (x - mu) invstd (prev: s1, s2) reduced
-//      over the row's 8 threads into fp64 atomics, dxhat stored (8-byte stores);
+//   2. row pass, item = (row, frame), three lanes per item (6 output joints
+//      each, their 6 columns of A held in 108 registers, so a 16-byte LDS read
+//      of H feeds 24 FMAs instead of 4 of A^T), 21 items per wave: dxhat[w] =
+//      sum_v H[v] A[v][w], x rebuilt as k_spatial_bwd5's row pass does (prev
+//      mode: ReLU(BN2_prev(U)), its mask and uhat), BN1(x) written back over x,
+//      the BN1 sums sd += dxhat, sdn += dxhat (x - mu) invstd (prev: s1, s2)
+//      combined over the item's lanes and added per row in LDS (fp64), dxhat
+//      stored (consecutive lanes: consecutive 24-byte pieces of a row);
 //   3. dA partials: thread = (6-joint v block, 6-joint w block, 1/56 of the
 //      (row, frame) pairs), 36 register accumulators over both halves;
 // then the partials meet in LDS and each dA entry is summed in a fixed order
-// and added atomically (as k_spatial_bwd5 does). Arithmetic per element is
-// that of k_spatial_bwd5 (fp32, sums in fp64), so the results match it.
+// and added atomically (as k_spatial_bwd5 does), and the per-row sums go out
+// with one fp64 atomic per row and statistic. Arithmetic per element is that of
+// k_spatial_bwd5 (fp32, sums in fp64), so the results match it.
 // ---------------------------------------------------------------------------
 constexpr int kSpbAt = 18 * 20;  // A transposed, rows padded to 20 (16-byte aligned)
 // H and x images of one 64-row half + A^T
-// image pitch: 272 = 16 mod 64 banks puts the row pass's 64 lanes (8 rows x 8
-// frame groups, 8-byte reads) on distinct bank pairs (260: two-way)
+// image pitch: 272 = 16 mod 64 banks (conflict-free 8-byte reads across rows)
 constexpr int kSpbPitch = 272;
-constexpr int kSpbLds = (2 * 64 * kSpbPitch + kSpbAt) * 4;
+constexpr int kSpbRowTab = 2 * 64 * 8;  // per-row parameters [MR * 64][8] (MR <= 2)
+constexpr int kSpbLds = (2 * 64 * kSpbPitch + kSpbAt + kSpbRowTab) * 4 + 2 * 64 * 4 * 8;
 
 template <int MR>
 __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
                                              float *smem, int n, int r0, int m0, int mi,
                                              int nj0) {
   constexpr int V = 18, FT = kTileCols / V, NCOLS = FT * V, P = kSpbPitch;
-  constexpr int NSUB = 56;  // threads per (v block, w block) combination of dA
+  constexpr int NSUB = 56;   // threads per (v block, w block) combination of dA
+  constexpr int NSLOT = 21;  // row-pass items per wave (lanes 3 s + jb; lane 63 idle)
   float *const Himg = smem, *const Ximg = smem + 64 * P, *const At = smem + 2 * 64 * P;
+  float *const rtab = At + kSpbAt;                                      // [MR * 64][8]
+  double *const rsum = reinterpret_cast<double *>(rtab + kSpbRowTab);  // [MR][64][4]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int C = p.R, T = p.T_dst;
@@ -259,6 +266,36 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
   const bool pv = p.prev.mean != nullptr;
   const int combo = tid / NSUB, sub = tid - combo * NSUB;
   const int vb = combo / 3, wb = combo - (combo / 3) * 3;
+  // The per-row parameters (thread tid < MR * 64: row tid), loaded here, before
+  // any of the epilogue's stores (vmcnt counts stores and loads in one in-order
+  // counter: a load waited for after a store waits for that store too), and
+  // written to LDS once the main loop's buffers are free
+  float rp[8];  // mu, invstd, a = invstd g, beta; prev: mu, invstd, a, beta
+  {
+    const int c = r0 + tid;
+    const bool rok = tid < MR * 64 && c < C, pok = pv && rok;
+    const int cc = rok ? c : 0;  // (a valid address either way)
+    const float *pm = pv ? p.prev.mean : p.mean1, *pi = pv ? p.prev.invstd : p.invstd1;
+    const float *pg = pv ? p.prev.g : p.g1, *pbb = pv ? p.prev.b : p.b1;
+    const float mu = p.mean1[cc], is = p.invstd1[cc], g = p.g1[cc], be = p.b1[cc];
+    const float qmu = pm[cc], qis = pi[cc], qg = pg[cc], qb = pbb[cc];
+    rp[0] = rok ? mu : 0.f;
+    rp[1] = rok ? is : 0.f;
+    rp[2] = rok ? is * g : 0.f;
+    rp[3] = rok ? be : 0.f;
+    rp[4] = pok ? qmu : 0.f;
+    rp[5] = pok ? qis : 1.f;
+    rp[6] = pok ? qis * qg : 1.f;
+    rp[7] = pok ? qb : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(rp[i]));
+  f2v dacc[18];  // (v, w pair) of this thread's 6 x 6 block
+#pragma unroll
+  for (int i = 0; i < 18; ++i) dacc[i] = (f2v){0.f, 0.f};
+  // row pass lanes: item slot sl of the wave's 21, joint block jb (output joints 6 jb ..)
+  const int jb = lane % 3, sl = lane / 3;
+  const bool lact = lane < 3 * NSLOT;
 
 #pragma unroll
   for (int h = 0; h < MR; ++h) {
@@ -270,11 +307,17 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
         for (int j = 0; j < 2; ++j)
           acc_to_img<P>(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
     }
-    if (h == 0)  // A^T[w][v] (broadcast 16-byte LDS reads in the contraction)
+    if (h == 0) {  // A^T[w][v], the row table, zeroed row sums
       for (int i = tid; i < kSpbAt; i += 512) {
         const int w = i / 20, v = i - w * 20;
         At[i] = v < V ? p.sA[v * V + w] : 0.f;
       }
+      if (tid < MR * 64) {
+        *reinterpret_cast<float4 *>(rtab + tid * 8) = make_float4(rp[0], rp[1], rp[2], rp[3]);
+        *reinterpret_cast<float4 *>(rtab + tid * 8 + 4) = make_float4(rp[4], rp[5], rp[6], rp[7]);
+      }
+      for (int i = tid; i < MR * 64 * 4; i += 512) rsum[i] = 0.0;
+    }
     asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
     for (int rr = wave; rr < 64 && !(STGCN_SPB_EXP & 4); rr += 8) {
       const int c = r0 + h * 64 + rr;
@@ -294,49 +337,60 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!(STGCN_SPB_EXP & 2)) {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
-      const int rl = tid >> 3, fg = tid & 7;
-      const int c = r0 + h * 64 + rl;
-      const bool rok = c < C;
-      const float mu = rok ? p.mean1[c] : 0.f, is = rok ? p.invstd1[c] : 0.f;
-      const float a = is * (rok ? p.g1[c] : 0.f), be = rok ? p.b1[c] : 0.f;
-      const float pmu = pv && rok ? p.prev.mean[c] : 0.f, pis = pv && rok ? p.prev.invstd[c] : 1.f;
-      const float pa = pv && rok ? pis * p.prev.g[c] : 1.f, pb = pv && rok ? p.prev.b[c] : 0.f;
-      double sv[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int f = fg; f < nvf; f += 8) {
-        const float *hr = Himg + rl * P + f * V;
-        float *xr = Ximg + rl * P + f * V;
-        float hv[V];
+      float a6[V][6];  // A[v][6 jb + j]
 #pragma unroll
-        for (int i = 0; i < V / 2; ++i) {
-          const float2 a2 = *reinterpret_cast<const float2 *>(hr + 2 * i);
-          hv[2 * i] = a2.x;
-          hv[2 * i + 1] = a2.y;
+      for (int j = 0; j < 6; ++j) {
+        const float *ac = At + (jb * 6 + j) * 20;
+#pragma unroll
+        for (int v4 = 0; v4 < 16; v4 += 4) {
+          const float4 q = *reinterpret_cast<const float4 *>(ac + v4);
+          a6[v4][j] = q.x;
+          a6[v4 + 1][j] = q.y;
+          a6[v4 + 2][j] = q.z;
+          a6[v4 + 3][j] = q.w;
         }
-        float *dst = (p.out && rok) ? p.out + ((int64_t)n * C + c) * cT +
-                                          (int64_t)(p.s_out * (m0 + f) + p.p_out) * V
-                                    : nullptr;
+        const float2 q = *reinterpret_cast<const float2 *>(ac + 16);
+        a6[16][j] = q.x;
+        a6[17][j] = q.y;
+      }
+      const float *rt = rtab + h * 64 * 8;
+      for (int it0 = wave * NSLOT; it0 < 64 * FT; it0 += 8 * NSLOT) {
+        const int it = it0 + sl;
+        const int rr = it / FT, f = it - rr * FT;
+        const bool ok = lact && it < 64 * FT && f < nvf;
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        if (ok) {
+          const float4 q0 = *reinterpret_cast<const float4 *>(rt + rr * 8);
+          const float4 q1 = *reinterpret_cast<const float4 *>(rt + rr * 8 + 4);
+          const float mu = q0.x, is = q0.y, a = q0.z, be = q0.w;
+          const float pmu = q1.x, pis = q1.y, pa = q1.z, pb = q1.w;
+          const int c = r0 + h * 64 + rr;
+          const float *hr = Himg + rr * P + f * V;
+          float hv[V];
 #pragma unroll
-        for (int i = 0; i < V / 2; ++i) {  // joints w = 2i, 2i + 1
-          float d[2];
+          for (int i = 0; i < V / 2; ++i) {
+            const float2 a2 = *reinterpret_cast<const float2 *>(hr + 2 * i);
+            hv[2 * i] = a2.x;
+            hv[2 * i + 1] = a2.y;
+          }
+          float d[6];
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {  // dxhat[w] = sum_v H[v] A[v][w] (A^T rows: 16-byte reads)
-            const float *ac = At + (2 * i + e) * 20;
+          for (int j = 0; j < 6; ++j) {  // dxhat[w] = sum_v H[v] A[v][w], v in order
             float acc1 = 0.f;
 #pragma unroll
-            for (int v4 = 0; v4 < 20; v4 += 4) {
-              const float4 q = *reinterpret_cast<const float4 *>(ac + v4);
-              acc1 = fmaf(hv[v4], q.x, acc1);
-              acc1 = fmaf(hv[v4 + 1], q.y, acc1);
-              if (v4 + 2 < V) acc1 = fmaf(hv[v4 + 2], q.z, acc1);
-              if (v4 + 3 < V) acc1 = fmaf(hv[v4 + 3], q.w, acc1);
-            }
-            d[e] = acc1;
+            for (int v = 0; v < V; ++v) acc1 = fmaf(hv[v], a6[v][j], acc1);
+            d[j] = acc1;
           }
-          const float2 x2 = *reinterpret_cast<const float2 *>(xr + 2 * i);
-          float xs[2] = {x2.x, x2.y};
+          float *xr = Ximg + rr * P + f * V + jb * 6;
+          float xs[6];
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
+          for (int i = 0; i < 3; ++i) {
+            const float2 x2 = *reinterpret_cast<const float2 *>(xr + 2 * i);
+            xs[2 * i] = x2.x;
+            xs[2 * i + 1] = x2.y;
+          }
+#pragma unroll
+          for (int e = 0; e < 6; ++e) {
             float xx = xs[e], uh = 0.f;
             bool pm = false;
             if (pv) {  // the previous block's output x = ReLU(BN2(U)) as its output pass formed it
@@ -352,36 +406,41 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
               s2 += d[e];
               s3 = fmaf(d[e], uh, s3);
             }
-            xs[e] = rok ? bn : 0.f;
+            xs[e] = c < C ? bn : 0.f;
           }
-          *reinterpret_cast<float2 *>(xr + 2 * i) = make_float2(xs[0], xs[1]);
-          if (dst) *reinterpret_cast<float2 *>(dst + 2 * i) = make_float2(d[0], d[1]);
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            *reinterpret_cast<float2 *>(xr + 2 * i) = make_float2(xs[2 * i], xs[2 * i + 1]);
+          if (p.out && c < C && !(STGCN_SPB_EXP & 16)) {
+            float *dst = p.out + ((int64_t)n * C + c) * cT +
+                         (int64_t)(p.s_out * (m0 + f) + p.p_out) * V + jb * 6;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+              *reinterpret_cast<float2 *>(dst + 2 * i) = make_float2(d[2 * i], d[2 * i + 1]);
+          }
         }
-        sv[0] += s0;
-        sv[1] += s1;
-        sv[2] += s2;
-        sv[3] += s3;
-      }
+        // the item's three lanes -> lane jb = 0 (fp64), then the row's LDS sums
+        double sv[4] = {(double)s0, (double)s1, (double)s2, (double)s3};
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sv[i] += __shfl_xor(sv[i], o, 64);
-      if (fg == 0 && rok) {
-        if (!p.sd_given) atomicAdd(p.sd + c, sv[0]);
-        atomicAdd(p.sdn + c, sv[1]);
-        if (pv) {
-          atomicAdd(p.prev.s1 + c, sv[2]);
-          atomicAdd(p.prev.s2 + c, sv[3]);
+        for (int i = 0; i < 4; ++i) {
+          const double t1 = __shfl_down(sv[i], 1, 64), t2 = __shfl_down(sv[i], 2, 64);
+          sv[i] += t1 + t2;
+        }
+        if (ok && jb == 0 && !(STGCN_SPB_EXP & 8)) {
+          double *rs = rsum + (h * 64 + rr) * 4;
+          atomicAdd(rs, sv[0]);
+          atomicAdd(rs + 1, sv[1]);
+          if (pv) {
+            atomicAdd(rs + 2, sv[2]);
+            atomicAdd(rs + 3, sv[3]);
+          }
         }
       }
     }
-    __syncthreads();  // BN1(x) and H images complete
+    __syncthreads();  // BN1(x) and H images complete (and this half's row sums)
     // dA partials over this half's (row, frame) pairs: thread = (v block, w block,
-    // 1 / 56 of the pairs), then the partials meet in LDS (over the H image) and
-    // each entry is summed over its 56 threads in a fixed order
-    f2v dacc[18];  // (v, w pair) of this thread's 6 x 6 block
-#pragma unroll
-    for (int i = 0; i < 18; ++i) dacc[i] = (f2v){0.f, 0.f};
+    // 1 / 56 of the pairs); after the last half the partials meet in LDS (over
+    // the H image) and each entry is summed over its 56 threads in a fixed order
     if (STGCN_SPB_EXP & 1) continue;
     if (combo < 9) {
       for (int q = sub; q < 64 * FT; q += NSUB) {
@@ -406,24 +465,39 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
             dacc[i * 3 + j] = __builtin_elementwise_fma((f2v){hv[i], hv[i]}, xv[j], dacc[i * 3 + j]);
       }
     }
-    __syncthreads();  // the images are read
-    constexpr int PP = 37;  // partial pitch (odd: conflict-free column reads)
-    float *part = smem;
-    if (combo < 9) {
-#pragma unroll
-      for (int i = 0; i < 18; ++i) {
-        part[(combo * NSUB + sub) * PP + 2 * i] = dacc[i].x;
-        part[(combo * NSUB + sub) * PP + 2 * i + 1] = dacc[i].y;
+  }
+  // the BN1 / chain sums: one fp64 atomic per row and statistic (rsum complete:
+  // the barrier after the last row pass)
+  if (!(STGCN_SPB_EXP & 2) && !(STGCN_SPB_EXP & 8) && tid < MR * 64) {
+    const int c = r0 + tid;
+    if (c < C) {
+      const double *rs = rsum + tid * 4;
+      if (!p.sd_given) atomicAdd(p.sd + c, rs[0]);
+      atomicAdd(p.sdn + c, rs[1]);
+      if (pv) {
+        atomicAdd(p.prev.s1 + c, rs[2]);
+        atomicAdd(p.prev.s2 + c, rs[3]);
       }
     }
-    __syncthreads();
-    if (tid < V * V) {
-      const int v = tid / V, w = tid - (tid / V) * V;
-      const int cb = (v / 6) * 3 + w / 6, i = (v % 6) * 6 + (w % 6);
-      float sum = 0.f;
-      for (int k = 0; k < NSUB; ++k) sum += part[(cb * NSUB + k) * PP + i];
-      atomicAdd(p.dA + tid, sum);
+  }
+  if (STGCN_SPB_EXP & 1) return;
+  __syncthreads();  // the images are read
+  constexpr int PP = 37;  // partial pitch (odd: conflict-free column reads)
+  float *part = smem;
+  if (combo < 9) {
+#pragma unroll
+    for (int i = 0; i < 18; ++i) {
+      part[(combo * NSUB + sub) * PP + 2 * i] = dacc[i].x;
+      part[(combo * NSUB + sub) * PP + 2 * i + 1] = dacc[i].y;
     }
+  }
+  __syncthreads();
+  if (tid < V * V) {
+    const int v = tid / V, w = tid - (tid / V) * V;
+    const int cb = (v / 6) * 3 + w / 6, i = (v % 6) * 6 + (w % 6);
+    float sum = 0.f;
+    for (int k = 0; k < NSUB; ++k) sum += part[(cb * NSUB + k) * PP + i];
+    if (!(STGCN_SPB_EXP & 32)) atomicAdd(p.dA + tid, sum);
   }
 }
 
@@ -960,7 +1034,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     }
     // (one-plane bf16 path: the output may be stored in bf16, p.out_bf16 -- the
     // data gradient dZ of capi.hip dz_bf16)
-    conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS, NPL == 1>(
+    conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS, NPL == 1, NPL != 1>(
         p, smem, smem + G::ROWS * kEpiPitch, n, r0, m0);
     return;
   }
@@ -981,7 +1055,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[2 + j][i] = ho[(j * 16 + i) * 64 + lane];
-    conv_tile_epilogue<V, G::NCOLS, false, NPL == 1>(p, acc, n, r0, m0, smem);
+    conv_tile_epilogue<V, G::NCOLS, false, NPL == 1, NPL != 1>(p, acc, n, r0, m0, smem);
   } else if (p.stat_sum) {
     __syncthreads();  // the epilogue's one barrier (statistics)
   }
