@@ -7,6 +7,10 @@
 
 #include "internal.h"
 
+#ifndef STGCN_EPI_EXP  // epilogue timing experiments only (results wrong): bit 1 no BN
+#define STGCN_EPI_EXP 0  // statistics atomics in conv_tile_store_rows
+#endif
+
 namespace stgcn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -453,7 +457,7 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
       s += __shfl_xor(s, o, 64);
       sq += __shfl_xor(sq, o, 64);
     }
-    if (q == 0 && rok) {
+    if (q == 0 && rok && !(STGCN_EPI_EXP & 1)) {
       atomicAdd(p.stat_sum + row, s);
       atomicAdd(p.stat_sq + row, sq);
     }

@@ -453,17 +453,17 @@ __global__ __launch_bounds__(256) void k_fold_tq(const double *cs, int nz, int R
   const int64_t zs = (int64_t)R * To * V;
   double a = 0.0;
   if (ph < PH) {
-    double a1 = 0.0;  // (two chains for the loads' latency)
+    double ak[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // (eight loads in flight)
     for (int z = 0; z < nz; ++z) {
       const double *c = cs + z * zs + (int64_t)o * To * V + v;
       int t = ph;
-      for (; t + PH < To; t += 2 * PH) {
-        a += c[(int64_t)t * V];
-        a1 += c[(int64_t)(t + PH) * V];
-      }
-      if (t < To) a += c[(int64_t)t * V];
+      for (; t + 7 * PH < To; t += 8 * PH)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ak[k] += c[(int64_t)(t + k * PH) * V];
+      for (; t < To; t += PH) ak[0] += c[(int64_t)t * V];
     }
-    a += a1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a += ak[k];
     for (int sl = ph; sl < nsl; sl += PH) {
       const int t = fold_slot_frame(sl, nb0, tb1);
       double b = 0.0;

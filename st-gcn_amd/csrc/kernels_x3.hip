@@ -288,8 +288,15 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     rp[6] = pok ? qis * qg : 1.f;
     rp[7] = pok ? qb : 0.f;
   }
+  static_assert(kSpbAt <= 512, "one A^T element per thread");
+  float sa = 0.f;  // A^T element tid
+  if (tid < kSpbAt) {
+    const int w = tid / 20, v = tid - w * 20;
+    sa = v < V ? p.sA[v * V + w] : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(rp[i]));
+  asm volatile("" : "+v"(sa));
   f2v dacc[18];  // (v, w pair) of this thread's 6 x 6 block
 #pragma unroll
   for (int i = 0; i < 18; ++i) dacc[i] = (f2v){0.f, 0.f};
@@ -300,24 +307,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
 #pragma unroll
   for (int h = 0; h < MR; ++h) {
     __syncthreads();  // every wave is done with the main loop's buffers / the last half
-    if (MR == 1 || mi == h) {
-#pragma unroll
-      for (int rb = 0; rb < MR; ++rb)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc_to_img<P>(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
-    }
-    if (h == 0) {  // A^T[w][v], the row table, zeroed row sums
-      for (int i = tid; i < kSpbAt; i += 512) {
-        const int w = i / 20, v = i - w * 20;
-        At[i] = v < V ? p.sA[v * V + w] : 0.f;
-      }
-      if (tid < MR * 64) {
-        *reinterpret_cast<float4 *>(rtab + tid * 8) = make_float4(rp[0], rp[1], rp[2], rp[3]);
-        *reinterpret_cast<float4 *>(rtab + tid * 8 + 4) = make_float4(rp[4], rp[5], rp[6], rp[7]);
-      }
-      for (int i = tid; i < MR * 64 * 4; i += 512) rsum[i] = 0.0;
-    }
+    // (the x rows' DMA first: its latency runs under the H image and table writes)
     asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
     for (int rr = wave; rr < 64 && !(STGCN_SPB_EXP & 4); rr += 8) {
       const int c = r0 + h * 64 + rr;
@@ -334,24 +324,42 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
             : "memory");
       }
     }
+    if (MR == 1 || mi == h) {
+#pragma unroll
+      for (int rb = 0; rb < MR; ++rb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc_to_img<P>(Himg, acc[rb * 2 + j], MR == 2 ? rb * 32 : mi * 32, (nj0 + j) * 32);
+    }
+    if (h == 0) {  // A^T[w][v], the row table, zeroed row sums
+      if (tid < kSpbAt) At[tid] = sa;
+      if (tid < MR * 64) {
+        *reinterpret_cast<float4 *>(rtab + tid * 8) = make_float4(rp[0], rp[1], rp[2], rp[3]);
+        *reinterpret_cast<float4 *>(rtab + tid * 8 + 4) = make_float4(rp[4], rp[5], rp[6], rp[7]);
+      }
+      for (int i = tid; i < MR * 64 * 4; i += 512) rsum[i] = 0.0;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!(STGCN_SPB_EXP & 2)) {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
-      float a6[V][6];  // A[v][6 jb + j]
+      f2v a6[V][3];  // A[v][6 jb + 2 j2 + {0, 1}] (joint pairs: packed FMA)
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const float *ac = At + (jb * 6 + j) * 20;
+        float av[V];
 #pragma unroll
         for (int v4 = 0; v4 < 16; v4 += 4) {
           const float4 q = *reinterpret_cast<const float4 *>(ac + v4);
-          a6[v4][j] = q.x;
-          a6[v4 + 1][j] = q.y;
-          a6[v4 + 2][j] = q.z;
-          a6[v4 + 3][j] = q.w;
+          av[v4] = q.x;
+          av[v4 + 1] = q.y;
+          av[v4 + 2] = q.z;
+          av[v4 + 3] = q.w;
         }
         const float2 q = *reinterpret_cast<const float2 *>(ac + 16);
-        a6[16][j] = q.x;
-        a6[17][j] = q.y;
+        av[16] = q.x;
+        av[17] = q.y;
+#pragma unroll
+        for (int v = 0; v < V; ++v) a6[v][j >> 1][j & 1] = av[v];
       }
       const float *rt = rtab + h * 64 * 8;
       for (int it0 = wave * NSLOT; it0 < 64 * FT; it0 += 8 * NSLOT) {
@@ -375,11 +383,13 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
           }
           float d[6];
 #pragma unroll
-          for (int j = 0; j < 6; ++j) {  // dxhat[w] = sum_v H[v] A[v][w], v in order
-            float acc1 = 0.f;
+          for (int j2 = 0; j2 < 3; ++j2) {  // dxhat[w] = sum_v H[v] A[v][w], v in order
+            f2v acc2 = (f2v){0.f, 0.f};
 #pragma unroll
-            for (int v = 0; v < V; ++v) acc1 = fmaf(hv[v], a6[v][j], acc1);
-            d[j] = acc1;
+            for (int v = 0; v < V; ++v)
+              acc2 = __builtin_elementwise_fma((f2v){hv[v], hv[v]}, a6[v][j2], acc2);
+            d[2 * j2] = acc2.x;
+            d[2 * j2 + 1] = acc2.y;
           }
           float *xr = Ximg + rr * P + f * V + jb * 6;
           float xs[6];
@@ -492,11 +502,16 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     }
   }
   __syncthreads();
-  if (tid < V * V) {
+  if (tid < V * V) {  // (four interleaved chains: 14 dependent LDS reads, not 56)
     const int v = tid / V, w = tid - (tid / V) * V;
     const int cb = (v / 6) * 3 + w / 6, i = (v % 6) * 6 + (w % 6);
-    float sum = 0.f;
-    for (int k = 0; k < NSUB; ++k) sum += part[(cb * NSUB + k) * PP + i];
+    const float *pc = part + cb * NSUB * PP + i;
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NSUB; k += 4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += pc[(k + u) * PP];
+    const float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     if (!(STGCN_SPB_EXP & 32)) atomicAdd(p.dA + tid, sum);
   }
 }
