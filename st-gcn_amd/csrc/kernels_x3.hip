@@ -303,6 +303,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
   // row pass lanes: item slot sl of the wave's 21, joint block jb (output joints 6 jb ..)
   const int jb = lane % 3, sl = lane / 3;
   const bool lact = lane < 3 * NSLOT;
+  const bool need_s0 = !p.sd_given;  // (uniform)
 
 #pragma unroll
   for (int h = 0; h < MR; ++h) {
@@ -410,7 +411,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
               xx = pm ? t : 0.f;
             }
             const float bn = (xx - mu) * a + be;
-            s0 += d[e];
+            if (need_s0) s0 += d[e];
             s1 = fmaf(d[e], (xx - mu) * is, s1);
             if (pm) {
               s2 += d[e];
@@ -429,20 +430,25 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
               *reinterpret_cast<float2 *>(dst + 2 * i) = make_float2(d[2 * i], d[2 * i + 1]);
           }
         }
-        // the item's three lanes -> lane jb = 0 (fp64), then the row's LDS sums
-        double sv[4] = {(double)s0, (double)s1, (double)s2, (double)s3};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const double t1 = __shfl_down(sv[i], 1, 64), t2 = __shfl_down(sv[i], 2, 64);
-          sv[i] += t1 + t2;
+        // the item's three lanes -> lane jb = 0 (fp32, as one 18-joint frame
+        // sum), then the row's LDS sums in fp64; only the sums in use (sd comes
+        // from the fp64 dU sums on the folded block: p.sd_given)
+        auto red3 = [&](float v) {
+          return v + (__shfl_down(v, 1, 64) + __shfl_down(v, 2, 64));
+        };
+        s1 = red3(s1);
+        if (need_s0) s0 = red3(s0);
+        if (pv) {
+          s2 = red3(s2);
+          s3 = red3(s3);
         }
         if (ok && jb == 0 && !(STGCN_SPB_EXP & 8)) {
           double *rs = rsum + (h * 64 + rr) * 4;
-          atomicAdd(rs, sv[0]);
-          atomicAdd(rs + 1, sv[1]);
+          if (need_s0) atomicAdd(rs, (double)s0);
+          atomicAdd(rs + 1, (double)s1);
           if (pv) {
-            atomicAdd(rs + 2, sv[2]);
-            atomicAdd(rs + 3, sv[3]);
+            atomicAdd(rs + 2, (double)s2);
+            atomicAdd(rs + 3, (double)s3);
           }
         }
       }
@@ -453,9 +459,12 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     // the H image) and each entry is summed over its 56 threads in a fixed order
     if (STGCN_SPB_EXP & 1) continue;
     if (combo < 9) {
+      // (a fixed 16 pairs per thread, unrolled so the LDS reads run ahead; frames
+      // >= nvf add nothing: their x image columns are zero -- OOB DMA, no row pass)
+      static_assert((64 * FT) % NSUB == 0, "whole pair rounds");
+#pragma unroll 4
       for (int q = sub; q < 64 * FT; q += NSUB) {
         const int rr = q / FT, f = q - rr * FT;
-        if (f >= nvf) continue;
         const float *hr = Himg + rr * P + f * V + vb * 6;
         const float *xr = Ximg + rr * P + f * V + wb * 6;
         float hv[6];
