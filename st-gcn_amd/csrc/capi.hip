@@ -116,20 +116,23 @@ bool fused_spb50(const stgcn_desc_t *d) { return fused_spb(d) && d->V == 50; }
 // SpatialConv channel GEMM W' folds into the temporal conv's weights
 // (Wc_q = Wt_q W'), so the temporal conv reads G = BN1(x) A^T (C_in channels)
 // and Z / dZ are never formed; the backward's data gradient yields H directly.
-// fp32 split path (cfg2: V = 18, K = 1), non-residual blocks over >= 16 input
-// and output channels (the data gradient reduces over C_out: k_conv_x3 needs
-// >= 16 there, and only k_conv_x3 runs the fused SpatialConv backward epilogue)
-// whose spatial backward is the unfused pair (STGCN_AB_NO_FOLD build: the
+// fp32 split path, K = 1: V = 18 (cfg2) and V = 25 (the reference's default
+// L_STGCN graph: NTU joints, unilabeling partition, lightning_model.py:271),
+// non-residual blocks over >= 16 input and output channels (the data gradient
+// reduces over C_out: k_conv_x3 needs >= 16 there) (STGCN_AB_NO_FOLD build: the
 // unfolded kernels, A/B only).
 bool fold_w(const stgcn_desc_t *d) {
   constexpr bool off = STGCN_AB_NO_FOLD != 0;
   return !off && f32x3(d) && !residual(d) && d->K == 1 && d->C_in >= 16 && d->C_out >= 16 &&
-         d->V == 18 && !fused_spb(d);
+         (d->V == 18 || d->V == 25) && !fused_spb(d);
 }
 // The folded block's SpatialConv backward inside its data gradient (kernels_x3.hip
-// spb_epilogue): dxhat = H A, dA, the BN1 / chain sums from the tile while H is
-// on chip (STGCN_AB_SPB_PAIR build: H stored + k_spatial_bwd5, A/B only)
-bool fold_spb(const stgcn_desc_t *d) { return fold_w(d) && STGCN_AB_SPB_PAIR == 0; }
+// spb_epilogue, V = 18): dxhat = H A, dA, the BN1 / chain sums from the tile
+// while H is on chip. V = 25 (and the STGCN_AB_SPB_PAIR build): the data gradient
+// stores H and the unfused spatial backward (k_spatial_bwd5) reads it.
+bool fold_spb(const stgcn_desc_t *d) {
+  return fold_w(d) && d->V == 18 && STGCN_AB_SPB_PAIR == 0;
+}
 
 // The folded block's temporal GEMMs on 2-way fp16 splits (STGCN_F_F16X2; k_conv_x3 /
 // k_wgrad_x3 with NPL = 2), operand scales from max |x| words (launch_absmax)
@@ -140,7 +143,10 @@ bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
 // gradient at N = 32, T = 300), which the folded block takes from the fp64 dU
 // sums instead (kernels_fold.hip k_fold_sd). STGCN_AB_F16X2_DGRAD=0 build: the
 // 3-way bf16 splits there (A/B only).
-bool f16x2_dgrad(const stgcn_desc_t *d) { return f16x2(d) && STGCN_AB_F16X2_DGRAD != 0; }
+// (only where BN1's sum comes from the fp64 dU sums: the fused backward, fold_spb)
+bool f16x2_dgrad(const stgcn_desc_t *d) {
+  return f16x2(d) && fold_spb(d) && STGCN_AB_F16X2_DGRAD != 0;
+}
 // ... and G never formed (north star N1; kernels_x3.hip bna_contract): the
 // forward GEMM reads x, applies BN1 in its window loader and the joint
 // contraction with A in its epilogue (U = A U' + BT), the weight gradient reads
@@ -373,8 +379,13 @@ struct FwdLayout {
   float *Wc, *BT;  // the folded block: composite weights, per-frame bias table
   double *bq;      // ... and its per-tap bias products
   float *fscr;     // ... and its GEMM operand re-layouts
+  double *s2part;  // ... and its BN2 statistics per GEMM tile [N * n_mtiles][2][C_out]
   size_t dbl_bytes, total;
 };
+
+int fold_stat_tiles(const stgcn_desc_t *d) {
+  return d->N * ((d->T_out + conv_ft(d->V) - 1) / conv_ft(d->V));
+}
 
 FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
   Carve c(ws);
@@ -396,6 +407,7 @@ FwdLayout fwd_layout(const stgcn_desc_t *d, void *ws) {
     L.BT = c.take<float>((size_t)R * nTo(d));
     L.bq = c.take<double>((size_t)9 * R * d->V);
     L.fscr = c.take<float>(fold_fwd_scratch_floats(R, C, d->V));
+    if (d->training) L.s2part = c.take<double>((size_t)fold_stat_tiles(d) * 2 * R);
   }
   L.total = c.off;
   return L;
@@ -918,6 +930,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   if (res) return residual_fwd_tail(d, a, L, s);
   // Temporal (9,1) conv, stride (s,1), pad (4,0), bias (st_graphconv.py:41-43,99),
   // with the BN2 batch statistics accumulated in the epilogue.
+  bool stat_parts = false;
   {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = a->Z;
@@ -988,11 +1001,18 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.T_src = T;
     p.T_dst = To;
     conv_tiles(p);
+    // (the folded forward on k_conv_x3: BN2 statistics as per-tile partials)
+    stat_parts = fold && d->training && L.s2part && p.bf16 == 3 && conv_x3_supported(p);
+    if (stat_parts) p.stat_part = L.s2part;
     HIP_TRY(launch_conv_gemm(p, s));
   }
   // BN2 (st_graphconv.py:100) + ReLU (:105)
-  HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * To * V, d->eps, d->momentum,
-                             d->training, a->rm2, a->rv2, mean2, invstd2, s));
+  if (stat_parts)
+    HIP_TRY(launch_bn_finalize_parts(L.s2part, fold_stat_tiles(d), R, (int64_t)N * To * V, d->eps,
+                                     d->momentum, d->training, a->rm2, a->rv2, mean2, invstd2, s));
+  else
+    HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * To * V, d->eps, d->momentum,
+                               d->training, a->rm2, a->rv2, mean2, invstd2, s));
   double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
   const Dropout ydrop = make_dropout(d, a->dropout_p, a->seed);
   // (ABI 5: y_stats holds 5 * C_out sums; the last three -- over the ReLU mask --

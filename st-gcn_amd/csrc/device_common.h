@@ -457,7 +457,13 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
       s += __shfl_xor(s, o, 64);
       sq += __shfl_xor(sq, o, 64);
     }
-    if (q == 0 && rok && !(STGCN_EPI_EXP & 1)) {
+    if (p.stat_part) {  // (uniform) per-tile partials, plain stores
+      if (q == 0 && rok) {
+        double *pt = p.stat_part + ((int64_t)n * p.n_mtiles + m0 / (NCOLS / V)) * 2 * p.R;
+        pt[row] = s;
+        pt[p.R + row] = sq;
+      }
+    } else if (q == 0 && rok && !(STGCN_EPI_EXP & 1)) {
       atomicAdd(p.stat_sum + row, s);
       atomicAdd(p.stat_sq + row, sq);
     }

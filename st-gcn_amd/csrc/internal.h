@@ -57,6 +57,11 @@ struct ConvGemmParams {
   const float *bias_r;   // [R] or null
   const float *bias_rv;  // [R][V] or null
   double *stat_sum, *stat_sq;  // [R] per-row sum / sum of squares, or null
+  // (k_conv_x3's row-major epilogue: per-tile partials [n * n_mtiles + mt][2][R]
+  // written with plain stores instead of the stat_sum / stat_sq atomics --
+  // launch_bn_finalize_parts reduces them; deterministic, and no fp64 atomics
+  // whose latency ends every tile)
+  double *stat_part;
   int64_t in_bstride, out_bstride;  // elements per clip
   int64_t w_sr, w_sc, w_sq;
   int C, R, NQ;
@@ -334,6 +339,11 @@ hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K
 // G = f(BN1(x)) A^T with f = identity, or ReLU when relu != 0 (residual block)
 // amax (or null): max |G| as float bits (atomicMax; zeroed by the caller), the
 // f16x2 operand bound of the folded temporal GEMMs
+// BN statistics from per-tile partials [ntiles][2][C] (ConvGemmParams.stat_part):
+// one workgroup per channel, fixed summation order
+hipError_t launch_bn_finalize_parts(const double *part, int ntiles, int C, int64_t M, float eps,
+                                    float momentum, int training, float *rm, float *rv,
+                                    float *mean_out, float *invstd_out, hipStream_t s);
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, int relu, hipStream_t s,

@@ -515,10 +515,12 @@ static bool launch_tconv_ck(const ConvGemmParams &p, int CK, int nblk, size_t ld
 }
 
 hipError_t launch_conv_gemm(const ConvGemmParams &p0, hipStream_t s) {
+  // (per-tile statistics partials: k_conv_x3's row-major epilogue only)
+  if (p0.stat_part && (p0.s_out != 1 || !p0.stat_sum)) return hipErrorInvalidValue;
   if (p0.bf16 == 3 && conv_x3_supported(p0)) return launch_conv_x3(p0, s);
   // (the fused SpatialConv backward epilogue and the fp16 operand scales exist in
   // k_conv_x3 only: any other kernel would ignore them and write H / wrong results)
-  if (p0.spb || p0.f16x2) return hipErrorInvalidValue;
+  if (p0.spb || p0.f16x2 || p0.stat_part) return hipErrorInvalidValue;
   if (p0.bf16 == 1 && conv_b1_supported(p0)) return launch_conv_b1(p0, s);
   if (p0.bf16 == 1 && conv_bf16_supported(p0)) return launch_conv_bf16(p0, s);
   // (bf16-stored operands: only the kernels above read / write them)
@@ -1509,6 +1511,51 @@ __global__ void k_bn_finalize(const double *sum, const double *sq, int C, int64_
     mean_out[c] = rm[c];
     invstd_out[c] = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
   }
+}
+
+// one workgroup per channel: the tile partials summed in a fixed order (strided
+// per thread, then a fixed tree), then k_bn_finalize's arithmetic
+__global__ __launch_bounds__(256) void k_bn_finalize_parts(const double *part, int ntiles, int C,
+                                                           int64_t M, float eps, float momentum,
+                                                           int training, float *rm, float *rv,
+                                                           float *mean_out, float *invstd_out) {
+  __shared__ double red[2][256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int t = tid; t < ntiles; t += 256) {
+    a += part[(int64_t)t * 2 * C + c];
+    b += part[(int64_t)t * 2 * C + C + c];
+  }
+  red[0][tid] = a;
+  red[1][tid] = b;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (tid < h) {
+      red[0][tid] += red[0][tid + h];
+      red[1][tid] += red[1][tid + h];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const double mean = red[0][0] / (double)M;
+  double var = red[1][0] / (double)M - mean * mean;
+  if (var < 0.0) var = 0.0;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (training && rm) {
+    const double unb = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * mean);
+    rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * unb);
+  }
+}
+
+hipError_t launch_bn_finalize_parts(const double *part, int ntiles, int C, int64_t M, float eps,
+                                    float momentum, int training, float *rm, float *rv,
+                                    float *mean_out, float *invstd_out, hipStream_t s) {
+  if (!training) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_finalize_parts, dim3(C), dim3(256), 0, s, part, ntiles, C, M, eps,
+                     momentum, training, rm, rv, mean_out, invstd_out);
+  return hipGetLastError();
 }
 
 hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M, float eps,

@@ -128,6 +128,12 @@ def test_block_plan_pins_the_paths(pkg, lib):
     p = plan(flags=5)                                        # residual: never folded
     assert not p & hl.PLAN_FOLD and p & hl.PLAN_WSP_SPLIT, p
     assert not plan(flags=4, V=25, K=3) & hl.PLAN_FOLD       # K = 3
+    # the reference's default graph (V = 25, unilabeling K = 1) folds too, with the
+    # unfused SpatialConv backward (the fused epilogue is V = 18 only)
+    p = plan(flags=12, V=25, K=1)
+    assert p & hl.PLAN_FOLD and p & hl.PLAN_F16X2 and not p & hl.PLAN_SP_BWD_FUSED, p
+    assert not p & hl.PLAN_X_FROM_U, p
+    assert not plan(flags=12, V=50, K=1) & hl.PLAN_FOLD      # (no V = 50 split instances)
     p = plan(flags=2, V=25, K=3)
     assert p & hl.PLAN_SP_FWD_FUSED and p & hl.PLAN_SP_BWD_FUSED and not p & hl.PLAN_FOLD, p
     assert plan() == 0
@@ -147,7 +153,7 @@ def test_fold_prep_sizes(pkg, lib):
     block C_in = 3, K = 3, residual, bf16, exact fp32 MFMA)."""
     fl = pkg.hip_lib
     folded = [dict(C_in=64, flags=12), dict(C_in=64, C_out=128, stride=2, T_out=150, flags=12),
-              dict(C_in=64, flags=4), dict(C_in=64, flags=28)]
+              dict(C_in=64, flags=4), dict(C_in=64, flags=28), dict(C_in=64, V=25, flags=12)]
     for kw in folded:
         assert lib.stgcn_fold_prep_bytes(ctypes.byref(_desc(pkg, **kw))) > 0, kw
     for kw in (dict(C_in=3, flags=12), dict(V=25, K=3, flags=4), dict(C_in=64, flags=13),

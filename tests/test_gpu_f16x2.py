@@ -214,3 +214,28 @@ def test_fold_prep_matches_own_operands(pkg, case, gemm):
     want, floor = _oracle(arrays, b)
     _compare(b, want, floor=floor)
 
+
+
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T: the reference's default L_STGCN graph
+    # (lightning_model.py:271: NTU joints, partitioning 0 = unilabeling, K = 1)
+    (64, 64, 1, 25, 1, 3, 40),
+    (64, 128, 2, 25, 1, 2, 31),     # stride 2, odd T
+    (128, 128, 1, 25, 1, 2, 30),    # 128-row tiles
+    (24, 40, 1, 25, 1, 2, 23),      # partial chunk / rows
+])
+@pytest.mark.parametrize("gemm", ["f16x2", "f32x3"])
+def test_fold_default_graph_v25(pkg, case, gemm):
+    """V = 25, K = 1 folds (STGCN_PLAN_FOLD): forward and weight gradient on the
+    fp16 splits (f16x2), the data gradient on the 3-way bf16 splits with H
+    stored and the unfused SpatialConv backward (the fused epilogue and the
+    analytic BN1 sum are V = 18 only), all at the fp32 gate."""
+    arrays, x, g = _random_case(pkg, *case)
+    got = _check(pkg, arrays, x, g, gemm=gemm)
+    plan = _plan(pkg, x, case[1], case[2], gemm=gemm)
+    hl = pkg.hip_lib
+    assert plan & hl.PLAN_FOLD and not plan & hl.PLAN_SP_BWD_FUSED, plan
+    assert bool(plan & hl.PLAN_F16X2) == (gemm == "f16x2"), plan
+    if gemm == "f16x2":
+        ref = _run_hip(pkg, arrays, x, g, gemm="f32x3")
+        assert not torch.equal(got["y"], ref["y"]), "fp16-split forward did not run"

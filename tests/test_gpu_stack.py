@@ -291,6 +291,10 @@ def test_stack_chain_matches_unchained(pkg, residual, drop):
 
 @pytest.mark.parametrize("V,K,gemm,T", [(18, 1, "fp32", 40), (18, 1, "x3", 300),
                                          (18, 1, "f16", 300),
+                                         # the reference's default graph: V = 25,
+                                         # unilabeling (K = 1), folded, unfused
+                                         # SpatialConv backward
+                                         (25, 1, "f16", 60), (25, 1, "x3", 40),
                                          (25, 3, "bf16", 40), (50, 3, "bf16", 24),
                                          (25, 3, "fp32", 40)])
 def test_stack_deferred_dx_matches_unchained(pkg, monkeypatch, V, K, gemm, T):
