@@ -379,9 +379,16 @@ struct FwdLayout {
   float *Wc, *BT;  // the folded block: composite weights, per-frame bias table
   double *bq;      // ... and its per-tap bias products
   float *fscr;     // ... and its GEMM operand re-layouts
-  double *s2part;  // ... and its BN2 statistics per GEMM tile [N * n_mtiles][2][C_out]
+  double *s2part;  // ... and its BN2 statistics per GEMM tile [2][C_out][N * n_mtiles]
   size_t dbl_bytes, total;
 };
+
+ConvGemmParams fold_fwd_wparams(const stgcn_desc_t *d, const float *Wc);
+// The folded training forward's BN2 statistics as per-tile partials
+// (k_conv_x3's row-major epilogue; ConvGemmParams.stat_part)
+bool fold_stat_parts(const stgcn_desc_t *d) {
+  return fold_w(d) && d->training && conv_x3_supported(fold_fwd_wparams(d, nullptr));
+}
 
 int fold_stat_tiles(const stgcn_desc_t *d) {
   return d->N * ((d->T_out + conv_ft(d->V) - 1) / conv_ft(d->V));
@@ -847,7 +854,12 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   float *mean1 = a->stats, *invstd1 = a->stats + C;
   float *mean2 = a->stats + 2 * C, *invstd2 = a->stats + 2 * C + R;
 
-  HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
+  // (folded training forward with the previous block's statistics: nothing in the
+  // workspace's fp64 area accumulates -- BN2 goes to per-tile partials -- except
+  // the f16x2 max |G| / |Wc| words, which the BN1 finalize zeroes: no memset)
+  const bool stat_parts = fold_stat_parts(d) && L.s2part;
+  const bool no_memset = stat_parts && a->x_stats;
+  if (!no_memset) HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
   // BN1 statistics of the block input (st_graphconv.py:98)
   // (the caller may hand over the previous block's y statistics: x_stats)
   const double *xs1 = L.s1, *xq1 = L.q1;
@@ -863,7 +875,8 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     HIP_TRY(launch_absmax(a->x, (int64_t)N * C * T * V, L.amax, s));
   }
   HIP_TRY(launch_bn_finalize(xs1, xq1, C, (int64_t)N * T * V, d->eps, d->momentum, d->training,
-                             a->rm1, a->rv1, mean1, invstd1, s));
+                             a->rm1, a->rv1, mean1, invstd1, s, no_memset ? L.amax : nullptr,
+                             no_memset ? 2 * kAmaxWords : 0));
   // (the folded block: G only; W' rides on the temporal conv's weights)
   const bool fold = fold_w(d);
   // (ABI 7: the folded block's weight-only operands from stgcn_fold_prep)
@@ -930,7 +943,6 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   if (res) return residual_fwd_tail(d, a, L, s);
   // Temporal (9,1) conv, stride (s,1), pad (4,0), bias (st_graphconv.py:41-43,99),
   // with the BN2 batch statistics accumulated in the epilogue.
-  bool stat_parts = false;
   {
     ConvGemmParams p = conv_base(d, L.wpk);
     p.in = a->Z;
@@ -1002,24 +1014,24 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.T_dst = To;
     conv_tiles(p);
     // (the folded forward on k_conv_x3: BN2 statistics as per-tile partials)
-    stat_parts = fold && d->training && L.s2part && p.bf16 == 3 && conv_x3_supported(p);
     if (stat_parts) p.stat_part = L.s2part;
     HIP_TRY(launch_conv_gemm(p, s));
   }
   // BN2 (st_graphconv.py:100) + ReLU (:105)
-  if (stat_parts)
+  double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
+  if (stat_parts)  // (zeroes y_stats on the way)
     HIP_TRY(launch_bn_finalize_parts(L.s2part, fold_stat_tiles(d), R, (int64_t)N * To * V, d->eps,
-                                     d->momentum, d->training, a->rm2, a->rv2, mean2, invstd2, s));
+                                     d->momentum, d->training, a->rm2, a->rv2, mean2, invstd2, s,
+                                     ys, kAmaxWords));
   else
     HIP_TRY(launch_bn_finalize(L.s2, L.q2, R, (int64_t)N * To * V, d->eps, d->momentum,
                                d->training, a->rm2, a->rv2, mean2, invstd2, s));
-  double *ys = (d->training && a->y_stats) ? a->y_stats : nullptr;
   const Dropout ydrop = make_dropout(d, a->dropout_p, a->seed);
   // (ABI 5: y_stats holds 5 * C_out sums; the last three -- over the ReLU mask --
   // feed the next block's deferred-dx chain, meaningless under dropout; ABI 7:
   // then max y in STGCN_STATS_AMAX_WORDS words, the next block's operand bound;
   // ABI 8, y null: only these -- k_bn_relu_stats)
-  if (ys) HIP_TRY(hipMemsetAsync(ys, 0, y_stats_bytes(R), s));
+  if (ys && !stat_parts) HIP_TRY(hipMemsetAsync(ys, 0, y_stats_bytes(R), s));
   HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
                              ys ? ys + R : nullptr, ydrop, s,
                              (ys && !ydrop.thresh) ? ys + 2 * R : nullptr,

@@ -459,9 +459,10 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
     }
     if (p.stat_part) {  // (uniform) per-tile partials, plain stores
       if (q == 0 && rok) {
-        double *pt = p.stat_part + ((int64_t)n * p.n_mtiles + m0 / (NCOLS / V)) * 2 * p.R;
-        pt[row] = s;
-        pt[p.R + row] = sq;
+        const int64_t nt = (int64_t)p.N * p.n_mtiles;  // [2][R][tiles]: channel-major
+        double *pt = p.stat_part + (int64_t)row * nt + (int64_t)n * p.n_mtiles + m0 / (NCOLS / V);
+        pt[0] = s;
+        pt[(int64_t)p.R * nt] = sq;
       }
     } else if (q == 0 && rok && !(STGCN_EPI_EXP & 1)) {
       atomicAdd(p.stat_sum + row, s);

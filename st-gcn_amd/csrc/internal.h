@@ -57,7 +57,7 @@ struct ConvGemmParams {
   const float *bias_r;   // [R] or null
   const float *bias_rv;  // [R][V] or null
   double *stat_sum, *stat_sq;  // [R] per-row sum / sum of squares, or null
-  // (k_conv_x3's row-major epilogue: per-tile partials [n * n_mtiles + mt][2][R]
+  // (k_conv_x3's row-major epilogue: per-tile partials [2][R][n * n_mtiles + mt]
   // written with plain stores instead of the stat_sum / stat_sq atomics --
   // launch_bn_finalize_parts reduces them; deterministic, and no fp64 atomics
   // whose latency ends every tile)
@@ -280,7 +280,8 @@ hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, dou
                            hipStream_t s, unsigned *amax = nullptr);
 hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M,
                               float eps, float momentum, int training, float *rm, float *rv,
-                              float *mean_out, float *invstd_out, hipStream_t s);
+                              float *mean_out, float *invstd_out, hipStream_t s, unsigned *zw = nullptr,
+                              int nzw = 0);
 // y = ReLU(BN(U)); ysum/ysq (or null): per-channel sum / sum of squares of y;
 // yext (or null, 3*C: [cnt | su | xu]): with the ReLU mask m = y > 0 and
 // uhat = (U - mean) * invstd, cnt += sum m, su += sum m * uhat, xu += sum y * uhat
@@ -339,11 +340,12 @@ hipError_t launch_bias_rv(const float *A, const float *bW, float *bias_rv, int K
 // G = f(BN1(x)) A^T with f = identity, or ReLU when relu != 0 (residual block)
 // amax (or null): max |G| as float bits (atomicMax; zeroed by the caller), the
 // f16x2 operand bound of the folded temporal GEMMs
-// BN statistics from per-tile partials [ntiles][2][C] (ConvGemmParams.stat_part):
+// BN statistics from per-tile partials [2][C][ntiles] (ConvGemmParams.stat_part):
 // one workgroup per channel, fixed summation order
 hipError_t launch_bn_finalize_parts(const double *part, int ntiles, int C, int64_t M, float eps,
                                     float momentum, int training, float *rm, float *rv,
-                                    float *mean_out, float *invstd_out, hipStream_t s);
+                                    float *mean_out, float *invstd_out, hipStream_t s,
+                                    double *ys_zero = nullptr, int nw = 0);
 hipError_t launch_gather_fwd(const float *x, const float *mean, const float *invstd,
                              const float *g, const float *b, const float *A, float *G, int N,
                              int C, int T, int V, int K, int relu, hipStream_t s,

@@ -1491,10 +1491,14 @@ hipError_t launch_bn_stats(const float *x, int N, int C, int L, double *sum, dou
   return hipGetLastError();
 }
 
+// (zw non-null: also zeroes nzw words for the kernels that follow -- the f16x2
+// max |x| words of the folded forward -- instead of a memset launch)
 __global__ void k_bn_finalize(const double *sum, const double *sq, int C, int64_t M, float eps,
                               float momentum, int training, float *rm, float *rv, float *mean_out,
-                              float *invstd_out) {
+                              float *invstd_out, unsigned *zw, int nzw) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (zw)
+    for (int i = c; i < nzw; i += gridDim.x * blockDim.x) zw[i] = 0u;
   if (c >= C) return;
   if (training) {
     const double mean = sum[c] / (double)M;
@@ -1515,16 +1519,27 @@ __global__ void k_bn_finalize(const double *sum, const double *sq, int C, int64_
 
 // one workgroup per channel: the tile partials summed in a fixed order (strided
 // per thread, then a fixed tree), then k_bn_finalize's arithmetic
+// (ys non-null: also zeroes the block's y_stats -- 5 C doubles, then nw words --
+// for the output pass that follows: no memset launch)
 __global__ __launch_bounds__(256) void k_bn_finalize_parts(const double *part, int ntiles, int C,
                                                            int64_t M, float eps, float momentum,
                                                            int training, float *rm, float *rv,
-                                                           float *mean_out, float *invstd_out) {
+                                                           float *mean_out, float *invstd_out,
+                                                           double *ys, int nw) {
   __shared__ double red[2][256];
   const int c = blockIdx.x, tid = threadIdx.x;
+  if (ys) {
+    if (tid < 5) ys[(int64_t)tid * C + c] = 0.0;
+    const int per = (nw + C - 1) / C;
+    unsigned *w = reinterpret_cast<unsigned *>(ys + 5 * (int64_t)C);
+    for (int i = tid; i < per; i += 256)
+      if (c * per + i < nw) w[c * per + i] = 0u;
+  }
   double a = 0.0, b = 0.0;
-  for (int t = tid; t < ntiles; t += 256) {
-    a += part[(int64_t)t * 2 * C + c];
-    b += part[(int64_t)t * 2 * C + C + c];
+  const double *pa = part + (int64_t)c * ntiles, *pb = pa + (int64_t)C * ntiles;
+  for (int t = tid; t < ntiles; t += 256) {  // (contiguous per channel: coalesced)
+    a += pa[t];
+    b += pb[t];
   }
   red[0][tid] = a;
   red[1][tid] = b;
@@ -1551,18 +1566,20 @@ __global__ __launch_bounds__(256) void k_bn_finalize_parts(const double *part, i
 
 hipError_t launch_bn_finalize_parts(const double *part, int ntiles, int C, int64_t M, float eps,
                                     float momentum, int training, float *rm, float *rv,
-                                    float *mean_out, float *invstd_out, hipStream_t s) {
+                                    float *mean_out, float *invstd_out, hipStream_t s,
+                                    double *ys_zero, int nw) {
   if (!training) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_finalize_parts, dim3(C), dim3(256), 0, s, part, ntiles, C, M, eps,
-                     momentum, training, rm, rv, mean_out, invstd_out);
+                     momentum, training, rm, rv, mean_out, invstd_out, ys_zero, nw);
   return hipGetLastError();
 }
 
 hipError_t launch_bn_finalize(const double *sum, const double *sq, int C, int64_t M, float eps,
                               float momentum, int training, float *rm, float *rv,
-                              float *mean_out, float *invstd_out, hipStream_t s) {
+                              float *mean_out, float *invstd_out, hipStream_t s, unsigned *zw,
+                              int nzw) {
   hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, sum, sq, C, M, eps,
-                     momentum, training, rm, rv, mean_out, invstd_out);
+                     momentum, training, rm, rv, mean_out, invstd_out, zw, nzw);
   return hipGetLastError();
 }
 
