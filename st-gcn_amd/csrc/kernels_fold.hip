@@ -438,32 +438,41 @@ hipError_t launch_fold_fwd(const float *Wt, const float *W, const float *bt, con
 // over the clip chunks; LDS reduce; threads v < V form the nine taps. tqT (or
 // null): Tq also as the fp64 re-layout launch_fold_sdz reads ([q][Vp][Rp], zero
 // padded; blocks o >= R only write their padding column)
-__global__ __launch_bounds__(256) void k_fold_tq(const double *cs, int nz, int R, int V, int T,
-                                                 int To, int st, int nb0, int tb1, double *Tq,
-                                                 double *tqT) {
-  __shared__ double ts[256], bs[8 * 256];  // (boundary slots x joints, V <= 256)
+// (1024 threads: 56 frame phases at V = 18, so each thread's loads are few and
+// all in flight -- the kernel is latency-bound with one block per channel)
+constexpr int kTqThreads = 1024;
+__global__ __launch_bounds__(kTqThreads) void k_fold_tq(const double *cs, int nz, int R, int V,
+                                                        int T, int To, int st, int nb0, int tb1,
+                                                        double *Tq, double *tqT) {
+  __shared__ double ts[kTqThreads], bs[8 * 256];  // (boundary slots x joints, V <= 256)
   const int o = blockIdx.x, tid = threadIdx.x;
   const int Rp = pad32(R), Vp = pad32(V);
   if (o >= R) {  // (tqT's zero padding columns)
-    for (int e = tid; e < 9 * Vp; e += 256) tqT[(int64_t)e * Rp + o] = 0.0;
+    for (int e = tid; e < 9 * Vp; e += kTqThreads) tqT[(int64_t)e * Rp + o] = 0.0;
     return;
   }
-  const int PH = 256 / V, ph = tid / V, v = tid - ph * V;
+  const int PH = kTqThreads / V, ph = tid / V, v = tid - ph * V;
   const int nsl = nb0 + (To - tb1);
   const int64_t zs = (int64_t)R * To * V;
   double a = 0.0;
   if (ph < PH) {
-    double ak[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // (eight loads in flight)
-    for (int z = 0; z < nz; ++z) {
-      const double *c = cs + z * zs + (int64_t)o * To * V + v;
-      int t = ph;
-      for (; t + 7 * PH < To; t += 8 * PH)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) ak[k] += c[(int64_t)(t + k * PH) * V];
-      for (; t < To; t += PH) ak[0] += c[(int64_t)t * V];
+    // (the (chunk, frame) pairs flattened, four loads in flight per round)
+    const int nj = nz * To;
+    auto at = [&](int j) {
+      const int z = j / To, t = j - z * To;
+      return cs[z * zs + ((int64_t)o * To + t) * V + v];
+    };
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int j = ph;
+    for (; j + 3 * PH < nj; j += 4 * PH) {
+      const double x0 = at(j), x1 = at(j + PH), x2 = at(j + 2 * PH), x3 = at(j + 3 * PH);
+      a0 += x0;
+      a1 += x1;
+      a2 += x2;
+      a3 += x3;
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a += ak[k];
+    for (; j < nj; j += PH) a0 += at(j);
+    a = (a0 + a1) + (a2 + a3);
     for (int sl = ph; sl < nsl; sl += PH) {
       const int t = fold_slot_frame(sl, nb0, tb1);
       double b = 0.0;
@@ -501,7 +510,7 @@ hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V,
   if (V > 256) return hipErrorInvalidValue;  // (checked before any launch)
   int nb0, tb1;
   fold_slots(T, To, st, nb0, tb1);
-  hipLaunchKernelGGL(k_fold_tq, dim3(tqT ? pad32(R) : R), dim3(256), 0, s, cs, nz, R, V, T, To, st,
+  hipLaunchKernelGGL(k_fold_tq, dim3(tqT ? pad32(R) : R), dim3(kTqThreads), 0, s, cs, nz, R, V, T, To, st,
                      nb0, tb1, Tq, tqT);
   return hipGetLastError();
 }
