@@ -1601,27 +1601,40 @@ __device__ __forceinline__ void bn_relu_fwd_body(const float *U, const float *me
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   double s = 0.0, q = 0.0, cnt = 0.0, su = 0.0, xu = 0.0;
   float ym = 0.f;  // max y (y >= 0): the next block's fp16 operand bound
+  // (two vectors' loads issued before either's math; the sums stay fp64 per
+  // element: the chain sums su / xu feed nearly cancelling BN2 backward terms)
+  auto vec = [&](int64_t base, int i, float (&v)[VEC]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float uh = (v[j] - mu) * is;
+      const float t = (v[j] - mu) * a + be;
+      v[j] = t > 0.f ? t : 0.f;
+      if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
+      s += (double)v[j];
+      q += (double)v[j] * (double)v[j];
+      ym = fmaxf(ym, v[j]);
+      if (yext && t > 0.f) {
+        cnt += 1.0;
+        su += (double)uh;
+        xu += (double)v[j] * (double)uh;
+      }
+    }
+    if constexpr (WY) vst<VEC>(y + base + i, v);
+  };
   for (int n = n0; n < n1; ++n) {
     const int64_t base = ((int64_t)n * C + c) * L;
-    for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
-      float v[VEC];
-      vld<VEC>(U + base + i, v);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        const float uh = (v[j] - mu) * is;
-        const float t = (v[j] - mu) * a + be;
-        v[j] = t > 0.f ? t : 0.f;
-        if (drop.thresh) v[j] = dropout_keep(drop, base + i + j) ? v[j] * drop.scale : 0.f;
-        s += (double)v[j];
-        q += (double)v[j] * (double)v[j];
-        ym = fmaxf(ym, v[j]);
-        if (yext && t > 0.f) {
-          cnt += 1.0;
-          su += (double)uh;
-          xu += (double)v[j] * (double)uh;
-        }
-      }
-      if constexpr (WY) vst<VEC>(y + base + i, v);
+    int i = threadIdx.x * VEC;
+    for (; i + 256 * VEC < L; i += 512 * VEC) {
+      float v0[VEC], v1[VEC];
+      vld<VEC>(U + base + i, v0);
+      vld<VEC>(U + base + i + 256 * VEC, v1);
+      vec(base, i, v0);
+      vec(base, i + 256 * VEC, v1);
+    }
+    if (i < L) {
+      float v0[VEC];
+      vld<VEC>(U + base + i, v0);
+      vec(base, i, v0);
     }
   }
   if (ysum) block_sum2_atomic<256>(s, q, ysum + c, ysq + c, red);
@@ -1813,24 +1826,30 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
   }
   double s = 0.0, col[VEC] = {};
   if (i < L) {
-    // (the next clip's operands are loaded before this clip's math and stores)
-    float un[VEC], dn[VEC];
+    // (two clips' operands in flight ahead of this clip's math and stores:
+    // register sets A (even steps) and B (odd steps), loaded two clips ahead)
+    float ua[VEC], da[VEC], ub[VEC], db[VEC];
+    const int64_t cl = (int64_t)C * L;  // floats per clip
+    const int64_t b0 = ((int64_t)n0 * C + c) * L + i;
     if (n0 < n1) {
-      const int64_t base = ((int64_t)n0 * C + c) * L;
-      vld<VEC>(U + base + i, un);
-      vld<VEC>(dy + base + i, dn);
+      vld<VEC>(U + b0, ua);
+      vld<VEC>(dy + b0, da);
     }
-    for (int n = n0; n < n1; ++n) {
+    if (n0 + 1 < n1) {
+      vld<VEC>(U + b0 + cl, ub);
+      vld<VEC>(dy + b0 + cl, db);
+    }
+    auto clip = [&](int n, float (&ur)[VEC], float (&dr)[VEC]) __attribute__((always_inline)) {
       const int64_t base = ((int64_t)n * C + c) * L;
       float u[VEC], d[VEC], o[VEC];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
-        u[j] = un[j];
-        d[j] = dn[j];
+        u[j] = ur[j];
+        d[j] = dr[j];
       }
-      if (n + 1 < n1) {
-        vld<VEC>(U + base + (int64_t)C * L + i, un);
-        vld<VEC>(dy + base + (int64_t)C * L + i, dn);
+      if (n + 2 < n1) {
+        vld<VEC>(U + base + 2 * cl + i, ur);
+        vld<VEC>(dy + base + 2 * cl + i, dr);
       }
       if (dy_coef) {
 #pragma unroll
@@ -1869,6 +1888,10 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
       } else {
         vst<VEC>(dU + base + i, o);
       }
+    };
+    for (int n = n0; n < n1; n += 2) {
+      clip(n, ua, da);
+      if (n + 1 < n1) clip(n + 1, ub, db);
     }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) cs[((int64_t)blockIdx.z * C + c) * L + i + j] = col[j];
