@@ -1411,6 +1411,10 @@ struct WgX3Geo {
   // buffer written between two barriers (stride 2, three planes: 15 Q frames)
   static constexpr int NBUF = 2 * BUF <= 160 * 1024 ? 2 : 1;
   static constexpr int LDS = NBUF * BUF;
+  // (the epilogue's slab tile [ROWS][CB][9] reuses the staging LDS; the launch
+  // allocates at least that much -- one workgroup per CU either way)
+  static constexpr int TILE = ROWS * CB * 9 * 4;
+  static constexpr int LDSK = LDS > TILE ? LDS : TILE;
   static constexpr int PG = FT * G4;  // 4-joint groups per P row
   static constexpr int QG = QF * G4;  // ... per Q row
   static constexpr int NGRP = ROWS * PG + CB * QG;
@@ -1694,23 +1698,44 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       if (STGCN_WG_EXP & 8) continue;  // (no barrier: timing experiment only)
       __syncthreads();
     }
-    float *slab = p.slab + (int64_t)split * p.R * p.C * 9;
-    const int c = c0 + lo;
+    // the tile [ROWS][CB channels][9 taps] through LDS (the staging buffers are
+    // free after the last item's barrier), then whole 16-byte pieces of each
+    // row's CB * 9 contiguous slab floats: 4-byte stores at a 36-byte stride
+    // (per tap and channel) measured ~6x the slab's bytes in HBM writes
+    float *tile = reinterpret_cast<float *>(lds);
+    static_assert(G::TILE <= G::LDSK && G::LDSK <= 160 * 1024, "slab tile LDS");
 #pragma unroll
     for (int mb = 0; mb < MR; ++mb)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int r = r0 + mb * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+          const int rl = mb * 64 + mi * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
           float v;
           if constexpr (MR == 2)
             v = acm[mb][t][i] * pow2f(-p_se) * pow2f(-q_se);
           else
             v = NPL == 2 ? (acc[t][i] + acl[t][i]) * pow2f(-p_se) * pow2f(-q_se)
                          : acc[t][i] + acl[t][i];
-          if (r < p.R && c < p.C) slab[((int64_t)r * p.C + c) * 9 + q0 + t] = v;
+          tile[(rl * G::CB + lo) * 9 + q0 + t] = v;
         }
+    __syncthreads();
+    float *slab = p.slab + (int64_t)split * p.R * p.C * 9;
+    const int ncw = min(G::CB, p.C - c0) * 9;  // valid floats of a tile row
+    constexpr int RF = G::CB * 9;              // tile row pitch (floats)
+    const bool v4 = (p.C % 4) == 0;            // (16-byte aligned slab rows)
+    for (int e = tid; e < G::ROWS * (RF / 4); e += 512) {
+      const int rl = e / (RF / 4), f = (e - rl * (RF / 4)) * 4;
+      const int r = r0 + rl;
+      if (r >= p.R || f >= ncw) continue;
+      float *dst = slab + ((int64_t)r * p.C + c0) * 9 + f;
+      const float *src = tile + rl * RF + f;
+      if (v4 && f + 4 <= ncw) {
+        *reinterpret_cast<float4 *>(dst) = *reinterpret_cast<const float4 *>(src);
+      } else {
+        for (int k = 0; k < 4 && f + k < ncw; ++k) dst[k] = src[k];
+      }
+    }
   };
   if (it0 < it1) {
     load_item(it0);
@@ -1747,16 +1772,16 @@ hipError_t launch_wgrad_x3(const WgradParams &p0, hipStream_t s) {
     constexpr int ex = (4 * 33 + 8) * 4;  // the Q channel table + block_max_all's scratch
     if (p.s_in == 1 && p.x3_mr == 2)
       hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 2, true>), dim3(nblk), dim3(512),
-                         (WgX3Geo<18, 1, 2, 2>::LDS + ex), s, p);
+                         (WgX3Geo<18, 1, 2, 2>::LDSK + ex), s, p);
     else if (p.s_in == 1)
       hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 1, true>), dim3(nblk), dim3(512),
-                         (WgX3Geo<18, 1, 2>::LDS + ex), s, p);
+                         (WgX3Geo<18, 1, 2>::LDSK + ex), s, p);
     else if (p.x3_mr == 2)
       hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 2, true>), dim3(nblk), dim3(512),
-                         (WgX3Geo<18, 2, 2, 2>::LDS + ex), s, p);
+                         (WgX3Geo<18, 2, 2, 2>::LDSK + ex), s, p);
     else
       hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 1, true>), dim3(nblk), dim3(512),
-                         (WgX3Geo<18, 2, 2>::LDS + ex), s, p);
+                         (WgX3Geo<18, 2, 2>::LDSK + ex), s, p);
     return hipGetLastError();
   }
   if (p0.f16x2) {  // 2-way fp16 splits (NPL = 2)
@@ -1764,24 +1789,24 @@ hipError_t launch_wgrad_x3(const WgradParams &p0, hipStream_t s) {
     const WgradParams &p = p0;
     if (p.x3_mr == 2 && p.R % 128 != 0) return hipErrorInvalidValue;
     if (p.s_in == 1 && p.x3_mr == 2)
-      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2, 2>::LDS),
+      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2, 2>::LDSK),
                          s, p);
     else if (p.s_in == 1)
-      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2>::LDS), s, p);
+      hipLaunchKernelGGL((k_wgrad_x3<18, 1, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 1, 2>::LDSK), s, p);
     else if (p.x3_mr == 2)
-      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2, 2>::LDS),
+      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2, 2>::LDSK),
                          s, p);
     else
-      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2>::LDS), s, p);
+      hipLaunchKernelGGL((k_wgrad_x3<18, 2, 2>), dim3(nblk), dim3(512), (WgX3Geo<18, 2, 2>::LDSK), s, p);
     return hipGetLastError();
   }
   const WgradParams &p = p0;
   if (p.x3_mr != 1) return hipErrorInvalidValue;  // (128-row tiles: fp16 splits only)
   if (p.s_in == 1) {
-    constexpr int lds = WgX3Geo<18, 1>::LDS;
+    constexpr int lds = WgX3Geo<18, 1>::LDSK;
     hipLaunchKernelGGL((k_wgrad_x3<18, 1>), dim3(nblk), dim3(512), lds, s, p);
   } else {
-    constexpr int lds = WgX3Geo<18, 2>::LDS;
+    constexpr int lds = WgX3Geo<18, 2>::LDSK;
     hipLaunchKernelGGL((k_wgrad_x3<18, 2>), dim3(nblk), dim3(512), lds, s, p);
   }
   return hipGetLastError();
