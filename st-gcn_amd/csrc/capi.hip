@@ -137,6 +137,16 @@ bool fold_spb(const stgcn_desc_t *d) {
 // The folded block's temporal GEMMs on 2-way fp16 splits (STGCN_F_F16X2; k_conv_x3 /
 // k_wgrad_x3 with NPL = 2), operand scales from max |x| words (launch_absmax)
 bool f16x2(const stgcn_desc_t *d) { return fold_w(d) && f16x2_flag(d); }
+// ... and the unfolded K = 1 split block (the first block: C_in < 16) with its
+// temporal conv forward and weight gradient on fp16 splits: max |Z| by a pass
+// over Z, kept after G for the backward;
+// its data gradient stays on the 3-way splits (it feeds BN1's nearly cancelling sums)
+bool f16x2_unfold(const stgcn_desc_t *d) {
+  return f16x2_flag(d) && f32x3(d) && !fold_w(d) && !residual(d) && d->K == 1 && d->V == 18 &&
+         d->C_out >= 16;
+}
+// the temporal forward / weight gradient on fp16 splits (folded or not)
+bool f16x2_tw(const stgcn_desc_t *d) { return f16x2(d) || f16x2_unfold(d); }
 // ... the data gradient included: its output feeds BN1's sum of dxhat over N T V
 // elements of a zero-mean dU (heavy cancellation; the 2^-22 operand
 // representation measured 2.5x the fp32 reference's own error on the BN1 bias
@@ -291,7 +301,7 @@ WgradParams make_wgrad_taps(const stgcn_desc_t *d, const float *dU, const float 
   if (bf16(d)) plan_wgrad_bf16(w);
   // k_wgrad_x3 where it covers the shape (its S x R x C x 9 slab fits the fp32
   // plan's: twice the tiles, half the splits)
-  if (f32x3(d)) plan_wgrad_x3(w, f16x2(d));
+  if (f32x3(d)) plan_wgrad_x3(w, f16x2_tw(d));
   return w;
 }
 
@@ -738,7 +748,7 @@ int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan) {
     WgradParams w = make_wgrad_taps(d, nullptr, nullptr, nullptr, fold_w(d) ? d->C_in : 0);
     if (w.bf16 == 3) f |= STGCN_PLAN_TWGRAD_SPLIT;
   }
-  if (f16x2(d)) f |= STGCN_PLAN_F16X2;
+  if (f16x2_tw(d)) f |= STGCN_PLAN_F16X2;
   if (fold_bna(d)) f |= STGCN_PLAN_FOLD_NO_G;
   if (x_from_u(d)) f |= STGCN_PLAN_X_FROM_U;
   *plan = f;
@@ -757,7 +767,7 @@ size_t stgcn_keep_g_bytes(const stgcn_desc_t *d) {
   if (fold_bna(d)) return sizeof(unsigned) * kAmaxWords;
   // (f16x2: + one word after G, its max |G| for the backward's weight gradient)
   return sizeof(float) * (size_t)d->N * d->K * d->C_in * d->T * d->V +
-         (f16x2(d) ? sizeof(unsigned) * kAmaxWords : 0);
+         (f16x2_tw(d) ? sizeof(unsigned) * kAmaxWords : 0);
 }
 
 size_t stgcn_fold_prep_bytes(const stgcn_desc_t *d) {
@@ -938,6 +948,10 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.T_dst = T;
     conv_tiles(p);
     HIP_TRY(launch_conv_gemm(p, s));
+    // (the unfolded fp16-split block: max |Z| for the temporal GEMMs' operand
+    // scale, one pass over Z -- tracking it in the spatial GEMM's epilogue cost
+    // that kernel 65 registers, half its occupancy)
+    if (f16x2_unfold(d)) HIP_TRY(launch_absmax(a->Z, (int64_t)N * R * T * V, L.amax, s));
   }
   }
   if (res) return residual_fwd_tail(d, a, L, s);
@@ -1003,6 +1017,13 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
       p.in_bstride = (int64_t)C * T * V;
       p.w_sr = (int64_t)C * 9;
       p.C = C;
+    } else if (f16x2_unfold(d)) {  // fp16 splits: max |Z| (spatial epilogue), max |Wt|
+      HIP_TRY(launch_absmax(a->Wt, (int64_t)R * R * 9, L.amax + kAmaxWords, s));
+      p.f16x2 = 1;
+      p.amax_in = L.amax;
+      p.amax_w = L.amax + kAmaxWords;
+      if (a->G)  // (the kept G carries max |Z| to the backward's weight gradient)
+        p.amax_keep = reinterpret_cast<unsigned *>(a->G + (size_t)N * K * C * T * V);
     }
     p.NQ = 9;
     p.s_in = d->stride;
@@ -1113,7 +1134,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       HIP_TRY(launch_bn_relu_bwd_apply_cols(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
                                             L.dU, L.sdu, N, R, To * V, d->training, drop, s,
                                             du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs,
-                                            f16x2(d) ? L.amax : nullptr));  // (f16x2: max |dU|)
+                                            f16x2_tw(d) ? L.amax : nullptr));  // (f16x2: max |dU|)
       HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.ftq, tqT,
                              s));
     } else {
@@ -1330,6 +1351,19 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     WgradParams w = make_wgrad_taps(d, L.dU, res ? a->Za : a->Z, L.slab);
     w.q_bf16 = z_bf16(d) ? 1 : 0;
     w.p_bf16 = du_bf16(d) ? 1 : 0;
+    if (f16x2_unfold(d) && w.bf16 == 3) {  // fp16 splits: max |dU| (apply pass), max |Z|
+      if (!cols_sums(d))  // (the apply pass without the column sums forms no max |dU|)
+        HIP_TRY(launch_absmax(L.dU, (int64_t)N * R * To * V, L.amax, s));
+      const unsigned *zmax =
+          a->G ? reinterpret_cast<const unsigned *>(a->G + (size_t)N * K * C * T * V) : nullptr;
+      if (!zmax) {  // (no kept G: a pass over Z)
+        HIP_TRY(launch_absmax(a->Z, (int64_t)N * R * T * V, L.amax + 3 * kAmaxWords, s));
+        zmax = L.amax + 3 * kAmaxWords;
+      }
+      w.f16x2 = 1;
+      w.amax_p = L.amax;
+      w.amax_q = zmax;
+    }
     HIP_TRY(launch_wgrad_taps(w, s));
     HIP_TRY(launch_slab_reduce(L.slab, w.S, (int64_t)R * R * 9, a->dWt, 0, R, 1, R, s));
   }
@@ -1553,7 +1587,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
   const int CZ = fold ? C : R;
   const double tflops = 2.0 * 9 * R * (double)CZ * To * V * N;
   float *wpk = c.take<float>(wpk_floats(d));
-  if (f16x2(d) && which <= 2) P.amax = c.take<unsigned>(2 * kAmaxWords);
+  if (f16x2_tw(d) && which <= 2) P.amax = c.take<unsigned>(2 * kAmaxWords);
   if (which == 0) {
     ConvGemmParams p = conv_base(d, wpk);
     p.in = c.take<float>((size_t)N * CZ * T * V);
@@ -1591,9 +1625,9 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       p.amax_in = P.amax;
       p.amax_w = P.amax + kAmaxWords;
       P.ax[0] = p.in;
-      P.an[0] = (int64_t)N * C * T * V;
+      P.an[0] = (int64_t)N * CZ * T * V;
       P.ax[1] = p.w;
-      P.an[1] = (int64_t)R * C * 9;
+      P.an[1] = (int64_t)R * CZ * 9;
     }
     if (fold_bna(d)) {  // x in: BN1 in the loader, the joint contraction in the epilogue
       p.bna = 1;

@@ -140,7 +140,9 @@ def test_block_plan_pins_the_paths(pkg, lib):
     # STGCN_F_F16X2 (with F32X3): the folded GEMMs on fp16 splits; unfolded blocks unchanged
     p = plan(flags=12)
     assert p & hl.PLAN_FOLD and p & hl.PLAN_F16X2, p
-    assert not plan(flags=12, C_in=3) & hl.PLAN_F16X2
+    # the unfolded first block (C_in = 3): forward and weight gradient on fp16 splits
+    p = plan(flags=12, C_in=3)
+    assert p & hl.PLAN_F16X2 and not p & hl.PLAN_FOLD, p
     assert not plan(flags=13) & hl.PLAN_F16X2
     d = _desc(pkg, N=0)
     out = ctypes.c_uint32(7)

@@ -99,6 +99,9 @@ def test_f16x2_backward_without_kept_bound(pkg, monkeypatch):
     monkeypatch.setattr(pkg.fused, "_keep_g", lambda ctx, x, desc: None)
     arrays, x, g = _random_case(pkg, 64, 128, 2, 18, 1, 2, 29, seed=6)
     _check(pkg, arrays, x, g, gemm="f16x2_nog")
+    # (the unfolded first block: max |Z| by a pass over Z in the backward)
+    arrays, x, g = _random_case(pkg, 3, 64, 1, 18, 1, 2, 30, seed=7)
+    _check(pkg, arrays, x, g, need_dx=False)
 
 
 @pytest.mark.parametrize("gemm", MODES)
@@ -172,24 +175,46 @@ def test_narrow_output_blocks_not_folded(pkg, case, gemm):
     _compare(got, want, floor=floor)
 
 
-def test_f16x2_unfolded_blocks_keep_bf16x3(pkg):
-    """Where the block does not fold (first block C_in = 3, residual, K = 3) the
-    flag changes nothing: the plan has no F16X2 bit and the results are
-    bit-identical to the bf16x3 path (the adjacency gradient up to the order of
-    its fp32 atomic partial sums, which differs from run to run)."""
+def test_f16x2_residual_block_keeps_bf16x3(pkg):
+    """Where the block neither folds nor is the unfolded K = 1 first block (the
+    residual block) the flag changes nothing: no F16X2 bit, results bit-identical
+    to the bf16x3 path (the adjacency gradient up to the order of its fp32 atomic
+    partial sums, which differs from run to run)."""
     hl = pkg.hip_lib
-    for case, residual in (((3, 64, 1, 18, 1, 2, 30), False), ((64, 64, 1, 18, 1, 2, 30), True)):
-        arrays, x, g = _random_case(pkg, *case, residual=residual)
-        d = pkg.fused.make_desc(tuple(x.shape), case[1], 1, case[2], 4, 1e-5, 0.1, True,
-                                residual=residual, f16x2=True)
-        assert not hl.block_plan(d) & hl.PLAN_F16X2
-        a = _run_hip(pkg, arrays, x, g, gemm="f16x2")
-        b = _run_hip(pkg, arrays, x, g, gemm="f32x3")
-        for k in a:
-            if k == "grad.spatialConv.A":
-                torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6 * b[k].abs().max())
-            else:
-                assert torch.equal(a[k], b[k]), k
+    case = (64, 64, 1, 18, 1, 2, 30)
+    arrays, x, g = _random_case(pkg, *case, residual=True)
+    d = pkg.fused.make_desc(tuple(x.shape), case[1], 1, case[2], 4, 1e-5, 0.1, True,
+                            residual=True, f16x2=True)
+    assert not hl.block_plan(d) & hl.PLAN_F16X2
+    a = _run_hip(pkg, arrays, x, g, gemm="f16x2")
+    b = _run_hip(pkg, arrays, x, g, gemm="f32x3")
+    for k in a:
+        if k == "grad.spatialConv.A":
+            torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-6 * b[k].abs().max())
+        else:
+            assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("case", [
+    # C_in, C_out, stride, V, K, N, T: the first block (C_in = 3, not folded)
+    (3, 64, 1, 18, 1, 2, 30),
+    (3, 64, 1, 18, 1, 4, 300),      # cfg2 L0 at T = 300
+    (3, 32, 2, 18, 1, 2, 23),       # stride 2, odd T
+])
+@pytest.mark.parametrize("need_dx", [False, True])
+def test_f16x2_first_block(pkg, case, need_dx):
+    """The unfolded K = 1 first block under STGCN_F_F16X2: the temporal conv
+    forward and weight gradient on fp16 splits (max |Z| by a pass over Z,
+    carried to the backward after the kept G), the data gradient on the 3-way
+    splits; held to the fp32 gate."""
+    arrays, x, g = _random_case(pkg, *case)
+    got = _check(pkg, arrays, x, g, need_dx=need_dx)
+    plan = _plan(pkg, x, case[1], case[2])
+    hl = pkg.hip_lib
+    assert plan & hl.PLAN_F16X2 and not plan & hl.PLAN_FOLD, plan
+    ref = _run_hip(pkg, arrays, x, g, need_dx=need_dx, gemm="f32x3")
+    assert not torch.equal(got["y"], ref["y"]), "fp16-split forward did not run"
+    assert not torch.equal(got["grad.temporalConv.weight"], ref["grad.temporalConv.weight"])
 
 
 @pytest.mark.parametrize("gemm", ["f32x3", "f16x2", "f16x2_nog"])
