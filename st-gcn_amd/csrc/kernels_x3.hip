@@ -162,7 +162,18 @@ struct ConvX3Geo {
   static constexpr int NCOLS = FT * V;
   static constexpr int SPAN = (SIN * (FT - 1) + NQ) * V;  // window positions
   static constexpr int SLOTS = 2 * NPL + 1;       // (plane, octet) slots + 1 pad (odd)
-  static constexpr int IMG = SPAN * SLOTS * 16;   // window bytes
+  // stride-2 windows: FPAD spare slots after every frame. A 16-lane group of a
+  // B-fragment read spans two output frames, i.e. input frames 2 apart, and
+  // with the plain pitch those rows land on the same banks (2-way on every
+  // read; the stride-2 forward measured 1.26 conflict cycles per LDS-active
+  // cycle). The pads (bank model over every column tile and tap: 2.0 -> 1.06)
+  // are taken where the LDS plan stays the same; V = 25 has no such pad.
+  static constexpr int FPAD = SIN != 2 ? 0
+                              : V == 18 ? (NPL == 2 ? 3 : NPL == 3 ? 1 : 0)
+                              : V == 50 ? (NPL == 1 ? 5 : NPL == 2 ? 3 : 1)
+                                        : 0;
+  static constexpr int FP = V * SLOTS + FPAD;     // slots per window frame
+  static constexpr int IMG = (SPAN / V) * FP * 16;  // window bytes
   static constexpr int NG = NQ / TG;              // steps per chunk
   static constexpr int WST = NPL * TG * 2 * 1024 * MR;  // packed weight bytes per step
   static constexpr int WDMA = WST / 1024;         // 1 KiB DMA pieces per step
@@ -670,7 +681,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     const int col = (nj0 + j) * 32 + lo;
     const int mf = col / V;
     const int cp = col < G::NCOLS ? SIN * mf * V + (col - mf * V) : 0;
-    bo[j] = (cp * G::SLOTS + hi) * 16;
+    bo[j] = (cp * G::SLOTS + (cp / V) * G::FPAD + hi) * 16;
   }
   // window staging items (octet o, position pp), dealt over all 8 waves
   unsigned voff[G::IPT];
@@ -682,7 +693,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     const int g = g0 + pp;
     const bool ok = e < G::NIT && g >= 0 && g < cstride;
     voff[k] = ok ? (unsigned)(o * 8 * cstride + g) * 4u : kOOB;
-    loff[k] = e < G::NIT ? (pp * G::SLOTS + o) * 16 : -1;
+    loff[k] = e < G::NIT ? (pp * G::SLOTS + (pp / V) * G::FPAD + o) * 16 : -1;
     ioct[k] = o;
   }
   // BNA: the BN1 table [mu | a | be] (Cp entries each) and the rows of A past
@@ -861,7 +872,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         f.b[pl][j] =
-            *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * V * G::SLOTS + 2 * pl) * 16);
+            *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * G::FP + 2 * pl) * 16);
   };
   // the six products (plane of A, plane of B) of one tap over the MR x 2 tiles
   // (NPL = 1: the one product)
@@ -972,7 +983,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 #pragma unroll
           for (int j = 0; j < 2; ++j)
             fr.b[pl][j] =
-                *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * V * G::SLOTS + 2 * pl) * 16);
+                *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * G::FP + 2 * pl) * 16);
         };
 #pragma unroll
         for (int qq = 0; qq < TG; ++qq) {
