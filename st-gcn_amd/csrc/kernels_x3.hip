@@ -963,6 +963,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         // neither plane-0 fragment, which are the last ones refilled
         Frag &fr = f[0];
         auto grp = [&](int pa, int pb) {
+          if (STGCN_X3_EXP & 16) return;
 #pragma unroll
           for (int rb = 0; rb < MR; ++rb)
 #pragma unroll
