@@ -88,11 +88,19 @@ extern "C" {
                             * their max |x| (so h <= 2^14 and no element underflows
                             * relative to the tensor's maximum); the result is scaled back
                             * exactly. Same fp32 gate as STGCN_F_F32X3, half its MFMAs.
-                            * The data gradient runs on the fp16 splits too; BN1's
+                            * At V = 18 the data gradient runs on the fp16 splits too
+                            * (with the SpatialConv backward fused into it); BN1's
                             * nearly cancelling sum of dxhat (its bias gradient) is
                             * formed from the fp64 per-tap dU sums instead of from the
                             * 22-bit data gradient. (The 3-way bf16 data gradient is an
-                            * A/B measurement build only: STGCN_AB_F16X2_DGRAD=0.) */
+                            * A/B measurement build only: STGCN_AB_F16X2_DGRAD=0.) At
+                            * V = 25 (folded, K = 1) the data gradient stays on the
+                            * 3-way bf16 splits. ABI 8: an unfolded non-residual V = 18,
+                            * K = 1 block with C_out >= 16 (the first block, C_in = 3)
+                            * runs its temporal forward and weight gradient on the fp16
+                            * splits (bounds by max-|x| passes over Z and Wt), its data
+                            * gradient on the 3-way bf16 splits. stgcn_block_plan reports
+                            * STGCN_PLAN_F16X2 wherever any GEMM of the block uses them. */
 
 #define STGCN_F_NO_G 16    /* ABI 7, with STGCN_F_F16X2 only (memory-lean folded block):
                             * G = BN1(x) A^T is never formed or kept -- the forward GEMM
