@@ -412,6 +412,19 @@ def pmc_profile(config):
                   f"newest: {os.path.relpath(found[-1][0], ROOT) if found else 'none'}")
 
 
+def pmc_lookup(table, sym):
+    """table[sym] where the PMC file names the kernel as the timing does; else
+    the one rocprof name that only appends template arguments left at their
+    default (false), e.g. k_conv_x3<..,false,true> -> k_conv_x3<..,false,true,false>."""
+    if sym in table:
+        return table[sym]
+    head = sym[:-1] + ","
+    hits = [k for k in table
+            if k.startswith(head) and k.endswith(">") and
+            all(a == "false" for a in k[len(head):-1].split(","))]
+    return table[hits[0]] if len(hits) == 1 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -612,8 +625,8 @@ def main():
             sym = max(symbols, key=lambda k: symbols[k][0])
             ms_tot, fl_tot, nl, nb_tot = symbols[sym]
             pmc, pmc_src = pmc_profile(args.config)
-            traffic = pmc["hbm_bytes_per_launch"].get(sym) if pmc else None
-            mfma_busy = pmc.get("mfma_busy", {}).get(sym) if pmc else None
+            traffic = pmc_lookup(pmc["hbm_bytes_per_launch"], sym) if pmc else None
+            mfma_busy = pmc_lookup(pmc.get("mfma_busy", {}), sym) if pmc else None
             # split kernels: the fp32-work ceiling is the bf16/fp16 MFMA rate over
             # the products per fp32 product (6 for bf16 x3, 3 for the fp16 x2 planes)
             split = sym.startswith("k_conv_x3") or sym.startswith("k_wgrad_x3")
