@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 8
+#define STGCN_ABI_VERSION 9
 
 /* ABI 7: words of max |y| after the 5 * C sums of a y_stats block */
 #define STGCN_STATS_AMAX_WORDS 2048
@@ -146,7 +146,9 @@ typedef struct stgcn_fwd_args {
   const float *g1, *b1, *g2, *b2;       /* batch_n / batch_n_2 affine         */
   float *rm1, *rv1, *rm2, *rv2;         /* running stats (updated if training)*/
   float *y;                             /* out: N,C_out,T_out,V (ABI 8: may be
-                                         * null, see prev_U below)            */
+                                         * null, see prev_U below; ABI 9: null
+                                         * with y_stats null, see
+                                         * stgcn_head_fwd_u)                  */
   float *Z;                             /* saved: spatial output N,C_out,T,V
                                          * (fp32-sized; opaque under STGCN_F_BF16) */
   float *U;                             /* saved: temporal output N,C_out,T_out,V */
@@ -364,6 +366,17 @@ int stgcn_head_fwd(const stgcn_head_desc_t *d, const float *y, const float *W, c
 int stgcn_head_bwd(const stgcn_head_desc_t *d, const float *pooled, const float *logits,
                    const float *W, const int64_t *labels, const float *dloss, float *dlogits,
                    float *dpooled, float *dy, float *dW, float *dbias, void *stream);
+/* ABI 9: stgcn_head_fwd with the last block's output never written: the pool
+ * reads that block's pre-BN2 tensor U (N, C, L) and forms y = ReLU(BN2(U)) on
+ * load with the block's stats2 = [mean2 (C) | invstd2 (C)] (its stats buffer
+ * from C_in * 2 on) and BN2 affine g2 / b2, as the block's output pass would
+ * (bit-identical pooled). The block runs with stgcn_fwd_args_t.y and .y_stats
+ * both null (training, non-residual, no dropout: no output pass at all).
+ * stgcn_head_bwd is unchanged (its dy is the gradient of that unwritten y). */
+int stgcn_head_fwd_u(const stgcn_head_desc_t *d, const float *U, const float *stats2,
+                     const float *g2, const float *b2, const float *W, const float *bias,
+                     const int64_t *labels, float *pooled, float *logits, float *lossv,
+                     float *loss, void *stream);
 
 /* Multi-tensor Adam (torch.optim.Adam, amsgrad=False, maximize=False;
  * lightning_model.py:196-197): ONE launch updates every tensor of a table.

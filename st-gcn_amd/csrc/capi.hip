@@ -843,8 +843,11 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   // ABI 8: x from the previous block's U (STGCN_PLAN_X_FROM_U); y null: statistics only
   const bool xu = a && a->prev_U;
   const bool ystats_only = a && !a->y && a->y_stats && d->training && !res && a->dropout_p == 0.f;
+  // ABI 9: y and y_stats both null: no output pass (stgcn_head_fwd_u pools from U)
+  const bool no_out = a && !a->y && !a->y_stats && d->training && !res && a->dropout_p == 0.f;
   if (!a || (!a->x && !xu) || !a->A || !a->W || !a->bW || !a->Wt || !a->bWt || !a->g1 ||
-      !a->b1 || !a->g2 || !a->b2 || (!a->y && !ystats_only) || !a->Z || (!res && !a->U) ||
+      !a->b1 || !a->g2 || !a->b2 || (!a->y && !ystats_only && !no_out) || !a->Z ||
+      (!res && !a->U) ||
       !a->stats)
     return fail(STGCN_E_INVALID, "null tensor argument");
   if (res && (!a->Za || (projection(d) && (!a->Wr || !a->br))))
@@ -1051,7 +1054,9 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   // (ABI 5: y_stats holds 5 * C_out sums; the last three -- over the ReLU mask --
   // feed the next block's deferred-dx chain, meaningless under dropout; ABI 7:
   // then max y in STGCN_STATS_AMAX_WORDS words, the next block's operand bound;
-  // ABI 8, y null: only these -- k_bn_relu_stats)
+  // ABI 8, y null: only these -- k_bn_relu_stats; ABI 9, y and y_stats null:
+  // nothing -- the consumer forms ReLU(BN2(U)) itself)
+  if (!a->y && !ys) return STGCN_OK;
   if (ys && !stat_parts) HIP_TRY(hipMemsetAsync(ys, 0, y_stats_bytes(R), s));
   HIP_TRY(launch_bn_relu_fwd(a->U, mean2, invstd2, a->g2, a->b2, a->y, N, R, To * V, ys,
                              ys ? ys + R : nullptr, ydrop, s,

@@ -98,6 +98,29 @@ __global__ __launch_bounds__(256) void k_head_pool(const float *y, float *pooled
   if (lane == 0) pooled[row] = s / (float)L;
 }
 
+// ABI 9: the same mean over y = ReLU(BN2(U)) formed on load from the last
+// block's pre-BN2 tensor U (its y is never written): the element arithmetic of
+// k_bn_relu_fwd (kernels.hip bn_relu_fwd_body), the summation order of
+// k_head_pool, so pooled is bit-identical to pooling the written y
+__global__ __launch_bounds__(256) void k_head_pool_u(const float *U, const float *mean,
+                                                     const float *invstd, const float *g,
+                                                     const float *b, float *pooled, int64_t rows,
+                                                     int C, int L) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int c = (int)(row % C);
+  const float mu = mean[c], a = invstd[c] * g[c], be = b[c];
+  const float *src = U + row * L;
+  float s = 0.f;
+  for (int l = lane; l < L; l += 64) {
+    const float t = (src[l] - mu) * a + be;
+    s += t > 0.f ? t : 0.f;
+  }
+  s = wave_sumf(s);
+  if (lane == 0) pooled[row] = s / (float)L;
+}
+
 // one block per clip: logits = pooled W^T + b, per-clip CE loss (log-sum-exp)
 __global__ __launch_bounds__(256) void k_head_fc_ce(const float *pooled, const float *W,
                                                     const float *bias, const int64_t *labels,
@@ -280,6 +303,29 @@ int stgcn_head_fwd(const stgcn_head_desc_t *d, const float *y, const float *W, c
   const int64_t rows = (int64_t)d->N * d->C;
   hipLaunchKernelGGL(k_head_pool, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, y, pooled,
                      rows, d->L);
+  hipLaunchKernelGGL(k_head_fc_ce, dim3(d->N), dim3(256),
+                     (size_t)(d->C + d->classes + 8) * sizeof(float), s, pooled, W, bias, labels,
+                     logits, lossv, d->C, d->classes);
+  hipLaunchKernelGGL(k_head_loss_mean, dim3(1), dim3(64), 0, s, lossv, loss, d->N);
+  HIP_TRY2(hipGetLastError());
+  return STGCN_OK;
+}
+
+int stgcn_head_fwd_u(const stgcn_head_desc_t *d, const float *U, const float *stats2,
+                     const float *g2, const float *b2, const float *W, const float *bias,
+                     const int64_t *labels, float *pooled, float *logits, float *lossv,
+                     float *loss, void *stream) {
+  if (!d || d->N <= 0 || d->C <= 0 || d->L <= 0 || d->classes <= 0)
+    return fail(STGCN_E_INVALID, "head: bad descriptor");
+  if (!U || !stats2 || !g2 || !b2 || !W || !bias || !labels || !pooled || !logits || !lossv ||
+      !loss)
+    return fail(STGCN_E_INVALID, "head: null tensor argument");
+  if ((size_t)(d->C + d->classes + 8) * sizeof(float) > 64 * 1024)
+    return fail(STGCN_E_UNSUPPORTED, "head: C + classes too large");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = (int64_t)d->N * d->C;
+  hipLaunchKernelGGL(k_head_pool_u, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, U, stats2,
+                     stats2 + d->C, g2, b2, pooled, rows, d->C, d->L);
   hipLaunchKernelGGL(k_head_fc_ce, dim3(d->N), dim3(256),
                      (size_t)(d->C + d->classes + 8) * sizeof(float), s, pooled, W, bias, labels,
                      logits, lossv, d->C, d->classes);

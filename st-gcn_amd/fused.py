@@ -90,6 +90,9 @@ class ChainCtx:
         # ABI 8: this block's y is not written (the next block forms it from U);
         # this block's input is the previous block's ReLU(BN2(prev_U)) (x unwritten)
         self.y_lazy, self.x_from_u = False, False
+        # ABI 9: the last block's y is read by the head only, which pools it from
+        # U (stgcn_head_fwd_u): neither y nor its statistics are formed
+        self.y_head = False
 
 
 def stack_descs(blocks, x_shape, training=True):
@@ -113,6 +116,14 @@ def _hooked(m):
     return bool(m._forward_hooks or m._forward_pre_hooks
                 or getattr(_mod, "_global_forward_hooks", None)
                 or getattr(_mod, "_global_forward_pre_hooks", None))
+
+
+def head_link_ok(blk):
+    """True when the last block's output can stay unwritten because only the
+    fused head reads it (ABI 9, stgcn_head_fwd_u): non-residual, no dropout,
+    no forward hooks that could observe it."""
+    drop = blk.dropout.p if blk.dropout is not None else 0.0
+    return not blk.residual and drop == 0 and not _hooked(blk)
 
 
 def lazy_links(blocks, x_shape):

@@ -21,7 +21,7 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
     import sys
     print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
-ABI_VERSION = 8
+ABI_VERSION = 9
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -104,7 +104,7 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
             "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
             "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes",
-            "stgcn_block_plan", "stgcn_fold_prep_bytes", "stgcn_fold_prep")
+            "stgcn_block_plan", "stgcn_fold_prep_bytes", "stgcn_fold_prep", "stgcn_head_fwd_u")
 
 _LIB = None
 
@@ -138,6 +138,8 @@ def load_library(path=LIB_PATH):
     lib.stgcn_time_kernel.restype = ctypes.c_int
     lib.stgcn_head_fwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 8 + [_vp]
     lib.stgcn_head_fwd.restype = ctypes.c_int
+    lib.stgcn_head_fwd_u.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 11 + [_vp]
+    lib.stgcn_head_fwd_u.restype = ctypes.c_int
     lib.stgcn_head_bwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 10 + [_vp]
     lib.stgcn_head_bwd.restype = ctypes.c_int
     lib.stgcn_adam_table_bytes.argtypes = [ctypes.c_int]

@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 
 from .graph import Strategy, get_normalized_adjacency_matrices
-from .fused import FoldPrep, lazy_links
+from .fused import FoldPrep, head_link_ok, lazy_links
 from .network import SpatialTemporalConv, StackChain
 from .train_ops import StgcnHeadFn
 
@@ -57,9 +57,11 @@ class STGCNStack(nn.Module):
         self.conv = nn.Sequential(*blocks).float()
         self.fc_layer = nn.Linear(256, nr_classes).float()
 
-    def _chain(self, x):
+    def _chain(self, x, head=False):
         """The StackChain of a training forward, with the stack's folded blocks'
-        weight-only operands formed for this step (fused.FoldPrep, ABI 7)."""
+        weight-only operands formed for this step (fused.FoldPrep, ABI 7).
+        head: the fused head follows (forward_loss), so the last block's output
+        can stay unwritten too (ABI 9)."""
         if not self.training:
             return None
         chain = StackChain(defer_counts=True)
@@ -70,7 +72,10 @@ class STGCNStack(nn.Module):
             # (ABI 8: block outputs that only the next block reads stay unwritten;
             # self.lazy_links = False writes every one)
             if getattr(self, "lazy_links", True):
-                chain.set_lazy(lazy_links(list(self.conv), tuple(x.shape)))
+                flags = lazy_links(list(self.conv), tuple(x.shape))
+                if head and head_link_ok(self.conv[-1]):
+                    flags[-1] = "head"
+                chain.set_lazy(flags)
         return chain
 
     def forward_nctv(self, x):
@@ -95,11 +100,15 @@ class STGCNStack(nn.Module):
         NCTV, labels int64 (N) -> (mean cross-entropy loss, logits); the same
         arithmetic as F.cross_entropy(self.forward_nctv(x), labels)
         (lightning_model.py:105-107, :202)."""
-        chain = self._chain(x)
+        chain = self._chain(x, head=True)
         for blk in self.conv:
             x = blk(x, chain=chain)
         if chain is not None:
             chain.flush_counts()
+            if chain.head_ready(x):  # (ABI 9: x was never written; pooled from U)
+                U, stats2 = chain.u_stats
+                return StgcnHeadFn.apply(x, self.fc_layer.weight, self.fc_layer.bias, labels,
+                                         (U, stats2) + tuple(chain.g2b2))
         return StgcnHeadFn.apply(x, self.fc_layer.weight, self.fc_layer.bias, labels)
 
 

@@ -44,6 +44,12 @@ class StackChain:
         decides, knowing the next block)."""
         self.lazy = list(flags)
 
+    def head_ready(self, y):
+        """The stack's last output y was left unwritten for the fused head (ABI 9):
+        the head pools ReLU(BN2(U)) from the last block's U."""
+        return (self.y_lazy and self.y is y and y._version == self.y_version
+                and self.u_stats is not None and self.g2b2 is not None)
+
     def next_lazy(self):
         lazy = getattr(self, "lazy", None)
         return lazy.pop(0) if lazy else False
@@ -187,6 +193,8 @@ class SpatialTemporalConv(nn.Module):
                           prep=chain.next_prep(),
                           out_link=None if (self.residual or drop > 0) else Link())
             cc.y_lazy = bool(lazy) and cc.out_link is not None
+            if cc.y_lazy and lazy == "head":  # (ABI 9: the fused head pools it from U)
+                cc.y_head, cc.y_stats = True, None
             if chain.y is not None and x is chain.y and x._version == chain.y_version:
                 cc.x_stats = chain.y_stats
                 if chain.link is not None:

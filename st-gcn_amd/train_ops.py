@@ -22,10 +22,13 @@ def _check_f32(t, name):
 class StgcnHeadFn(torch.autograd.Function):
     """forward(y (N,C,T,V), W (classes,C), b (classes), labels int64 (N)) ->
     (loss (scalar, mean cross entropy), logits (N, classes), non-differentiable).
-    Same arithmetic as ``F.cross_entropy(fc_layer(avg_pool2d(y, (T,V)).view(N,C)), labels)``."""
+    Same arithmetic as ``F.cross_entropy(fc_layer(avg_pool2d(y, (T,V)).view(N,C)), labels)``.
+    from_u = (U, stats2, g2, b2) (ABI 9, model.STGCNStack.forward_loss): y is the
+    last block's UNWRITTEN output; the pool forms y = ReLU(BN2(U)) on load
+    (stgcn_head_fwd_u, bit-identical); y still receives the gradient."""
 
     @staticmethod
-    def forward(ctx, y, W, b, labels):
+    def forward(ctx, y, W, b, labels, from_u=None):
         lib = hip_lib.lib()
         y = y.contiguous()
         for t, n in ((y, "y"), (W, "W"), (b, "b")):
@@ -44,8 +47,18 @@ class StgcnHeadFn(torch.autograd.Function):
         logits = torch.empty((N, classes), device=dev, dtype=torch.float32)
         lossv = torch.empty(N, device=dev, dtype=torch.float32)
         loss = torch.empty((), device=dev, dtype=torch.float32)
-        hip_lib.check(lib.stgcn_head_fwd(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
-            y, W, b, labels, pooled, logits, lossv, loss)], hip_lib.stream_handle(dev)))
+        if from_u is not None:
+            U, stats2, g2, b2 = from_u
+            for t, n in ((U, "U"), (stats2, "stats2"), (g2, "g2"), (b2, "b2")):
+                _check_f32(t, n)
+            if U.shape != y.shape or stats2.numel() < 2 * C or g2.numel() != C or b2.numel() != C:
+                raise RuntimeError("head: U / BN2 parameters do not match y")
+            hip_lib.check(lib.stgcn_head_fwd_u(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
+                U, stats2, g2, b2, W, b, labels, pooled, logits, lossv, loss)],
+                hip_lib.stream_handle(dev)))
+        else:
+            hip_lib.check(lib.stgcn_head_fwd(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
+                y, W, b, labels, pooled, logits, lossv, loss)], hip_lib.stream_handle(dev)))
         ctx.save_for_backward(pooled, logits, W, labels)
         ctx.shape = y.shape
         ctx.mark_non_differentiable(logits)
@@ -71,7 +84,7 @@ class StgcnHeadFn(torch.autograd.Function):
         hip_lib.check(lib.stgcn_head_bwd(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
             pooled, logits, W, labels, dloss, dlogits, dpooled, dy, dW, db)],
             hip_lib.stream_handle(dev)))
-        return dy, dW, db, None
+        return dy, dW, db, None, None
 
 
 class FusedAdam(torch.optim.Optimizer):

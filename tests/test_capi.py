@@ -29,7 +29,7 @@ def test_header_declares_entry_points(pkg):
 def test_library_exports_every_header_symbol(pkg, lib):
     for name in _header_functions():
         assert hasattr(lib, name), name
-    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 8
+    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 9
 
 
 def _desc(pkg, **kw):
@@ -192,3 +192,23 @@ def test_x_from_u_plan_and_argument_checks(pkg, lib):
     b.G = one
     assert lib.stgcn_block_bwd(ctypes.byref(d), ctypes.byref(b), None, 0, None) == -1
     assert b"x null" in lib.stgcn_last_error()
+
+
+def test_head_link_decision(pkg):
+    """ABI 9: the last block's output is left to the fused head only for a
+    non-residual block without dropout and without forward hooks."""
+    import contextlib
+    import io
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = pkg.STGCNStack(3, 10, A)
+        mr = pkg.STGCNStack(3, 10, A, residual=True)
+        md = pkg.STGCNStack(3, 10, A, dropout_rate=0.5)
+    assert pkg.fused.head_link_ok(m.conv[-1])
+    assert not pkg.fused.head_link_ok(mr.conv[-1])
+    assert not pkg.fused.head_link_ok(md.conv[-1])
+    h = m.conv[-1].register_forward_hook(lambda *a: None)
+    assert not pkg.fused.head_link_ok(m.conv[-1])
+    h.remove()
+    assert pkg.fused.head_link_ok(m.conv[-1])

@@ -696,3 +696,68 @@ def test_stack_lazy_links_bit_identical(pkg, f32_gemm):
             assert torch.equal(a, b), (step, k)
         if step == 1:
             assert torch.equal(seen["y4"], seen["y4_ref"])
+
+
+@pytest.mark.parametrize("f32_gemm", ["f16x2", "mfma"])
+def test_stack_head_pools_from_u(pkg, f32_gemm):
+    """ABI 9 (stgcn_head_fwd_u): in a training step the last block's output is
+    read only by the fused head, so neither it nor its statistics are formed;
+    the head pools ReLU(BN2(U)) from the last block's U. Loss and logits are
+    bit-identical to the stack that writes every output; a forward hook on the
+    last block brings the written output back (and the hook sees it)."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    torch.manual_seed(5)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 60, A, f32_gemm=f32_gemm).cuda().train()
+        m2 = pkg.STGCNStack(3, 60, A, f32_gemm=f32_gemm).cuda().train()
+    m2.load_state_dict(m1.state_dict())
+    m2.lazy_links = False
+    x = torch.randn(3, 3, 64, 18, generator=torch.Generator().manual_seed(6)).cuda()
+    lab = torch.randint(0, 60, (3,), generator=torch.Generator().manual_seed(7)).cuda()
+    lib = pkg.hip_lib.lib()
+    orig = lib.stgcn_head_fwd_u
+    calls = []
+
+    def counted(*a):
+        calls.append(1)
+        return orig(*a)
+    lib.stgcn_head_fwd_u = counted
+    try:
+        for step in range(3):
+            seen = {}
+            hooks = []
+            if step == 2:  # observed last output: written, the ordinary head
+                hooks = [m.conv[-1].register_forward_hook(
+                    lambda mod, i, o, key=key: seen.__setitem__(key, o.detach().clone()))
+                    for m, key in ((m1, "y"), (m2, "y_ref"))]
+            n0 = len(calls)
+            loss1, out1 = m1.forward_loss(x, lab)
+            n1 = len(calls)
+            loss2, out2 = m2.forward_loss(x, lab)
+            assert len(calls) == n1, "the unlazy stack must use the ordinary head"
+            assert n1 - n0 == (0 if step == 2 else 1), step
+            for h in hooks:
+                h.remove()
+            m1.zero_grad()
+            m2.zero_grad()
+            loss1.backward()
+            loss2.backward()
+            torch.cuda.synchronize()
+            assert torch.equal(out1, out2) and torch.equal(loss1, loss2), step
+            g2 = {k: b.grad for k, b in m2.named_parameters()}
+            for k, a in m1.named_parameters():
+                b = g2[k]
+                if k.endswith("temporalConv.bias") or k.endswith("batch_n_2.weight"):
+                    scale = g2[k.rsplit(".", 1)[0] + ".bias"].abs().max().item() if \
+                        k.endswith("weight") else 1.0
+                    assert (a.grad - b).abs().max().item() <= 1e-5 * scale, (step, k)
+                    continue
+                tol = 2e-3 if k.endswith("spatialConv.A") else 1e-5
+                assert rel_to_max(a.grad.cpu().numpy(), b.cpu().numpy()) < tol, (step, k)
+            for (k, a), b in zip(m1.named_buffers(), m2.buffers()):
+                assert torch.equal(a, b), (step, k)
+            if step == 2:
+                assert torch.equal(seen["y"], seen["y_ref"])
+    finally:
+        lib.stgcn_head_fwd_u = orig
