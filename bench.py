@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -90,6 +91,33 @@ def cpu_model():
         pass
     import platform
     return platform.processor() or "unknown"
+
+
+def gpu_state_start():
+    """Starts a rocm-smi sample of the GPUs' clocks and power (read-only), so a
+    bench line carries the clock state it ran at: box-to-box spread of the same
+    tree is +-5 %, and a lower sclk under load is one cause."""
+    try:
+        return subprocess.Popen(["rocm-smi", "--showclocks", "--showpower", "--showmaxpower",
+                                 "--json"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                text=True)
+    except OSError:
+        return None
+
+
+def gpu_state_read(proc):
+    """{card: {sclk, mclk, fclk, power, power cap ...}} from gpu_state_start, or None."""
+    if proc is None:
+        return None
+    try:
+        out, _ = proc.communicate(timeout=30)
+        data = json.loads(out)
+    except (subprocess.TimeoutExpired, ValueError):
+        proc.kill()
+        return None
+    keys = ("sclk", "mclk", "fclk", "socclk", "power")
+    return {card: {k: v for k, v in vals.items() if any(s in k.lower() for s in keys)}
+            for card, vals in data.items() if card.startswith("card")} or None
 
 
 def cgroup_cpu_quota():
@@ -518,7 +546,10 @@ def main():
     # two more windows of the same K steps (same brackets), for the median of
     # three; `value` stays the first window, timed exactly as the contract says
     runs = [clips]
-    for _ in range(2 if args.repeats else 0):
+    smi = None  # rocm-smi sample taken during the last repeat window (under load)
+    for rep in range(2 if args.repeats else 0):
+        if rep == 1 and rank == 0:
+            smi = gpu_state_start()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -613,6 +644,8 @@ def main():
             "median_clips_s": round(sorted(runs)[len(runs) // 2], 2),
             "loss": round(float(loss.item()), 5),
         }
+        out["gpu_state_under_load"] = gpu_state_read(smi)
+        out["gpu_state_after"] = gpu_state_read(gpu_state_start())
         if alt is not None:
             out["alt_fp32_modes"] = alt
         if sweep is not None:

@@ -69,6 +69,9 @@
 #ifndef STGCN_AB_SPB_PAIR        // the folded block's H stored + k_spatial_bwd5 (no fused epilogue)
 #define STGCN_AB_SPB_PAIR 0
 #endif
+#ifndef STGCN_AB_X3_NOW4        // the 8-wave 128-row k_conv_x3 for the fp16-split stride-1 forward
+#define STGCN_AB_X3_NOW4 0
+#endif
 #ifndef STGCN_AB_F16X2_DGRAD     // 0: the folded data gradient on 3-way bf16 splits under STGCN_F_F16X2
 #define STGCN_AB_F16X2_DGRAD 1
 #endif

@@ -166,6 +166,13 @@ bool f16x2_dgrad(const stgcn_desc_t *d) {
 // backward): measured 4% slower per cfg2 step than forming G once with k_gather4
 //  -- the joint contraction then runs on the VALU inside
 // latency-bound GEMM kernels instead of inside an HBM-bound pass.
+bool fold_bna(const stgcn_desc_t *d);
+// The fp16-split stride-1 temporal forward (folded, or the unfolded first
+// block) on 4-wave 64-row tiles, two workgroups per CU (kernels_x3.hip x3_w4):
+// marks the GEMM's parameters wherever its weights are packed or it is launched
+bool fwd_w4(const stgcn_desc_t *d) {
+  return d->stride == 1 && ((f16x2(d) && !fold_bna(d)) || f16x2_unfold(d));
+}
 bool fold_bna(const stgcn_desc_t *d) {
   if (!f16x2(d) || !(d->flags & STGCN_F_NO_G)) return false;
   ConvGemmParams p{};
@@ -460,6 +467,7 @@ ConvGemmParams fold_fwd_wparams(const stgcn_desc_t *d, const float *Wc) {
   p.NQ = 9;
   p.s_in = d->stride;
   p.s_out = 1;
+  p.w4 = fwd_w4(d) ? 1 : 0;
   return p;
 }
 ConvGemmParams fold_dgrad_wparams(const stgcn_desc_t *d, const float *Wc, int ph) {
@@ -1036,6 +1044,7 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
     p.M = To;
     p.T_src = T;
     p.T_dst = To;
+    p.w4 = fwd_w4(d) ? 1 : 0;
     conv_tiles(p);
     // (the folded forward on k_conv_x3: BN2 statistics as per-tile partials)
     if (stat_parts) p.stat_part = L.s2part;
@@ -1634,6 +1643,7 @@ TimedPlan plan_timed(const stgcn_desc_t *d, int which, void *scratch) {
       P.ax[1] = p.w;
       P.an[1] = (int64_t)R * CZ * 9;
     }
+    p.w4 = fwd_w4(d) ? 1 : 0;
     if (fold_bna(d)) {  // x in: BN1 in the loader, the joint contraction in the epilogue
       p.bna = 1;
       p.sA = c.take<float>((size_t)V * V);

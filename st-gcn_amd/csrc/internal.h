@@ -109,6 +109,10 @@ struct ConvGemmParams {
   // loader and the joint contraction with sA in the epilogue -- G is never formed;
   // amax_in holds max |x| (the fp16 operand bound is formed in the kernel)
   int bna;
+  // w4 (the fp16-split stride-1 forward; kernels_x3.hip x3_w4): 4-wave 64-row
+  // tiles, two workgroups per CU. Set by the caller where it packs AND where it
+  // launches (capi.hip fwd_w4), so the weight layout and the kernel agree
+  int w4;
 };
 
 // Weight-gradient GEMM with split-K partial slabs:

@@ -50,6 +50,9 @@
 #ifndef STGCN_WG_EXP  // k_wgrad_x3 timing experiments only (results wrong): bit 1 no
 #define STGCN_WG_EXP 0  // staging, 2 no MFMAs, 4 no fragment reads, 8 no item barrier
 #endif
+#ifndef STGCN_X3_STAG  // k_conv_x3: waves 4-7 run each step's last tap after the next barrier
+#define STGCN_X3_STAG 1
+#endif
 #ifndef STGCN_X3_EXP  // timing experiments only (bits skip work; results wrong)
 #define STGCN_X3_EXP 0
 #endif
@@ -154,9 +157,18 @@ __device__ __forceinline__ void wait_img(float (&st)[4][8]) {
 }
 #undef X3_ST8
 
-template <int NQ, int TG, int V, int SIN, int MR, int NPL>
+// NW = 8: two row halves of 32 MR rows (waves w, w ^ 1), ROWS = 64 MR, one
+// workgroup per CU (fp32 splits) or two (bf16). NW = 4 (the fp16-split stride-1
+// forward, x3_w4): one 64-row half, ROWS = 32 MR = 64, each wave 64 rows x two
+// column tiles (the 128-row wave shape), LDS <= 80 KiB: TWO workgroups per CU,
+// whose barriers, DMA waits, window staging, prologue and epilogue are
+// independent -- each covers the other's with its MFMAs.
+template <int NQ, int TG, int V, int SIN, int MR, int NPL, int NW = 8>
 struct ConvX3Geo {
-  static constexpr int ROWS = 64 * MR;            // output rows per workgroup
+  static_assert(NW == 8 || (NW == 4 && MR == 2 && NPL == 2), "4-wave tiles: 64 rows, fp16 splits");
+  static constexpr int NT = NW * 64;              // threads per workgroup
+  static constexpr int RH = NW == 8 ? 2 : 1;      // row halves
+  static constexpr int ROWS = 32 * MR * RH;       // output rows per workgroup
   static constexpr int CK = 16;                   // channels per chunk (one k-step)
   static constexpr int FT = kTileCols / V;
   static constexpr int NCOLS = FT * V;
@@ -175,13 +187,13 @@ struct ConvX3Geo {
   static constexpr int FP = V * SLOTS + FPAD;     // slots per window frame
   static constexpr int IMG = (SPAN / V) * FP * 16;  // window bytes
   static constexpr int NG = NQ / TG;              // steps per chunk
-  static constexpr int WST = NPL * TG * 2 * 1024 * MR;  // packed weight bytes per step
+  static constexpr int WST = NPL * TG * 2 * ROWS * 16;  // packed weight bytes per step
   static constexpr int WDMA = WST / 1024;         // 1 KiB DMA pieces per step
   // LDS plan, first that fits: window double-buffered with a 3-step weight ring
   // (prefetch distance 2), double-buffered with a 2-step ring, or a single
   // window (written between two barriers) with a 3- or 2-step ring
   // (NPL = 1: two workgroups per CU)
-  static constexpr int BUDGET = NPL == 1 ? 80 * 1024 : 160 * 1024;
+  static constexpr int BUDGET = (NPL == 1 || NW == 4) ? 80 * 1024 : 160 * 1024;
   static constexpr int PLAN = 3 * WST + 2 * IMG <= BUDGET   ? 0
                               : 2 * WST + 2 * IMG <= BUDGET ? 1
                               : 3 * WST + IMG <= BUDGET     ? 2
@@ -193,10 +205,10 @@ struct ConvX3Geo {
   static constexpr int MAIN = NWB * WST + NWIN * IMG;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   static constexpr int NIT = SPAN * 2;            // (position, octet) staging items
-  static constexpr int IPT = (NIT + 511) / 512;   // staging items per thread
+  static constexpr int IPT = (NIT + NT - 1) / NT;  // staging items per thread
   static_assert(IPT >= 2 && IPT <= 4, "wait_img overloads");
-  static constexpr int DPW = (WDMA + 7) / 8;      // DMA pieces per wave and step (max)
-  static constexpr int DPWMIN = WDMA / 8;         // ... issued by every wave
+  static constexpr int DPW = (WDMA + NW - 1) / NW;  // DMA pieces per wave and step (max)
+  static constexpr int DPWMIN = WDMA / NW;          // ... issued by every wave
   // vmcnt allowance at step g's barrier (DMA(s) must have landed): the VMEM
   // operations every wave issued after DMA(s) in steady state — the pieces of
   // the PD-1 later weight steps and the window loads of the chunk-start steps
@@ -647,10 +659,11 @@ __device__ __forceinline__ void bna_contract(float *img, const float *ar) {
 // BNA (V = 18, NPL = 2): the folded forward from x (BN1 in the loader, A in the
 // epilogue; see bna_contract)
 template <int NQ, int TG, int V, int SIN, int MR, int NPL, bool IB = false, bool SPB = false,
-          bool BNA = false>
-__global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
-  using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL>;
+          bool BNA = false, int NW = 8>
+__global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv_x3(ConvGemmParams p) {
+  using G = ConvX3Geo<NQ, TG, V, SIN, MR, NPL, NW>;
   static_assert(!BNA || (V == 18 && NPL == 2 && !SPB), "bna: the folded fp16-split forward");
+  static_assert(NW == 8 || (!SPB && !BNA && SIN == 1), "4-wave tiles: the plain stride-1 forward");
   static_assert(kBnaAr <= 512, "one A element per thread");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   char *lds = reinterpret_cast<char *>(smem);
@@ -670,7 +683,8 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   const int nchunks = (p.C + G::CK - 1) / G::CK;
   const int nsteps = nchunks * G::NG;
   const char *wblk = reinterpret_cast<const char *>(p.wpk) + (int64_t)rt * nsteps * G::WST;
-  const int mi = wave & 1, nj0 = ((wave >> 1) & 1) * 4 + half * 2;
+  const int mi = NW == 8 ? wave & 1 : 0;
+  const int nj0 = NW == 8 ? ((wave >> 1) & 1) * 4 + half * 2 : wave * 2;
 
   // A fragment (plane 0, tap 0, octet hi, row block 0) and B fragments (tap 0,
   // plane 0, octet hi); wave rows mi*32*MR .. +32*MR-1 (MR 32-row blocks)
@@ -688,7 +702,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   int loff[G::IPT], ioct[G::IPT];
 #pragma unroll
   for (int k = 0; k < G::IPT; ++k) {
-    const int e = k * 512 + tid;
+    const int e = k * G::NT + tid;
     const int o = e / G::SPAN, pp = e - o * G::SPAN;
     const int g = g0 + pp;
     const bool ok = e < G::NIT && g >= 0 && g < cstride;
@@ -826,7 +840,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   auto dma_w = [&](int step, int buf) {
 #pragma unroll
     for (int i = 0; i < G::DPW; ++i) {
-      const int d = i * 8 + wave;
+      const int d = i * NW + wave;
       if (d < G::WDMA) {
         const unsigned voffw = (unsigned)(step * G::WST + d * 1024 + lane * 16);
         const unsigned m0v = lds0 + (unsigned)(buf * G::WST + d * 1024);
@@ -846,7 +860,10 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
   // Tile (row block rb, column tile j) -> acc[rb*2 + j] (MR = 1: acc[2..3] are
   // the hand-over registers of the stride-2 epilogue)
   // (NPL = 1: plain bf16 operands, acc only)
-  constexpr int NACL = NPL >= 2 ? 2 * MR : 1;
+  // (NW = 4: every product in acc -- one fp32 chain per tile, small products
+  // first within a tap; the 64 registers of acl would spill the 4-wave kernel)
+  constexpr bool kOneAcc = NW == 4;
+  constexpr int NACL = NPL >= 2 && !kOneAcc ? 2 * MR : 1;
   floatx16 acc[4], acl[NACL];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -866,7 +883,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
 #pragma unroll
       for (int rb = 0; rb < MR; ++rb)
         f.a[pl][rb] = *reinterpret_cast<const bf16x8_t *>(
-            wa + ((pl * TG + qq) * 2 * MR) * 1024 + rb * 32 * 16);
+            wa + (pl * TG + qq) * 2 * G::ROWS * 16 + rb * 32 * 16);
 #pragma unroll
     for (int pl = 0; pl < NPL; ++pl)
 #pragma unroll
@@ -894,6 +911,28 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         }
   };
 
+  // Stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): the two waves of
+  // a SIMD are wave w and w + 4 of this workgroup, and with one barrier per step
+  // they reach every step's wait, barrier and first fragment reads together while
+  // the matrix pipe idles. Waves 4-7 therefore run each step's LAST tap of MFMAs
+  // after the next step's barrier, beside that step's first fragment reads: their
+  // partner's exposed reads after the barrier are covered by these MFMAs, and
+  // their own wait at the barrier by the partner's last tap. Only register-held
+  // fragments cross the barrier (every LDS read of step s still happens between
+  // barriers s and s + 1), so the buffer hand-offs are unchanged, and every
+  // accumulator sees the same MFMAs in the same order (bit-identical results).
+  // (not where the fragments held across the window staging push the kernel
+  // past its register budget: the 128-row stride-2 forward spills, and the
+  // 64-row bf16 V = 50 stride-2 forward would lose its second workgroup per CU)
+  constexpr bool kStag = STGCN_X3_STAG && (NPL == 2   ? !(MR == 2 && SIN == 2)
+                                           : NPL == 3 ? MR == 1
+                                                      : !(V == 50 && SIN == 2));
+  const bool stag = kStag && half == 1;  // (wave-uniform)
+  // MR = 1: fragment sets in flight, tap qq of a step in f[qq % NF]; the deferred
+  // last tap must not share a set with the next step's tap 0
+  constexpr int NF = MR == 1 ? (kStag && TG % 2 == 1 ? 3 : 2) : 1;
+  static_assert(!kStag || MR != 1 || (TG > 1 && (TG - 1) % NF != 0), "deferred tap's fragment set");
+  Frag f[NF];
 #pragma unroll
   for (int d = 0; d < G::PD; ++d)
     if (d < nsteps) dma_w(d, d);
@@ -909,6 +948,93 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     in_se = f16x2_se_bits(__builtin_bit_cast(unsigned, bound));
     in_scale = pow2f(in_se);
   }
+  // MR = 1: tap qq's MFMAs (fragment set fm) with the NEXT tap's fragment reads
+  // (set fl from weights wl / window wn, tap ql, window frame qn) interleaved
+  constexpr int NR1 = NPL * (MR + 2), NM1 = (NPL == 3 ? 6 : (NPL == 2 ? 3 : 1)) * 2 * MR;
+  constexpr int NI1 = NR1 < NM1 ? NR1 : NM1;
+  auto mm_ld1 = [&](const Frag &fm, const char *wl, const char *wn, int ql, int qn, Frag &fl) {
+    ld(wl, wn, ql, qn, fl);
+    if (!(STGCN_X3_EXP & 16)) mm(fm);
+#pragma unroll
+    for (int i = 0; i < NI1; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+    if constexpr (NM1 > NI1) __builtin_amdgcn_sched_group_barrier(0x008, NM1 - NI1, 0);
+    if constexpr (NR1 > NI1) __builtin_amdgcn_sched_group_barrier(0x100, NR1 - NI1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // MR = 2: one fragment set, refilled in place for the next tap as its planes
+  // retire (48 instead of 96 fragment registers live). Product order per tap:
+  // mm, lh, hl, mh, hm, hh -- the first (a1 x b1) uses neither plane-0
+  // fragment, which are the last ones refilled. tap2(nx, wl, wn, ql, qn): the
+  // MFMAs of the tap in f[0], refilled (nx) with tap ql / window frame qn
+  auto grp = [&](int pa, int pb) {
+    if (STGCN_X3_EXP & 16) return;
+    Frag &fr = f[0];
+#pragma unroll
+    for (int rb = 0; rb < MR; ++rb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if ((pa == 0 && pb == 0) || kOneAcc)
+          acc[rb * 2 + j] =
+              mfma_p<NPL>(fr.a[pa % NPL][rb], fr.b[pb % NPL][j], acc[rb * 2 + j]);
+        else
+          acl[(rb * 2 + j) % NACL] =
+              mfma_p<NPL>(fr.a[pa % NPL][rb], fr.b[pb % NPL][j], acl[(rb * 2 + j) % NACL]);
+      }
+  };
+  auto lda = [&](const char *wl, int qq, int pl) {
+#pragma unroll
+    for (int rb = 0; rb < MR; ++rb)
+      f[0].a[pl][rb] = *reinterpret_cast<const bf16x8_t *>(
+          wl + (pl * TG + qq) * 2 * G::ROWS * 16 + rb * 32 * 16);
+  };
+  auto ldb = [&](const char *wn, int q, int pl) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      f[0].b[pl][j] = *reinterpret_cast<const bf16x8_t *>(wn + bo[j] + (q * G::FP + 2 * pl) * 16);
+  };
+  auto tap2 = [&](bool nx, const char *wl, const char *wn, int ql, int qn) {
+    if constexpr (NPL == 2) {
+      // fp16 (h, l): products lh, hl, hh; plane 1 of A / B refilled as it retires
+      grp(1, 0);
+      if (nx) lda(wl, ql, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(0, 1);
+      if (nx) ldb(wn, qn, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(0, 0);
+      if (nx) {
+        lda(wl, ql, 0);
+        ldb(wn, qn, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      grp(1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(2, 0);
+      if (nx) lda(wl, ql, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(0, 2);
+      if (nx) ldb(wn, qn, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(1, 0);
+      if (nx) lda(wl, ql, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(0, 1);
+      if (nx) ldb(wn, qn, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(0, 0);
+      if (nx) {
+        lda(wl, ql, 0);
+        ldb(wn, qn, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  constexpr int FL = (TG - 1) % NF;  // MR = 1: the last tap's fragment set
+
   wait_img<0>(st);
   write_img(win0, 0);
   for (int c = 0; c < nchunks; ++c) {
@@ -926,106 +1052,38 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!(STGCN_X3_EXP & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       const char *wa = wbuf0 + (s % G::NWB) * G::WST + ao;
-      Frag f[2];
-      ld(wa, win, 0, g * TG, f[0]);
+      // tap 0's fragment reads; a staggered wave runs the previous step's last
+      // tap beside them
+      const bool defer = stag && s > 0;
+      if constexpr (MR == 1) {
+        if (defer)
+          mm_ld1(f[FL], wa, win, 0, g * TG, f[0]);
+        else
+          ld(wa, win, 0, g * TG, f[0]);
+      } else {
+        if (defer) {
+          tap2(true, wa, win, 0, g * TG);
+        } else {
+          ld(wa, win, 0, g * TG, f[0]);
+        }
+      }
       // next step's weights and (first step) chunk c+1's window, issued after
       // this step's first fragment reads (a compiler wait placed before those
       // reads then finds no load of ours in flight). The window load is
       // unconditional: chunk == nchunks loads zeros and is never read.
       if (!(STGCN_X3_EXP & 2) && s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
       if (!(STGCN_X3_EXP & 4) && g == 0) load_img(c + 1);
-      if constexpr (MR == 1) {
-        // per tap: NR fragment reads, NM MFMAs
-        constexpr int NR = NPL * (MR + 2), NM = (NPL == 3 ? 6 : (NPL == 2 ? 3 : 1)) * 2 * MR;
-        constexpr int NI = NR < NM ? NR : NM;
 #pragma unroll
-        for (int qq = 0; qq < TG; ++qq) {
-          if (qq + 1 < TG) {
-            // tap qq+1's fragment reads among tap qq's MFMAs
-            ld(wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) & 1]);
-            if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-            }
-            if constexpr (NM > NI) __builtin_amdgcn_sched_group_barrier(0x008, NM - NI, 0);
-            if constexpr (NR > NI) __builtin_amdgcn_sched_group_barrier(0x100, NR - NI, 0);
-          } else {
-            if (!(STGCN_X3_EXP & 16)) mm(f[qq & 1]);
-          }
+      for (int qq = 0; qq < TG; ++qq) {
+        const bool nx = qq + 1 < TG;
+        if constexpr (MR == 1) {
+          if (nx)  // tap qq+1's fragment reads among tap qq's MFMAs
+            mm_ld1(f[qq % NF], wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) % NF]);
+          else if (!stag && !(STGCN_X3_EXP & 16))
+            mm(f[qq % NF]);
           __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        // MR = 2: one fragment set, refilled in place for the next tap as its
-        // planes retire (48 instead of 96 fragment registers live). Product
-        // order per tap: mm, lh, hl, mh, hm, hh -- the first (a1 x b1) uses
-        // neither plane-0 fragment, which are the last ones refilled
-        Frag &fr = f[0];
-        auto grp = [&](int pa, int pb) {
-          if (STGCN_X3_EXP & 16) return;
-#pragma unroll
-          for (int rb = 0; rb < MR; ++rb)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              if (pa == 0 && pb == 0)
-                acc[rb * 2 + j] = mfma_p<NPL>(fr.a[0][rb], fr.b[0][j], acc[rb * 2 + j]);
-              else
-                acl[rb * 2 + j] = mfma_p<NPL>(fr.a[pa % NPL][rb], fr.b[pb % NPL][j], acl[rb * 2 + j]);
-            }
-        };
-        auto lda = [&](int qq, int pl) {
-#pragma unroll
-          for (int rb = 0; rb < MR; ++rb)
-            fr.a[pl][rb] = *reinterpret_cast<const bf16x8_t *>(
-                wa + ((pl * TG + qq) * 2 * MR) * 1024 + rb * 32 * 16);
-        };
-        auto ldb = [&](int q, int pl) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            fr.b[pl][j] =
-                *reinterpret_cast<const bf16x8_t *>(win + bo[j] + (q * G::FP + 2 * pl) * 16);
-        };
-#pragma unroll
-        for (int qq = 0; qq < TG; ++qq) {
-          const bool nx = qq + 1 < TG;
-          const int q1 = g * TG + qq + 1;
-          if constexpr (NPL == 2) {
-            // fp16 (h, l): products lh, hl, hh; plane 1 of A / B refilled as it retires
-            grp(1, 0);
-            if (nx) lda(qq + 1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(0, 1);
-            if (nx) ldb(q1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(0, 0);
-            if (nx) {
-              lda(qq + 1, 0);
-              ldb(q1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          } else {
-            grp(1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(2, 0);
-            if (nx) lda(qq + 1, 2);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(0, 2);
-            if (nx) ldb(q1, 2);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(1, 0);
-            if (nx) lda(qq + 1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(0, 1);
-            if (nx) ldb(q1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            grp(0, 0);
-            if (nx) {
-              lda(qq + 1, 0);
-              ldb(q1, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-          }
+        } else {
+          if (nx || !stag) tap2(nx, wa, win, qq + 1, g * TG + qq + 1);
         }
       }
       if (!(STGCN_X3_EXP & 1) && g == G::NG - 1) {
@@ -1037,13 +1095,20 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
       }
     }
   }
+  if (stag) {  // the tile's last tap (register operands only)
+    if constexpr (MR == 1) {
+      if (!(STGCN_X3_EXP & 16)) mm(f[FL]);
+    } else {
+      tap2(false, wbuf0, win0, 0, 0);
+    }
+  }
   if constexpr (NPL == 3) {
 #pragma unroll
     for (int j = 0; j < 2 * MR; ++j) acc[j] += acl[j];
   } else if constexpr (NPL == 2) {  // undo the operand scales (powers of two: exact)
     const float ia = pow2f(-in_se), iw = pow2f(-f16x2_se(p.amax_w));
 #pragma unroll
-    for (int j = 0; j < 2 * MR; ++j) acc[j] = (acc[j] + acl[j]) * ia * iw;
+    for (int j = 0; j < 2 * MR; ++j) acc[j] = (kOneAcc ? acc[j] : acc[j] + acl[j]) * ia * iw;
   }
   if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
     if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
@@ -1070,7 +1135,7 @@ __global__ __launch_bounds__(512, NPL == 1 ? 2 : 1) void k_conv_x3(ConvGemmParam
     }
     // (one-plane bf16 path: the output may be stored in bf16, p.out_bf16 -- the
     // data gradient dZ of capi.hip dz_bf16)
-    conv_tile_store_rows<V, G::NCOLS, 512, G::ROWS, NPL == 1, NPL != 1>(
+    conv_tile_store_rows<V, G::NCOLS, G::NT, G::ROWS, NPL == 1, NPL != 1>(
         p, smem, smem + G::ROWS * kEpiPitch, n, r0, m0);
     return;
   }
@@ -1216,6 +1281,20 @@ static bool x3_wide_rows(const ConvGemmParams &p) {
   constexpr bool off = STGCN_AB_X3_MR1 != 0;
   return !off && p.NQ == 9 && p.s_out == 1 && p.R % 128 == 0;
 }
+// 4-wave 64-row tiles, two workgroups per CU (ConvX3Geo NW = 4): the fp16-split
+// stride-1 forward where the caller marked it (p.w4: capi.hip fwd_w4). Decides
+// the packed weight layout (64-row tiles) and the kernel alike.
+static bool x3_w4(const ConvGemmParams &p, int npl) {
+  constexpr bool off = STGCN_AB_X3_NOW4 != 0;
+  return !off && p.w4 && npl == 2 && !p.spb && !p.bna && p.NQ == 9 && p.s_in == 1 &&
+         p.s_out == 1 && (p.V == 18 || p.V == 25);
+}
+template <int V>
+static void launch_cx_w4(const ConvGemmParams &p, int nblk, hipStream_t s) {
+  using G = ConvX3Geo<9, 3, V, 1, 2, 2, 4>;
+  hipLaunchKernelGGL((k_conv_x3<9, 3, V, 1, 2, 2, false, false, false, 4>), dim3(nblk),
+                     dim3(G::NT), G::LDS, s, p);
+}
 
 template <int NQ, int V, int SIN, int MR, int NPL>
 static bool launch_cx_if(const ConvGemmParams &p, int nblk, hipStream_t s) {
@@ -1268,7 +1347,7 @@ static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
 // (STGCN_F_BF16), the same pipeline with one plane and two workgroups per CU
 // The pack job of a launch_conv_planes call (same layout, same scales)
 static PackJob pack_job(const ConvGemmParams &p, int npl) {
-  const bool wide = npl >= 2 && x3_wide_rows(p);
+  const bool wide = npl >= 2 && x3_wide_rows(p) && !x3_w4(p, npl);
   const int rows = wide ? 128 : 64;
   PackJob j{};
   j.w = p.w;
@@ -1312,7 +1391,8 @@ hipError_t launch_pack_jobs(const PackJob *jobs, int n, hipStream_t s) {
 }
 
 static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStream_t s) {
-  const bool wide = npl >= 2 && x3_wide_rows(p0);
+  const bool w4 = x3_w4(p0, npl);
+  const bool wide = npl >= 2 && x3_wide_rows(p0) && !w4;
   ConvGemmParams p = p0;
   const int rows = wide ? 128 : 64;
   p.n_rtiles = (p.R + rows - 1) / rows;
@@ -1325,7 +1405,11 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
   }
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   bool done = false;
-  if (wide && npl == 2) {
+  if (w4) {
+    if (p.V == 18) launch_cx_w4<18>(p, nblk, s);
+    else launch_cx_w4<25>(p, nblk, s);
+    done = true;
+  } else if (wide && npl == 2) {
     done = launch_cx_v<9, 2, 2>(p, nblk, s);
   } else if (wide) {
     done = launch_cx_v<9, 2, 3>(p, nblk, s);
@@ -1671,18 +1755,31 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0][2 % NPL], f.b[0][t], acl[t]);
       }
     };
+    // Stagger (as in k_conv_x3): waves 4-7 (all NT = 2) run each item's last
+    // k-step of MFMAs after the item barrier, beside the next item's first
+    // fragment reads, so the two waves of a SIMD (w, w + 4) do not wait at the
+    // barrier and on the first reads together. Only registers cross the barrier.
+    // (not with BN1 staging: it pushes the kernel past its register budget)
+    const bool stag = STGCN_X3_STAG && !QBN && NT == 2 && wave >= 4;  // (wave-uniform)
+    // fragment sets: k-step s in f[s % NF]; the deferred last k-step must not
+    // share a set with the next item's first
+    constexpr int NF = NT == 2 && STGCN_X3_STAG && !QBN ? 3 : 2;
+    constexpr int FL = (G::KSTEPS - 1) % NF;
+    static_assert(NF == 2 || FL != 0, "deferred k-step's fragment set");
+    Frag f[NF];
     for (int it = it0; it < it1; ++it) {
       const char *cur = lds + (G::NBUF == 2 ? ((it - it0) & 1) * G::BUF : 0);
       char *nxt = lds + (G::NBUF == 2 ? ((it - it0 + 1) & 1) * G::BUF : 0);
       // next item (the last iteration reloads its own item into the idle buffer:
       // unconditional, so no register copies across the loop)
       if (!(STGCN_WG_EXP & 1)) load_item(it + 1 < it1 ? it + 1 : it);
-      Frag f[2];
       ld(cur, 0, f[0]);
+      if (stag && it > it0 && !(STGCN_WG_EXP & 2)) mm(f[FL]);  // the previous item's last k-step
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
-        if (!(STGCN_WG_EXP & 4) && s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) & 1]);
-        if (!(STGCN_WG_EXP & 2)) mm(f[s & 1]);
+        if (!(STGCN_WG_EXP & 4) && s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) % NF]);
+        if (!(STGCN_WG_EXP & 2) && (s + 1 < G::KSTEPS || !stag)) mm(f[s % NF]);
         if constexpr (G::NBUF == 2 && STGCN_WG_WSTART < G::KSTEPS && !(STGCN_WG_EXP & 1)) {
           // double buffer: the next item's split + LDS writes ride in the MFMA
           // shadow of k-steps WSTART.. (the loads were issued at the item start)
@@ -1710,6 +1807,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       if (STGCN_WG_EXP & 8) continue;  // (no barrier: timing experiment only)
       __syncthreads();
     }
+    if (stag && it0 < it1 && !(STGCN_WG_EXP & 2)) mm(f[FL]);  // the last item's last k-step
     // the tile [ROWS][CB channels][9 taps] through LDS (the staging buffers are
     // free after the last item's barrier), then whole 16-byte pieces of each
     // row's CB * 9 contiguous slab floats: 4-byte stores at a 36-byte stride

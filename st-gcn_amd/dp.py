@@ -37,7 +37,9 @@ import torch.distributed as dist
 
 
 class GradAllReduce:
-    def __init__(self, model, world_size=None, bucket_bytes=4 << 20, group=None):
+    TRACE_MAX = 1 << 16
+
+    def __init__(self, model, world_size=None, bucket_bytes=4 << 20, group=None, trace=False):
         self.group = group
         self.world = world_size or dist.get_world_size(group)
         params = [p for p in model.parameters() if p.requires_grad]
@@ -67,11 +69,13 @@ class GradAllReduce:
             self._flat.append(flat)
         self._install_views()
         self._sync = True
-        # observable overlap: (kind, index) in arrival order -- ("grad", i) when
-        # parameter i's gradient has been accumulated (i in model.parameters()
-        # order), ("launch", b) when bucket b's all-reduce is issued; reset by
-        # synchronize(), kept in ``last_trace``
+        # observable overlap (trace=True, a diagnostic: off in training): (kind,
+        # index) in arrival order -- ("grad", i) when parameter i's gradient has
+        # been accumulated (i in model.parameters() order), ("launch", b) when
+        # bucket b's all-reduce is issued; reset by synchronize(), kept in
+        # ``last_trace``, at most TRACE_MAX entries (no_sync steps accumulate)
         self._index = {p: i for i, p in enumerate(params)}
+        self._trace_on = trace
         self.trace, self.last_trace = [], []
         self._handles = [p.register_post_accumulate_grad_hook(self._hook) for p in params]
         self._handles += [p.register_hook(self._guard(p)) for p in params]
@@ -129,7 +133,8 @@ class GradAllReduce:
         if p.grad is not v:  # not accumulated into the bucket: move it there
             v.copy_(p.grad)
             p.grad = v
-        self.trace.append(("grad", self._index[p]))
+        if self._trace_on and len(self.trace) < self.TRACE_MAX:
+            self.trace.append(("grad", self._index[p]))
         if not self._sync:
             return
         self._seen.add(p)
@@ -139,7 +144,8 @@ class GradAllReduce:
             self._launch(bi)
 
     def _launch(self, bi):
-        self.trace.append(("launch", bi))
+        if self._trace_on and len(self.trace) < self.TRACE_MAX:
+            self.trace.append(("launch", bi))
         self._work[bi] = dist.all_reduce(self._flat[bi], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True)
 

@@ -268,13 +268,21 @@ class StgcnBlockFn(torch.autograd.Function):
         lib = hip_lib.lib()
         # (the caller's input tensor: a hook / retain_grad() on it turns deferred dx off)
         ctx.xref = weakref.ref(x) if cc is not None else None
-        x = x.contiguous()
+        # ABI 8: x never written (the previous block's ReLU(BN2(U)) formed on load:
+        # x is that block's placeholder, shape only); y not written (the next
+        # block does the same, or the fused head pools from U): a one-element
+        # placeholder of y's shape, so no dead activation is allocated or saved
+        xu = cc is not None and cc.x_from_u
+        y_lazy = cc is not None and cc.y_lazy
+        if not xu:
+            x = x.contiguous()
         names = ("x", "A", "W", "bW", "Wt", "bWt", "g1", "b1", "g2", "b2",
                  "rm1", "rv1", "rm2", "rv2")
         tensors = (x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2)
         seed = _dropout_seed(drop, training)
         for t, n in zip(tensors, names):
-            _f32c(t, n)
+            if not (xu and n == "x"):
+                _f32c(t, n)
         N, C_in, T, V = x.shape
         K = A.shape[0]
         C_out = Wt.shape[0]
@@ -282,18 +290,16 @@ class StgcnBlockFn(torch.autograd.Function):
                          **_gemm_flags(gemm))
         hip_lib.check(lib.stgcn_check_desc(ctypes.byref(desc)))
         dev = x.device
-        y = torch.empty((N, C_out, desc.T_out, V), device=dev, dtype=torch.float32)
+        y_shape = (N, C_out, desc.T_out, V)
+        y = (torch.empty(1, device=dev, dtype=torch.float32).expand(y_shape) if y_lazy
+             else torch.empty(y_shape, device=dev, dtype=torch.float32))
         Z = torch.empty((N, C_out, T, V), device=dev, dtype=torch.float32)
-        U = torch.empty_like(y)
+        U = torch.empty(y_shape, device=dev, dtype=torch.float32)
         stats = torch.empty(2 * C_in + 2 * C_out, device=dev, dtype=torch.float32)
         G = _keep_g(ctx, x, desc)
         nbytes = lib.stgcn_fwd_workspace_bytes(ctypes.byref(desc))
         ws = torch.empty(nbytes, device=dev, dtype=torch.uint8)
         prep = cc.prep if cc is not None else None
-        # ABI 8: x never written (the previous block's ReLU(BN2(U)) formed on load);
-        # y not written (the next block does the same)
-        xu = cc is not None and cc.x_from_u
-        y_lazy = cc is not None and cc.y_lazy
         args = _args(hip_lib.FwdArgs, [hip_lib.ptr(t) for t in (
             None if xu else x, A, W, bW, Wt, bWt, g1, b1, g2, b2, rm1, rv1, rm2, rv2,
             None if y_lazy else y, Z, U, stats,

@@ -192,7 +192,13 @@ class SpatialTemporalConv(nn.Module):
                               device=x.device, dtype=torch.float64),
                           prep=chain.next_prep(),
                           out_link=None if (self.residual or drop > 0) else Link())
-            cc.y_lazy = bool(lazy) and cc.out_link is not None
+            # (an unwritten y is read back only by the next block's backward, which
+            # rebuilds it from U while deferring dx into this block; it can defer
+            # only if y needs a gradient -- not when this block and its input are
+            # frozen, e.g. fine-tuning the later blocks: then y is written)
+            y_grad = (not torch.is_grad_enabled() or x.requires_grad
+                      or any(p.requires_grad for p in self.parameters()))
+            cc.y_lazy = bool(lazy) and cc.out_link is not None and y_grad
             if cc.y_lazy and lazy == "head":  # (ABI 9: the fused head pools it from U)
                 cc.y_head, cc.y_stats = True, None
             if chain.y is not None and x is chain.y and x._version == chain.y_version:

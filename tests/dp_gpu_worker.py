@@ -3,7 +3,8 @@
 Launched by torch.distributed.run with WORLD_SIZE ranks that all share the one
 GPU of the box (cuda:0) over the gloo backend (RCCL refuses two ranks on one
 device; the 8-GPU RCCL run is the driver's). Each rank runs the benched step
-on its own shard: STGCNStack (bf16x3 fp32 path, StackChain, fused head) +
+on its own shard: STGCNStack (the benched f16x2 fp32 path: stgcn_fold_prep,
+unwritten block outputs, the head pooling from U; StackChain, fused head) +
 dp.GradAllReduce (bucket-view gradients) + FusedAdam. Rank 0 then recomputes,
 in the same process and without any collective, the per-shard HIP gradients
 of every rank on a fresh copy of the initial model, and checks
@@ -30,7 +31,7 @@ from stgcn_loader import load  # noqa: E402
 def build(pkg, A):
     torch.manual_seed(0)
     with contextlib.redirect_stdout(io.StringIO()):
-        m = pkg.STGCNStack(3, 60, A, f32_gemm="bf16x3")
+        m = pkg.STGCNStack(3, 60, A, f32_gemm="f16x2")
     return m.cuda().train()
 
 
@@ -49,7 +50,7 @@ def main():
     model = build(pkg, A)
     p_init = [p.detach().clone() for p in model.parameters()]
     opt = pkg.FusedAdam(list(model.parameters()), lr=1e-3)
-    dp = pkg.dp.GradAllReduce(model, world, bucket_bytes=1 << 20)
+    dp = pkg.dp.GradAllReduce(model, world, bucket_bytes=1 << 20, trace=True)
     dp.zero_grad()
     loss, _ = model.forward_loss(xs[rank].cuda(), ys[rank].cuda())
     loss.backward()

@@ -60,7 +60,7 @@ def _worker(rank, world, port, out_q, T, bucket_bytes):
         xs = torch.randn(world, N, T, 18, 3, generator=gen)
         ys = torch.randint(0, 5, (world, N), generator=gen)
         model = OracleStackModule(params, buffers)
-        dp = pkg.dp.GradAllReduce(model, world, bucket_bytes=bucket_bytes)
+        dp = pkg.dp.GradAllReduce(model, world, bucket_bytes=bucket_bytes, trace=True)
         loss = nn.functional.cross_entropy(model(xs[rank]), ys[rank])
         loss.backward()
         dp.synchronize()

@@ -761,3 +761,48 @@ def test_stack_head_pools_from_u(pkg, f32_gemm):
                 assert torch.equal(seen["y"], seen["y_ref"])
     finally:
         lib.stgcn_head_fwd_u = orig
+
+
+@pytest.mark.gpu
+def test_stack_frozen_first_blocks(pkg):
+    """with blocks 0-1 frozen (fine-tuning the later ones) and an
+    input that needs no gradient, block 1's output needs no gradient either, so
+    block 2's backward cannot defer its dx into block 1: the chain must write
+    that output instead of leaving it to be formed from U (ABI 8), and the
+    backward must run. Same loss, logits and trainable gradients as the stack
+    that writes every output; the frozen blocks get no gradient."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(0, 1, graph=gr.graph_for(18))
+    torch.manual_seed(8)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 60, A, f32_gemm="f16x2").cuda().train()
+        m2 = pkg.STGCNStack(3, 60, A, f32_gemm="f16x2").cuda().train()
+    m2.load_state_dict(m1.state_dict())
+    m2.lazy_links = False
+    for m in (m1, m2):
+        m.conv[0].requires_grad_(False)
+        m.conv[1].requires_grad_(False)
+    x = torch.randn(3, 3, 64, 18, generator=torch.Generator().manual_seed(9)).cuda()
+    lab = torch.randint(0, 60, (3,), generator=torch.Generator().manual_seed(10)).cuda()
+    for step in range(2):
+        loss1, out1 = m1.forward_loss(x, lab)
+        loss2, out2 = m2.forward_loss(x, lab)
+        m1.zero_grad()
+        m2.zero_grad()
+        loss1.backward()
+        loss2.backward()
+        torch.cuda.synchronize()
+        assert torch.equal(out1, out2) and torch.equal(loss1, loss2), step
+        g2 = {k: b.grad for k, b in m2.named_parameters()}
+        for k, a in m1.named_parameters():
+            if not a.requires_grad:
+                assert a.grad is None and g2[k] is None, k
+                continue
+            b = g2[k]
+            if k.endswith("temporalConv.bias") or k.endswith("batch_n_2.weight"):
+                scale = g2[k.rsplit(".", 1)[0] + ".bias"].abs().max().item() if \
+                    k.endswith("weight") else 1.0
+                assert (a.grad - b).abs().max().item() <= 1e-5 * scale, (step, k)
+                continue
+            tol = 2e-3 if k.endswith("spatialConv.A") else 1e-5
+            assert rel_to_max(a.grad.cpu().numpy(), b.cpu().numpy()) < tol, (step, k)
