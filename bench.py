@@ -475,6 +475,8 @@ def main():
     ap.add_argument("--no-sweep", dest="sweep", action="store_false",
                     help="skip the per-GPU batch sweep (SURVEY.md §8(d): N in 32, 64, 256 "
                          "besides the bench batch; N=1 process only)")
+    ap.add_argument("--no-lazy-links", action="store_true",
+                    help="A/B only: write every block output (no ABI 8/9 unwritten outputs)")
     ap.add_argument("--torch-ops", action="store_true",
                     help="head + cross entropy + Adam from torch instead of the HIP library")
     args = ap.parse_args()
@@ -498,6 +500,8 @@ def main():
     cfg = dict(CONFIGS[args.config], N=args.batch, f32_gemm=args.f32_gemm)
 
     model = build_model(pkg, cfg, device)
+    if args.no_lazy_links:
+        model.lazy_links = False
     params = [p for p in model.parameters()]
     # FusedAdam: torch.optim.Adam semantics, one libstgcn_hip launch per step
     opt = (torch.optim.Adam(params, lr=1e-3) if args.torch_ops

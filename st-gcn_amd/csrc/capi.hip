@@ -189,9 +189,16 @@ bool fold_bna(const stgcn_desc_t *d) {
 // G (k_gather4) can read its input as ReLU(BN2_prev(U_prev)) of the previous
 // block -- that block then writes only y's statistics, not y -- and its fused
 // backward (spb_epilogue, deferred dx) already reads U_prev in place of x
+// The bf16 blocks (cfg3 / cfg5) too (verdict r5 item 4): their fused spatial
+// forward (k_sp_fwd_bf16 / k_sp_fwd_wide) forms ReLU(BN2_prev(U_prev)) on
+// staging, and their spatial backward (k_sp_bwd_fused, k_sp50_*, or the H GEMM
+// + joint kernel) reads U_prev in prev mode wherever dx defers; the weight
+// gradient of W' reads the kept bf16 G -- so x is read by nothing.
 bool x_from_u(const stgcn_desc_t *d) {
-  return d->training && fold_spb(d) && !fold_bna(d) && d->K == 1 &&
-         gather_prev_supported(d->C_in, d->T, d->V);
+  if (!d->training || residual(d)) return false;
+  if (fused_sp(d))
+    return fused_spb(d) || spatial_dx_prev_supported(d->N, d->C_in, d->T, d->V, d->K);
+  return fold_spb(d) && !fold_bna(d) && d->K == 1 && gather_prev_supported(d->C_in, d->T, d->V);
 }
 
 // sum_{n,t} dZ of the non-residual block from per-tap sums of dU (clip-chunk
@@ -915,10 +922,19 @@ int stgcn_block_fwd(const stgcn_desc_t *d, const stgcn_fwd_args_t *a, void *work
   if (fused_sp(d)) {
     // bf16 path: BN1 + joint contraction + W' GEMM in one kernel; G kept in bf16
     // for the backward when the caller asks (stgcn_keep_g_bytes)
-    HIP_TRY(launch_sp_fwd_bf16(a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W, L.biasZ, L.wpk,
-                               a->Z, z_bf16(d) ? 1 : 0, reinterpret_cast<__bf16 *>(a->G),
+    PrevBn pv;  // (x = ReLU(BN2_prev(prev_U)) formed on staging)
+    if (xu) {
+      pv.mean = a->prev_stats;
+      pv.invstd = a->prev_stats + C;
+      pv.g = a->prev_g2;
+      pv.b = a->prev_b2;
+    }
+    HIP_TRY(launch_sp_fwd_bf16(xu ? a->prev_U : a->x, mean1, invstd1, a->g1, a->b1, a->A, a->W,
+                               L.biasZ, L.wpk, a->Z, z_bf16(d) ? 1 : 0,
+                               reinterpret_cast<__bf16 *>(a->G),
                                (res && d->training) ? L.s2 : nullptr,
-                               (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s));
+                               (res && d->training) ? L.q2 : nullptr, N, C, R, T, V, K, res, s,
+                               xu ? &pv : nullptr));
   } else if (!bna) {
   float *G = a->G ? a->G : L.G;  // kept for the backward when the caller asks
   PrevBn pv;  // (x = ReLU(BN2_prev(prev_U)) formed on load)
@@ -1079,11 +1095,12 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   int rc = stgcn_check_desc(d);
   if (rc) return rc;
   const bool res = residual(d);
-  // ABI 8: x null after a forward from prev_U -- the fused folded backward reads
-  // prev_U (deferred dx) and the kept G, nothing else reads x
+  // ABI 8: x null after a forward from prev_U -- the fused folded backward (or the
+  // bf16 spatial backward in prev mode) reads prev_U (deferred dx) and the kept
+  // G, nothing else reads x
   const bool xnull = a && !a->x;
-  if (xnull && (res || !fold_spb(d) || fold_bna(d) || !a->G))
-    return fail(STGCN_E_INVALID, "x null: needs a folded block (STGCN_PLAN_X_FROM_U) and its kept G");
+  if (xnull && (!x_from_u(d) || !a->G))
+    return fail(STGCN_E_INVALID, "x null: needs STGCN_PLAN_X_FROM_U and the kept G");
   if (!a || !a->dy || (!a->x && !xnull) || !a->Z || (!res && !a->U) || !a->stats || !a->A || !a->W ||
       !a->bW || !a->Wt || !a->g1 || !a->b1 || !a->g2 || !a->b2 || !a->dA || !a->dW || !a->dbW ||
       !a->dWt || !a->dbWt || !a->dg1 || !a->db1 || !a->dg2 || !a->db2 || (d->need_dx && !a->dx))

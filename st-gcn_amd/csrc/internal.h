@@ -382,7 +382,7 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
                               const float *biasZ, void *wpk, float *Z, int z_bf16, __bf16 *Gk,
                               double *ssum,
                               double *ssq, int N, int C, int R, int T, int V, int K, int relu,
-                              hipStream_t s);
+                              hipStream_t s, const PrevBn *prev = nullptr);
 // dW' = dZ Gk^T from the kept bf16 G (P = dZ fp32, Q = Gk, C = K*C_in).
 void plan_wgrad_gk(WgradParams &w, int T);
 hipError_t launch_wgrad_gk(const WgradParams &p, hipStream_t s);

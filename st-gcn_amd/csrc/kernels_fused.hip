@@ -74,7 +74,7 @@ struct SpFwdGeo {
   static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = A_IMG;
   static constexpr int OFF_G = OFF_X + X_BYTES, OFF_W = OFF_G + G_BYTES;
   static constexpr int OFF_BN = OFF_W + 2 * W_BYTES;
-  static constexpr int LDS = OFF_BN + 2 * 3 * 16 * 4;
+  static constexpr int LDS = OFF_BN + 2 * 6 * 16 * 4;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(LDS >= 2048 + 64 * V * 4, "epilogue scratch fits");
   static_assert(IPT <= 16, "staging registers");
@@ -82,6 +82,10 @@ struct SpFwdGeo {
 
 struct SpFwdParams {
   const float *x, *mean, *invstd, *g, *b, *A;
+  // ABI 8 (STGCN_PLAN_X_FROM_U; pmean non-null): x holds the previous block's U
+  // and the input is ReLU(BN2_prev(U)), formed on staging as k_bn_relu_fwd forms
+  // its y (the previous block then writes only y's statistics)
+  const float *pmean, *pinvstd, *pg, *pb;
   const __bf16 *aimg;  // the LDS image of the A planes (k_pack_sp_a), DMA'd per workgroup
   const __bf16 *wpk;  // [rt][chunk][k][octet][64][8]
   __bf16 *Gk;         // optional kept G (bf16 tile layout), or null
@@ -155,31 +159,45 @@ __global__ __launch_bounds__(256, 2) void k_sp_fwd_bf16(SpFwdParams P) {
                    : "v"(goff[k]), "s"(rs)
                    : "memory");
   };
-  float *bnt = reinterpret_cast<float *>(lds + G::OFF_BN);  // [2][3][16]: mean, a, beta
+  float *bnt = reinterpret_cast<float *>(lds + G::OFF_BN);  // [2][6][16]: mean, a, beta; prev
   auto bn_table = [&](int chunk, int slot) {
     if (tid < 16) {
       const int c = chunk * G::CK + tid;
-      float mu = 0.f, a = 0.f, be = 0.f;
+      float mu = 0.f, a = 0.f, be = 0.f, pmu = 0.f, pa = 0.f, pbe = 0.f;
       if (c < P.C) {
         mu = P.mean[c];
         a = P.invstd[c] * P.g[c];
         be = P.b[c];
+        if (P.pmean) {
+          pmu = P.pmean[c];
+          pa = P.pinvstd[c] * P.pg[c];
+          pbe = P.pb[c];
+        }
       }
-      bnt[slot * 48 + tid] = mu;
-      bnt[slot * 48 + 16 + tid] = a;
-      bnt[slot * 48 + 32 + tid] = be;
+      float *tb = bnt + slot * 96;
+      tb[tid] = mu;
+      tb[16 + tid] = a;
+      tb[32 + tid] = be;
+      tb[48 + tid] = pmu;
+      tb[64 + tid] = pa;
+      tb[80 + tid] = pbe;
     }
   };
   auto write_x = [&](int chunk, int slot) {
     __bf16 *xi = reinterpret_cast<__bf16 *>(lds + G::OFF_X);
-    const float *tb = bnt + slot * 48;
+    const float *tb = bnt + slot * 96;
 #pragma unroll
     for (int k = 0; k < G::IPT; ++k)
       if (loff[k] >= 0) {
         const int ch = ich[k];
         float v = 0.f;
         if (chunk * G::CK + ch < P.C && goff[k] != kOOB) {
-          v = (st[k] - tb[ch]) * tb[16 + ch] + tb[32 + ch];
+          float xx = st[k];
+          if (P.pmean) {
+            const float u = (xx - tb[48 + ch]) * tb[64 + ch] + tb[80 + ch];
+            xx = u > 0.f ? u : 0.f;
+          }
+          v = (xx - tb[ch]) * tb[16 + ch] + tb[32 + ch];
           if (P.relu) v = fmaxf(v, 0.f);
         }
         xi[loff[k]] = (__bf16)v;
@@ -373,7 +391,7 @@ struct SpWideGeo {
   static constexpr int OFF_AH = 0, OFF_AM = A_BYTES, OFF_X = A_IMG;
   static constexpr int OFF_G = OFF_X + X_BYTES, OFF_W = OFF_G + G_BYTES;
   static constexpr int OFF_BN = OFF_W + 2 * W_BYTES;
-  static constexpr int MAIN = OFF_BN + 2 * 3 * 16 * 4;
+  static constexpr int MAIN = OFF_BN + 2 * 6 * 16 * 4;
   static constexpr int EROWS = ROWS < 128 ? ROWS : 128;  // LDS-image epilogue rows
   static constexpr int EPI = ROWS == 256 ? 0 : (EROWS * kEpiPitch + EROWS * V) * 4;
   static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
@@ -439,24 +457,33 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
                  : "+v"(st[0]), "+v"(st[1]), "+v"(st[2]), "+v"(st[3]), "+v"(st[4]), "+v"(st[5]),
                    "+v"(st[6]), "+v"(st[7])::"memory");
   };
-  float *bnt = reinterpret_cast<float *>(lds + G::OFF_BN);  // [2][3][16]: mean, a, beta
+  float *bnt = reinterpret_cast<float *>(lds + G::OFF_BN);  // [2][6][16]: mean, a, beta; prev
   auto bn_table = [&](int chunk, int slot) {
     if (tid < 16) {
       const int c = chunk * G::CK + tid;
-      float mu = 0.f, a = 0.f, be = 0.f;
+      float mu = 0.f, a = 0.f, be = 0.f, pmu = 0.f, pa = 0.f, pbe = 0.f;
       if (c < P.C) {
         mu = P.mean[c];
         a = P.invstd[c] * P.g[c];
         be = P.b[c];
+        if (P.pmean) {
+          pmu = P.pmean[c];
+          pa = P.pinvstd[c] * P.pg[c];
+          pbe = P.pb[c];
+        }
       }
-      bnt[slot * 48 + tid] = mu;
-      bnt[slot * 48 + 16 + tid] = a;
-      bnt[slot * 48 + 32 + tid] = be;
+      float *tb = bnt + slot * 96;
+      tb[tid] = mu;
+      tb[16 + tid] = a;
+      tb[32 + tid] = be;
+      tb[48 + tid] = pmu;
+      tb[64 + tid] = pa;
+      tb[80 + tid] = pbe;
     }
   };
   auto write_x = [&](int chunk, int slot) {
     __bf16 *xi = reinterpret_cast<__bf16 *>(lds + G::OFF_X);
-    const float *tb = bnt + slot * 48;
+    const float *tb = bnt + slot * 96;
 #pragma unroll
     for (int k = 0; k < G::IPT; ++k) {
       const int e = k * G::NT + tid;
@@ -465,7 +492,12 @@ __global__ __launch_bounds__(512, 1) void k_sp_fwd_wide(SpFwdParams P) {
       if (e < G::NIT) {
         float v = 0.f;
         if (chunk * G::CK + ch < P.C && pos < pos_lim) {
-          v = (st[k] - tb[ch]) * tb[16 + ch] + tb[32 + ch];
+          float xx = st[k];
+          if (P.pmean) {
+            const float u = (xx - tb[48 + ch]) * tb[64 + ch] + tb[80 + ch];
+            xx = u > 0.f ? u : 0.f;
+          }
+          v = (xx - tb[ch]) * tb[16 + ch] + tb[32 + ch];
           if (P.relu) v = fmaxf(v, 0.f);
         }
         xi[(t * 16 + ch) * G::XP + w] = (__bf16)v;
@@ -753,7 +785,7 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
                               const float *biasZ, void *wpk, float *Z, int z_bf16, __bf16 *Gk,
                               double *ssum,
                               double *ssq, int N, int C, int R, int T, int V, int K, int relu,
-                              hipStream_t s) {
+                              hipStream_t s, const PrevBn *prev) {
   if (!sp_fwd_bf16_supported(C, V, K, R, relu != 0)) return hipErrorInvalidValue;
   // all output channels per workgroup: the two-person graph, and V = 25 with
   // K = 3 (STGCN_AB_SPF_NARROW25 build: the 64-row k_sp_fwd_bf16 there, A/B only)
@@ -785,6 +817,12 @@ hipError_t launch_sp_fwd_bf16(const float *x, const float *mean, const float *in
   P.g = g;
   P.b = b;
   P.A = A;
+  if (prev && prev->mean) {
+    P.pmean = prev->mean;
+    P.pinvstd = prev->invstd;
+    P.pg = prev->g;
+    P.pb = prev->b;
+  }
   P.wpk = reinterpret_cast<const __bf16 *>(wpk);
   P.Gk = Gk;
   P.C = C;

@@ -1139,26 +1139,28 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         p, smem, smem + G::ROWS * kEpiPitch, n, r0, m0);
     return;
   }
-  if constexpr (MR == 2) return;  // (never: 128-row tiles are launched for s_out == 1 only)
-  // hand-over: waves 4-7 give their two column tiles to waves 0-3 (same rows,
-  // next two tiles), which run the shared 4-wave epilogue
-  float *ho = smem + 1024 + (wave & 3) * 2 * 64 * 16;
-  __syncthreads();  // every wave is done with the buffers
-  if (half == 1) {
+  // (MR >= 2: never -- 128-row tiles are launched for s_out == 1 only)
+  if constexpr (MR == 1) {
+    // hand-over: waves 4-7 give their two column tiles to waves 0-3 (same rows,
+    // next two tiles), which run the shared 4-wave epilogue
+    float *ho = smem + 1024 + (wave & 3) * 2 * 64 * 16;
+    __syncthreads();  // every wave is done with the buffers
+    if (half == 1) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) ho[(j * 16 + i) * 64 + lane] = acc[j][i];
-  }
-  __syncthreads();
-  if (half == 0) {
+        for (int i = 0; i < 16; ++i) ho[(j * 16 + i) * 64 + lane] = acc[j][i];
+    }
+    __syncthreads();
+    if (half == 0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[2 + j][i] = ho[(j * 16 + i) * 64 + lane];
-    conv_tile_epilogue<V, G::NCOLS, false, NPL == 1, NPL != 1>(p, acc, n, r0, m0, smem);
-  } else if (p.stat_sum) {
-    __syncthreads();  // the epilogue's one barrier (statistics)
+        for (int i = 0; i < 16; ++i) acc[2 + j][i] = ho[(j * 16 + i) * 64 + lane];
+      conv_tile_epilogue<V, G::NCOLS, false, NPL == 1, NPL != 1>(p, acc, n, r0, m0, smem);
+    } else if (p.stat_sum) {
+      __syncthreads();  // the epilogue's one barrier (statistics)
+    }
   }
 }
 
@@ -1282,12 +1284,14 @@ static bool x3_wide_rows(const ConvGemmParams &p) {
   return !off && p.NQ == 9 && p.s_out == 1 && p.R % 128 == 0;
 }
 // 4-wave 64-row tiles, two workgroups per CU (ConvX3Geo NW = 4): the fp16-split
-// stride-1 forward where the caller marked it (p.w4: capi.hip fwd_w4). Decides
+// stride-1 forward where the caller marked it (p.w4: capi.hip fwd_w4), up to 128
+// output rows (at 256 the second read of each window per 128 rows costs what
+// the overlap gains: L8 0.668 vs 0.654 ms, profiles/r6b_kbench.txt). Decides
 // the packed weight layout (64-row tiles) and the kernel alike.
 static bool x3_w4(const ConvGemmParams &p, int npl) {
   constexpr bool off = STGCN_AB_X3_NOW4 != 0;
   return !off && p.w4 && npl == 2 && !p.spb && !p.bna && p.NQ == 9 && p.s_in == 1 &&
-         p.s_out == 1 && (p.V == 18 || p.V == 25);
+         p.s_out == 1 && (p.V == 18 || p.V == 25) && p.R <= 128;
 }
 template <int V>
 static void launch_cx_w4(const ConvGemmParams &p, int nblk, hipStream_t s) {
@@ -1347,7 +1351,8 @@ static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
 // (STGCN_F_BF16), the same pipeline with one plane and two workgroups per CU
 // The pack job of a launch_conv_planes call (same layout, same scales)
 static PackJob pack_job(const ConvGemmParams &p, int npl) {
-  const bool wide = npl >= 2 && x3_wide_rows(p) && !x3_w4(p, npl);
+  const bool w4 = x3_w4(p, npl);
+  const bool wide = npl >= 2 && x3_wide_rows(p) && !w4;
   const int rows = wide ? 128 : 64;
   PackJob j{};
   j.w = p.w;
@@ -1406,8 +1411,10 @@ static hipError_t launch_conv_planes(const ConvGemmParams &p0, int npl, hipStrea
   const int nblk = p.N * p.n_mtiles * p.n_rtiles;
   bool done = false;
   if (w4) {
-    if (p.V == 18) launch_cx_w4<18>(p, nblk, s);
-    else launch_cx_w4<25>(p, nblk, s);
+    if (p.V == 18)
+      launch_cx_w4<18>(p, nblk, s);
+    else
+      launch_cx_w4<25>(p, nblk, s);
     done = true;
   } else if (wide && npl == 2) {
     done = launch_cx_v<9, 2, 2>(p, nblk, s);

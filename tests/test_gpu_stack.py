@@ -806,3 +806,49 @@ def test_stack_frozen_first_blocks(pkg):
                 continue
             tol = 2e-3 if k.endswith("spatialConv.A") else 1e-5
             assert rel_to_max(a.grad.cpu().numpy(), b.cpu().numpy()) < tol, (step, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V", [25, 50])
+def test_stack_lazy_links_bf16(pkg, V):
+    """ABI 8 on the bf16 blocks (cfg3 / cfg5, verdict r5 item 4): every block
+    output that only the next block reads stays unwritten -- the next block's
+    fused spatial forward (k_sp_fwd_bf16 / k_sp_fwd_wide) forms
+    ReLU(BN2_prev(U_prev)) on staging, and its spatial backward reads U_prev in
+    prev mode -- and the last output is pooled from U by the fused head. Loss,
+    logits and running stats are bit-identical to the stack that writes every
+    output; gradients agree to the order of the atomic adds."""
+    gr = pkg.graph
+    A = gr.get_normalized_adjacency_matrices(2, 1, distances=gr.synthetic_distances(V),
+                                             graph=gr.graph_for(V))
+    torch.manual_seed(11)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m1 = pkg.STGCNStack(3, 60, A, gemm_dtype=torch.bfloat16).cuda().train()
+        m2 = pkg.STGCNStack(3, 60, A, gemm_dtype=torch.bfloat16).cuda().train()
+    m2.load_state_dict(m1.state_dict())
+    m2.lazy_links = False
+    x = torch.randn(4, 3, 40, V, generator=torch.Generator().manual_seed(12)).cuda()
+    lab = torch.randint(0, 60, (4,), generator=torch.Generator().manual_seed(13)).cuda()
+    flags = pkg.fused.lazy_links(list(m1.conv), tuple(x.shape))
+    assert flags == [True] * 9 + [False], flags
+    for step in range(2):
+        loss1, out1 = m1.forward_loss(x, lab)
+        loss2, out2 = m2.forward_loss(x, lab)
+        m1.zero_grad()
+        m2.zero_grad()
+        loss1.backward()
+        loss2.backward()
+        torch.cuda.synchronize()
+        assert torch.equal(out1, out2) and torch.equal(loss1, loss2), step
+        g2 = {k: b.grad for k, b in m2.named_parameters()}
+        for k, a in m1.named_parameters():
+            b = g2[k]
+            if k.endswith("temporalConv.bias") or k.endswith("batch_n_2.weight"):
+                scale = g2[k.rsplit(".", 1)[0] + ".bias"].abs().max().item() if \
+                    k.endswith("weight") else 1.0
+                assert (a.grad - b).abs().max().item() <= 1e-5 * scale, (step, k)
+                continue
+            tol = 2e-3 if k.endswith("spatialConv.A") else 1e-5
+            assert rel_to_max(a.grad.cpu().numpy(), b.cpu().numpy()) < tol, (step, k)
+        for (k, a), b in zip(m1.named_buffers(), m2.buffers()):
+            assert torch.equal(a, b), (step, k)
