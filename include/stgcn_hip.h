@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 9
+#define STGCN_ABI_VERSION 10
 
 /* ABI 7: words of max |y| after the 5 * C sums of a y_stats block */
 #define STGCN_STATS_AMAX_WORDS 2048
@@ -247,6 +247,13 @@ typedef struct stgcn_bwd_args {
   const float *dy_coef;
   /* ABI 7, optional: the same stgcn_fold_prep buffer as the forward's */
   const void *prep;
+  /* ABI 10, optional: the gradient of y is constant over (T_out, V) --
+   * dy[n, c, t, v] = dy_nc[n * C_out + c] (N * C_out floats), as the average-pool
+   * head gives it (stgcn_head_bwd_nc) -- and dy may be null: the ReLU + BN2
+   * backward reads one value per (clip, channel) instead of the dy tensor.
+   * Non-residual blocks; STGCN_E_UNSUPPORTED where the block's backward needs
+   * the full dy (the caller then passes it). */
+  const float *dy_nc;
   /* ABI 8: x may be null when the forward took its input from prev_U
    * (STGCN_PLAN_X_FROM_U); the call then needs the kept G and the deferred-dx
    * arguments (prev_U, prev_stats, prev_g2, prev_b2, prev_sums, x_stats, dx_coef,
@@ -366,6 +373,13 @@ int stgcn_head_fwd(const stgcn_head_desc_t *d, const float *y, const float *W, c
 int stgcn_head_bwd(const stgcn_head_desc_t *d, const float *pooled, const float *logits,
                    const float *W, const int64_t *labels, const float *dloss, float *dlogits,
                    float *dpooled, float *dy, float *dW, float *dbias, void *stream);
+/* ABI 10: stgcn_head_bwd with the gradient of y as its per-(n, c) value only:
+ * dy_nc (N, C) = dpooled / L, the value stgcn_head_bwd writes to every one of
+ * the L positions of row (n, c) -- for stgcn_bwd_args_t.dy_nc (no (N, C, L)
+ * tensor written or read). */
+int stgcn_head_bwd_nc(const stgcn_head_desc_t *d, const float *pooled, const float *logits,
+                      const float *W, const int64_t *labels, const float *dloss, float *dlogits,
+                      float *dpooled, float *dy_nc, float *dW, float *dbias, void *stream);
 /* ABI 9: stgcn_head_fwd with the last block's output never written: the pool
  * reads that block's pre-BN2 tensor U (N, C, L) and forms y = ReLU(BN2(U)) on
  * load with the block's stats2 = [mean2 (C) | invstd2 (C)] (its stats buffer

@@ -32,11 +32,18 @@ def main(path, steps=10):
     agg, cnt = defaultdict(float), defaultdict(int)
     for r in seg:
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
-        k = name.split("(")[0][:60]
+        k = name.split("(")[0][:90]
         agg[k] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 / steps
         cnt[k] += 1
     for k, v in sorted(agg.items(), key=lambda x: -x[1])[:40]:
         print(f"{v:8.3f} ms/step  {cnt[k] / steps:5.1f}x  {k}")
+    # the last step's launches in order, with their durations
+    last = rows[adam[-2] + 1: adam[-1] + 1]
+    print("\nlast step, in launch order (us):")
+    for r in last:
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:90]
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        print(f"{d:9.1f}  {name}")
 
 
 if __name__ == "__main__":

@@ -330,8 +330,32 @@ struct BwdLayout {
   double *fcs, *ftq, *f64scr, *SdH;
   float *dWc, *fscr;  // the fold GEMMs' operand re-layouts (kernels_fold.hip)
   float *Wc, *bZ;
+  // deterministic dA: the spatial backward's per-workgroup partials (dA_cap
+  // slots of K V V floats) and the reduction's fp64 scratch
+  float *dApart;
+  double *dAlvl;
+  int64_t dA_cap;
   size_t dbl_bytes, total;
 };
+
+// Partial slots the block's dA-producing launches need (0: fp32 atomics stay):
+// the folded data gradient's workgroups (spb_epilogue; both stride-2 phases,
+// counted at 64-row tiles: an upper bound), or the unfused spatial backward's
+// joint kernel -- persistent k_spatial_bwd5 (<= 2048 workgroups) / _bwd6 (two
+// slots per workgroup, <= 512), or the flat-row k_spatial_bwd3 (>= 64 rows per
+// workgroup). (The fused bf16 spatial backward kernels keep their atomics.)
+static int64_t dA_part_cap(const stgcn_desc_t *d) {
+  const int64_t N = d->N, C = d->C_in, T = d->T;
+  if (fold_spb(d)) {
+    const int FT = conv_ft(d->V);
+    const int64_t mt = d->stride == 1 ? (T + FT - 1) / FT
+                                      : ((T + 1) / 2 + FT - 1) / FT + (T / 2 + FT - 1) / FT;
+    return N * mt * ((C + 63) / 64);
+  }
+  if (fused_spb(d)) return 0;
+  const int64_t bwd3 = C < 16 ? (N * C * T + 63) / 64 : 0;
+  return std::max<int64_t>(d->V == 50 ? 512 : 2048, bwd3);
+}
 
 BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   Carve c(ws);
@@ -391,6 +415,12 @@ BwdLayout bwd_layout(const stgcn_desc_t *d, void *ws) {
   L.slab = c.take<float>(slab);
   L.wpk = c.take<float>(wpk_floats(d));
   L.Wpk = c.take<float>((size_t)R * K * C);
+  L.dA_cap = dA_part_cap(d);
+  if (L.dA_cap) {
+    const size_t kvv = (size_t)K * d->V * d->V;
+    L.dApart = c.take<float>((size_t)L.dA_cap * kvv);
+    L.dAlvl = c.take<double>((size_t)kDaLvl * kvv);
+  }
   L.total = c.off;
   return L;
 }
@@ -1101,7 +1131,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
   const bool xnull = a && !a->x;
   if (xnull && (!x_from_u(d) || !a->G))
     return fail(STGCN_E_INVALID, "x null: needs STGCN_PLAN_X_FROM_U and the kept G");
-  if (!a || !a->dy || (!a->x && !xnull) || !a->Z || (!res && !a->U) || !a->stats || !a->A || !a->W ||
+  if (!a || (!a->dy && !a->dy_nc) || (!a->x && !xnull) || !a->Z || (!res && !a->U) || !a->stats || !a->A || !a->W ||
       !a->bW || !a->Wt || !a->g1 || !a->b1 || !a->g2 || !a->b2 || !a->dA || !a->dW || !a->dbW ||
       !a->dWt || !a->dbWt || !a->dg1 || !a->db1 || !a->dg2 || !a->db2 || (d->need_dx && !a->dx))
     return fail(STGCN_E_INVALID, "null tensor argument");
@@ -1109,6 +1139,11 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     return fail(STGCN_E_INVALID, "residual block: null Za / y / projection tensors");
   if (res && a->dy_sums)
     return fail(STGCN_E_INVALID, "dy_sums applies to the non-residual block only");
+  // ABI 10: dy as one value per (clip, channel): the three ReLU + BN2 backward
+  // passes of the non-residual block (not the residual block's ReLU backward, nor
+  // the frame-wise dU A pass of the block without G)
+  if (a->dy_nc && (res || (cols_sums(d) && fold_bna(d))))
+    return fail(STGCN_E_UNSUPPORTED, "dy_nc: this block's backward needs the full dy");
   const Dropout drop = make_dropout(d, a->dropout_p, a->seed);
   if (drop.thresh && a->dy_sums)
     return fail(STGCN_E_INVALID, "dy_sums cannot be combined with dropout");
@@ -1150,7 +1185,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       sgu = a->dy_sums + R;
     } else {
       HIP_TRY(launch_bn_relu_bwd_reduce(a->dy, a->U, mean2, invstd2, a->g2, a->b2, N, R, To * V,
-                                        L.sg, L.sgu, drop, s));
+                                        L.sg, L.sgu, drop, s, a->dy_nc));
     }
     // (with the clip-chunk sums of dU: sum_{n,t} dZ follows from them per tap,
     // no pass over dZ)
@@ -1165,13 +1200,14 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
       HIP_TRY(launch_bn_relu_bwd_apply_cols(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu,
                                             L.dU, L.sdu, N, R, To * V, d->training, drop, s,
                                             du_bf16(d) ? 1 : 0, a->dy_coef, L.fcs,
-                                            f16x2_tw(d) ? L.amax : nullptr));  // (f16x2: max |dU|)
+                                            f16x2_tw(d) ? L.amax : nullptr,  // (f16x2: max |dU|)
+                                            a->dy_nc));
       HIP_TRY(launch_fold_tq(L.fcs, apply_cols_chunks(N), R, T, To, V, d->stride, L.ftq, tqT,
                              s));
     } else {
       HIP_TRY(launch_bn_relu_bwd_apply(a->dy, a->U, mean2, invstd2, a->g2, a->b2, sg, sgu, L.dU,
                                        L.sdu, N, R, To * V, d->training, drop, s,
-                                       du_bf16(d) ? 1 : 0, a->dy_coef));
+                                       du_bf16(d) ? 1 : 0, a->dy_coef, a->dy_nc));
     }
     HIP_TRY(launch_bn_grads_out(sg, sgu, L.sdu, R, a->dg2, a->db2, a->dbWt, s));
   } else {
@@ -1258,6 +1294,18 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
         p.sdn = L.sdn;
         p.dA = a->dA;
       }
+      // (deterministic dA: every workgroup's partial in its own slot, summed below)
+      int64_t dparts = 0;
+      const int dnpl = f16x2_dgrad(d) ? 2 : 3;
+      auto dA_slots = [&](ConvGemmParams &q) {
+        q.dA_part = nullptr;  // (no slots: fp32 atomics into dA)
+        if (!fold_spb(d) || !L.dApart) return;
+        const int rows = conv_x3_tile_rows(q, dnpl);
+        const int64_t nb = (int64_t)N * q.n_mtiles * ((q.R + rows - 1) / rows);
+        if (dparts + nb > L.dA_cap) return;
+        q.dA_part = L.dApart + dparts * V * V;
+        dparts += nb;
+      };
       p.in_bstride = (int64_t)R * To * V;
       p.out_bstride = (int64_t)C * T * V;
       p.w_sr = 9;
@@ -1280,6 +1328,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
           p.wpk_ready = 1;
         }
         conv_tiles(p);
+        dA_slots(p);
         HIP_TRY(launch_conv_gemm(p, s));
       } else {
         for (int ph = 0; ph < 2; ++ph) {
@@ -1296,9 +1345,11 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
           }
           if (p.M <= 0) continue;
           conv_tiles(p);
+          dA_slots(p);
           HIP_TRY(launch_conv_gemm(p, s));
         }
       }
+      HIP_TRY(launch_dA_reduce(L.dApart, dparts, V * V, L.dAlvl, a->dA, s));
     }
     if (fold_bna(d)) {  // dWc = sum (dU A) BN1(x): Q = x with BN1 at staging, P = dU A
       const unsigned *xmax = reinterpret_cast<const unsigned *>(a->G);  // (the forward's max |x|)
@@ -1469,6 +1520,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     Wz = L.Wpk;
   }
   const int NSL = spatial_bwd_slice(d);
+  int64_t sparts = 0;  // (deterministic dA: the joint kernel's workgroup partials, if it takes them)
   for (int n0 = 0; n0 < N; n0 += NSL) {
   const int ns = std::min(NSL, N - n0);
   const int64_t xo = (int64_t)n0 * C * T * V;
@@ -1501,10 +1553,15 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     conv_tiles(p);
     HIP_TRY(launch_conv_gemm(p, s));
   }
+  int64_t np = 0;
   HIP_TRY(launch_spatial_dx(L.H, xin + xo, mean1, invstd1, a->g1, a->b1, a->A,
                             a->dx ? a->dx + xo : nullptr, a->dA, L.sd, L.sdn, ns, C, T, V, K,
-                            d->need_dx, res, bf16(d) ? 1 : 0, s, defer ? &pvb : nullptr));
+                            d->need_dx, res, bf16(d) ? 1 : 0, s, defer ? &pvb : nullptr,
+                            L.dApart ? L.dApart + sparts * K * V * V : nullptr,
+                            L.dA_cap - sparts, &np));
+  sparts += np;
   }
+  HIP_TRY(launch_dA_reduce(L.dApart, sparts, K * V * V, L.dAlvl, a->dA, s));
   }
   if (defer) {
     HIP_TRY(launch_chain_coef(L.sd, L.sdn, mean1, invstd1, a->g1, L.s1, L.s2, a->x_stats, C,

@@ -45,6 +45,17 @@ __device__ __forceinline__ unsigned amax_read(const unsigned *amax) {
   return m;
 }
 
+// amax_read for a whole wave (every lane active): one slot per lane and a
+// shuffle max -- 1 load per lane instead of kAmaxSlots (the per-element weight
+// packs read the bound once per element)
+__device__ __forceinline__ unsigned amax_read_wave(const unsigned *amax) {
+  static_assert(kAmaxSlots == 64, "one slot per lane");
+  unsigned m = amax[(threadIdx.x & 63) * kAmaxStride];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  return m;
+}
+
 // Block (NT threads) max of m >= 0 into amax's slot of this workgroup; every
 // thread of the block must call it (one barrier).
 template <int NT>

@@ -102,6 +102,11 @@ struct ConvGemmParams {
   PrevBn prev;
   double *sd, *sdn;
   float *dA;
+  // dA_part (non-null): the workgroup's dA partial (V*V floats, summed in a fixed
+  // order) is stored at dA_part[blockIdx.x * V * V] instead of added to dA with
+  // fp32 atomics; launch_dA_reduce then adds the partials to dA in launch order
+  // (run-to-run deterministic dA)
+  float *dA_part;
   // wpk already holds the packed split planes of w (stgcn_fold_prep): no pack launch
   int wpk_ready;
   // bna (with f16x2, V = 18, the folded block's forward; kernels_x3.hip): in[] is
@@ -201,7 +206,7 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
                                          double *sdu, int N, int C, int L, int training,
                                          Dropout drop, hipStream_t s, int du_bf16,
                                          const float *dy_coef, double *cs,
-                                         unsigned *amax = nullptr);
+                                         unsigned *amax = nullptr, const float *dync = nullptr);
 // ... frame-wise (V = 18), also writing dUA = dU A (the folded block without G,
 // capi.hip fold_bna) and the fp16 operand bounds max |dU| (amax), max |dUA| (amaxa)
 hipError_t launch_bn_relu_bwd_apply_fr(const float *dy, const float *U, const float *mean,
@@ -298,13 +303,15 @@ hipError_t launch_bn_relu_fwd(const float *U, const float *mean, const float *in
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b,
                                      int N, int C, int L, double *sg, double *sgu, Dropout drop,
-                                     hipStream_t s);
+                                     hipStream_t s, const float *dync = nullptr);
 hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float *mean,
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU,
                                     double *sdu, int N, int C, int L, int training,
                                     Dropout drop, hipStream_t s, int du_bf16 = 0,
-                                    const float *dy_coef = nullptr);
+                                    const float *dy_coef = nullptr, const float *dync = nullptr);
+// (dync non-null, ABI 10 stgcn_bwd_args_t.dy_nc: dy[n, c, :] == dync[n * C + c];
+// the three ReLU + BN2 backward passes then read no dy tensor)
 // Deferred-dx chain: block i's BN1 backward folded into block i-1's ReLU+BN2
 // backward. dy_coef (5*C: [a | md | mu | is | mdn], launch_chain_coef) makes
 // launch_bn_relu_bwd_apply read dy as the next block's dxhat and form
@@ -365,7 +372,15 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b,
                              const float *A, float *dx, float *dA, double *sd, double *sdn,
                              int N, int C, int T, int V, int K, int write_dx, int relu,
-                             int bf16ops, hipStream_t s, const PrevBn *prev = nullptr);
+                             int bf16ops, hipStream_t s, const PrevBn *prev = nullptr,
+                             float *dA_part = nullptr, int64_t part_cap = 0,
+                             int64_t *nparts = nullptr);
+int conv_x3_tile_rows(const ConvGemmParams &p, int npl);
+// Deterministic dA: adds nparts partials part[i][n] (i in order) to dA[n], in two
+// fixed-order passes (lvl: kDaLvl * n doubles of scratch)
+constexpr int kDaLvl = 64;
+hipError_t launch_dA_reduce(const float *part, int64_t nparts, int n, double *lvl, float *dA,
+                            hipStream_t s);
 // launch_spatial_dx takes a PrevBn for this shape (its k_spatial_bwd5 / _bwd6
 // paths; 16-byte aligned tensors assumed, as torch allocates them)
 bool spatial_dx_prev_supported(int N, int C, int T, int V, int K);

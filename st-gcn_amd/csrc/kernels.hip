@@ -1686,16 +1686,22 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
                                                             const float *invstd, const float *g,
                                                             const float *b, int C, int L,
                                                             double *sg, double *sgu,
-                                                            Dropout drop) {
+                                                            Dropout drop, const float *dync) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
+  const float dv = dync ? dync[(int64_t)n * C + c] : 0.f;  // (ABI 10: dy constant per row)
   double s = 0.0, q = 0.0;
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float u[VEC], d[VEC];
     vld<VEC>(U + base + i, u);
-    vld<VEC>(dy + base + i, d);
+    if (dync) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) d[j] = dv;
+    } else {
+      vld<VEC>(dy + base + i, d);
+    }
     if (drop.thresh) {  // gradient through the fused dropout
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
@@ -1715,9 +1721,9 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_reduce(const float *dy, con
 hipError_t launch_bn_relu_bwd_reduce(const float *dy, const float *U, const float *mean,
                                      const float *invstd, const float *g, const float *b, int N,
                                      int C, int L, double *sg, double *sgu, Dropout drop,
-                                     hipStream_t s) {
+                                     hipStream_t s, const float *dync) {
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_reduce, slice_vec(L, {dy, U}), dim3(C, N), dy, U, mean, invstd,
-                   g, b, C, L, sg, sgu, drop);
+                   g, b, C, L, sg, sgu, drop, dync);
   return hipGetLastError();
 }
 
@@ -1725,10 +1731,11 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
     const float *dy, const float *U, const float *mean, const float *invstd, const float *g,
     const float *b, const double *sg, const double *sgu, float *dU, double *sdu, int C, int L,
-    double invM, Dropout drop, int du_bf16, const float *dy_coef) {
+    double invM, Dropout drop, int du_bf16, const float *dy_coef, const float *dync) {
   __shared__ double red[8];
   const int c = blockIdx.x, n = blockIdx.y;
   const int64_t base = ((int64_t)n * C + c) * L;
+  const float dv = dync ? dync[(int64_t)n * C + c] : 0.f;  // (ABI 10: dy constant per row)
   const float mu = mean[c], is = invstd[c], a = is * g[c], be = b[c];
   const float mg = (float)(sg[c] * invM), mgu = (float)(sgu[c] * invM);
   // deferred dx of the next block: dy = ca * (dxhat - cmd - (y - cmu) * cis * cmdn)
@@ -1744,7 +1751,12 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply(
   for (int i = threadIdx.x * VEC; i < L; i += 256 * VEC) {
     float u[VEC], d[VEC], o[VEC];
     vld<VEC>(U + base + i, u);
-    vld<VEC>(dy + base + i, d);
+    if (dync) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) d[j] = dv;
+    } else {
+      vld<VEC>(dy + base + i, d);
+    }
     if (dy_coef) {
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
@@ -1788,11 +1800,12 @@ hipError_t launch_bn_relu_bwd_apply(const float *dy, const float *U, const float
                                     const float *invstd, const float *g, const float *b,
                                     const double *sg, const double *sgu, float *dU, double *sdu,
                                     int N, int C, int L, int training, Dropout drop,
-                                    hipStream_t s, int du_bf16, const float *dy_coef) {
+                                    hipStream_t s, int du_bf16, const float *dy_coef,
+                                    const float *dync) {
   // eval mode (constant running statistics): no batch-mean terms
   const double invM = training ? 1.0 / ((double)N * L) : 0.0;
   STGCN_VEC_LAUNCH(k_bn_relu_bwd_apply, slice_vec(L, {dy, U, dU}), dim3(C, N), dy, U, mean,
-                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop, du_bf16, dy_coef);
+                   invstd, g, b, sg, sgu, dU, sdu, C, L, invM, drop, du_bf16, dy_coef, dync);
   return hipGetLastError();
 }
 
@@ -1807,7 +1820,8 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
     const float *__restrict__ dy, const float *__restrict__ U, const float *mean,
     const float *invstd, const float *g, const float *b, const double *sg, const double *sgu,
     float *__restrict__ dU, double *sdu, int N, int C, int L, double invM, Dropout drop,
-    int du_bf16, const float *dy_coef, double *__restrict__ cs, unsigned *amax) {
+    int du_bf16, const float *dy_coef, double *__restrict__ cs, unsigned *amax,
+    const float *dync) {
   __shared__ double red[8];
   float om = 0.f;  // max |dU| (f16x2 operand bound)
   const int c = blockIdx.x;
@@ -1831,13 +1845,23 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
     float ua[VEC], da[VEC], ub[VEC], db[VEC];
     const int64_t cl = (int64_t)C * L;  // floats per clip
     const int64_t b0 = ((int64_t)n0 * C + c) * L + i;
+    // (ABI 10, dync: dy constant over the row -- one value per clip, no dy tensor)
+    auto ldy = [&](int64_t off, int nn, float (&dr)[VEC]) __attribute__((always_inline)) {
+      if (dync) {
+        const float dv = dync[(int64_t)nn * C + c];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) dr[j] = dv;
+      } else {
+        vld<VEC>(dy + off, dr);
+      }
+    };
     if (n0 < n1) {
       vld<VEC>(U + b0, ua);
-      vld<VEC>(dy + b0, da);
+      ldy(b0, n0, da);
     }
     if (n0 + 1 < n1) {
       vld<VEC>(U + b0 + cl, ub);
-      vld<VEC>(dy + b0 + cl, db);
+      ldy(b0 + cl, n0 + 1, db);
     }
     auto clip = [&](int n, float (&ur)[VEC], float (&dr)[VEC]) __attribute__((always_inline)) {
       const int64_t base = ((int64_t)n * C + c) * L;
@@ -1849,7 +1873,7 @@ __global__ __launch_bounds__(256) void k_bn_relu_bwd_apply_cols(
       }
       if (n + 2 < n1) {
         vld<VEC>(U + base + 2 * cl + i, ur);
-        vld<VEC>(dy + base + 2 * cl + i, dr);
+        ldy(base + 2 * cl + i, n + 2, dr);
       }
       if (dy_coef) {
 #pragma unroll
@@ -2031,7 +2055,8 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
                                          const double *sg, const double *sgu, float *dU,
                                          double *sdu, int N, int C, int L, int training,
                                          Dropout drop, hipStream_t s, int du_bf16,
-                                         const float *dy_coef, double *cs, unsigned *amax) {
+                                         const float *dy_coef, double *cs, unsigned *amax,
+                                         const float *dync) {
   const double invM = training ? 1.0 / ((double)N * L) : 0.0;
   // (whole-row vectors: every row start VEC-aligned needs L % VEC == 0)
   int vec = slice_vec(L, {dy, U, dU});
@@ -2039,7 +2064,7 @@ hipError_t launch_bn_relu_bwd_apply_cols(const float *dy, const float *U, const 
 #define COLS_LAUNCH(VV)                                                                     \
   hipLaunchKernelGGL((k_bn_relu_bwd_apply_cols<VV>), dim3(C, (L + 256 * VV - 1) / (256 * VV), nz), \
                      dim3(256), 0, s, dy, U, mean, invstd, g, b, sg, sgu, dU, sdu, N, C, L,  \
-                     invM, drop, du_bf16, dy_coef, cs, amax)
+                     invM, drop, du_bf16, dy_coef, cs, amax, dync)
   if (vec == 4)
     COLS_LAUNCH(4);
   else if (vec == 2)
@@ -2451,7 +2476,7 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx, int relu) {
+    int K, int64_t rows, int write_dx, int relu, float *dA_part) {
   constexpr int VP = JointCfg<V>::VP;
   constexpr int NT = (V + 31) / 32;
   constexpr int MAXSEG = 32;
@@ -2550,12 +2575,13 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
       atomicAdd(sdn + cc, seg_n[tid]);
     }
   }
-  // dA on MFMA over the block's rows (wave takes row pairs kk = wave, +nw, ...)
+  // dA on MFMA over the block's rows (wave takes row pairs kk = wave, +nw, ...);
+  // each wave's tiles go to its own slice [wave][K][DW][DW] (one owner lane per
+  // entry: plain stores), summed over the waves in wave order below
   const int nw = RB / 64;
   const int nk = RB / 2;
-  float *dred = XBs + RB * VP;  // [K][NT*32][NT*32] (zeroed below)
   const int DW = NT * 32;
-  for (int i = tid; i < K * DW * DW; i += RB) dred[i] = 0.f;
+  float *dred = XBs + RB * VP + wave * K * DW * DW;
   __syncthreads();
   for (int k = 0; k < K; ++k) {
     floatx16 dacc[NT][NT];
@@ -2588,13 +2614,19 @@ __global__ __launch_bounds__(256) void k_spatial_bwd3(
         for (int i = 0; i < 16; ++i) {
           const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
           const int w = q2 * 32 + lo;
-          if (v < V && w < V) atomicAdd(dred + (k * DW + v) * DW + w, dacc[p2][q2][i]);
+          if (v < V && w < V) dred[(k * DW + v) * DW + w] = dacc[p2][q2][i];
         }
   }
   __syncthreads();
+  const float *dw0 = XBs + RB * VP;
   for (int i = tid; i < K * V * V; i += RB) {
     const int k = i / (V * V), rem = i - k * V * V, v = rem / V, w = rem - v * V;
-    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
+    float sum = 0.f;
+    for (int wv = 0; wv < nw; ++wv) sum += dw0[((wv * K + k) * DW + v) * DW + w];
+    if (dA_part)  // (deterministic: launch_dA_reduce adds the partials in order)
+      dA_part[(int64_t)blockIdx.x * K * V * V + i] = sum;
+    else
+      atomicAdd(dA + i, sum);
   }
 }
 
@@ -2649,7 +2681,7 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx, int relu, PrevBn prev) {
+    int K, int64_t rows, int write_dx, int relu, PrevBn prev, float *dA_part) {
   constexpr int VH = (V + 1) / 2;           // MFMA k-steps over v
   constexpr int NW = bwd5_nw(KMAX);         // waves
   constexpr int NH = NW / 4;                // reduction halves of the dx GEMM
@@ -2861,14 +2893,36 @@ __global__ __launch_bounds__(bwd5_nw(KMAX) * 64) void k_spatial_bwd5(
     }
   }
   if constexpr (DREG) {
+    // the waves' register tiles into the zeroed LDS accumulator one wave after
+    // the other (plain adds, one owner lane per entry): a fixed order
+    __syncthreads();
+    for (int wv = 0; wv < NW; ++wv) {
+      if (wave == wv) {
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-      if (k < K) flush_dacc(k);
+        for (int k = 0; k < KMAX; ++k)
+          if (k < K) {
+#pragma unroll
+            for (int p2 = 0; p2 < NT; ++p2)
+#pragma unroll
+              for (int q2 = 0; q2 < NT; ++q2)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                  const int v = p2 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hi;
+                  const int w = q2 * 32 + lo;
+                  if (v < V && w < V) dred[(k * DW + v) * DW + w] += dacc[k][p2][q2][i];
+                }
+          }
+      }
+      __syncthreads();
+    }
   }
   __syncthreads();
   for (int i = tid; i < K * V * V; i += NW * 64) {
     const int k = i / (V * V), rm = i - k * V * V, v = rm / V, w = rm - v * V;
-    atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
+    if (dA_part)  // (deterministic: launch_dA_reduce adds the partials in order)
+      dA_part[(int64_t)blockIdx.x * K * V * V + i] = dred[(k * DW + v) * DW + w];
+    else
+      atomicAdd(dA + i, dred[(k * DW + v) * DW + w]);
   }
 }
 
@@ -2885,15 +2939,18 @@ static bool launch_bwd5(const float *H, const float *x, const float *mean, const
                         const float *g, const float *b, const float *A, float *dx, float *dA,
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
                         int write_dx, int relu, hipStream_t s, const PrevBn &prev,
-                        bool dry = false) {
+                        bool dry = false, float *dA_part = nullptr, int64_t part_cap = 0,
+                        int64_t *nparts = nullptr) {
   const size_t lds = bwd5_lds<V, RB>(K);
   if (lds > 160 * 1024 - 1024 || ((int64_t)C * T) % RB != 0 || rows >= (int64_t)1 << 31) return false;
   const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 1024))));
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256 * per_cu));
   if (K != KT) return false;
   if (dry) return true;
+  float *part = dA_part && (int64_t)grid.x <= part_cap ? dA_part : nullptr;
+  if (part && nparts) *nparts = grid.x;
   hipLaunchKernelGGL((k_spatial_bwd5<V, RB, KT>), grid, dim3(bwd5_nw(KT) * 64), lds, s, H, x, mean, invstd, g,
-                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, prev);
+                     b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, prev, part);
   return true;
 }
 
@@ -2941,7 +2998,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
     const float *__restrict__ H, const float *__restrict__ x, const float *__restrict__ mean,
     const float *__restrict__ invstd, const float *__restrict__ g, const float *__restrict__ b,
     const float *__restrict__ A, float *dx, float *dA, double *sd, double *sdn, int C, int T,
-    int K, int64_t rows, int write_dx, int relu, PrevBn prev) {
+    int K, int64_t rows, int write_dx, int relu, PrevBn prev, float *dA_part) {
   constexpr int RB = 64, NW = 8;
   static_assert(V > 32 && V <= 64, "two 32-column tiles");
   constexpr int MAXSEG = 32;
@@ -3178,7 +3235,15 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       for (int e = 0; e < 16; ++e) {
         const int v = p2 * 32 + (e & 3) + 8 * (e >> 2) + 4 * hi;
         const int w = q2 * 32 + lo;
-        if (v < V && w < V) atomicAdd(dA + (k * V + v) * V + w, dacc[i][e] + dacl[i][e]);
+        if (v < V && w < V) {
+          // (deterministic: one slot per row half -- waves w, w + 4 hold the same
+          // entries -- added in order by launch_dA_reduce)
+          if (dA_part)
+            dA_part[((int64_t)blockIdx.x * 2 + (wave >> 2)) * K * V * V + (k * V + v) * V + w] =
+                dacc[i][e] + dacl[i][e];
+          else
+            atomicAdd(dA + (k * V + v) * V + w, dacc[i][e] + dacl[i][e]);
+        }
       }
     }
   }
@@ -3189,7 +3254,8 @@ static bool launch_bwd6(const float *H, const float *x, const float *mean, const
                         const float *g, const float *b, const float *A, float *dx, float *dA,
                         double *sd, double *sdn, int C, int T, int K, int64_t rows,
                         int write_dx, int relu, hipStream_t s, const PrevBn &prev,
-                        bool dry = false) {
+                        bool dry = false, float *dA_part = nullptr, int64_t part_cap = 0,
+                        int64_t *nparts = nullptr) {
   constexpr int RB = 64;
   constexpr int PL = (RB * V + 255) / 256 * 256;
   const size_t lds = sizeof(float) * ((size_t)(2 * (K + 1) + 2) * PL) + 3 * (size_t)V * (RB + 8) * 2;
@@ -3198,8 +3264,10 @@ static bool launch_bwd6(const float *H, const float *x, const float *mean, const
     return false;
   if (dry) return true;
   const dim3 grid((unsigned)std::min<int64_t>(rows / RB, 256));
+  float *part = dA_part && 2 * (int64_t)grid.x <= part_cap ? dA_part : nullptr;
+  if (part && nparts) *nparts = 2 * (int64_t)grid.x;
   hipLaunchKernelGGL((k_spatial_bwd6<V, KT, BF>), grid, dim3(512), lds, s, H, x, mean, invstd, g, b,
-                     A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, prev);
+                     A, dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, prev, part);
   return true;
 }
 
@@ -3617,7 +3685,9 @@ __global__ __launch_bounds__(256) void k_spatial_dx(const float *H, const float 
 static bool launch_bwd56(const float *H, const float *x, const float *mean, const float *invstd,
                          const float *g, const float *b, const float *A, float *dx, float *dA,
                          double *sd, double *sdn, int N, int C, int T, int V, int K, int write_dx,
-                         int relu, bool bf6, hipStream_t s, const PrevBn &prev, bool dry) {
+                         int relu, bool bf6, hipStream_t s, const PrevBn &prev, bool dry,
+                         float *dA_part = nullptr, int64_t part_cap = 0,
+                         int64_t *nparts = nullptr) {
   constexpr bool joint3 = STGCN_AB_JOINT3 != 0;  // A/B builds only (ab_switches.h)
   const bool aligned = ((int64_t)N * C * T * V) % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
                        ((uintptr_t)H & 15) == 0 && ((uintptr_t)dx & 15) == 0;
@@ -3626,7 +3696,7 @@ static bool launch_bwd56(const float *H, const float *x, const float *mean, cons
     bool done = false;
 #define STGCN_BWD5(VV, RR, KK)                                                              \
   launch_bwd5<VV, RR, KK>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, \
-                          relu, s, prev, dry)
+                          relu, s, prev, dry, dA_part, part_cap, nparts)
     // partitions K: 1 (uniform), 2 (distance), 3 (spatial) labelling
     if (V == 18)
       done = STGCN_BWD5(18, 128, 1) || STGCN_BWD5(18, 64, 1) || STGCN_BWD5(18, 128, 2) ||
@@ -3644,7 +3714,7 @@ static bool launch_bwd56(const float *H, const float *x, const float *mean, cons
     bool done = false;
 #define STGCN_BWD6(KK, BF)                                                                     \
   launch_bwd6<50, KK, BF>(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, K, rows, write_dx, \
-                          relu, s, prev, dry)
+                          relu, s, prev, dry, dA_part, part_cap, nparts)
     if (bf6)
       done = STGCN_BWD6(1, true) || STGCN_BWD6(2, true) || STGCN_BWD6(3, true);
     else
@@ -3666,13 +3736,15 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
                              const float *invstd, const float *g, const float *b, const float *A,
                              float *dx, float *dA, double *sd, double *sdn, int N, int C, int T,
                              int V, int K, int write_dx, int relu, int bf16ops, hipStream_t s,
-                             const PrevBn *prev) {
+                             const PrevBn *prev, float *dA_part, int64_t part_cap,
+                             int64_t *nparts) {
+  if (nparts) *nparts = 0;
   // (STGCN_AB_BWD6_EXACT: the exact-split k_spatial_bwd6 for bf16 blocks too)
   constexpr bool exact6 = STGCN_AB_BWD6_EXACT != 0;
   const bool bf6 = bf16ops && !exact6;
   const PrevBn pv = prev ? *prev : PrevBn();
   if (launch_bwd56(H, x, mean, invstd, g, b, A, dx, dA, sd, sdn, N, C, T, V, K, write_dx, relu,
-                   bf6, s, pv, false))
+                   bf6, s, pv, false, dA_part, part_cap, nparts))
     return hipGetLastError();
   if (pv.mean) return hipErrorInvalidValue;  // (callers check spatial_dx_prev_supported)
   if (joint_fast(V) && K <= 3) {
@@ -3681,23 +3753,89 @@ hipError_t launch_spatial_dx(const float *H, const float *x, const float *mean,
     const int64_t rows = (int64_t)N * C * T;
     const int DW3 = (V + 31) / 32 * 32;
     const size_t lds3 = sizeof(float) * ((size_t)K * V * VP + (size_t)K * RB * V + (size_t)RB * VP +
-                                         (size_t)K * DW3 * DW3);
+                                         (size_t)(RB / 64) * K * DW3 * DW3);
     const dim3 grid3((unsigned)((rows + RB - 1) / RB));
+    // (per-workgroup dA partials where the caller's buffer holds them all)
+    float *part = dA_part && (int64_t)grid3.x <= part_cap ? dA_part : nullptr;
+    if (part && nparts) *nparts = grid3.x;
     if (V == 18)
       hipLaunchKernelGGL(k_spatial_bwd3<18>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, part);
     else if (V == 25)
       hipLaunchKernelGGL(k_spatial_bwd3<25>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, part);
     else
       hipLaunchKernelGGL(k_spatial_bwd3<50>, grid3, dim3(RB), lds3, s, H, x, mean, invstd, g, b, A,
-                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu);
+                         dx, dA, sd, sdn, C, T, K, rows, write_dx, relu, part);
     return hipGetLastError();
   }
   if (K * V * V > 8192) return hipErrorInvalidValue;
   const size_t lds = sizeof(float) * (2 * (size_t)K * V * V + kDxTC * V + (size_t)K * kDxTC * V);
   hipLaunchKernelGGL(k_spatial_dx, dim3((T + kDxTC - 1) / kDxTC, N), dim3(256), lds, s, H, x,
                      mean, invstd, g, b, A, dx, dA, sd, sdn, C, T, V, K, write_dx, relu);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic dA (the spatial backward's per-workgroup partials, dA_part):
+// pass 1 sums the partials of chunk y in a fixed order (four interleaved fp64
+// chains per entry, combined in order) into lvl[y][e]; pass 2 adds
+// sum_y lvl[y][e] (in y order, fp64) to dA[e]. Replaces the fp32 atomics whose
+// arrival order made dA differ from run to run at the 1e-3 level on this
+// heavily cancelling gradient.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dA_reduce1(const float *__restrict__ part, int64_t nparts,
+                                                    int n, int64_t chunk, double *lvl) {
+  __shared__ double sm[4][64];
+  const int t = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + t;
+  const int64_t p0 = (int64_t)blockIdx.y * chunk, p1 = min(nparts, p0 + chunk);
+  double s = 0.0;
+  if (e < n) {
+    int64_t q = p0 + g;
+    for (; q + 12 < p1; q += 16) {  // (four loads in flight)
+      const float a0 = part[q * n + e], a1 = part[(q + 4) * n + e];
+      const float a2 = part[(q + 8) * n + e], a3 = part[(q + 12) * n + e];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; q < p1; q += 4) s += part[q * n + e];
+  }
+  sm[g][t] = s;
+  __syncthreads();
+  if (g == 0 && e < n) lvl[(int64_t)blockIdx.y * n + e] = ((sm[0][t] + sm[1][t]) + sm[2][t]) + sm[3][t];
+}
+
+__global__ __launch_bounds__(256) void k_dA_reduce2(const double *__restrict__ lvl, int ny, int n,
+                                                    float *dA) {
+  // (four groups of 64 lanes, each over every fourth level with all its loads
+  // in flight, combined in group order)
+  __shared__ double sm[4][64];
+  const int t = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + t;
+  double s = 0.0;
+  if (e < n) {
+#pragma unroll
+    for (int y = g; y < kDaLvl; y += 4)
+      if (y < ny) s += lvl[(int64_t)y * n + e];
+  }
+  sm[g][t] = s;
+  __syncthreads();
+  if (g == 0 && e < n)
+    dA[e] = (float)((double)dA[e] + (((sm[0][t] + sm[1][t]) + sm[2][t]) + sm[3][t]));
+}
+
+hipError_t launch_dA_reduce(const float *part, int64_t nparts, int n, double *lvl, float *dA,
+                            hipStream_t s) {
+  if (nparts <= 0) return hipSuccess;
+  if (!part || !lvl || !dA || n <= 0) return hipErrorInvalidValue;
+  const int ny = (int)std::min<int64_t>(kDaLvl, nparts);
+  const int64_t chunk = (nparts + ny - 1) / ny;
+  const int nb = (n + 63) / 64;
+  hipLaunchKernelGGL(k_dA_reduce1, dim3(nb, ny), dim3(256), 0, s, part, nparts, n, chunk, lvl);
+  hipLaunchKernelGGL(k_dA_reduce2, dim3(nb), dim3(256), 0, s, lvl, ny, n, dA);
   return hipGetLastError();
 }
 

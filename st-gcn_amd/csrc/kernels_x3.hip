@@ -544,7 +544,10 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
 #pragma unroll
       for (int u = 0; u < 4; ++u) s4[u] += pc[(k + u) * PP];
     const float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-    if (!(STGCN_SPB_EXP & 32)) atomicAdd(p.dA + tid, sum);
+    if (p.dA_part)  // (deterministic: launch_dA_reduce adds the partials in order)
+      p.dA_part[(int64_t)blockIdx.x * (V * V) + tid] = sum;
+    else if (!(STGCN_SPB_EXP & 32))
+      atomicAdd(p.dA + tid, sum);
   }
 }
 
@@ -1172,6 +1175,8 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
                                  int nch, int rows, int npl, int64_t w_sr, int64_t w_sc,
                                  int64_t w_sq, int64_t total, const unsigned *amax_w) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // (the fp16 planes' operand scale: read once per wave, before any lane leaves)
+  const int se = npl == 2 ? f16x2_se_bits(amax_w ? amax_read_wave(amax_w) : 0x3f800000u) : 0;
   if (idx >= total) return;
   const int jj = (int)(idx & 7);
   int64_t t = idx >> 3;
@@ -1192,7 +1197,7 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
   float v = 0.f;
   if (r < R && c < C) v = w[(int64_t)r * w_sr + (int64_t)c * w_sc + (int64_t)q * w_sq];
   if (npl == 2) {  // fp16 (h, l) of the power-of-two-scaled weight
-    const float vs = v * pow2f(f16x2_se(amax_w));
+    const float vs = v * pow2f(se);
     const _Float16 h = (_Float16)vs;
     const _Float16 l = (_Float16)(vs - (float)h);
     reinterpret_cast<_Float16 *>(wpk)[idx] = pl == 0 ? h : l;
@@ -1207,20 +1212,23 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
 
 // The pack of several weight tensors in one launch (stgcn_fold_prep: every
 // folded block's forward and data-gradient weights once per step): job i covers
-// flat indices [start[i], start[i + 1]) of the concatenated jobs.
+// flat indices [start[i], start[i] + total) of the concatenated jobs, its start
+// a multiple of the 256-thread block (one job per block: the operand scale is
+// read once per wave).
 struct PackJobs {
   PackJob j[kPackJobs];
   int64_t start[kPackJobs + 1];
   int n;
 };
 
-__global__ void k_pack_conv_w_x3_multi(PackJobs js) {
+__global__ __launch_bounds__(256) void k_pack_conv_w_x3_multi(PackJobs js) {
   const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gi >= js.start[js.n]) return;
-  int k = 0;
+  int k = 0;  // (uniform: job starts are multiples of the block)
   while (k + 1 < js.n && gi >= js.start[k + 1]) ++k;
   const PackJob &q = js.j[k];
+  const int se = q.npl == 2 ? f16x2_se_bits(q.amax_w ? amax_read_wave(q.amax_w) : 0x3f800000u) : 0;
   const int64_t idx = gi - js.start[k];
+  if (idx >= q.total) return;
   const int jj = (int)(idx & 7);
   int64_t t = idx >> 3;
   const int rl = (int)(t % q.rows);
@@ -1240,7 +1248,7 @@ __global__ void k_pack_conv_w_x3_multi(PackJobs js) {
   float v = 0.f;
   if (r < q.R && c < q.C) v = q.w[(int64_t)r * q.w_sr + (int64_t)c * q.w_sc + (int64_t)tap * q.w_sq];
   if (q.npl == 2) {
-    const float vs = v * pow2f(f16x2_se(q.amax_w));
+    const float vs = v * pow2f(se);
     const _Float16 h = (_Float16)vs;
     const _Float16 l = (_Float16)(vs - (float)h);
     reinterpret_cast<_Float16 *>(q.wpk)[idx] = pl == 0 ? h : l;
@@ -1286,7 +1294,7 @@ static bool x3_wide_rows(const ConvGemmParams &p) {
 // 4-wave 64-row tiles, two workgroups per CU (ConvX3Geo NW = 4): the fp16-split
 // stride-1 forward where the caller marked it (p.w4: capi.hip fwd_w4), up to 128
 // output rows (at 256 the second read of each window per 128 rows costs what
-// the overlap gains: L8 0.668 vs 0.654 ms, profiles/r6b_kbench.txt). Decides
+// the overlap gains: L8 0.668 vs 0.654 ms, profiles/r6b_kbench_w4.txt). Decides
 // the packed weight layout (64-row tiles) and the kernel alike.
 static bool x3_w4(const ConvGemmParams &p, int npl) {
   constexpr bool off = STGCN_AB_X3_NOW4 != 0;
@@ -1350,6 +1358,12 @@ static bool launch_cx_v(const ConvGemmParams &p, int nblk, hipStream_t s) {
 // npl = 3: fp32 as exact 3-way splits (STGCN_F_F32X3); npl = 1: bf16 operands
 // (STGCN_F_BF16), the same pipeline with one plane and two workgroups per CU
 // The pack job of a launch_conv_planes call (same layout, same scales)
+// rows per workgroup tile of a launch_conv_x3 launch (its grid: N x n_mtiles x
+// ceil(R / rows) workgroups)
+int conv_x3_tile_rows(const ConvGemmParams &p, int npl) {
+  return npl >= 2 && x3_wide_rows(p) && !x3_w4(p, npl) ? 128 : 64;
+}
+
 static PackJob pack_job(const ConvGemmParams &p, int npl) {
   const bool w4 = x3_w4(p, npl);
   const bool wide = npl >= 2 && x3_wide_rows(p) && !w4;
@@ -1385,7 +1399,7 @@ hipError_t launch_pack_jobs(const PackJob *jobs, int n, hipStream_t s) {
     js.start[0] = 0;
     for (int k = 0; k < js.n; ++k) {
       js.j[k] = jobs[i0 + k];
-      js.start[k + 1] = js.start[k] + js.j[k].total;
+      js.start[k + 1] = js.start[k] + (js.j[k].total + 255) / 256 * 256;
     }
     const int64_t tot = js.start[js.n];
     if (tot > 0)

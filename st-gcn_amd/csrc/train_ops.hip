@@ -231,6 +231,13 @@ __global__ __launch_bounds__(256) void k_head_bcast(const float *dpooled, float 
   for (int l = threadIdx.x; l < L; l += 256) dst[l] = v;
 }
 
+// the per-row value k_head_bcast writes at every position (same arithmetic)
+__global__ __launch_bounds__(256) void k_head_dync(const float *dpooled, float *dy_nc, int64_t rows,
+                                                   int L) {
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row < rows) dy_nc[row] = dpooled[row] / (float)L;
+}
+
 }  // namespace
 
 extern "C" {
@@ -352,6 +359,28 @@ int stgcn_head_bwd(const stgcn_head_desc_t *d, const float *pooled, const float 
                      pooled, dW, dbias, d->N, d->C, d->classes);
   hipLaunchKernelGGL(k_head_bcast, dim3((unsigned)rows), dim3(256), 0, s, dpooled, dy, rows,
                      d->L);
+  HIP_TRY2(hipGetLastError());
+  return STGCN_OK;
+}
+
+int stgcn_head_bwd_nc(const stgcn_head_desc_t *d, const float *pooled, const float *logits,
+                      const float *W, const int64_t *labels, const float *dloss, float *dlogits,
+                      float *dpooled, float *dy_nc, float *dW, float *dbias, void *stream) {
+  if (!d || d->N <= 0 || d->C <= 0 || d->L <= 0 || d->classes <= 0)
+    return fail(STGCN_E_INVALID, "head: bad descriptor");
+  if (!pooled || !logits || !W || !labels || !dloss || !dlogits || !dpooled || !dy_nc || !dW ||
+      !dbias)
+    return fail(STGCN_E_INVALID, "head: null tensor argument");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = (int64_t)d->N * d->C;
+  hipLaunchKernelGGL(k_head_bwd_rows, dim3(d->N), dim3(256),
+                     (size_t)(d->classes + 8) * sizeof(float), s, logits, W, labels, dloss,
+                     dlogits, dpooled, d->N, d->C, d->classes);
+  const int64_t nw = (int64_t)d->classes * (d->C + 1);
+  hipLaunchKernelGGL(k_head_wgrad, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, dlogits,
+                     pooled, dW, dbias, d->N, d->C, d->classes);
+  hipLaunchKernelGGL(k_head_dync, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, dpooled,
+                     dy_nc, rows, d->L);
   HIP_TRY2(hipGetLastError());
   return STGCN_OK;
 }

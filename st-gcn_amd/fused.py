@@ -233,6 +233,17 @@ def _dropout_seed(drop, training):
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
+def _per_row(dy):
+    """The (N, C) base of a gradient expanded over its last two axes (strides
+    (C, 1, 0, 0) over a contiguous (N, C) tensor), else None (ABI 10 dy_nc)."""
+    if dy.dim() != 4 or dy.stride(2) != 0 or dy.stride(3) != 0:
+        return None
+    N, C = dy.shape[0], dy.shape[1]
+    if dy.stride(1) != 1 or (N > 1 and dy.stride(0) != C) or dy.dtype != torch.float32:
+        return None
+    return dy
+
+
 def _args(cls, ptrs, drop, seed, **extra):
     a = cls(*ptrs)
     a.dropout_p = float(drop)
@@ -327,12 +338,16 @@ class StgcnBlockFn(torch.autograd.Function):
         x, Z, U, stats, A, W, bW, Wt, g1, b1, g2, b2, G = ctx.saved_tensors
         stride, pad, eps, momentum, training = ctx.cfg
         need_dx = bool(ctx.needs_input_grad[0])
-        dy = dy.contiguous()
         C_out = Wt.shape[0]
+        # ABI 10: a gradient constant over (T, V) (the pooling head's, expanded
+        # from (N, C_out)) goes in as dy_nc; anything else as a contiguous dy
+        dy_nc = _per_row(dy)
+        dy_full = dy
+        dy = None if dy_nc is not None else dy.contiguous()
         desc = make_desc(x.shape, C_out, A.shape[0], stride, pad, eps, momentum, training,
                          need_dx=need_dx, **_gemm_flags(ctx.gemm))
         dy_sums, dy_coef, pg2, pb2, psums, pU, pst, xst, dx_coef = _chain_bwd_args(
-            ctx.cc, dy, need_dx, x.shape[1], x.device, ctx.xref)
+            ctx.cc, dy_full, need_dx, x.shape[1], x.device, ctx.xref)
         deferred = ctypes.c_int32(0)
         dx = torch.empty_like(x) if need_dx else None
         grads = [torch.empty_like(t) for t in (A, W, bW, Wt)]
@@ -347,10 +362,15 @@ class StgcnBlockFn(torch.autograd.Function):
             prev_U=hip_lib.ptr(pU), prev_stats=hip_lib.ptr(pst), x_stats=hip_lib.ptr(xst),
             dx_coef=hip_lib.ptr(dx_coef),
             dx_deferred=ctypes.addressof(deferred) if dx_coef is not None else None,
-            dy_coef=hip_lib.ptr(dy_coef), prep=hip_lib.ptr(ctx.prep))
-        hip_lib.check(lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args),
-                                          hip_lib.ptr(ws), nbytes,
-                                          hip_lib.stream_handle(x.device)))
+            dy_coef=hip_lib.ptr(dy_coef), prep=hip_lib.ptr(ctx.prep), dy_nc=hip_lib.ptr(dy_nc))
+        rc = lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args), hip_lib.ptr(ws), nbytes,
+                                 hip_lib.stream_handle(x.device))
+        if rc == hip_lib.E_UNSUPPORTED and dy_nc is not None:  # (needs the full dy)
+            dy = dy_full.contiguous()
+            args.dy, args.dy_nc = hip_lib.ptr(dy), None
+            rc = lib.stgcn_block_bwd(ctypes.byref(desc), ctypes.byref(args), hip_lib.ptr(ws),
+                                     nbytes, hip_lib.stream_handle(x.device))
+        hip_lib.check(rc)
         _chain_publish(ctx.cc, psums, dx, dx_coef if deferred.value else None)
         dA, dW, dbW, dWt = grads
         return (dx, dA, dW, dbW, dWt, dbWt, dg1, db1, dg2, db2,

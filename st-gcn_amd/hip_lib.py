@@ -21,7 +21,7 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
     import sys
     print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
-ABI_VERSION = 9
+ABI_VERSION = 10
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -76,7 +76,7 @@ class BwdArgs(ctypes.Structure):
          ] + [("prev_U", _vp), ("prev_stats", _vp)  # ABI 4: chain conditioning fallback
               ] + [("x_stats", _vp), ("dx_coef", _vp), ("dx_deferred", _vp),  # ABI 5:
                    ("dy_coef", _vp)                                          # deferred dx
-                   ] + [("prep", _vp)]                                       # ABI 7
+                   ] + [("prep", _vp)] + [("dy_nc", _vp)]                    # ABI 7, 10
 
 
 class FoldWeights(ctypes.Structure):  # ABI 7: stgcn_fold_prep
@@ -104,7 +104,8 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_time_kernel", "stgcn_head_fwd", "stgcn_head_bwd", "stgcn_adam_table_bytes",
             "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
             "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes",
-            "stgcn_block_plan", "stgcn_fold_prep_bytes", "stgcn_fold_prep", "stgcn_head_fwd_u")
+            "stgcn_block_plan", "stgcn_fold_prep_bytes", "stgcn_fold_prep", "stgcn_head_fwd_u",
+            "stgcn_head_bwd_nc")
 
 _LIB = None
 
@@ -142,6 +143,8 @@ def load_library(path=LIB_PATH):
     lib.stgcn_head_fwd_u.restype = ctypes.c_int
     lib.stgcn_head_bwd.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 10 + [_vp]
     lib.stgcn_head_bwd.restype = ctypes.c_int
+    lib.stgcn_head_bwd_nc.argtypes = [ctypes.POINTER(HeadDesc)] + [_vp] * 10 + [_vp]
+    lib.stgcn_head_bwd_nc.restype = ctypes.c_int
     lib.stgcn_adam_table_bytes.argtypes = [ctypes.c_int]
     lib.stgcn_adam_table_bytes.restype = ctypes.c_size_t
     lib.stgcn_adam_build_table.argtypes = [ctypes.POINTER(AdamTensor), ctypes.c_int, _vp,
@@ -179,6 +182,9 @@ def lib():
                                "is False); there is no CPU fallback")
         _LIB = load_library()
     return _LIB
+
+
+E_INVALID, E_UNSUPPORTED, E_HIP = -1, -2, -3  # (stgcn_hip.h stgcn_status)
 
 
 def check(rc):

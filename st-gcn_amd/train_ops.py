@@ -30,8 +30,11 @@ class StgcnHeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, W, b, labels, from_u=None):
         lib = hip_lib.lib()
-        y = y.contiguous()
-        for t, n in ((y, "y"), (W, "W"), (b, "b")):
+        if from_u is None:
+            y = y.contiguous()
+            _check_f32(y, "y")
+        # (from_u: y is the block's unwritten output, a shape-only placeholder)
+        for t, n in ((W, "W"), (b, "b")):
             _check_f32(t, n)
         if labels.dtype != torch.int64 or not labels.is_cuda:
             raise RuntimeError("labels: expected an int64 GPU tensor")
@@ -78,12 +81,17 @@ class StgcnHeadFn(torch.autograd.Function):
         dloss = dloss.reshape(1).float().contiguous()
         dlogits = torch.empty((N, classes), device=dev, dtype=torch.float32)
         dpooled = torch.empty((N, C), device=dev, dtype=torch.float32)
-        dy = torch.empty(ctx.shape, device=dev, dtype=torch.float32)
         dW = torch.empty_like(W)
         db = torch.empty(classes, device=dev, dtype=torch.float32)
-        hip_lib.check(lib.stgcn_head_bwd(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
-            pooled, logits, W, labels, dloss, dlogits, dpooled, dy, dW, db)],
+        # ABI 10: the pool's gradient is constant over (T, V): only its value per
+        # (n, c) is formed, returned as that (N, C) tensor expanded (stride 0) to
+        # y's shape. A HIP block takes it as stgcn_bwd_args_t.dy_nc (no dy tensor
+        # written or read); any other consumer materialises it (.contiguous()).
+        dy_nc = torch.empty((N, C), device=dev, dtype=torch.float32)
+        hip_lib.check(lib.stgcn_head_bwd_nc(ctypes.byref(d), *[hip_lib.ptr(t) for t in (
+            pooled, logits, W, labels, dloss, dlogits, dpooled, dy_nc, dW, db)],
             hip_lib.stream_handle(dev)))
+        dy = dy_nc.view(N, C, *([1] * (len(ctx.shape) - 2))).expand(ctx.shape)
         return dy, dW, db, None, None
 
 

@@ -29,7 +29,7 @@ def test_header_declares_entry_points(pkg):
 def test_library_exports_every_header_symbol(pkg, lib):
     for name in _header_functions():
         assert hasattr(lib, name), name
-    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 9
+    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 10
 
 
 def _desc(pkg, **kw):
@@ -168,17 +168,21 @@ def test_fold_prep_sizes(pkg, lib):
 
 def test_x_from_u_plan_and_argument_checks(pkg, lib):
     """ABI 8 (host logic, no GPU): STGCN_PLAN_X_FROM_U on the folded training
-    blocks that form G (cfg2 f16x2 / split paths); not in eval, not without G
-    (STGCN_F_NO_G), not where the block does not fold. A forward with prev_U on a
-    block without the plan, and a backward with x null outside it, fail before any
-    launch."""
+    blocks that form G (cfg2 f16x2 / split paths) and, round 6, on the bf16
+    blocks whose fused spatial forward stages x (cfg3 / cfg5: V = 25, 50 with
+    K = 3); not in eval, not without G (STGCN_F_NO_G), not on residual blocks,
+    not where the block neither folds nor runs the bf16 fused forward. A forward
+    with prev_U on a block without the plan, and a backward with x null outside
+    it, fail before any launch."""
     hl = pkg.hip_lib
     plan = lambda **kw: hl.block_plan(_desc(pkg, **kw))  # noqa: E731
     for kw in (dict(flags=12), dict(flags=4), dict(flags=12, C_in=128, C_out=256, stride=2,
-                                                  T=150, T_out=75)):
+                                                  T=150, T_out=75),
+               dict(flags=2, V=25, K=3), dict(flags=2, V=50, K=3)):
         assert plan(**kw) & hl.PLAN_X_FROM_U, kw
     for kw in (dict(flags=12, training=0), dict(flags=28), dict(flags=12, C_in=3),
-               dict(flags=13), dict(flags=2, V=25, K=3), dict(flags=0)):
+               dict(flags=13), dict(flags=3, V=25, K=3), dict(flags=2, V=25, K=3, training=0),
+               dict(flags=0)):
         assert not plan(**kw) & hl.PLAN_X_FROM_U, kw
     one = ctypes.c_void_p(256)
     d = _desc(pkg, flags=0)  # exact fp32 MFMA: no X_FROM_U

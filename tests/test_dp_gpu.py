@@ -37,10 +37,10 @@ def test_dp_two_ranks_on_hip(tmp_path, world):
     print(res)
     assert res["bucket_views"] and res["buckets"] >= 2
     assert res["ranks_identical"]
+    # every gradient (dA included: deterministic partials) at 1e-6 of the mean
+    # of the per-shard gradients, and a re-run of a shard is bit-identical
     assert res["grad_err"] < 1e-6, res
-    # dA: within the run-to-run spread of the atomically accumulated dA of one
-    # shard (dp_gpu_worker.py measures it by re-running every shard), floor 1e-5
-    assert res["grad_err_A"] <= max(1e-5, 4 * res["dA_rerun_spread"]), res
+    assert res["rerun_exact"], res
     # overlap: at least one bucket's all-reduce is issued before block 0's
     # backward has produced a gradient (block 0 runs last in backward)
     assert res["first_launch_pos"] < res["first_block0_grad_pos"], res
