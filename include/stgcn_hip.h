@@ -330,7 +330,10 @@ int stgcn_block_plan(const stgcn_desc_t *d, uint32_t *plan);
  * stack instead of ~11 small launches per block. stgcn_fold_prep_bytes(d) is the
  * block's buffer size (0: the block does not fold); the buffer is then passed as
  * stgcn_fwd_args_t.prep / stgcn_bwd_args_t.prep of that block in the same step
- * (same weights). Blocks whose size is 0 are skipped. */
+ * (same weights). Blocks whose size is 0 are skipped. The block's backward also
+ * uses the buffer's fp64 scratch for its activation-dependent per-tap dU sums
+ * (the Tq re-layout): one prep buffer must not serve two backward passes that
+ * run concurrently (e.g. micro-batches on separate streams). */
 typedef struct stgcn_fold_weights {
   const float *A, *W, *bW, *Wt, *bWt;   /* as in stgcn_fwd_args_t            */
 } stgcn_fold_weights_t;

@@ -39,11 +39,14 @@ def main(path, steps=10):
         print(f"{v:8.3f} ms/step  {cnt[k] / steps:5.1f}x  {k}")
     # the last step's launches in order, with their durations
     last = rows[adam[-2] + 1: adam[-1] + 1]
-    print("\nlast step, in launch order (us):")
+    print("\nlast step, in launch order (us: duration, idle gap before the launch):")
+    prev_end = None
     for r in last:
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:90]
-        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        print(f"{d:9.1f}  {name}")
+        s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s0 - prev_end) / 1e3 if prev_end is not None else 0.0
+        prev_end = e0 if prev_end is None else max(prev_end, e0)
+        print(f"{(e0 - s0) / 1e3:9.1f} {gap:7.1f}  {name}")
 
 
 if __name__ == "__main__":

@@ -149,8 +149,9 @@ class FoldPrep:
     stgcn_fold_prep: every folded block's Wc, bias table, max |Wc|, packed
     forward / data-gradient weights and backward re-layouts in about a dozen
     launches for the whole stack, instead of ~11 small launches per block).
-    Buffers are cached per input shape and reused every step; a step's
-    forward and backward use the same weights, so they read the same buffers."""
+    One buffer per block, reused every step while (C, T, V) and the GEMM mode
+    stay the same; a step's forward and backward use the same weights, so they
+    read the same buffers."""
 
     def __init__(self):
         self._bufs = {}
@@ -166,11 +167,15 @@ class FoldPrep:
             nbytes = lib.stgcn_fold_prep_bytes(ctypes.byref(desc))
             buf = None
             if nbytes:
-                key = (i, tuple(x_shape), gemm, nbytes)
-                buf = self._bufs.get(key)
-                if buf is None or buf.device != dev:
+                # (the contents depend on the weights and (C, T, V) only: keyed
+                # without the batch, one buffer per block, replaced when the
+                # shape changes -- a ragged last batch reuses it)
+                key = (tuple(x_shape[1:]), gemm, nbytes, dev)
+                held = self._bufs.get(i)
+                buf = held[1] if held is not None and held[0] == key else None
+                if buf is None:
                     buf = torch.empty(nbytes, device=dev, dtype=torch.uint8)
-                    self._bufs[key] = buf
+                    self._bufs[i] = (key, buf)
                 descs.append(desc)
                 weights.append(hip_lib.FoldWeights(*[hip_lib.ptr(t) for t in (
                     sc.A, sc.W.weight, sc.W.bias, tc.weight, tc.bias)]))
