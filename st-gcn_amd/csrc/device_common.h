@@ -7,9 +7,6 @@
 
 #include "internal.h"
 
-#ifndef STGCN_EPI_EXP  // epilogue timing experiments only (results wrong), conv_tile_store_rows:
-#define STGCN_EPI_EXP 0  // bit 1 no BN statistics atomics, 2 no statistics at all, 4 no
-#endif                   // global stores, 8 no bias-table load, 16 no LDS image reads
 
 namespace stgcn {
 
@@ -358,7 +355,7 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
   const bool rok = row < p.R;
   const int ostride = p.T_dst * V;
   const int ncv = min(NCOLS, (p.M - m0) * V);  // valid columns of the tile
-  if (p.bias_rv && !(STGCN_EPI_EXP & 8)) {  // the tile's rows of the bias table, coalesced (uniform branch)
+  if (p.bias_rv) {  // the tile's rows of the bias table, coalesced (uniform branch)
     const int nrow = min(ROWS, p.R - r0);
     for (int i = tid; i < nrow * V; i += NT) sbv[i] = p.bias_rv[r0 * V + i];
     __syncthreads();
@@ -402,8 +399,7 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
     const int pc = q + k * TPR;
     if (pc >= NP) break;
     const int c0 = pc * 4;
-    const float4 a = (STGCN_EPI_EXP & 16) ? make_float4(br, br, 1.f, 2.f)
-                                          : *reinterpret_cast<const float4 *>(img + r * kEpiPitch + c0);
+    const float4 a = *reinterpret_cast<const float4 *>(img + r * kEpiPitch + c0);
     float v[4] = {a.x, a.y, a.z, a.w};
     const bool full = rok && c0 + 3 < ncv;
     float rv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -425,20 +421,18 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
       const int col = c0 + e;
       const bool ok = rok && col < ncv;
       float val = v[e] + br;
-      if (p.bias_rv && ok && !(STGCN_EPI_EXP & 8)) val += sbv[r * V + col % V];
+      if (p.bias_rv && ok) val += sbv[r * V + col % V];
       val += rv[e];
       if (p.relu_out) val = fmaxf(val, 0.f);
       if (p.drop.thresh && ok)
         val = dropout_keep(p.drop, (uint64_t)(obase + col)) ? val * p.drop.scale : 0.f;
       v[e] = val;
-      if (p.stat_sum && ok && !(STGCN_EPI_EXP & 2)) {
+      if (p.stat_sum && ok) {
         s += (double)val;
         sq += (double)val * (double)val;
       }
     }
-    if (STGCN_EPI_EXP & 4) {  // (keeps the values live without storing them)
-      if (v[0] == 1.2345e-30f && v[1] == v[2] + v[3]) p.out[threadIdx.x] = 0.f;
-    } else if (OB && p.out_bf16) {  // bf16 output: 8-byte pieces where the row allows
+    if (OB && p.out_bf16) {  // bf16 output: 8-byte pieces where the row allows
       __bf16 *ob = reinterpret_cast<__bf16 *>(p.out) + obase;
       const unsigned w0 = __builtin_bit_cast(unsigned short, (__bf16)v[0]) |
                           ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)v[1]) << 16);
@@ -465,7 +459,7 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
         if (c0 + e < ncv) out[c0 + e] = v[e];
     }
   }
-  if (p.stat_sum && !(STGCN_EPI_EXP & 2)) {  // per-row sums over the TPR adjacent lanes of the row
+  if (p.stat_sum) {  // per-row sums over the TPR adjacent lanes of the row
 #pragma unroll
     for (int o = 1; o < TPR; o <<= 1) {
       s += __shfl_xor(s, o, 64);
@@ -478,7 +472,7 @@ __device__ __forceinline__ void conv_tile_store_rows(const ConvGemmParams &p, co
         pt[0] = s;
         pt[(int64_t)p.R * nt] = sq;
       }
-    } else if (q == 0 && rok && !(STGCN_EPI_EXP & 1)) {
+    } else if (q == 0 && rok) {
       atomicAdd(p.stat_sum + row, s);
       atomicAdd(p.stat_sq + row, sq);
     }

@@ -2985,9 +2985,6 @@ __device__ __forceinline__ floatx16 bwd6_mfma(uint4 a, uint4 b, floatx16 c) {
                                                  __builtin_bit_cast(bwd6_bf8, b), c, 0, 0, 0);
 }
 
-#ifndef STGCN_BWD6_EXP  // timing experiments only (bits skip work; results wrong)
-#define STGCN_BWD6_EXP 0
-#endif
 // BF (STGCN_F_BF16 blocks): H and A to 2^-16 (h + m planes; the dropped terms
 // are below 2^-16 of each product), f(BN1(x)) of the dA GEMM to bf16: three
 // products for dx and two for dA instead of six each. (H to bf16 alone moved
@@ -3087,7 +3084,6 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
         if (k < K) {
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
-            if (STGCN_BWD6_EXP & 2) continue;
             const int v0 = 32 * kh + 16 * ks + 8 * hi;
             const float *hr = Hs + k * PL + (rt * 32 + lo) * V + v0;
             float av[8];
@@ -3119,7 +3115,7 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       }
     }
     __syncthreads();  // dx tile halves complete
-    if (!(STGCN_BWD6_EXP & 4)) {  // per row (8 threads each): dx = sum of halves, BN1 sums, BN1(x) in place (see bwd5)
+    {  // per row (8 threads each): dx = sum of halves, BN1 sums, BN1(x) in place (see bwd5)
       constexpr int TPR = NW * 64 / RB;
       const int rl = tid / TPR, part = tid % TPR;
       const int rem = rem0 + rl;
@@ -3185,7 +3181,6 @@ __global__ __launch_bounds__(512, 1) void k_spatial_bwd6(
       const int cv = p2 * 32 + lo, cw = q2 * 32 + lo;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        if (STGCN_BWD6_EXP & 1) continue;
         const int rb = kh * 32 + ks * 16 + 8 * hi;  // this lane's 8 rows
         uint4 bh = {0, 0, 0, 0}, bm = bh, bl = bh;
         if (cw < V) {
@@ -3818,8 +3813,10 @@ __global__ __launch_bounds__(256) void k_dA_reduce2(const double *__restrict__ l
   double s = 0.0;
   if (e < n) {
 #pragma unroll
-    for (int y = g; y < kDaLvl; y += 4)
+    for (int i = 0; i < kDaLvl / 4; ++i) {
+      const int y = g + 4 * i;
       if (y < ny) s += lvl[(int64_t)y * n + e];
+    }
   }
   sm[g][t] = s;
   __syncthreads();

@@ -103,9 +103,6 @@ __device__ __forceinline__ void spb_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-#ifndef STGCN_SPB_EXP  // timing experiments only (bits skip work; results wrong)
-#define STGCN_SPB_EXP 0
-#endif
 
 // (a, b) -> packed bf16 planes h, m, l (a == h + m + l exactly; kernels_x3.hip)
 __device__ __forceinline__ void spb_split3(float a, float b, unsigned &h, unsigned &m,
@@ -355,7 +352,6 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
       spb_barrier();  // chunk gch in LDS for every wave; chunk gch - 1 retired
       if (gch + D - 1 < nchunks) issue_chunk();
       const int slot = gch % D;
-      if (STGCN_SPB_EXP & 1) continue;
       // A operand: dZ[r = 8 hi + j][frame f, joint lo] (0 past V: read at a
       // clamped joint, then selected, so the 8 reads issue back to back); row
       // 8 hi + j starts (8 hi + j) * TV mod 4 = j * TV mod 4 floats into its LDS row
@@ -411,7 +407,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     }
 
     // ---- dx^T[w][ci] = sum_k sum_v A_k[v][w] H_k^T[v][ci] -> dx row image [ci][f*V + w]
-    if (!(STGCN_SPB_EXP & 2)) {
+    {
       floatx16 dxp[K][NACC];  // one chain per partition, summed at the end
 #pragma unroll
       for (int kk = 0; kk < K; ++kk)
@@ -458,7 +454,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
 
     // ---- row pass, 16 threads per channel: ReLU mask, BN1 sums, dx store, and
     // f(BN1(x)) into the dA operand image (row (frame, w), slot of ci; bf16 planes)
-    if (!(STGCN_SPB_EXP & 4)) {
+    {
       const int ci = tid >> 4, part = tid & 15;
       const int c = cb * G::CB + ci;
       const float mu = tab[c], is = tab[G::CMAX + c];
@@ -542,7 +538,7 @@ __global__ __launch_bounds__(512, 1) void k_sp_bwd_fused(SpBwdParams P) {
     if (k + 1 < myitems) issue_x(first + (k + 1) * NG);
 
     // ---- dA_k[v][w] += sum_ci H_k[ci][v] f(BN1(x))[ci][w] (this frame's 32 channels)
-    if (!(STGCN_SPB_EXP & 8)) {
+    {
       const int row = lo < V ? f * V + lo : G::NPOS;  // joints past V: the zero row
       const char *xb = lds + G::OFF_XB + row * G::XBP + hi * 16;
 #pragma unroll
@@ -682,9 +678,6 @@ __global__ void k_pack_spb_a(const float *A, __bf16 *img, int K, int V, int NP) 
 // W' with fp32 accumulation, H and A to 2^-16 (h + m planes, three products) in
 // dx, H to 2^-16 and f(BN1(x)) to bf16 (two products) in dA.
 // ---------------------------------------------------------------------------
-#ifndef STGCN_SP50_EXP  // timing experiments only (bits skip work; results wrong): 1 x
-#define STGCN_SP50_EXP 0  // loads, 2 dx stores, 4 dx / dA MFMAs, 8 chunk MFMAs
-#endif
 template <int K>
 struct Sp50Geo {
   static constexpr int V = 50, FT = 4, NPOS = FT * V;         // 200 positions per item
@@ -851,7 +844,6 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
     return ok ? (unsigned)(((int64_t)c * TV + (int64_t)t * 50 + w) * 4) : kOOB;
   };
   auto load_x = [&](int item) {
-    if (STGCN_SP50_EXP & 1) return;
     int n, ft, cbb;
     ring.decode(item, n, ft, cbb);
     const spb_i4 rx = spb_rsrc(P.x + (int64_t)n * P.C * TV, (int64_t)P.C * TV * 4);
@@ -874,7 +866,7 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
   int mark_x = 0;
   if (myitems > 0) {
     load_x(first);
-    issued += (STGCN_SP50_EXP & 1) ? 0 : 16;
+    issued += 16;
     mark_x = issued;
   }
 #pragma unroll
@@ -918,7 +910,6 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
 #pragma unroll
       for (int kk = 0; kk < K; ++kk) {
         const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
-        if (STGCN_SP50_EXP & 8) { T[kk][0][0] += __builtin_bit_cast(float, a0.x ^ w.y); T[kk][1][0] += __builtin_bit_cast(float, a1.x); continue; }
         T[kk][0] = spb_mfma(a0, w, T[kk][0]);  // [v][ci] = sum_r dZ[r][v] W_k[r][ci]
         T[kk][1] = spb_mfma(a1, w, T[kk][1]);
       }
@@ -941,7 +932,6 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
           const int fr = (((kk * 2 + wt) * 2 + vt) * 2 + ks) * 2;
           const uint4 am0 = *reinterpret_cast<const uint4 *>(aim + fr * 1024);
           const uint4 am1 = *reinterpret_cast<const uint4 *>(aim + (fr + 1) * 1024);
-          if (STGCN_SP50_EXP & 4) { dxa[ks] += __builtin_bit_cast(float, am0.x ^ am1.y ^ bpl[0].x ^ bpl[1].y); continue; }
           dxa = spb_mfma(am0, bpl[0], dxa);
           dxa = spb_mfma(am1, bpl[0], dxa);
           dxa = spb_mfma(am0, bpl[1], dxa);
@@ -982,7 +972,7 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
     dn += sn;
     d1 += s1;
     d2 += s2;
-    if (P.write_dx && !(STGCN_SP50_EXP & 2)) {  // (dx stores: masked positions go past the clip's resource)
+    if (P.write_dx) {  // (dx stores: masked positions go past the clip's resource)
       const spb_i4 rdx = spb_rsrc(P.dx + (int64_t)n * P.C * TV, (int64_t)P.C * TV * 4);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq)
@@ -998,7 +988,7 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dx(Sp50Params P) {
     }
     if (k + 1 < myitems) {
       load_x(item + NG);
-      issued += (STGCN_SP50_EXP & 1) ? 0 : 16;
+      issued += 16;
       mark_x = issued;
     }
   }
@@ -1052,7 +1042,6 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dA(Sp50Params P) {
     reinterpret_cast<unsigned *>(lds + G::L2_XB + G::NPOS * G::XBP)[e] = 0u;
   float xr[NQ];
   auto load_x = [&](int item) {
-    if (STGCN_SP50_EXP & 1) return;
     int n, ft, cbb;
     ring.decode(item, n, ft, cbb);
     const spb_i4 rx = spb_rsrc(P.x + (int64_t)n * P.C * TV, (int64_t)P.C * TV * 4);
@@ -1073,7 +1062,7 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dA(Sp50Params P) {
   int mark_x = 0;
   if (myitems > 0) {
     load_x(first);
-    issued += (STGCN_SP50_EXP & 1) ? 0 : NQ;
+    issued += NQ;
     mark_x = issued;
   }
 #pragma unroll
@@ -1124,7 +1113,6 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dA(Sp50Params P) {
 #pragma unroll
       for (int kk = 0; kk < K; ++kk) {
         const uint4 w = *reinterpret_cast<const uint4 *>(wb + kk * 1024);
-        if (STGCN_SP50_EXP & 8) { S[kk][0] += __builtin_bit_cast(float, w.x ^ bz.y); continue; }
         S[kk] = spb_mfma(w, bz, S[kk]);  // [ci][v] = sum_r W_k[r][ci] dZ[r][v]
       }
     }
@@ -1154,7 +1142,7 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dA(Sp50Params P) {
     spb_barrier();  // f(BN1(x)) image complete
     if (k + 1 < myitems) {
       load_x(item + NG);
-      issued += (STGCN_SP50_EXP & 1) ? 0 : NQ;
+      issued += NQ;
       mark_x = issued;
     }
     // ---- dA_k[v][w] += sum_ci H_k[ci][v] f(BN1(x))[ci][w], v in tile vt
@@ -1176,7 +1164,6 @@ __global__ __launch_bounds__(512, 1) void k_sp50_dA(Sp50Params P) {
         spb_planes<2>(sv, sp);
 #pragma unroll
         for (int wt = 0; wt < 2; ++wt) {
-          if (STGCN_SP50_EXP & 4) { dacc[kk][wt][ks] += __builtin_bit_cast(float, sp[0].x ^ sp[1].y ^ xv[wt].z); continue; }
           dacc[kk][wt] = spb_mfma(sp[0], xv[wt], dacc[kk][wt]);
           dacc[kk][wt] = spb_mfma(sp[1], xv[wt], dacc[kk][wt]);
         }

@@ -44,24 +44,8 @@
 #include "device_common.h"
 #include "internal.h"
 
-#ifndef STGCN_WG_WSTART  // k_wgrad_x3: first k-step carrying the next item's writes
-#define STGCN_WG_WSTART 1  // (>= KSTEPS: after the k-steps)
-#endif
-#ifndef STGCN_WG_EXP  // k_wgrad_x3 timing experiments only (results wrong): bit 1 no
-#define STGCN_WG_EXP 0  // staging, 2 no MFMAs, 4 no fragment reads, 8 no item barrier
-#endif
-#ifndef STGCN_X3_STAG  // k_conv_x3: waves 4-7 run each step's last tap after the next barrier
-#define STGCN_X3_STAG 1
-#endif
-#ifndef STGCN_X3_EXP  // timing experiments only (bits skip work; results wrong)
-#define STGCN_X3_EXP 0
-#endif
-#ifndef STGCN_SPB_EXP  // spb_epilogue timing experiments only (results wrong): bit 1 no dA
-#define STGCN_SPB_EXP 0  // partials / atomics, 2 no dxhat / BN1 pass, 4 no x DMA, 8 no BN1 /
-#endif                   // chain sum atomics, 16 no dxhat stores, 32 no dA atomics
-#ifndef STGCN_BNA_EXP  // bna timing experiments only (results wrong): bit 1 no epilogue
-#define STGCN_BNA_EXP 0  // contraction, 2 no loader BN1, 4 no table / bound setup
-#endif
+// k_wgrad_x3: first k-step carrying the next item's LDS writes (>= KSTEPS: after the k-steps)
+constexpr int kWgWriteStart = 1;
 
 namespace stgcn {
 
@@ -333,7 +317,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     __syncthreads();  // every wave is done with the main loop's buffers / the last half
     // (the x rows' DMA first: its latency runs under the H image and table writes)
     asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
-    for (int rr = wave; rr < 64 && !(STGCN_SPB_EXP & 4); rr += 8) {
+    for (int rr = wave; rr < 64; rr += 8) {
       const int c = r0 + h * 64 + rr;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -365,7 +349,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (!(STGCN_SPB_EXP & 2)) {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
+    {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
       f2v a6[V][3];  // A[v][6 jb + 2 j2 + {0, 1}] (joint pairs: packed FMA)
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
@@ -445,7 +429,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
 #pragma unroll
           for (int i = 0; i < 3; ++i)
             *reinterpret_cast<float2 *>(xr + 2 * i) = make_float2(xs[2 * i], xs[2 * i + 1]);
-          if (p.out && c < C && !(STGCN_SPB_EXP & 16)) {
+          if (p.out && c < C) {
             float *dst = p.out + ((int64_t)n * C + c) * cT +
                          (int64_t)(p.s_out * (m0 + f) + p.p_out) * V + jb * 6;
 #pragma unroll
@@ -465,7 +449,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
           s2 = red3(s2);
           s3 = red3(s3);
         }
-        if (ok && jb == 0 && !(STGCN_SPB_EXP & 8)) {
+        if (ok && jb == 0) {
           double *rs = rsum + (h * 64 + rr) * 4;
           if (need_s0) atomicAdd(rs, (double)s0);
           atomicAdd(rs + 1, (double)s1);
@@ -480,7 +464,6 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     // dA partials over this half's (row, frame) pairs: thread = (v block, w block,
     // 1 / 56 of the pairs); after the last half the partials meet in LDS (over
     // the H image) and each entry is summed over its 56 threads in a fixed order
-    if (STGCN_SPB_EXP & 1) continue;
     if (combo < 9) {
       // (a fixed 16 pairs per thread, unrolled so the LDS reads run ahead; frames
       // >= nvf add nothing: their x image columns are zero -- OOB DMA, no row pass)
@@ -510,7 +493,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
   }
   // the BN1 / chain sums: one fp64 atomic per row and statistic (rsum complete:
   // the barrier after the last row pass)
-  if (!(STGCN_SPB_EXP & 2) && !(STGCN_SPB_EXP & 8) && tid < MR * 64) {
+  if (tid < MR * 64) {
     const int c = r0 + tid;
     if (c < C) {
       const double *rs = rsum + tid * 4;
@@ -522,7 +505,6 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
       }
     }
   }
-  if (STGCN_SPB_EXP & 1) return;
   __syncthreads();  // the images are read
   constexpr int PP = 37;  // partial pitch (odd: conflict-free column reads)
   float *part = smem;
@@ -546,7 +528,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     const float sum = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     if (p.dA_part)  // (deterministic: launch_dA_reduce adds the partials in order)
       p.dA_part[(int64_t)blockIdx.x * (V * V) + tid] = sum;
-    else if (!(STGCN_SPB_EXP & 32))
+    else
       atomicAdd(p.dA + tid, sum);
   }
 }
@@ -721,7 +703,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   // issued, so the two latencies overlap; Cp <= 512 and kBnaAr <= 512: one
   // channel and one A element per thread)
   float t_mu = 0.f, t_a = 0.f, t_be = 0.f, t_ar = 0.f, t_bm = 0.f;
-  if constexpr (BNA && !(STGCN_BNA_EXP & 4)) {
+  if constexpr (BNA) {
     const float M = __builtin_bit_cast(float, amax_read(p.amax_in));
     if (tid < Cp) t_bm = bn1_bound(p, tid, M, t_mu, t_a, t_be);
     if (tid < kBnaAr) {
@@ -798,7 +780,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         float xv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) xv[j] = st[k][j];
-        if constexpr (BNA && !(STGCN_BNA_EXP & 2)) {  // BN1 of the item's 8 channels; 0 in padded frames
+        if constexpr (BNA) {  // BN1 of the item's 8 channels; 0 in padded frames
           const float *tb = btab + cch + ioct[k] * 8;
           float mu[8], a[8], be[8];
 #pragma unroll
@@ -914,33 +896,15 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         }
   };
 
-  // Stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): the two waves of
-  // a SIMD are wave w and w + 4 of this workgroup, and with one barrier per step
-  // they reach every step's wait, barrier and first fragment reads together while
-  // the matrix pipe idles. Waves 4-7 therefore run each step's LAST tap of MFMAs
-  // after the next step's barrier, beside that step's first fragment reads: their
-  // partner's exposed reads after the barrier are covered by these MFMAs, and
-  // their own wait at the barrier by the partner's last tap. Only register-held
-  // fragments cross the barrier (every LDS read of step s still happens between
-  // barriers s and s + 1), so the buffer hand-offs are unchanged, and every
-  // accumulator sees the same MFMAs in the same order (bit-identical results).
-  // (not where the fragments held across the window staging push the kernel
-  // past its register budget: the 128-row stride-2 forward spills, and the
-  // 64-row bf16 V = 50 stride-2 forward would lose its second workgroup per CU)
-  constexpr bool kStag = STGCN_X3_STAG && (NPL == 2   ? !(MR == 2 && SIN == 2)
-                                           : NPL == 3 ? MR == 1
-                                                      : !(V == 50 && SIN == 2));
-  const bool stag = kStag && half == 1;  // (wave-uniform)
-  // MR = 1: fragment sets in flight, tap qq of a step in f[qq % NF]; the deferred
-  // last tap must not share a set with the next step's tap 0
-  constexpr int NF = MR == 1 ? (kStag && TG % 2 == 1 ? 3 : 2) : 1;
-  static_assert(!kStag || MR != 1 || (TG > 1 && (TG - 1) % NF != 0), "deferred tap's fragment set");
+  // MR = 1: two fragment sets (tap qq of a step in f[qq % 2]); MR = 2: one,
+  // refilled in place (tap2)
+  constexpr int NF = MR == 1 ? 2 : 1;
   Frag f[NF];
 #pragma unroll
   for (int d = 0; d < G::PD; ++d)
     if (d < nsteps) dma_w(d, d);
   load_img(0);
-  if constexpr (BNA && !(STGCN_BNA_EXP & 4)) {  // the BN1 table, A's rows, the operand bound
+  if constexpr (BNA) {  // the BN1 table, A's rows, the operand bound
     if (tid < Cp) {
       btab[tid] = t_mu;
       btab[Cp + tid] = t_a;
@@ -957,7 +921,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   constexpr int NI1 = NR1 < NM1 ? NR1 : NM1;
   auto mm_ld1 = [&](const Frag &fm, const char *wl, const char *wn, int ql, int qn, Frag &fl) {
     ld(wl, wn, ql, qn, fl);
-    if (!(STGCN_X3_EXP & 16)) mm(fm);
+    mm(fm);
 #pragma unroll
     for (int i = 0; i < NI1; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -973,7 +937,6 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   // fragment, which are the last ones refilled. tap2(nx, wl, wn, ql, qn): the
   // MFMAs of the tap in f[0], refilled (nx) with tap ql / window frame qn
   auto grp = [&](int pa, int pb) {
-    if (STGCN_X3_EXP & 16) return;
     Frag &fr = f[0];
 #pragma unroll
     for (int rb = 0; rb < MR; ++rb)
@@ -1036,7 +999,6 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  constexpr int FL = (TG - 1) % NF;  // MR = 1: the last tap's fragment set
 
   wait_img<0>(st);
   write_img(win0, 0);
@@ -1053,56 +1015,35 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::wait_n(g)) : "memory");
       else  // a tile's last steps: fewer weight steps were issued after DMA(s)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!(STGCN_X3_EXP & 8)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       const char *wa = wbuf0 + (s % G::NWB) * G::WST + ao;
-      // tap 0's fragment reads; a staggered wave runs the previous step's last
-      // tap beside them
-      const bool defer = stag && s > 0;
-      if constexpr (MR == 1) {
-        if (defer)
-          mm_ld1(f[FL], wa, win, 0, g * TG, f[0]);
-        else
-          ld(wa, win, 0, g * TG, f[0]);
-      } else {
-        if (defer) {
-          tap2(true, wa, win, 0, g * TG);
-        } else {
-          ld(wa, win, 0, g * TG, f[0]);
-        }
-      }
+      ld(wa, win, 0, g * TG, f[0]);  // tap 0's fragment reads
       // next step's weights and (first step) chunk c+1's window, issued after
       // this step's first fragment reads (a compiler wait placed before those
       // reads then finds no load of ours in flight). The window load is
       // unconditional: chunk == nchunks loads zeros and is never read.
-      if (!(STGCN_X3_EXP & 2) && s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
-      if (!(STGCN_X3_EXP & 4) && g == 0) load_img(c + 1);
+      if (s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
+      if (g == 0) load_img(c + 1);
 #pragma unroll
       for (int qq = 0; qq < TG; ++qq) {
         const bool nx = qq + 1 < TG;
         if constexpr (MR == 1) {
           if (nx)  // tap qq+1's fragment reads among tap qq's MFMAs
             mm_ld1(f[qq % NF], wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) % NF]);
-          else if (!stag && !(STGCN_X3_EXP & 16))
+          else
             mm(f[qq % NF]);
           __builtin_amdgcn_sched_barrier(0);
         } else {
-          if (nx || !stag) tap2(nx, wa, win, qq + 1, g * TG + qq + 1);
+          tap2(nx, wa, win, qq + 1, g * TG + qq + 1);
         }
       }
-      if (!(STGCN_X3_EXP & 1) && g == G::NG - 1) {
+      if (g == G::NG - 1) {
         // issued after the loads (step g = 0): the weight pieces of steps 1..NG-1
         wait_img<(G::NG - 1) * G::DPWMIN>(st);
         if (G::NWIN == 1)  // single window: every wave is done reading chunk c's
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         write_img(win0 + (G::NWIN == 2 ? ((c + 1) & 1) * G::IMG : 0), c + 1);
       }
-    }
-  }
-  if (stag) {  // the tile's last tap (register operands only)
-    if constexpr (MR == 1) {
-      if (!(STGCN_X3_EXP & 16)) mm(f[FL]);
-    } else {
-      tap2(false, wbuf0, win0, 0, 0);
     }
   }
   if constexpr (NPL == 3) {
@@ -1112,10 +1053,6 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
     const float ia = pow2f(-in_se), iw = pow2f(-f16x2_se(p.amax_w));
 #pragma unroll
     for (int j = 0; j < 2 * MR; ++j) acc[j] = (kOneAcc ? acc[j] : acc[j] + acl[j]) * ia * iw;
-  }
-  if (STGCN_X3_EXP & 64) {  // timing experiment: no epilogue (one store keeps the loop live)
-    if (acc[0][0] == 12345.f) p.out[tid] = acc[0][1] + acc[1][2];
-    return;
   }
   if constexpr (SPB) {
     static_assert(V == 18 && SIN == 1 && NPL >= 2, "the folded block's data gradient");
@@ -1132,7 +1069,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
       for (int j = 0; j < 2; ++j)
         acc_to_img(smem, acc[rb * 2 + j], mi * 32 * MR + rb * 32, (nj0 + j) * 32);
     __syncthreads();
-    if constexpr (BNA && !(STGCN_BNA_EXP & 1)) {  // U' -> U = A U' per (row, frame), in place
+    if constexpr (BNA) {  // U' -> U = A U' per (row, frame), in place
       bna_contract<G::ROWS>(smem, arow);
       __syncthreads();
     }
@@ -1776,36 +1713,23 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
         for (int t = 0; t < NT; ++t) acl[t] = mfma_x(f.a[0][2 % NPL], f.b[0][t], acl[t]);
       }
     };
-    // Stagger (as in k_conv_x3): waves 4-7 (all NT = 2) run each item's last
-    // k-step of MFMAs after the item barrier, beside the next item's first
-    // fragment reads, so the two waves of a SIMD (w, w + 4) do not wait at the
-    // barrier and on the first reads together. Only registers cross the barrier.
-    // (not with BN1 staging: it pushes the kernel past its register budget)
-    const bool stag = STGCN_X3_STAG && !QBN && NT == 2 && wave >= 4;  // (wave-uniform)
-    // fragment sets: k-step s in f[s % NF]; the deferred last k-step must not
-    // share a set with the next item's first
-    constexpr int NF = NT == 2 && STGCN_X3_STAG && !QBN ? 3 : 2;
-    constexpr int FL = (G::KSTEPS - 1) % NF;
-    static_assert(NF == 2 || FL != 0, "deferred k-step's fragment set");
-    Frag f[NF];
+    Frag f[2];
     for (int it = it0; it < it1; ++it) {
       const char *cur = lds + (G::NBUF == 2 ? ((it - it0) & 1) * G::BUF : 0);
       char *nxt = lds + (G::NBUF == 2 ? ((it - it0 + 1) & 1) * G::BUF : 0);
       // next item (the last iteration reloads its own item into the idle buffer:
       // unconditional, so no register copies across the loop)
-      if (!(STGCN_WG_EXP & 1)) load_item(it + 1 < it1 ? it + 1 : it);
+      load_item(it + 1 < it1 ? it + 1 : it);
       ld(cur, 0, f[0]);
-      if (stag && it > it0 && !(STGCN_WG_EXP & 2)) mm(f[FL]);  // the previous item's last k-step
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < G::KSTEPS; ++s) {
-        if (!(STGCN_WG_EXP & 4) && s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) % NF]);
-        if (!(STGCN_WG_EXP & 2) && (s + 1 < G::KSTEPS || !stag)) mm(f[s % NF]);
-        if constexpr (G::NBUF == 2 && STGCN_WG_WSTART < G::KSTEPS && !(STGCN_WG_EXP & 1)) {
+        if (s + 1 < G::KSTEPS) ld(cur, s + 1, f[(s + 1) & 1]);
+        mm(f[s & 1]);
+        if constexpr (G::NBUF == 2 && kWgWriteStart < G::KSTEPS) {
           // double buffer: the next item's split + LDS writes ride in the MFMA
           // shadow of k-steps WSTART.. (the loads were issued at the item start)
           using std::integral_constant;
-          constexpr int W0 = STGCN_WG_WSTART, NP = G::KSTEPS - W0, Q = G::GPT;
+          constexpr int W0 = kWgWriteStart, NP = G::KSTEPS - W0, Q = G::GPT;
           static_assert(W0 >= 1 && NP >= 1 && NP <= 4, "write parts");
           if (s == W0)
             write_part(nxt, integral_constant<int, 0>{}, integral_constant<int, Q / NP>{});
@@ -1822,13 +1746,11 @@ __global__ __launch_bounds__(512, 1) void k_wgrad_x3(WgradParams p) {
       if constexpr (G::NBUF == 1) {
         __syncthreads();  // every wave is done reading the buffer
         write_item(nxt);
-      } else if constexpr (STGCN_WG_WSTART >= G::KSTEPS && !(STGCN_WG_EXP & 1)) {
+      } else if constexpr (kWgWriteStart >= G::KSTEPS) {
         write_item(nxt);
       }
-      if (STGCN_WG_EXP & 8) continue;  // (no barrier: timing experiment only)
       __syncthreads();
     }
-    if (stag && it0 < it1 && !(STGCN_WG_EXP & 2)) mm(f[FL]);  // the last item's last k-step
     // the tile [ROWS][CB channels][9 taps] through LDS (the staging buffers are
     // free after the last item's barrier), then whole 16-byte pieces of each
     // row's CB * 9 contiguous slab floats: 4-byte stores at a 36-byte stride
