@@ -199,10 +199,17 @@ struct ConvX3Geo {
   // among the PD steps before s (fewer before that: the wait is conservative).
   // In a tile's last PD-1 steps fewer weight steps follow: the kernel waits
   // for everything there (vmcnt(0)).
+  // A step's weight DMA pieces and (chunk start) window loads are issued tap by
+  // tap (tap q: DMA pieces i with i % TG == q, then window loads [img_lo(q),
+  // img_lo(q + 1)) of the IPT * 8), not as one burst after the barrier (+0.5%
+  // cfg2 step, profiles/r6k_bench_spread_ab.txt)
+  static constexpr int img_lo(int q) { return q * IPT * 8 / TG; }
+  // window loads issued after a step's last DMA piece (that of tap min(DPW, TG) - 1)
+  static constexpr int img_tail() { return IPT * 8 - img_lo((DPW < TG ? DPW : TG) - 1); }
   static constexpr int wait_n(int g) {
     int n = (PD - 1) * DPWMIN;
     for (int k = 1; k <= PD; ++k)
-      if (((g - k) % NG + NG) % NG == 0) n += IPT * 8;
+      if (((g - k) % NG + NG) % NG == 0) n += k == PD ? img_tail() : IPT * 8;
     return n;
   }
   static_assert(NQ % TG == 0, "whole tap groups");
@@ -725,7 +732,8 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   float in_scale = pow2f(in_se);
   if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid < kAmaxSlots)  // (slot 0: the bound)
     p.amax_keep[tid * kAmaxStride] = tid == 0 ? amax_read(p.amax_in) : 0u;
-  auto load_img = [&](int chunk) {
+  // window loads [e0, e1) of the IPT * 8 (item k, channel j: e = 8 k + j)
+  auto load_img_part = [&](int chunk, int e0, int e1) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
     const int esz = inb ? 2 : 4;
     const int64_t rem = (int64_t)(p.C - chunk * G::CK) * cstride * esz;
@@ -739,22 +747,25 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
       for (int k = 0; k < G::IPT; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          asm volatile("buffer_load_ushort %0, %1, %2, 0 offen"
-                       : "=v"(st[k][j])
-                       : "v"(voff[k] == kOOB ? kOOB : (voff[k] >> 1) + (unsigned)(j * cstride * 2)),
-                         "s"(rs)
-                       : "memory");
+          if (8 * k + j >= e0 && 8 * k + j < e1)
+            asm volatile("buffer_load_ushort %0, %1, %2, 0 offen"
+                         : "=v"(st[k][j])
+                         : "v"(voff[k] == kOOB ? kOOB : (voff[k] >> 1) + (unsigned)(j * cstride * 2)),
+                           "s"(rs)
+                         : "memory");
     } else {
 #pragma unroll
       for (int k = 0; k < G::IPT; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
-                       : "=v"(st[k][j])
-                       : "v"(voff[k] + (unsigned)(j * cstride * 4)), "s"(rs)
-                       : "memory");
+          if (8 * k + j >= e0 && 8 * k + j < e1)
+            asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                         : "=v"(st[k][j])
+                         : "v"(voff[k] + (unsigned)(j * cstride * 4)), "s"(rs)
+                         : "memory");
     }
   };
+  auto load_img = [&](int chunk) { load_img_part(chunk, 0, G::IPT * 8); };
   auto write_img = [&](char *win, int chunk) {
     // (BNA: chunk nchunks is the pipeline's zero tail, never read: any table row)
     const int cch = min(chunk, nchunks - 1) * G::CK;
@@ -822,11 +833,12 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   const int4v rsw = {(int)(uint32_t)wsrc, (int)((wsrc >> 32) & 0xffff), nsteps * G::WST,
                      0x00020000};
   const unsigned lds0 = (unsigned)reinterpret_cast<uintptr_t>(wbuf0);
-  auto dma_w = [&](int step, int buf) {
+  // (qq >= 0: only the pieces i % TG == qq, issued with tap qq)
+  auto dma_w = [&](int step, int buf, int qq = -1) {
 #pragma unroll
     for (int i = 0; i < G::DPW; ++i) {
       const int d = i * NW + wave;
-      if (d < G::WDMA) {
+      if (d < G::WDMA && (qq < 0 || i % TG == qq)) {
         const unsigned voffw = (unsigned)(step * G::WST + d * 1024 + lane * 16);
         const unsigned m0v = lds0 + (unsigned)(buf * G::WST + d * 1024);
         unsigned keep;
@@ -1018,15 +1030,17 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       const char *wa = wbuf0 + (s % G::NWB) * G::WST + ao;
       ld(wa, win, 0, g * TG, f[0]);  // tap 0's fragment reads
-      // next step's weights and (first step) chunk c+1's window, issued after
-      // this step's first fragment reads (a compiler wait placed before those
-      // reads then finds no load of ours in flight). The window load is
-      // unconditional: chunk == nchunks loads zeros and is never read.
-      if (s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB);
-      if (g == 0) load_img(c + 1);
+      // (VMEM issue after this step's first fragment reads: a compiler wait
+      // placed before those reads then finds no load of ours in flight)
 #pragma unroll
       for (int qq = 0; qq < TG; ++qq) {
         const bool nx = qq + 1 < TG;
+        // this tap's share of the step's VMEM issue: the next weights' DMA
+        // pieces and (first step) chunk c+1's window loads (unconditional:
+        // chunk == nchunks loads zeros and is never read)
+        if (s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB, qq);
+        if (g == 0) load_img_part(c + 1, G::img_lo(qq), G::img_lo(qq + 1));
+        __builtin_amdgcn_sched_barrier(0);
         if constexpr (MR == 1) {
           if (nx)  // tap qq+1's fragment reads among tap qq's MFMAs
             mm_ld1(f[qq % NF], wa, win, qq + 1, g * TG + qq + 1, f[(qq + 1) % NF]);
