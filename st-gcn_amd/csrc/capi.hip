@@ -1169,13 +1169,11 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
                 "prev_sums, x_stats, dx_coef, dx_deferred)");
 
   HIP_TRY(hipMemsetAsync(workspace, 0, L.dbl_bytes, s));
-  // (Tq's fp64 re-layout goes straight into launch_fold_sdz's scratch)
+  // (Tq's fp64 re-layout goes straight into launch_fold_sdz's scratch slot in
+  // this call's workspace -- never into the prep buffer, which holds only the
+  // step's weight-only operands and may be shared by concurrent backwards)
   double *tqT = nullptr;
-  if (cols_sums(d))
-    tqT = fold_sdz_tq_slot(fold_spb(d) && a->prep && prep_applies(d)
-                               ? prep_layout(d, a->prep).f64
-                               : L.f64scr,
-                           R, C);
+  if (cols_sums(d)) tqT = fold_sdz_tq_slot(L.f64scr, R, C);
   if (!res) {
     // ReLU + BN2 backward -> dU, dgamma2, dbeta2, d(temporal bias); the
     // reduction comes from the next block when it was chained (dy_sums)
@@ -1265,7 +1263,7 @@ int stgcn_block_bwd(const stgcn_desc_t *d, const stgcn_bwd_args_t *a, void *work
     }
     if (fold_spb(d)) {  // dbW and the bias part of dA first: the data gradient adds to dA;
       // BN1's sd from the dU sums (fp64, exact against the cancellation in sum dxhat)
-      HIP_TRY(launch_fold_sdz(f64scr, a->Wt, Wc, L.ftq, R, C, V, L.SdZ, L.SdH, s, pre));
+      HIP_TRY(launch_fold_sdz(f64scr, a->Wt, Wc, L.ftq, R, C, V, L.SdZ, L.SdH, s, pre, tqT));
       HIP_TRY(launch_fold_small_sd(L.SdZ, a->A, a->bW, R, V, a->dbW, a->dA, L.SdH, C, L.sd, s));
     }
     if (f16x2_dgrad(d) && !pre)  // the fp16 splits' operand scales: max |dU| (apply pass), max |Wc|

@@ -173,10 +173,13 @@ hipError_t launch_fold_tq(const double *cs, int nz, int R, int T, int To, int V,
                           double *Tq, double *tqT, hipStream_t s);
 double *fold_sdz_tq_slot(double *scratch, int R, int C);
 // SdZ = sum_{n,t} dZ and (Wc, SdH non-null) SdH = sum_{n,t} H from Tq, fp64
-// (pre: the scratch already holds the Wt / Wc re-layouts, launch_fold_prep)
+// (pre: the scratch already holds the Wt / Wc re-layouts, launch_fold_prep;
+// tqT: where launch_fold_tq wrote Tq's re-layout, default the scratch's slot --
+// with pre the caller's own workspace, so the shared weight-only prep buffer
+// never holds step data)
 hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
                            int R, int C, int V, double *SdZ, double *SdH, hipStream_t s,
-                           bool pre = false);
+                           bool pre = false, const double *tqT = nullptr);
 // BN1's sd (db1) of the folded block from SdH: sd[c] = sum_v SdH[c][v] rowsum(A)[v]
 // launch_spatial_small (K = 1) and BN1's sd of the folded block (from SdH) in one launch
 hipError_t launch_fold_small_sd(const double *SdZ, const float *A, const float *bW, int R, int V,

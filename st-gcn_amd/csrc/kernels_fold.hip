@@ -258,7 +258,17 @@ __global__ __launch_bounds__(576) void k_fold_tr(TrJobs js) {
     } else {
       const float *p = reinterpret_cast<const float *>(g.src) + at;
       int k = 0;
-      for (; k + 4 <= g.S; k += 4) {  // (four loads in flight, summed in slab order)
+      // (sixteen loads in flight, summed in slab order: at S = 128 slabs -- the
+      // 64-channel blocks' weight gradient -- four in flight left the launch
+      // waiting 32 load latencies)
+      for (; k + 16 <= g.S; k += 16) {
+        float a[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) a[u] = p[(int64_t)(k + u) * g.sstride];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v += a[u];
+      }
+      for (; k + 4 <= g.S; k += 4) {
         const float a0 = p[k * g.sstride], a1 = p[(k + 1) * g.sstride],
                     a2 = p[(k + 2) * g.sstride], a3 = p[(k + 3) * g.sstride];
         v += a0;
@@ -682,9 +692,11 @@ size_t fold_sdz_scratch_doubles(int R, int C, int V) {
 
 // SdZ (and, with Wc, SdH); Wt [R][R][9], Wc [R][C][9] (o, c, q), Tq [9][R][V]
 hipError_t launch_fold_sdz(double *scratch, const float *Wt, const float *Wc, const double *Tq,
-                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s, bool pre) {
+                           int R, int C, int V, double *SdZ, double *SdH, hipStream_t s, bool pre,
+                           const double *tq_re) {
   const int Rp = pad32(R), Cp = pad32(C), Vp = pad32(V);
-  double *wtT = scratch, *wcT = wtT + (size_t)9 * Rp * Rp, *tqT = wcT + (size_t)9 * Cp * Rp;
+  double *wtT = scratch, *wcT = wtT + (size_t)9 * Rp * Rp;
+  const double *tqT = tq_re ? tq_re : wcT + (size_t)9 * Cp * Rp;
   const TrJob jt = tr_job(Wt, 0, 1, 0, 9, 1, (int64_t)R * 9, 9, R, R, nullptr, nullptr, nullptr, wtT);
   (void)Tq;  // (its re-layout tqT [q][Vp][Rp]: written by k_fold_tq, fold_sdz_tq_slot)
   if (pre) {

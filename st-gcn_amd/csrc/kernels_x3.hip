@@ -250,10 +250,13 @@ constexpr int kSpbPitch = 272;
 constexpr int kSpbRowTab = 2 * 64 * 8;  // per-row parameters [MR * 64][8] (MR <= 2)
 constexpr int kSpbLds = (2 * 64 * kSpbPitch + kSpbAt + kSpbRowTab) * 4 + 2 * 64 * 4 * 8;
 
+// MR = 1: the tile's x rows were loaded into registers during the main loop's
+// last chunk (xpre[4 i + k]: row wave + 8 i, compacted column k * 64 + lane --
+// the LDS-DMA pattern below), so only their LDS writes remain here
 template <int MR>
 __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (&acc)[4],
                                              float *smem, int n, int r0, int m0, int mi,
-                                             int nj0) {
+                                             int nj0, const float *xpre) {
   constexpr int V = 18, FT = kTileCols / V, NCOLS = FT * V, P = kSpbPitch;
   constexpr int NSUB = 56;   // threads per (v block, w block) combination of dA
   constexpr int NSLOT = 21;  // row-pass items per wave (lanes 3 s + jb; lane 63 idle)
@@ -324,7 +327,7 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
     __syncthreads();  // every wave is done with the main loop's buffers / the last half
     // (the x rows' DMA first: its latency runs under the H image and table writes)
     asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
-    for (int rr = wave; rr < 64; rr += 8) {
+    for (int rr = wave; rr < (MR == 1 ? 0 : 64); rr += 8) {
       const int c = r0 + h * 64 + rr;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -355,6 +358,12 @@ __device__ __forceinline__ void spb_epilogue(const ConvGemmParams &p, floatx16 (
       for (int i = tid; i < MR * 64 * 4; i += 512) rsum[i] = 0.0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (MR == 1) {  // the prefetched x rows (landed: vmcnt(0) above)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Ximg[(wave + 8 * i) * P + k * 64 + lane] = xpre[4 * i + k];
+    }
     __syncthreads();
     {  // dxhat, BN1(x) in place, the BN1 / chain sums, dxhat stores
       f2v a6[V][3];  // A[v][6 jb + 2 j2 + {0, 1}] (joint pairs: packed FMA)
@@ -733,7 +742,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   if (NPL == 2 && p.amax_keep && blockIdx.x == 0 && tid < kAmaxSlots)  // (slot 0: the bound)
     p.amax_keep[tid * kAmaxStride] = tid == 0 ? amax_read(p.amax_in) : 0u;
   // window loads [e0, e1) of the IPT * 8 (item k, channel j: e = 8 k + j)
-  auto load_img_part = [&](int chunk, int e0, int e1) {
+  auto load_img_part = [&](int chunk, int e0, int e1, float (&sx)[G::IPT][8]) {
     // chunk == nchunks (the pipeline's tail) has no channels: every load is OOB -> 0
     const int esz = inb ? 2 : 4;
     const int64_t rem = (int64_t)(p.C - chunk * G::CK) * cstride * esz;
@@ -749,7 +758,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         for (int j = 0; j < 8; ++j)
           if (8 * k + j >= e0 && 8 * k + j < e1)
             asm volatile("buffer_load_ushort %0, %1, %2, 0 offen"
-                         : "=v"(st[k][j])
+                         : "=v"(sx[k][j])
                          : "v"(voff[k] == kOOB ? kOOB : (voff[k] >> 1) + (unsigned)(j * cstride * 2)),
                            "s"(rs)
                          : "memory");
@@ -760,13 +769,48 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         for (int j = 0; j < 8; ++j)
           if (8 * k + j >= e0 && 8 * k + j < e1)
             asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
-                         : "=v"(st[k][j])
+                         : "=v"(sx[k][j])
                          : "v"(voff[k] + (unsigned)(j * cstride * 4)), "s"(rs)
                          : "memory");
     }
   };
-  auto load_img = [&](int chunk) { load_img_part(chunk, 0, G::IPT * 8); };
-  auto write_img = [&](char *win, int chunk) {
+  auto load_img = [&](int chunk) { load_img_part(chunk, 0, G::IPT * 8, st); };
+  // SPB, MR = 1 (XPF): the epilogue's 64 x rows (its LDS-DMA pattern: row
+  // wave + 8 i, compacted column k * 64 + lane, 0 outside the tile) loaded into
+  // registers in place of the last chunk's (never read) zero window, so their
+  // HBM latency runs under the last chunk's MFMAs instead of the epilogue
+  constexpr bool XPF = SPB && MR == 1;
+  constexpr int NXP = XPF ? 32 : 1;
+  float xpre[NXP];
+#pragma unroll
+  for (int i = 0; i < NXP; ++i) xpre[i] = 0.f;
+  auto load_x_part = [&](int e0, int e1) {
+    if constexpr (XPF) {
+      const int Cx = p.R, T = p.T_dst;
+      const int64_t cT = (int64_t)T * V;
+      const uint64_t xsrc = reinterpret_cast<uint64_t>(p.sx + (int64_t)n * Cx * cT);
+      const int64_t xbytes = (int64_t)Cx * cT * 4;
+      const int4v rsx = {(int)(uint32_t)xsrc, (int)((xsrc >> 32) & 0xffff),
+                         (int)(xbytes > 0x7fffffff ? 0x7fffffff : xbytes), 0x00020000};
+      const int nvf = min(G::FT, p.M - m0);
+      asm volatile("s_nop 4" ::: "memory");  // descriptor SGPRs -> buffer_load
+#pragma unroll
+      for (int e = 0; e < 32; ++e)
+        if (e >= e0 && e < e1) {
+          const int i = e >> 2, k = e & 3;
+          const int j = k * 64 + lane, mf = j / V, w = j - mf * V;
+          const int t = p.s_out * (m0 + mf) + p.p_out;
+          const int c = r0 + wave + 8 * i;
+          const bool ok = j < G::NCOLS && mf < nvf && t < T && c < Cx;
+          const unsigned voff = ok ? ((unsigned)(c * cT) + (unsigned)(t * V + w)) * 4u : kOOB;
+          asm volatile("buffer_load_dword %0, %1, %2, 0 offen"
+                       : "=v"(xpre[e])
+                       : "v"(voff), "s"(rsx)
+                       : "memory");
+        }
+    }
+  };
+  auto write_img = [&](char *win, int chunk, float (&sx)[G::IPT][8]) {
     // (BNA: chunk nchunks is the pipeline's zero tail, never read: any table row)
     const int cch = min(chunk, nchunks - 1) * G::CK;
 #pragma unroll
@@ -774,23 +818,23 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
       if (NPL == 1 && loff[k] >= 0) {  // bf16 operands: one rounded plane
         uint4 h;
         if constexpr (inb) {  // already bf16 (zero-extended shorts)
-          const auto u = [&](int j) { return __builtin_bit_cast(unsigned, st[k][j]); };
+          const auto u = [&](int j) { return __builtin_bit_cast(unsigned, sx[k][j]); };
           h.x = u(0) | (u(1) << 16);
           h.y = u(2) | (u(3) << 16);
           h.z = u(4) | (u(5) << 16);
           h.w = u(6) | (u(7) << 16);
         } else {
-          h.x = pk2(st[k][0], st[k][1]);
-          h.y = pk2(st[k][2], st[k][3]);
-          h.z = pk2(st[k][4], st[k][5]);
-          h.w = pk2(st[k][6], st[k][7]);
+          h.x = pk2(sx[k][0], sx[k][1]);
+          h.y = pk2(sx[k][2], sx[k][3]);
+          h.z = pk2(sx[k][4], sx[k][5]);
+          h.w = pk2(sx[k][6], sx[k][7]);
         }
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
       } else if (NPL == 2 && loff[k] >= 0) {  // fp16 (h, l) planes of the scaled input
         const float sc = in_scale;
         float xv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = st[k][j];
+        for (int j = 0; j < 8; ++j) xv[j] = sx[k][j];
         if constexpr (BNA) {  // BN1 of the item's 8 channels; 0 in padded frames
           const float *tb = btab + cch + ioct[k] * 8;
           float mu[8], a[8], be[8];
@@ -816,10 +860,10 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         *reinterpret_cast<uint4 *>(win + loff[k] + 32) = l;
       } else if (loff[k] >= 0) {
         uint4 h, m, l;
-        split2(st[k][0], st[k][1], h.x, m.x, l.x);
-        split2(st[k][2], st[k][3], h.y, m.y, l.y);
-        split2(st[k][4], st[k][5], h.z, m.z, l.z);
-        split2(st[k][6], st[k][7], h.w, m.w, l.w);
+        split2(sx[k][0], sx[k][1], h.x, m.x, l.x);
+        split2(sx[k][2], sx[k][3], h.y, m.y, l.y);
+        split2(sx[k][4], sx[k][5], h.z, m.z, l.z);
+        split2(sx[k][6], sx[k][7], h.w, m.w, l.w);
         *reinterpret_cast<uint4 *>(win + loff[k]) = h;
         *reinterpret_cast<uint4 *>(win + loff[k] + 32) = m;
         *reinterpret_cast<uint4 *>(win + loff[k] + 64) = l;
@@ -1013,7 +1057,7 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   };
 
   wait_img<0>(st);
-  write_img(win0, 0);
+  write_img(win0, 0, st);
   for (int c = 0; c < nchunks; ++c) {
     const char *win = win0 + (G::NWIN == 2 ? (c & 1) * G::IMG : 0);
 #pragma unroll
@@ -1023,7 +1067,10 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
       // steps earlier; later pieces and window loads stay in flight), then the
       // barrier publishes them and chunk c's window (written in the previous
       // chunk's last step)
-      if (s + G::PD - 1 < nsteps)
+      if (XPF && c + 1 == nchunks && s + G::PD - 1 < nsteps)  // (32 x loads, not IPT * 8)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::wait_n(g) + (g >= 1 ? 32 - G::IPT * 8 : 0))
+                     : "memory");
+      else if (s + G::PD - 1 < nsteps)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::wait_n(g)) : "memory");
       else  // a tile's last steps: fewer weight steps were issued after DMA(s)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1037,9 +1084,15 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
         const bool nx = qq + 1 < TG;
         // this tap's share of the step's VMEM issue: the next weights' DMA
         // pieces and (first step) chunk c+1's window loads (unconditional:
-        // chunk == nchunks loads zeros and is never read)
+        // chunk == nchunks loads zeros and is never read; XPF loads the
+        // epilogue's x rows in its place)
         if (s + G::PD < nsteps) dma_w(s + G::PD, (s + G::PD) % G::NWB, qq);
-        if (g == 0) load_img_part(c + 1, G::img_lo(qq), G::img_lo(qq + 1));
+        if (g == 0) {
+          if (XPF && c + 1 == nchunks)
+            load_x_part(qq * 32 / TG, (qq + 1) * 32 / TG);
+          else
+            load_img_part(c + 1, G::img_lo(qq), G::img_lo(qq + 1), st);
+        }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (MR == 1) {
           if (nx)  // tap qq+1's fragment reads among tap qq's MFMAs
@@ -1051,12 +1104,12 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
           tap2(nx, wa, win, qq + 1, g * TG + qq + 1);
         }
       }
-      if (g == G::NG - 1) {
+      if (g == G::NG - 1 && !(XPF && c + 1 == nchunks)) {
         // issued after the loads (step g = 0): the weight pieces of steps 1..NG-1
         wait_img<(G::NG - 1) * G::DPWMIN>(st);
         if (G::NWIN == 1)  // single window: every wave is done reading chunk c's
           asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        write_img(win0 + (G::NWIN == 2 ? ((c + 1) & 1) * G::IMG : 0), c + 1);
+        write_img(win0 + (G::NWIN == 2 ? ((c + 1) & 1) * G::IMG : 0), c + 1, st);
       }
     }
   }
@@ -1070,7 +1123,12 @@ __global__ __launch_bounds__(NW * 64, (NPL == 1 || NW == 4) ? 2 : 1) void k_conv
   }
   if constexpr (SPB) {
     static_assert(V == 18 && SIN == 1 && NPL >= 2, "the folded block's data gradient");
-    spb_epilogue<MR>(p, acc, smem, n, r0, m0, mi, nj0);
+    if constexpr (XPF) {  // (no consumer of xpre above the wait for its loads)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < NXP; ++i) asm volatile("" : "+v"(xpre[i]));
+    }
+    spb_epilogue<MR>(p, acc, smem, n, r0, m0, mi, nj0, xpre);
     return;
   }
   if (p.s_out == 1) {
@@ -1162,9 +1220,14 @@ __global__ void k_pack_conv_w_x3(const float *w, __bf16 *wpk, int R, int C, int 
 }
 
 // The pack of several weight tensors in one launch (stgcn_fold_prep: every
-// folded block's forward and data-gradient weights once per step): job i covers
-// flat indices [start[i], start[i] + total) of the concatenated jobs, its start
-// a multiple of the 256-thread block (one job per block: the operand scale is
+// folded block's forward and data-gradient weights once per step). Same layout
+// and arithmetic as k_pack_conv_w_x3, but one thread per run of 8 channels
+// (one 16-byte piece of every plane: unit u = (rt, chunk, tap group, tap in
+// group, octet, row), its npl pieces npl * 8 elements apart... written whole)
+// and 32-bit index arithmetic (a job packs < 2^31 elements): the per-element
+// form spent most of its time on 64-bit divisions. Job i covers units
+// [start[i], start[i] + total / (8 npl)) of the concatenated jobs, its start a
+// multiple of the 256-thread block (one job per block: the operand scale is
 // read once per wave).
 struct PackJobs {
   PackJob j[kPackJobs];
@@ -1178,38 +1241,71 @@ __global__ __launch_bounds__(256) void k_pack_conv_w_x3_multi(PackJobs js) {
   while (k + 1 < js.n && gi >= js.start[k + 1]) ++k;
   const PackJob &q = js.j[k];
   const int se = q.npl == 2 ? f16x2_se_bits(q.amax_w ? amax_read_wave(q.amax_w) : 0x3f800000u) : 0;
-  const int64_t idx = gi - js.start[k];
-  if (idx >= q.total) return;
-  const int jj = (int)(idx & 7);
-  int64_t t = idx >> 3;
-  const int rl = (int)(t % q.rows);
-  t /= q.rows;
-  const int o = (int)(t & 1);
+  const int npl = q.npl, rows = q.rows, TG = q.TG, NG = q.NQ / q.TG;
+  const int units = (int)(q.total / (8 * npl));
+  const int u0 = (int)(gi - js.start[k]);
+  if (u0 >= units) return;
+  int t = u0;
+  const int rl = t % rows;
+  t /= rows;
+  const int o = t & 1;
   t >>= 1;
-  const int qq = (int)(t % q.TG);
-  t /= q.TG;
-  const int pl = (int)(t % q.npl);
-  t /= q.npl;
-  const int NG = q.NQ / q.TG;
-  const int g = (int)(t % NG);
+  const int qq = t % TG;
+  t /= TG;
+  const int g = t % NG;
   t /= NG;
-  const int ch = (int)(t % q.nch);
-  const int rt = (int)(t / q.nch);
-  const int r = rt * q.rows + rl, c = ch * 16 + o * 8 + jj, tap = g * q.TG + qq;
-  float v = 0.f;
-  if (r < q.R && c < q.C) v = q.w[(int64_t)r * q.w_sr + (int64_t)c * q.w_sc + (int64_t)tap * q.w_sq];
-  if (q.npl == 2) {
-    const float vs = v * pow2f(se);
-    const _Float16 h = (_Float16)vs;
-    const _Float16 l = (_Float16)(vs - (float)h);
-    reinterpret_cast<_Float16 *>(q.wpk)[idx] = pl == 0 ? h : l;
+  const int ch = t % q.nch;
+  const int rt = t / q.nch;
+  const int r = rt * rows + rl, c0 = ch * 16 + o * 8, tap = g * TG + qq;
+  float v[8];
+  const bool rok = r < q.R;
+  const float *src = q.w + (int64_t)(rok ? r : 0) * q.w_sr + (int64_t)tap * q.w_sq;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj)
+    v[jj] = (rok && c0 + jj < q.C) ? src[(int64_t)(c0 + jj) * q.w_sc] : 0.f;
+  // element index of plane 0's piece; plane pl is pl * TG * 2 * rows * 8 further
+  const int64_t base = ((((int64_t)(rt * q.nch + ch) * NG + g) * npl * TG + qq) * 2 + o) *
+                           rows * 8 + (int64_t)rl * 8;
+  const int64_t pstride = (int64_t)TG * 2 * rows * 8;
+  if (npl == 2) {  // fp16 (h, l) of the power-of-two-scaled weight
+    const float sc = pow2f(se);
+    unsigned hw[4], lw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+      const float a = v[2 * i] * sc, b = v[2 * i + 1] * sc;
+      const _Float16 ha = (_Float16)a, hb = (_Float16)b;
+      const h2_t hv = {ha, hb}, lv = {(_Float16)(a - (float)ha), (_Float16)(b - (float)hb)};
+      hw[i] = __builtin_bit_cast(unsigned, hv);
+      lw[i] = __builtin_bit_cast(unsigned, lv);
+    }
+    _Float16 *out = reinterpret_cast<_Float16 *>(q.wpk);
+    *reinterpret_cast<uint4 *>(out + base) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    *reinterpret_cast<uint4 *>(out + base + pstride) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
     return;
   }
-  const __bf16 h = (__bf16)v;
-  const float r1 = v - (float)h;
-  const __bf16 m = (__bf16)r1;
-  const __bf16 l = (__bf16)(r1 - (float)m);
-  reinterpret_cast<__bf16 *>(q.wpk)[idx] = pl == 0 ? h : (pl == 1 ? m : l);
+  __bf16 pv[3][8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const __bf16 h = (__bf16)v[jj];
+    const float r1 = v[jj] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    pv[0][jj] = h;
+    pv[1][jj] = m;
+    pv[2][jj] = (__bf16)(r1 - (float)m);
+  }
+  __bf16 *out = reinterpret_cast<__bf16 *>(q.wpk);
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl)  // (npl = 1: h; npl = 3: h, m, l)
+    if (pl < npl) {
+      unsigned w4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x2_t pr = {pv[pl][2 * i], pv[pl][2 * i + 1]};
+        w4[i] = __builtin_bit_cast(unsigned, pr);
+      }
+      *reinterpret_cast<uint4 *>(out + base + pl * pstride) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    }
 }
 
 static int x3_tg(int NQ) { return NQ == 9 ? 3 : NQ; }
@@ -1350,7 +1446,8 @@ hipError_t launch_pack_jobs(const PackJob *jobs, int n, hipStream_t s) {
     js.start[0] = 0;
     for (int k = 0; k < js.n; ++k) {
       js.j[k] = jobs[i0 + k];
-      js.start[k + 1] = js.start[k] + (js.j[k].total + 255) / 256 * 256;
+      const int64_t units = js.j[k].total / (8 * js.j[k].npl);  // (threads of job k)
+      js.start[k + 1] = js.start[k] + (units + 255) / 256 * 256;
     }
     const int64_t tot = js.start[js.n];
     if (tot > 0)
