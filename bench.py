@@ -479,6 +479,9 @@ def main():
                     help="A/B only: write every block output (no ABI 8/9 unwritten outputs)")
     ap.add_argument("--torch-ops", action="store_true",
                     help="head + cross entropy + Adam from torch instead of the HIP library")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="run the timed steps eagerly (default at N=1: the step captured once "
+                         "in a HIP graph and replayed, train_ops.GraphedStep)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -503,9 +506,13 @@ def main():
     if args.no_lazy_links:
         model.lazy_links = False
     params = [p for p in model.parameters()]
+    # one process: the whole step (forward, backward, head, Adam) captured in a
+    # HIP graph and replayed (no per-launch host work; FusedAdam's step count on
+    # the device). With ranks: eager (the RCCL all-reduce hooks stay outside)
+    graph_on = world == 1 and not args.torch_ops and not args.no_graph
     # FusedAdam: torch.optim.Adam semantics, one libstgcn_hip launch per step
     opt = (torch.optim.Adam(params, lr=1e-3) if args.torch_ops
-           else pkg.FusedAdam(params, lr=1e-3))
+           else pkg.FusedAdam(params, lr=1e-3, capturable=graph_on))
     dp = pkg.dp.GradAllReduce(model, world) if world > 1 else None
     gen = torch.Generator(device="cpu").manual_seed(1 + rank)
     x = torch.randn(cfg["N"], cfg["C"], cfg["T"], cfg["V"], generator=gen).to(device)
@@ -527,20 +534,28 @@ def main():
         return loss
 
     progress(f"{args.config}: model built, {args.warmup} warm-up steps")
-    for _ in range(args.warmup):
-        step()
+    run = step
+    if graph_on:  # W eager warm-up steps, the capture, one untimed replay
+        run = pkg.GraphedStep(step, warmup=args.warmup)
+        run()
+    else:
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # the loss of the first timed window's last step (a graph's output tensor is
+    # rewritten by every later replay)
+    loss_first = float(loss.item())
     if world > 1:
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -560,7 +575,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            run()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -646,7 +661,8 @@ def main():
             "model_tflops": round(clips * gf_clip / 1e3, 2),
             "runs_clips_s": [round(r, 2) for r in runs],
             "median_clips_s": round(sorted(runs)[len(runs) // 2], 2),
-            "loss": round(float(loss.item()), 5),
+            "loss": round(loss_first, 5),
+            "step_mode": "hip_graph" if graph_on else "eager",
         }
         out["gpu_state_under_load"] = gpu_state_read(smi)
         out["gpu_state_after"] = gpu_state_read(gpu_state_start())

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define STGCN_ABI_VERSION 10
+#define STGCN_ABI_VERSION 11
 
 /* ABI 7: words of max |y| after the 5 * C sums of a y_stats block */
 #define STGCN_STATS_AMAX_WORDS 2048
@@ -417,6 +417,17 @@ int stgcn_adam_build_table(const stgcn_adam_tensor_t *tensors, int ntensors, voi
 int stgcn_adam_step(const void *dev_table, int ntensors, int64_t total_chunks, double lr,
                     double beta1, double beta2, double eps, double weight_decay, int64_t step,
                     void *stream);
+/* ABI 11: the same update with the step count in DEVICE memory (a float, as
+ * torch.optim.Adam(capturable=True) keeps it): *step += 1 on the stream, then
+ * the update with the bias corrections formed on the device from the new count
+ * (in double, rounded to float: the values stgcn_adam_step forms on the host).
+ * No host value changes between steps, so the launch can be captured once in a
+ * HIP graph and replayed every training step (train_ops.FusedAdam
+ * (capturable=True), train_ops.GraphedStep). Replaces the host-step launch of
+ * stgcn_adam_step (torch optim/adam.py _multi_tensor_adam, capturable branch). */
+int stgcn_adam_step_dev(const void *dev_table, int ntensors, int64_t total_chunks, double lr,
+                        double beta1, double beta2, double eps, double weight_decay, float *step,
+                        void *stream);
 
 #ifdef __cplusplus
 }

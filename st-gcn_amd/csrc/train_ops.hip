@@ -50,9 +50,11 @@ struct AdamScalars {
   float lerp_w, beta2, one_minus_beta2, neg_step_size, bc2_sqrt, eps, wd;
 };
 
-__global__ __launch_bounds__(256) void k_adam(const stgcn_adam_tensor_t *tab,
-                                              const int64_t *chunk_start, int ntensors,
-                                              AdamScalars s) {
+// the element loop of both launch forms (one function: the same instructions)
+__device__ __forceinline__ void adam_block(const stgcn_adam_tensor_t *tab,
+                                           const int64_t *chunk_start, int ntensors,
+                                           const AdamScalars &s) {
+#pragma clang fp contract(off)
   // tensor of this block: the last t with chunk_start[t] <= blockIdx.x
   const int64_t b = blockIdx.x;
   int lo = 0, hi = ntensors - 1;
@@ -65,6 +67,8 @@ __global__ __launch_bounds__(256) void k_adam(const stgcn_adam_tensor_t *tab,
   for (int i = threadIdx.x; i < kAdamChunk; i += 256) {
     const int64_t e = base + i;
     if (e >= t.numel) break;
+    // (every operation rounded on its own -- no fma contraction, whose choices
+    // differed between the two kernels -- as torch's unfused CPU loop rounds)
     float p = t.param[e];
     float g = t.grad[e];
     if (s.wd != 0.f) g = g + s.wd * p;
@@ -78,6 +82,41 @@ __global__ __launch_bounds__(256) void k_adam(const stgcn_adam_tensor_t *tab,
     t.exp_avg_sq[e] = v;
     t.param[e] = p;
   }
+}
+
+__global__ __launch_bounds__(256) void k_adam(const stgcn_adam_tensor_t *tab,
+                                              const int64_t *chunk_start, int ntensors,
+                                              AdamScalars s) {
+  adam_block(tab, chunk_start, ntensors, s);
+}
+
+// The device-step form (stgcn_adam_step_dev, ABI 11): k_adam_tick advances the
+// step count, then every block forms the scalars from it exactly as
+// stgcn_adam_step does on the host (double, rounded to float) -- thread 0 into
+// LDS -- and runs k_adam's element loop.
+__global__ void k_adam_tick(float *step) { *step = *step + 1.f; }
+
+__global__ __launch_bounds__(256) void k_adam_dev(const stgcn_adam_tensor_t *tab,
+                                                  const int64_t *chunk_start, int ntensors,
+                                                  const float *step, double lr, double beta1,
+                                                  double beta2, double eps, double wd) {
+  __shared__ AdamScalars sh;
+  if (threadIdx.x == 0) {
+    const double t = (double)*step;
+    const double bc1 = 1.0 - pow(beta1, t), bc2 = 1.0 - pow(beta2, t);
+    AdamScalars sc;
+    sc.lerp_w = (float)(1.0 - beta1);
+    sc.beta2 = (float)beta2;
+    sc.one_minus_beta2 = (float)(1.0 - beta2);
+    sc.neg_step_size = (float)(-(lr / bc1));
+    sc.bc2_sqrt = (float)sqrt(bc2);
+    sc.eps = (float)eps;
+    sc.wd = (float)wd;
+    sh = sc;
+  }
+  __syncthreads();
+  const AdamScalars s = sh;
+  adam_block(tab, chunk_start, ntensors, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -293,6 +332,21 @@ int stgcn_adam_step(const void *dev_table, int ntensors, int64_t total_chunks, d
                                                      (size_t)ntensors * sizeof(stgcn_adam_tensor_t));
   hipLaunchKernelGGL(k_adam, dim3((unsigned)total_chunks), dim3(256), 0, (hipStream_t)stream, tab,
                      cs, ntensors, sc);
+  HIP_TRY2(hipGetLastError());
+  return STGCN_OK;
+}
+
+int stgcn_adam_step_dev(const void *dev_table, int ntensors, int64_t total_chunks, double lr,
+                        double beta1, double beta2, double eps, double weight_decay, float *step,
+                        void *stream) {
+  if (!dev_table || ntensors <= 0 || total_chunks <= 0 || !step)
+    return fail(STGCN_E_INVALID, "adam: bad table / chunk count / step pointer");
+  const auto *tab = reinterpret_cast<const stgcn_adam_tensor_t *>(dev_table);
+  const auto *cs = reinterpret_cast<const int64_t *>(reinterpret_cast<const char *>(dev_table) +
+                                                     (size_t)ntensors * sizeof(stgcn_adam_tensor_t));
+  hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+  hipLaunchKernelGGL(k_adam_dev, dim3((unsigned)total_chunks), dim3(256), 0, (hipStream_t)stream,
+                     tab, cs, ntensors, step, lr, beta1, beta2, eps, weight_decay);
   HIP_TRY2(hipGetLastError());
   return STGCN_OK;
 }

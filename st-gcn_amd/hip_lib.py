@@ -21,7 +21,7 @@ if os.environ.get("STGCN_LIB_VARIANT"):  # A/B kernel experiments (scripts/), in
     LIB_PATH = os.path.join(LIB_DIR, f"libstgcn_hip_{os.environ['STGCN_LIB_VARIANT']}.so")
     import sys
     print(f"stgcn: loading the A/B variant library {LIB_PATH}", file=sys.stderr)
-ABI_VERSION = 10
+ABI_VERSION = 11
 F_RESIDUAL = 1  # stgcn_desc_t.flags
 F_BF16 = 2      # channel GEMMs on bf16 MFMA (fp32 accumulate, fp32 tensors)
 F_F32X3 = 4     # fp32 temporal GEMMs via exact 3-way bf16 operand splits (fp32 accuracy)
@@ -105,7 +105,7 @@ EXPORTED = ("stgcn_abi_version", "stgcn_last_error", "stgcn_check_desc",
             "stgcn_adam_build_table", "stgcn_adam_step", "stgcn_spatial_workspace_bytes",
             "stgcn_spatial_fwd", "stgcn_spatial_bwd", "stgcn_keep_g_bytes",
             "stgcn_block_plan", "stgcn_fold_prep_bytes", "stgcn_fold_prep", "stgcn_head_fwd_u",
-            "stgcn_head_bwd_nc")
+            "stgcn_head_bwd_nc", "stgcn_adam_step_dev")
 
 _LIB = None
 
@@ -153,6 +153,9 @@ def load_library(path=LIB_PATH):
     lib.stgcn_adam_step.argtypes = [_vp, ctypes.c_int, ctypes.c_int64] + \
         [ctypes.c_double] * 5 + [ctypes.c_int64, _vp]
     lib.stgcn_adam_step.restype = ctypes.c_int
+    lib.stgcn_adam_step_dev.argtypes = [_vp, ctypes.c_int, ctypes.c_int64] + \
+        [ctypes.c_double] * 5 + [_vp, _vp]
+    lib.stgcn_adam_step_dev.restype = ctypes.c_int
     lib.stgcn_spatial_workspace_bytes.argtypes = [ctypes.POINTER(SpatialDesc), ctypes.c_int]
     lib.stgcn_spatial_workspace_bytes.restype = ctypes.c_size_t
     lib.stgcn_spatial_fwd.argtypes = [ctypes.POINTER(SpatialDesc)] + [_vp] * 6 + \

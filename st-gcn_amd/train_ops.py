@@ -101,14 +101,26 @@ class FusedAdam(torch.optim.Optimizer):
     table (pointers of param / grad / exp_avg / exp_avg_sq) is rebuilt on the
     host only when a pointer changed (e.g. grads re-allocated after
     zero_grad(set_to_none=True)) and copied to the device asynchronously from
-    pinned memory; one table per parameter group (keyed by the group's index)."""
+    pinned memory; one table per parameter group (keyed by the group's index).
+
+    capturable=True (as torch.optim.Adam(capturable=True)): the step count lives
+    on the device (one float tensor per group, shared by the group's parameters'
+    ``state["step"]``) and is advanced by the library (stgcn_adam_step_dev, ABI
+    11), so ``step()`` reads nothing from the device and can be captured in a HIP
+    graph (``GraphedStep``). A table built during a capture (the captured
+    backward allocates new gradients) is written into a pinned buffer set aside
+    by the last eager build and kept alive with the table: every replay's copy
+    re-reads it."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
-                 amsgrad=False):
+                 amsgrad=False, capturable=False):
         if amsgrad:
             raise NotImplementedError("FusedAdam: amsgrad")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        self._tables = {}  # group index -> (key, device table, chunks, ntensors)
+        self.capturable = capturable
+        self._tables = {}  # group index -> (key, device table, chunks, ntensors, host table)
+        self._spare = {}   # group index -> unused pinned table buffer (capturable)
+        self._captured = []  # pinned tables a captured step's copies read
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -124,16 +136,20 @@ class FusedAdam(torch.optim.Optimizer):
             for p in plist:
                 _check_f32(p, "param")
                 _check_f32(p.grad, "grad")
-                st = self.state[p]
-                if not st:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] = st["step"] + 1  # (not in place: loaded state may share it)
-            steps = {int(self.state[p]["step"].item()) for p in plist}
-            if len(steps) != 1:
-                raise RuntimeError("FusedAdam: parameters of a group at different steps")
-            step = steps.pop()
+            if self.capturable:
+                dstep = self._device_step(plist)
+            else:
+                for p in plist:
+                    st = self.state[p]
+                    if not st:
+                        st["step"] = torch.tensor(0.0)
+                        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["step"] = st["step"] + 1  # (not in place: loaded state may share it)
+                steps = {int(self.state[p]["step"].item()) for p in plist}
+                if len(steps) != 1:
+                    raise RuntimeError("FusedAdam: parameters of a group at different steps")
+                step = steps.pop()
             tabs = [hip_lib.AdamTensor(p.data_ptr(), p.grad.data_ptr(),
                                        self.state[p]["exp_avg"].data_ptr(),
                                        self.state[p]["exp_avg_sq"].data_ptr(), p.numel())
@@ -144,18 +160,87 @@ class FusedAdam(torch.optim.Optimizer):
             if cached is None or cached[0] != key:
                 n = len(tabs)
                 nbytes = lib.stgcn_adam_table_bytes(n)
-                host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+                if torch.cuda.is_current_stream_capturing():
+                    # (no pinned allocation inside a capture: the spare buffer
+                    # the last eager build left, never yet read by a copy)
+                    host = self._spare.pop(gi, None)
+                    if host is None or host.numel() < nbytes:
+                        raise RuntimeError("FusedAdam: capture a step only after an eager "
+                                           "step of the same parameters (GraphedStep warm-up)")
+                    self._captured.append(host)  # (read by every replay: never freed)
+                else:
+                    host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+                    if self.capturable:
+                        self._spare[gi] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
                 chunks = ctypes.c_int64(0)
                 arr = (hip_lib.AdamTensor * n)(*tabs)
                 hip_lib.check(lib.stgcn_adam_build_table(arr, n, ctypes.c_void_p(host.data_ptr()),
                                                          nbytes, ctypes.byref(chunks)))
                 dev_table = torch.empty(nbytes, dtype=torch.uint8, device=dev)
                 dev_table.copy_(host, non_blocking=True)
-                cached = (key, dev_table, chunks.value, n)
+                cached = (key, dev_table, chunks.value, n, host)
                 self._tables[gi] = cached
-            _, dev_table, nchunks, n = cached
+            _, dev_table, nchunks, n, _ = cached
             b1, b2 = group["betas"]
-            hip_lib.check(lib.stgcn_adam_step(
-                hip_lib.ptr(dev_table), n, nchunks, group["lr"], b1, b2,
-                group["eps"], group["weight_decay"], step, hip_lib.stream_handle(dev)))
+            if self.capturable:
+                hip_lib.check(lib.stgcn_adam_step_dev(
+                    hip_lib.ptr(dev_table), n, nchunks, group["lr"], b1, b2,
+                    group["eps"], group["weight_decay"], hip_lib.ptr(dstep),
+                    hip_lib.stream_handle(dev)))
+            else:
+                hip_lib.check(lib.stgcn_adam_step(
+                    hip_lib.ptr(dev_table), n, nchunks, group["lr"], b1, b2,
+                    group["eps"], group["weight_decay"], step, hip_lib.stream_handle(dev)))
         return loss
+
+    def _device_step(self, plist):
+        """The group's device step count (float32, shape ()): created with the
+        state (0), or taken over from loaded state once (one host read, outside
+        any capture), then shared by every parameter of the group."""
+        dev = plist[0].device
+        shared = None
+        for p in plist:
+            st = self.state[p].get("step")
+            if torch.is_tensor(st) and st.is_cuda and st.dtype == torch.float32 and st.dim() == 0:
+                shared = st if shared is None else shared
+        if shared is None or any(self.state[p].get("step") is not shared for p in plist):
+            vals = {float(self.state[p]["step"]) for p in plist if "step" in self.state[p]}
+            if len(vals) > 1:
+                raise RuntimeError("FusedAdam: parameters of a group at different steps")
+            shared = torch.full((), vals.pop() if vals else 0.0, device=dev, dtype=torch.float32)
+            for p in plist:
+                st = self.state[p]
+                if "exp_avg" not in st:
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] = shared
+        return shared
+
+
+class GraphedStep:
+    """One training step captured in a HIP graph and replayed (torch.cuda.graph
+    over the caller's stream work: every libstgcn_hip launch goes to the capture
+    stream, allocations come from the graph's private pool, so replays reuse the
+    same buffers). ``step_fn()`` must be replay-safe: static inputs (copy new
+    data into them before ``__call__``), no host reads of device values, no
+    dropout (its seed is drawn on the host), optimizer ``FusedAdam(capturable=
+    True)``. ``warmup`` eager calls run first on a side stream (the torch
+    recipe: lazy allocations and table builds happen outside the capture).
+    ``__call__`` replays and returns the tensors the captured call returned
+    (their storage is rewritten by every replay)."""
+
+    def __init__(self, step_fn, warmup=3):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                step_fn()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()  # (the warm-up's host-to-device table copies have run)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = step_fn()
+
+    def __call__(self):
+        self.graph.replay()
+        return self.out

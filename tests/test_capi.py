@@ -29,7 +29,7 @@ def test_header_declares_entry_points(pkg):
 def test_library_exports_every_header_symbol(pkg, lib):
     for name in _header_functions():
         assert hasattr(lib, name), name
-    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 10
+    assert lib.stgcn_abi_version() == pkg.hip_lib.ABI_VERSION == 11
 
 
 def _desc(pkg, **kw):
