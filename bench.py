@@ -625,12 +625,17 @@ def main():
             progress(f"batch sweep: N={nb}")
             x = torch.randn(nb, cfg["C"], cfg["T"], cfg["V"], generator=gen).to(device)
             labels = torch.randint(0, cfg["classes"], (nb,), generator=gen).to(device)
-            for _ in range(2):
-                step()
+            sweep_run = step  # (the bench's step mode: a graph captured at this N)
+            if graph_on:
+                sweep_run = pkg.GraphedStep(step, warmup=2)
+                sweep_run()
+            else:
+                for _ in range(2):
+                    step()
             torch.cuda.synchronize()
             ts = time.perf_counter()
             for _ in range(5):
-                step()
+                sweep_run()
             torch.cuda.synchronize()
             sweep[str(nb)] = round(nb * 5 / (time.perf_counter() - ts), 2)
         sweep = dict(sorted(sweep.items(), key=lambda kv: int(kv[0])))

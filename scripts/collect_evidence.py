@@ -25,15 +25,19 @@ def top_text(path, n=30):
     return "\n".join(out) + "\n"
 
 
-def step_text(trace, steps=10):
+def step_text(trace, steps=10, skip=3):
     """Per-step kernel time over the FIRST `steps` Adam-delimited steps after
     the warmup of the first timed run (the bench's default path; cfg2 runs its
     exact fp32-MFMA alternative afterwards)."""
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
-    adam = [i for i, r in enumerate(rows) if "adam" in r["Kernel_Name"].lower()]
+    # one Adam update per step (the device-step form also launches its counter
+    # tick, k_adam_tick, which is not counted as a step boundary)
+    adam = [i for i, r in enumerate(rows)
+            if "adam" in r["Kernel_Name"].lower() and "tick" not in r["Kernel_Name"]]
     # bench: W warmup steps then K timed steps per run; the warmup is 3 in the
-    # evidence script, so the first timed step starts after the 3rd Adam
-    seg = rows[adam[2] + 1: adam[2 + steps] + 1]
+    # evidence script (+ one untimed replay in the HIP-graph step mode), so the
+    # first timed step starts after the skip-th Adam
+    seg = rows[adam[skip - 1] + 1: adam[skip - 1 + steps] + 1]
     t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
     per = {}
     for r in seg:
@@ -62,7 +66,10 @@ def main(tag, cfgs):
             open(os.path.join(dst, f"{tag}_kernel_stats_{c}.txt"), "w").write(top_text(st))
         tr = os.path.join(src, f"stats_{c}", "run_kernel_trace.csv")
         if os.path.exists(tr):
-            open(os.path.join(dst, f"{tag}_step_{c}.txt"), "w").write(step_text(tr))
+            sb = os.path.join(src, f"stats_bench_{c}.json")
+            graph = os.path.exists(sb) and json.load(open(sb)).get("step_mode") == "hip_graph"
+            open(os.path.join(dst, f"{tag}_step_{c}.txt"), "w").write(
+                step_text(tr, skip=4 if graph else 3))
     lg = os.path.join(src, "pytest_gpu.log")
     if os.path.exists(lg):
         lines = open(lg).read().splitlines()
