@@ -443,13 +443,14 @@ def pmc_profile(config):
 def pmc_lookup(table, sym):
     """table[sym] where the PMC file names the kernel as the timing does; else
     the one rocprof name that only appends template arguments left at their
-    default (false), e.g. k_conv_x3<..,false,true> -> k_conv_x3<..,false,true,false>."""
+    default (false, or k_conv_x3's wave count NW = 8), e.g.
+    k_conv_x3<..,false,true> -> k_conv_x3<..,false,true,false,8>."""
     if sym in table:
         return table[sym]
     head = sym[:-1] + ","
     hits = [k for k in table
             if k.startswith(head) and k.endswith(">") and
-            all(a == "false" for a in k[len(head):-1].split(","))]
+            all(a in ("false", "8") for a in k[len(head):-1].split(","))]
     return table[hits[0]] if len(hits) == 1 else None
 
 

@@ -24,6 +24,12 @@ def test_pmc_lookup_exact_and_defaulted_template_args():
     assert bench.pmc_lookup({"k_conv_x3<9,3,18,1,2,2,false,false,true>": 3},
                             "k_conv_x3<9,3,18,1,2,2,false,false>") is None
     assert bench.pmc_lookup(table, "k_wgrad_x3<18,1,2,2>") is None
+    # round 6: k_conv_x3's trailing wave count (NW = 8 by default, 4 for the
+    # two-workgroups-per-CU forward) -- 8 is a default, 4 a different kernel
+    t6 = {"k_conv_x3<9,3,18,1,2,2,false,true,false,8>": 5,
+          "k_conv_x3<9,3,18,1,2,2,false,false,false,4>": 6}
+    assert bench.pmc_lookup(t6, "k_conv_x3<9,3,18,1,2,2,false,true>") == 5
+    assert bench.pmc_lookup(t6, "k_conv_x3<9,3,18,1,2,2,false,false>") is None
 
 
 def test_pmc_profile_needs_this_source_hash(tmp_path, monkeypatch):
