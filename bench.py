@@ -536,9 +536,12 @@ def main():
 
     progress(f"{args.config}: model built, {args.warmup} warm-up steps")
     run = step
-    if graph_on:  # W eager warm-up steps, the capture, one untimed replay
-        run = pkg.GraphedStep(step, warmup=args.warmup)
-        run()
+    if graph_on:  # the W warm-up steps: a few eager (the capture needs one), the
+        # capture, then untimed replays
+        n_eager = max(1, min(args.warmup - 1, 2))
+        run = pkg.GraphedStep(step, warmup=n_eager)
+        for _ in range(max(1, args.warmup - n_eager)):
+            run()
     else:
         for _ in range(args.warmup):
             step()
