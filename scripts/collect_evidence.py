@@ -35,7 +35,7 @@ def step_text(trace, steps=10, skip=3):
     adam = [i for i, r in enumerate(rows)
             if "adam" in r["Kernel_Name"].lower() and "tick" not in r["Kernel_Name"]]
     # bench: W warmup steps then K timed steps per run; the warmup is 3 in the
-    # evidence script (+ one untimed replay in the HIP-graph step mode), so the
+    # evidence script (in the HIP-graph mode: eager steps + untimed replays), so the
     # first timed step starts after the skip-th Adam
     seg = rows[adam[skip - 1] + 1: adam[skip - 1 + steps] + 1]
     t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
@@ -66,10 +66,12 @@ def main(tag, cfgs):
             open(os.path.join(dst, f"{tag}_kernel_stats_{c}.txt"), "w").write(top_text(st))
         tr = os.path.join(src, f"stats_{c}", "run_kernel_trace.csv")
         if os.path.exists(tr):
+            # (W = 3 warm-up steps in either step mode: eager, or 2 eager + the
+            # capture + 1 untimed replay; r6x ran 3 eager + 1 replay: skip 4)
             sb = os.path.join(src, f"stats_bench_{c}.json")
             graph = os.path.exists(sb) and json.load(open(sb)).get("step_mode") == "hip_graph"
-            open(os.path.join(dst, f"{tag}_step_{c}.txt"), "w").write(
-                step_text(tr, skip=4 if graph else 3))
+            skip = 4 if graph and tag == "r6x" else 3
+            open(os.path.join(dst, f"{tag}_step_{c}.txt"), "w").write(step_text(tr, skip=skip))
     lg = os.path.join(src, "pytest_gpu.log")
     if os.path.exists(lg):
         lines = open(lg).read().splitlines()
