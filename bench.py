@@ -483,6 +483,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="run the timed steps eagerly (default at N=1: the step captured once "
                          "in a HIP graph and replayed, train_ops.GraphedStep)")
+    ap.add_argument("--dp-graph", action="store_true",
+                    help="N>1: forward + backward and Adam in two HIP graphs around the eager "
+                         "bucket all-reduces (train_ops.GraphedDPStep; default: eager)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -509,8 +512,12 @@ def main():
     params = [p for p in model.parameters()]
     # one process: the whole step (forward, backward, head, Adam) captured in a
     # HIP graph and replayed (no per-launch host work; FusedAdam's step count on
-    # the device). With ranks: eager (the RCCL all-reduce hooks stay outside)
-    graph_on = world == 1 and not args.torch_ops and not args.no_graph
+    # the device). With ranks: eager, the bucket all-reduces overlapped with
+    # backward; --dp-graph runs forward + backward and Adam in two graphs around
+    # the eager all-reduces (train_ops.GraphedDPStep: equal results, but 4x
+    # slower in the 2-rank gloo rehearsal on one GPU, profiles/r6dpg_*, and not
+    # measured over RCCL)
+    graph_on = not args.torch_ops and not args.no_graph and (world == 1 or args.dp_graph)
     # FusedAdam: torch.optim.Adam semantics, one libstgcn_hip launch per step
     opt = (torch.optim.Adam(params, lr=1e-3) if args.torch_ops
            else pkg.FusedAdam(params, lr=1e-3, capturable=graph_on))
@@ -535,11 +542,17 @@ def main():
         return loss
 
     progress(f"{args.config}: model built, {args.warmup} warm-up steps")
+    def fwd_bwd():  # (ranks > 1, graphed: dp.zero_grad / synchronize by GraphedDPStep)
+        loss, _ = model.forward_loss(x, labels)
+        loss.backward()
+        return loss
+
     run = step
     if graph_on:  # the W warm-up steps: a few eager (the capture needs one), the
         # capture, then untimed replays
         n_eager = max(1, min(args.warmup - 1, 2))
-        run = pkg.GraphedStep(step, warmup=n_eager)
+        run = (pkg.GraphedDPStep(fwd_bwd, dp, opt.step, warmup=n_eager) if dp is not None
+               else pkg.GraphedStep(step, warmup=n_eager))
         for _ in range(max(1, args.warmup - n_eager)):
             run()
     else:

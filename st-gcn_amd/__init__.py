@@ -8,7 +8,7 @@ library (``include/stgcn_hip.h``). Import via ``stgcn_loader.load()``.
 from . import graph, hip_lib, fused, network, model, dp, train_ops, data  # noqa: F401
 from .network import SpatialConv, SpatialTemporalConv  # noqa: F401
 from .model import STGCN, STGCNStack, flops_per_clip  # noqa: F401
-from .train_ops import FusedAdam, GraphedStep, StgcnHeadFn  # noqa: F401
+from .train_ops import FusedAdam, GraphedDPStep, GraphedStep, StgcnHeadFn  # noqa: F401
 
 __all__ = ["graph", "hip_lib", "fused", "network", "model", "train_ops", "data", "SpatialConv",
-           "SpatialTemporalConv", "STGCN", "STGCNStack", "flops_per_clip", "FusedAdam", "GraphedStep", "StgcnHeadFn"]
+           "SpatialTemporalConv", "STGCN", "STGCNStack", "flops_per_clip", "FusedAdam", "GraphedDPStep", "GraphedStep", "StgcnHeadFn"]

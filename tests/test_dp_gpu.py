@@ -48,6 +48,25 @@ def test_dp_two_ranks_on_hip(tmp_path, world):
     assert res["step_err"] < 1e-6, res
 
 
+def test_graphed_dp_step_matches_eager(tmp_path):
+    """train_ops.GraphedDPStep (bench.py's step mode at N > 1: forward +
+    backward and Adam in two HIP graphs, the bucket all-reduces eager between
+    them) against the eager DP step with the all-reduces issued from the
+    backward hooks: loss, logits and every parameter equal after 5 steps on
+    every rank (tests/dp_graph_worker.py)."""
+    out = tmp_path / "dpg.json"
+    env = dict(os.environ, DP_OUT=str(out), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dp_graph_worker.py")]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    print(res)
+    assert res["all_ranks_equal_eager"], res
+    assert res["ranks_identical"] and res["bucket_views"], res
+
+
 def test_bench_two_ranks_rehearsal():
     """bench.py's own N>1 branch (the one the driver launches per GPU over RCCL)
     run end to end with 2 ranks sharing the one GPU over gloo
@@ -68,3 +87,4 @@ def test_bench_two_ranks_rehearsal():
     assert out["config"]["parallelism"] == "dp2" and out["scaling"] == "weak"
     assert out["value"] > 0 and out["loss"] == out["loss"]  # finite, not NaN
     assert "cpu_baseline" not in out  # rank 0 at N=1 only
+    assert out["step_mode"] == "eager"  # (--dp-graph: train_ops.GraphedDPStep)
