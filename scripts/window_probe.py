@@ -3,7 +3,9 @@ graph step mode's first-timed-window dip). Builds the step as
 bench.py does (W = 5 warm-up: 2 eager + capture + 3 replays in graph mode),
 then times WP_WINDOWS windows of K = 20 steps exactly as bench.py brackets
 them, with HIP events around every step of the first two windows.
-WP_MODE: graph | eager; WP_SLEEP: seconds of host sleep before each window."""
+WP_MODE: graph | eager; WP_SLEEP: seconds of host sleep before each window;
+WP_ITEM=1: read the step's loss on the host after each window (as bench.py does
+after its first); WP_EVENTS=0: no per-step events."""
 import os
 import sys
 import time
@@ -17,6 +19,8 @@ from stgcn_loader import load  # noqa: E402
 mode = os.environ.get("WP_MODE", "graph")
 slp = float(os.environ.get("WP_SLEEP", "0"))
 nwin = int(os.environ.get("WP_WINDOWS", "6"))
+item = os.environ.get("WP_ITEM", "0") == "1"
+events = os.environ.get("WP_EVENTS", "1") == "1"
 K, W = 20, 5
 pkg = load()
 dev = torch.device("cuda", 0)
@@ -49,18 +53,20 @@ torch.cuda.synchronize()
 for w in range(nwin):
     if slp:
         time.sleep(slp)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)] if w < 2 else None
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 1)] if w < 2 and events else None
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
         if ev:
             ev[i].record()
-        run()
+        loss = run()
     if ev:
         ev[K].record()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    line = f"{mode} sleep={slp} window {w}: {cfg['N'] * K / dt:.1f} clips/s, {dt / K * 1e3:.3f} ms/step"
+    if item:
+        float(loss.item())
+    line = f"{mode} sleep={slp} item={int(item)} events={int(events)} window {w}: {cfg['N'] * K / dt:.1f} clips/s, {dt / K * 1e3:.3f} ms/step"
     if ev:
         line += " | steps ms " + " ".join(f"{ev[i].elapsed_time(ev[i + 1]):.2f}" for i in range(K))
     print(line, flush=True)
